@@ -1,0 +1,229 @@
+/*
+ * egraph.h -- C-ABI of libegraph.so, the MI355X (gfx950) evidence-graph correlation engine.
+ *
+ * Drop-in boundary for the reference's hot path (ShreyashDarade/Kubernetes-AIOps-Evidence-Graph).
+ * Plain C: pointers, sizes, status codes.  No torch / HIP types appear in any signature;
+ * `stream` arguments are hipStream_t passed as void* (NULL = the null stream).
+ * Device pointers are caller-owned (e.g. torch tensors) and are never retained past a call;
+ * egr_snapshot / egr_plan own the device buffers they allocate.
+ *
+ * Reference interfaces each group replaces (paths relative to the reference repo):
+ *   egr_rules_eval  <- RulesEngine.generate_hypotheses   src/services/rca/rules_engine.py:199-233
+ *                      (+ _extract_signals :264-376, _match_rule :378-397, _check_condition :399-441,
+ *                         _calculate_confidence :443-455, unknown fallback :457-478)
+ *                      fused with HypothesisRanker.rank  src/services/rca/hypothesis_ranker.py:13-80
+ *   egr_rank        <- HypothesisRanker.rank             src/services/rca/hypothesis_ranker.py:13-80
+ *   egr_graph_*     <- GraphService.create_entities_batch / create_relations_batch
+ *                                                        src/database/neo4j.py:95-113, :145-167
+ *   egr_snapshot_*  <- the Neo4j store the Cypher queries read (docker-compose.yml:26-33)
+ *   egr_plan_reach* <- GraphService.get_incident_graph -> apoc.path.subgraphAll(maxLevel=3)
+ *                                                        src/database/neo4j.py:169-202
+ *   egr_plan_hop / egr_plan_topk
+ *                   <- build-defined typed k-hop propagation + per-incident top-k (no reference
+ *                      counterpart; spec in DESIGN.md §A9)
+ *
+ * Every function returns EGR_OK (0) or a negative status; egr_last_error() describes the
+ * last failure on the calling thread.
+ */
+#ifndef EGRAPH_H_
+#define EGRAPH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EGR_OK 0
+#define EGR_EINVAL (-1)   /* bad argument (Python shim raises ValueError) */
+#define EGR_EDEVICE (-2)  /* HIP runtime / kernel failure (shim raises RuntimeError) */
+#define EGR_ENOMEM (-3)   /* allocation failure */
+#define EGR_ESTATE (-4)   /* object used in the wrong state */
+
+#define EGR_VERSION 1
+
+const char* egr_last_error(void);
+int egr_version(void);
+/* Number of HIP devices visible (0 on a GPU-less host; never fails). */
+int egr_device_count(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Rules (A1-A6).  Evidence rows are pre-encoded per row by the host encoder into 20 bytes:
+ *   row_flags  u32  EGR_F_* bits below (per-row predicates, rules_engine.py:315-376)
+ *   row_vocab  u32  bit i set = the row's waiting reason / terminated reason / log pattern is
+ *                   vocabulary entry i (vocabulary built from the rule table's value lists)
+ *   row_node   u32  pods_by_node key of the row (rules_engine.py:323-330), EGR_NO_NODE if the
+ *                   row does not count
+ *   row_err    f64  log error_count contribution (rules_engine.py:354); integral unless
+ *                   EGR_F_ERR_FLOAT is set (then the segment is summed in row order)
+ * Incident i owns rows [seg_off[i], seg_off[i+1]).
+ * ---------------------------------------------------------------------------------------- */
+#define EGR_F_RECENT_DEPLOY   (1u << 0)  /* deploy_change: is_recent_change truthy         :342 */
+#define EGR_F_IMAGE_CHANGED   (1u << 1)  /* image_change: image_changed truthy             :347 */
+#define EGR_F_MEMORY_HIGH     (1u << 2)  /* metric: memory & anomalous & current > 90      :360 */
+#define EGR_F_HPA_AT_MAX      (1u << 3)  /* metric: hpa & max & current == 1               :365 */
+#define EGR_F_LATENCY_HIGH    (1u << 4)  /* metric: latency & current > 1                  :368 */
+#define EGR_F_NODE_ISSUE      (1u << 5)  /* kubernetes_node: Ready.status != "True"        :375 */
+#define EGR_F_NOT_READY       (1u << 6)  /* pod: Ready cond != "True" and phase Running    :335 */
+#define EGR_F_READINESS_FAIL  (1u << 7)  /* ... and reason == "ContainersNotReady"        :337 */
+#define EGR_F_ERR_FLOAT       (1u << 8)  /* row_err holds a non-integral value              */
+#define EGR_NO_NODE 0xFFFFFFFFu
+
+/* condition type codes (rules_engine.py:403-434) */
+enum egr_cond {
+  EGR_C_WAITING_REASON = 0, EGR_C_TERMINATED_REASON = 1, EGR_C_RECENT_DEPLOY = 2,
+  EGR_C_NO_RECENT_DEPLOY = 3, EGR_C_MEMORY_USAGE_HIGH = 4, EGR_C_HPA_AT_MAX = 5,
+  EGR_C_LATENCY_HIGH = 6, EGR_C_LOG_PATTERN = 7, EGR_C_NODE_UNHEALTHY = 8,
+  EGR_C_MULTIPLE_PODS_SAME_NODE = 9, EGR_C_POD_NOT_READY = 10, EGR_C_READINESS_PROBE_FAILING = 11,
+  EGR_C_NETWORK_ERRORS_HIGH = 12, EGR_C_UNSUPPORTED = -1
+};
+
+#define EGR_MAX_RULES 32
+#define EGR_MAX_CONDS 4
+
+typedef struct egr_rule {
+  int32_t n_conds;                        /* 0 => never matches (rules_engine.py:390) */
+  int32_t cond_type[EGR_MAX_CONDS];       /* enum egr_cond */
+  uint32_t cond_mask[EGR_MAX_CONDS];      /* vocab bits for set-intersection conditions */
+  double cond_param[EGR_MAX_CONDS];       /* threshold for types 9 and 12 */
+  double cond_strength[EGR_MAX_CONDS];    /* fixed per type, rules_engine.py:404-433 */
+  double confidence_base;                 /* rules_engine.py:26 etc. */
+  double category_weight;                 /* hypothesis_ranker.py:28-40 (1.0 if absent) */
+} egr_rule;
+
+typedef struct egr_rule_table {
+  int32_t n_rules;                        /* <= EGR_MAX_RULES, evaluation order = list order */
+  uint32_t network_vocab_bit;             /* vocab bit of the literal "network" (:431) */
+  double unknown_confidence;              /* 0.3 (rules_engine.py:465) */
+  double unknown_category_weight;         /* weight of "unknown" (0.5) */
+  egr_rule rules[EGR_MAX_RULES];
+} egr_rule_table;
+
+/* Per-incident outputs; R = table->n_rules, slot R = the "unknown" hypothesis.
+ *   n_hyp[i]                 number of hypotheses (>= 1)
+ *   mask[i]                  bit r = rule r matched
+ *   order_conf[i*(R+1)+p]    slot index at position p in generate_hypotheses order (:228)
+ *   order_rank[i*(R+1)+p]    slot index at position p after HypothesisRanker.rank (:67)
+ *   confidence / final_score / strength [i*(R+1)+slot]  (float64, bit-exact with Python)   */
+typedef struct egr_rules_out {
+  uint32_t* mask;
+  uint8_t* n_hyp;
+  uint8_t* order_conf;
+  uint8_t* order_rank;
+  double* confidence;
+  double* final_score;
+  double* strength;
+} egr_rules_out;
+
+int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_flags, const uint32_t* row_vocab,
+                   const uint32_t* row_node, const double* row_err, const int64_t* seg_off,
+                   int32_t n_incidents, const egr_rules_out* out, void* stream);
+
+/* Ranker (A6) over arbitrary hypothesis lists.  List j owns entries [list_off[j], list_off[j+1]).
+ *   score = confidence * cat_weight; if support > 0: *= 1 + min(support,5)*0.05;
+ *   *= 1 + strength*0.2; final = round(score, 4); stable sort descending.
+ * out_order[list_off[j]+p] = index (within list j) of the entry ranked p+1.                */
+int egr_rank(const double* confidence, const double* cat_weight, const double* support,
+             const double* strength, const int64_t* list_off, int32_t n_lists,
+             double* out_final, int32_t* out_order, void* stream);
+
+/* Python-exact round(x, ndigits) for ndigits in [0, 15] (host; used by the CPU test suite to
+ * pin the device implementation, which is the same source). */
+double egr_py_round(double x, int32_t ndigits);
+
+/* ------------------------------------------------------------------------------------------
+ * Evidence graph (A7): host-side MERGE semantics of GraphService (neo4j.py:95-167).
+ * Strings are passed as one byte blob plus n+1 int64 offsets (UTF-8, not NUL-terminated).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct egr_graph egr_graph;
+
+int egr_graph_create(egr_graph** out);
+void egr_graph_free(egr_graph* g);
+/* MERGE (n:label {id}) per item, in order.  out_vertex[i] (optional) = vertex index. */
+int egr_graph_merge_nodes(egr_graph* g, const char* id_blob, const int64_t* id_off,
+                          const char* label_blob, const int64_t* label_off, int64_t n,
+                          int32_t* out_vertex);
+/* MATCH (s {id}) MATCH (t {id}) MERGE (s)-[:type]->(t) per item, in order.  Label-less match:
+ * every vertex carrying the id takes part; a missing endpoint drops the item silently.
+ * *out_new (optional) = number of edges actually created.                                 */
+int egr_graph_merge_edges(egr_graph* g, const char* src_blob, const int64_t* src_off,
+                          const char* dst_blob, const int64_t* dst_off, const char* type_blob,
+                          const int64_t* type_off, int64_t n, int64_t* out_new);
+int64_t egr_graph_num_vertices(const egr_graph* g);
+int64_t egr_graph_num_edges(const egr_graph* g);
+int32_t egr_graph_num_labels(const egr_graph* g);
+int32_t egr_graph_num_rel_types(const egr_graph* g);
+/* name of label / relationship-type `i`; returns length, copies up to cap bytes */
+int64_t egr_graph_label_name(const egr_graph* g, int32_t i, char* buf, int64_t cap);
+int64_t egr_graph_rel_type_name(const egr_graph* g, int32_t i, char* buf, int64_t cap);
+int64_t egr_graph_vertex_id(const egr_graph* g, int64_t v, char* buf, int64_t cap);
+/* first vertex (lowest index) whose id equals each query id, -1 if none */
+int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
+                     int32_t* out_vertex);
+/* vertex labels [V] and edge list (src, dst, type) [E] in creation order */
+int egr_graph_export(const egr_graph* g, uint8_t* vertex_label, int32_t* edge_src,
+                     int32_t* edge_dst, uint8_t* edge_type);
+/* Host copy of the symmetric typed CSR the snapshot uploads:
+ * row v lists (u, meta = type<<1 | dir) for every edge touching v, sorted by (u, type, dir);
+ * dir 0: edge u->v, dir 1: edge v->u.  val[e] = weight[type*2+dir] / deg(u) (fp32).
+ * Sizes: row_ptr [V+1], col/meta/val [2E].  weights: [n_types*2], n_types may be smaller
+ * than the graph's type count (missing types weigh 1.0).                                    */
+int egr_graph_csr(const egr_graph* g, const float* weights, int32_t n_types, uint32_t* row_ptr,
+                  uint32_t* col, uint8_t* meta, float* val);
+
+/* ------------------------------------------------------------------------------------------
+ * Snapshot: the CSR + node tables resident in HBM on one device.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct egr_snapshot egr_snapshot;
+
+int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_types, int32_t device,
+                        egr_snapshot** out);
+void egr_snapshot_free(egr_snapshot* s);
+int egr_snapshot_info(const egr_snapshot* s, int64_t* n_vertices, int64_t* n_entries);
+
+/* ------------------------------------------------------------------------------------------
+ * Plan: per-batch workspace for B incident columns on a snapshot (all device memory is
+ * allocated here, none in the launch functions, so a step can be captured into a hipGraph).
+ *   scores: fp32, tiled [B/TW][V][TW] with TW = 64 (B >= 64), 16 or 4.
+ *   reach : u64 words [ceil(B/64)][V], bit b%64 of word b/64 = vertex within `hops` of the
+ *           incident vertex of column b (undirected, all types: apoc.path.subgraphAll).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct egr_plan egr_plan;
+
+int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
+                    egr_plan** out);
+void egr_plan_free(egr_plan* p);
+int egr_plan_tile_width(const egr_plan* p);
+/* Seeds s0[v, b] = max over triples (seed_vertex, seed_col, seed_val) (device arrays). */
+int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t* seed_col,
+                       const float* seed_val, int64_t n_seeds, void* stream);
+/* Incident vertex per column (device array [n_cols]; EGR_NO_NODE = empty column).          */
+int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* stream);
+/* One propagation hop: s^{h+1}_v = s0_v + sum_{(u,t,d) in row v} val * s^h_u.               */
+int egr_plan_hop(egr_plan* p, void* stream);
+/* One reachability hop over the undirected graph.                                          */
+int egr_plan_reach_hop(egr_plan* p, void* stream);
+/* Per column: top-k vertices by final score (desc), vertex id asc on ties, over the reach
+ * set excluding vertices whose label is `exclude_label` (-1: none).  Outputs [n_cols*k];
+ * unused slots hold EGR_NO_NODE / -inf.                                                     */
+int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* out_scores,
+                  void* stream);
+/* Whole pass: seeds/sources must be set; runs `hops` of both recurrences then top-k.       */
+int egr_plan_run(egr_plan* p, int32_t hops, int32_t exclude_label, uint32_t* out_ids,
+                 float* out_scores, void* stream);
+/* Copies (device->device) of the current state, for inspection and tests.
+ * scores out: row-major [V][n_cols]; reach out: [ceil(n_cols/64)][V].                       */
+int egr_plan_read_scores(const egr_plan* p, float* out, void* stream);
+int egr_plan_read_reach(const egr_plan* p, uint64_t* out, void* stream);
+/* Induced subgraph of one column's reach set (get_incident_graph "relationships",
+ * neo4j.py:193-200): every edge whose both endpoints are in the set, as (src, dst, type).
+ * Writes min(total, cap) edges in unspecified order and the total to *out_n.  Synchronous
+ * (waits for `stream`); not a hot-path call.                                               */
+int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, uint32_t* out_dst,
+                           uint8_t* out_type, int64_t cap, int64_t* out_n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EGRAPH_H_ */

@@ -1,0 +1,221 @@
+// Host side of the evidence graph: MERGE semantics of the reference's GraphService and the
+// symmetric typed CSR that the device snapshot is built from.
+//
+// Reference: src/database/neo4j.py
+//   create_entities_batch (:95-113): per entity `MERGE (n:{type} {id: $id}) SET n += $props`
+//       -> a vertex is keyed by (label, id); re-merging an existing (label, id) creates nothing.
+//   create_relations_batch (:145-167): per relation
+//       `MATCH (source {id}) MATCH (target {id}) MERGE (source)-[r:{type}]->(target)`
+//       -> label-less match: every vertex carrying the id participates (cartesian product);
+//          an edge is keyed by (source vertex, type, target vertex); a missing endpoint drops
+//          the relation silently.
+// Properties are not stored here: the Python GraphService mirror keeps them (last write wins).
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "egr_internal.h"
+
+struct egr_graph {
+  std::vector<std::string> labels, rtypes;
+  std::unordered_map<std::string, int> label_idx, rtype_idx;
+  std::vector<std::string> vid;          // vertex id strings, creation order
+  std::vector<uint8_t> vlabel;
+  std::unordered_map<std::string, std::vector<int32_t>> by_id;  // id -> vertices, creation order
+  std::vector<int32_t> esrc, edst;
+  std::vector<uint8_t> etype;
+  struct EdgeKey {
+    int32_t s, d;
+    uint8_t t;
+    bool operator==(const EdgeKey& o) const { return s == o.s && d == o.d && t == o.t; }
+  };
+  struct EdgeHash {
+    size_t operator()(const EdgeKey& k) const {
+      uint64_t h = (uint64_t)(uint32_t)k.s * 0x9E3779B97F4A7C15ull;
+      h ^= ((uint64_t)(uint32_t)k.d << 8 | k.t) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+      return (size_t)h;
+    }
+  };
+  std::unordered_set<EdgeKey, EdgeHash> edges;
+};
+
+namespace {
+
+int intern(std::vector<std::string>& names, std::unordered_map<std::string, int>& idx,
+           std::string_view s, size_t max_names, const char* what) {
+  auto it = idx.find(std::string(s));
+  if (it != idx.end()) return it->second;
+  if (names.size() >= max_names) return egr::fail(EGR_EINVAL, std::string("too many distinct ") + what);
+  int i = (int)names.size();
+  names.emplace_back(s);
+  idx.emplace(names.back(), i);
+  return i;
+}
+
+inline std::string_view str_at(const char* blob, const int64_t* off, int64_t i) {
+  return std::string_view(blob + off[i], (size_t)(off[i + 1] - off[i]));
+}
+
+int64_t copy_out(const std::string& s, char* buf, int64_t cap) {
+  if (buf && cap > 0) memcpy(buf, s.data(), (size_t)std::min<int64_t>(cap, (int64_t)s.size()));
+  return (int64_t)s.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+int egr_graph_create(egr_graph** out) {
+  if (!out) return egr::fail(EGR_EINVAL, "egr_graph_create: out is NULL");
+  try {
+    *out = new egr_graph();
+  } catch (...) {
+    return egr::fail(EGR_ENOMEM, "egr_graph_create: allocation failed");
+  }
+  return EGR_OK;
+}
+
+void egr_graph_free(egr_graph* g) { delete g; }
+
+int egr_graph_merge_nodes(egr_graph* g, const char* id_blob, const int64_t* id_off,
+                          const char* label_blob, const int64_t* label_off, int64_t n,
+                          int32_t* out_vertex) {
+  if (!g || n < 0 || (n > 0 && (!id_blob || !id_off || !label_blob || !label_off)))
+    return egr::fail(EGR_EINVAL, "egr_graph_merge_nodes: bad arguments");
+  for (int64_t i = 0; i < n; ++i) {
+    std::string_view id = str_at(id_blob, id_off, i);
+    int lab = intern(g->labels, g->label_idx, str_at(label_blob, label_off, i), 255, "labels");
+    if (lab < 0) return lab;
+    auto& vs = g->by_id[std::string(id)];
+    int32_t v = -1;
+    for (int32_t c : vs)
+      if (g->vlabel[c] == lab) { v = c; break; }
+    if (v < 0) {
+      if (g->vid.size() >= 0x7FFFFFF0u) return egr::fail(EGR_EINVAL, "too many vertices");
+      v = (int32_t)g->vid.size();
+      g->vid.emplace_back(id);
+      g->vlabel.push_back((uint8_t)lab);
+      vs.push_back(v);
+    }
+    if (out_vertex) out_vertex[i] = v;
+  }
+  return EGR_OK;
+}
+
+int egr_graph_merge_edges(egr_graph* g, const char* src_blob, const int64_t* src_off,
+                          const char* dst_blob, const int64_t* dst_off, const char* type_blob,
+                          const int64_t* type_off, int64_t n, int64_t* out_new) {
+  if (!g || n < 0 || (n > 0 && (!src_blob || !src_off || !dst_blob || !dst_off || !type_blob || !type_off)))
+    return egr::fail(EGR_EINVAL, "egr_graph_merge_edges: bad arguments");
+  int64_t created = 0;
+  std::string key;
+  for (int64_t i = 0; i < n; ++i) {
+    key.assign(str_at(src_blob, src_off, i));
+    auto si = g->by_id.find(key);
+    if (si == g->by_id.end() || si->second.empty()) continue;
+    key.assign(str_at(dst_blob, dst_off, i));
+    auto di = g->by_id.find(key);
+    if (di == g->by_id.end() || di->second.empty()) continue;
+    int t = intern(g->rtypes, g->rtype_idx, str_at(type_blob, type_off, i), 127,
+                   "relationship types");
+    if (t < 0) return t;
+    for (int32_t s : si->second)
+      for (int32_t d : di->second) {
+        egr_graph::EdgeKey k{s, d, (uint8_t)t};
+        if (g->edges.insert(k).second) {
+          g->esrc.push_back(s);
+          g->edst.push_back(d);
+          g->etype.push_back((uint8_t)t);
+          ++created;
+        }
+      }
+  }
+  if (out_new) *out_new = created;
+  return EGR_OK;
+}
+
+int64_t egr_graph_num_vertices(const egr_graph* g) { return g ? (int64_t)g->vid.size() : -1; }
+int64_t egr_graph_num_edges(const egr_graph* g) { return g ? (int64_t)g->esrc.size() : -1; }
+int32_t egr_graph_num_labels(const egr_graph* g) { return g ? (int32_t)g->labels.size() : -1; }
+int32_t egr_graph_num_rel_types(const egr_graph* g) { return g ? (int32_t)g->rtypes.size() : -1; }
+
+int64_t egr_graph_label_name(const egr_graph* g, int32_t i, char* buf, int64_t cap) {
+  if (!g || i < 0 || i >= (int32_t)g->labels.size()) return -1;
+  return copy_out(g->labels[i], buf, cap);
+}
+
+int64_t egr_graph_rel_type_name(const egr_graph* g, int32_t i, char* buf, int64_t cap) {
+  if (!g || i < 0 || i >= (int32_t)g->rtypes.size()) return -1;
+  return copy_out(g->rtypes[i], buf, cap);
+}
+
+int64_t egr_graph_vertex_id(const egr_graph* g, int64_t v, char* buf, int64_t cap) {
+  if (!g || v < 0 || v >= (int64_t)g->vid.size()) return -1;
+  return copy_out(g->vid[v], buf, cap);
+}
+
+int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
+                     int32_t* out_vertex) {
+  if (!g || n < 0 || (n > 0 && (!blob || !off || !out_vertex)))
+    return egr::fail(EGR_EINVAL, "egr_graph_lookup: bad arguments");
+  std::string key;
+  for (int64_t i = 0; i < n; ++i) {
+    key.assign(str_at(blob, off, i));
+    auto it = g->by_id.find(key);
+    out_vertex[i] = (it == g->by_id.end() || it->second.empty()) ? -1 : it->second.front();
+  }
+  return EGR_OK;
+}
+
+int egr_graph_export(const egr_graph* g, uint8_t* vertex_label, int32_t* edge_src,
+                     int32_t* edge_dst, uint8_t* edge_type) {
+  if (!g) return egr::fail(EGR_EINVAL, "egr_graph_export: graph is NULL");
+  if (vertex_label && !g->vlabel.empty()) memcpy(vertex_label, g->vlabel.data(), g->vlabel.size());
+  const size_t E = g->esrc.size();
+  if (E) {
+    if (edge_src) memcpy(edge_src, g->esrc.data(), E * 4);
+    if (edge_dst) memcpy(edge_dst, g->edst.data(), E * 4);
+    if (edge_type) memcpy(edge_type, g->etype.data(), E);
+  }
+  return EGR_OK;
+}
+
+int egr_graph_csr(const egr_graph* g, const float* weights, int32_t n_types, uint32_t* row_ptr,
+                  uint32_t* col, uint8_t* meta, float* val) {
+  if (!g || !row_ptr || !col || !meta || !val || n_types < 0 || (n_types > 0 && !weights))
+    return egr::fail(EGR_EINVAL, "egr_graph_csr: bad arguments");
+  const size_t V = g->vid.size(), E = g->esrc.size();
+  if (2 * E >= 0xFFFFFFFFull) return egr::fail(EGR_EINVAL, "egr_graph_csr: too many edges for u32 CSR");
+  std::vector<uint32_t> cnt(V + 1, 0);
+  for (size_t e = 0; e < E; ++e) {
+    ++cnt[g->edst[e] + 1];  // dir 0 entry in the target's row
+    ++cnt[g->esrc[e] + 1];  // dir 1 entry in the source's row
+  }
+  for (size_t v = 0; v < V; ++v) cnt[v + 1] += cnt[v];
+  memcpy(row_ptr, cnt.data(), (V + 1) * sizeof(uint32_t));
+  std::vector<uint64_t> key(2 * E);  // (u << 9 | type << 1 | dir) sorts (u, type, dir)
+  std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+  for (size_t e = 0; e < E; ++e) {
+    const uint64_t s = (uint32_t)g->esrc[e], d = (uint32_t)g->edst[e], t = g->etype[e];
+    key[fill[d]++] = s << 9 | t << 1 | 0u;
+    key[fill[s]++] = d << 9 | t << 1 | 1u;
+  }
+  for (size_t v = 0; v < V; ++v) std::sort(key.begin() + cnt[v], key.begin() + cnt[v + 1]);
+  for (size_t i = 0; i < 2 * E; ++i) {
+    const uint32_t u = (uint32_t)(key[i] >> 9);
+    const uint32_t m = (uint32_t)(key[i] & 0x1FF);
+    const uint32_t t = m >> 1, dir = m & 1u;
+    const float w = ((int32_t)t < n_types) ? weights[t * 2 + dir] : 1.0f;
+    const float deg = (float)(cnt[u + 1] - cnt[u]);
+    col[i] = u;
+    meta[i] = (uint8_t)m;
+    val[i] = w / deg;
+  }
+  return EGR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,271 @@
+// Rules (A1-A6): batched deterministic diagnosis over encoded evidence rows, fused with the
+// hypothesis ranker, plus the stand-alone ranker kernel.
+//
+// One 64-lane wavefront per incident segment:
+//   * coalesced sweep of the segment's rows (20 B/row: flags, vocab, node key, error count),
+//     wave-level OR / SUM reductions = RulesEngine._extract_signals (rules_engine.py:264-376);
+//   * pods_by_node: max rows per node key by an exact in-register pairwise count (:323-330);
+//   * lane r evaluates rule r (:378-441), its confidence (:443-455) and ranker score
+//     (hypothesis_ranker.py:44-63) in float64 with Python-exact rounding;
+//   * both stable orders (by confidence, :228; then by final_score, hypothesis_ranker.py:67)
+//     by counting, with the unknown fallback (:230-231, :457-478).
+// The per-incident working set is a few KB, so the kernel is latency- not bandwidth-bound for
+// realistic batches; its HBM cost is one read of the rows.
+#include "egr_internal.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o, kWave);
+  return x;
+}
+
+__device__ __forceinline__ int wave_sum_i(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+  return x;
+}
+
+__device__ __forceinline__ int wave_max_i(int x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, kWave));
+  return x;
+}
+
+// exact for integral values whose partial sums stay below 2^53 (the encoder guarantees it)
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+  return x;
+}
+
+struct Signals {
+  uint32_t flags;    // OR of EGR_F_* over the segment
+  uint32_t vocab;    // OR of vocabulary bits (waiting / terminated reasons, log patterns)
+  int n_node_rows;   // rows counted into pods_by_node
+  int max_per_node;  // max(pods_by_node.values())
+  double errors;     // signals["error_count"]
+};
+
+__device__ bool condition_holds(int type, uint32_t mask, double param, const Signals& s,
+                                uint32_t network_bit) {
+  switch (type) {
+    case EGR_C_WAITING_REASON:
+    case EGR_C_TERMINATED_REASON:
+    case EGR_C_LOG_PATTERN:
+      return (s.vocab & mask) != 0u;
+    case EGR_C_RECENT_DEPLOY: return (s.flags & EGR_F_RECENT_DEPLOY) != 0u;
+    case EGR_C_NO_RECENT_DEPLOY: return (s.flags & EGR_F_RECENT_DEPLOY) == 0u;
+    case EGR_C_MEMORY_USAGE_HIGH: return (s.flags & EGR_F_MEMORY_HIGH) != 0u;
+    case EGR_C_HPA_AT_MAX: return (s.flags & EGR_F_HPA_AT_MAX) != 0u;
+    case EGR_C_LATENCY_HIGH: return (s.flags & EGR_F_LATENCY_HIGH) != 0u;
+    case EGR_C_NODE_UNHEALTHY: return (s.flags & EGR_F_NODE_ISSUE) != 0u;
+    case EGR_C_MULTIPLE_PODS_SAME_NODE:
+      return s.n_node_rows > 0 && (double)s.max_per_node >= param;
+    case EGR_C_POD_NOT_READY: return (s.flags & EGR_F_NOT_READY) != 0u;
+    case EGR_C_READINESS_PROBE_FAILING: return (s.flags & EGR_F_READINESS_FAIL) != 0u;
+    case EGR_C_NETWORK_ERRORS_HIGH:
+      return s.errors >= param && network_bit < 32u && ((s.vocab >> network_bit) & 1u);
+    default: return false;  // unknown condition types never match (:436-441)
+  }
+}
+
+__global__ __launch_bounds__(256) void rules_eval_kernel(
+    const egr_rule_table T, const uint32_t* __restrict__ row_flags,
+    const uint32_t* __restrict__ row_vocab, const uint32_t* __restrict__ row_node,
+    const double* __restrict__ row_err, const int64_t* __restrict__ seg_off, int n_incidents,
+    egr_rules_out out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int inc = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (inc >= n_incidents) return;  // wave-uniform; no block barrier below
+  const int64_t beg = seg_off[inc], end = seg_off[inc + 1];
+
+  // ---- signal extraction: one coalesced sweep -------------------------------------------
+  uint32_t f_or = 0, v_or = 0;
+  double esum = 0.0;
+  int n_node = 0;
+  for (int64_t r = beg + lane; r < end; r += kWave) {
+    f_or |= row_flags[r];
+    v_or |= row_vocab[r];
+    esum += row_err[r];
+    n_node += row_node[r] != EGR_NO_NODE;
+  }
+  Signals s;
+  s.flags = wave_or(f_or);
+  s.vocab = wave_or(v_or);
+  s.n_node_rows = wave_sum_i(n_node);
+  if (s.flags & EGR_F_ERR_FLOAT) {
+    // non-integral counts: replay Python's left-to-right accumulation exactly (:354)
+    double acc = 0.0;
+    if (lane == 0)
+      for (int64_t r = beg; r < end; ++r) acc = acc + row_err[r];
+    s.errors = __shfl(acc, 0, kWave);
+  } else {
+    s.errors = wave_sum_d(esum);
+  }
+
+  // ---- pods_by_node: max rows per node key ------------------------------------------------
+  s.max_per_node = s.n_node_rows > 0 ? 1 : 0;
+  if (s.n_node_rows >= 2) {
+    int best = 0;
+    for (int64_t ib = beg; ib < end; ib += kWave) {
+      const int64_t i = ib + lane;
+      const uint32_t ki = i < end ? row_node[i] : EGR_NO_NODE;
+      int c = 0;
+      for (int64_t jb = beg; jb < end; jb += kWave) {
+        const int64_t j = jb + lane;
+        const uint32_t kj = j < end ? row_node[j] : EGR_NO_NODE;
+        const int lim = (int)min<int64_t>(kWave, end - jb);
+        for (int p = 0; p < lim; ++p) c += __shfl(kj, p, kWave) == ki;
+      }
+      if (ki != EGR_NO_NODE) best = max(best, c);
+    }
+    s.max_per_node = wave_max_i(best);
+  }
+
+  // ---- rule r on lane r -----------------------------------------------------------------
+  const int R = T.n_rules;
+  bool matched = false;
+  double conf = 0.0, fin = 0.0, stren = 0.0;
+  if (lane < R) {
+    const egr_rule& rule = T.rules[lane];
+    const int nc = rule.n_conds;
+    int mc = 0;
+    double ssum = 0.0;
+    for (int c = 0; c < nc && c < EGR_MAX_CONDS; ++c) {
+      if (condition_holds(rule.cond_type[c], rule.cond_mask[c], rule.cond_param[c], s,
+                          T.network_vocab_bit)) {
+        ++mc;
+        ssum = ssum + rule.cond_strength[c];
+      }
+    }
+    matched = nc > 0 && mc == nc;
+    if (matched) {
+      stren = ssum / (double)(nc > 1 ? nc : 1);
+      conf = egr::rule_confidence(rule.confidence_base, mc, stren);
+      fin = egr::ranker_final_score(conf, rule.category_weight, (double)mc, stren);
+    }
+  }
+  const uint64_t mm = __ballot(matched);
+  const int nh = __popcll(mm);
+
+  // stable positions: by confidence desc (ties: rule order), then by final_score desc (ties:
+  // confidence order) -- exactly list.sort(reverse=True) applied twice
+  int pc = 0;
+  for (int j = 0; j < R; ++j) {
+    const double cj = __shfl(conf, j, kWave);
+    if ((mm >> j) & 1ull) pc += (cj > conf) || (cj == conf && j < lane);
+  }
+  int pr = 0;
+  for (int j = 0; j < R; ++j) {
+    const double fj = __shfl(fin, j, kWave);
+    const int pcj = __shfl(pc, j, kWave);
+    if ((mm >> j) & 1ull) pr += (fj > fin) || (fj == fin && pcj < pc);
+  }
+
+  // lane p owns output position p: find the rule that landed there (one writer per byte)
+  const int S = R + 1;
+  const int64_t base = (int64_t)inc * S;
+  uint32_t at_c = 0xFFu, at_r = 0xFFu;
+  for (int j = 0; j < R; ++j) {
+    const int pcj = __shfl(pc, j, kWave);
+    const int prj = __shfl(pr, j, kWave);
+    if ((mm >> j) & 1ull) {
+      if (pcj == lane) at_c = (uint32_t)j;
+      if (prj == lane) at_r = (uint32_t)j;
+    }
+  }
+  if (nh == 0 && lane == 0) at_c = at_r = (uint32_t)R;
+  if (lane < S) {
+    out.order_conf[base + lane] = (uint8_t)at_c;
+    out.order_rank[base + lane] = (uint8_t)at_r;
+  }
+  if (matched) {
+    out.confidence[base + lane] = conf;
+    out.final_score[base + lane] = fin;
+    out.strength[base + lane] = stren;
+  }
+  if (lane == 0) {
+    out.mask[inc] = (uint32_t)mm;
+    out.n_hyp[inc] = (uint8_t)(nh > 0 ? nh : 1);
+    if (nh == 0) {
+      const double uc = T.unknown_confidence;
+      out.confidence[base + R] = uc;
+      out.strength[base + R] = 0.0;
+      out.final_score[base + R] = egr::ranker_final_score(uc, T.unknown_category_weight, 0.0, 0.0);
+    }
+  }
+}
+
+// Stand-alone ranker: one wave per hypothesis list, stable descending order by counting.
+__global__ __launch_bounds__(256) void rank_kernel(
+    const double* __restrict__ conf, const double* __restrict__ catw,
+    const double* __restrict__ support, const double* __restrict__ strength,
+    const int64_t* __restrict__ list_off, int n_lists, double* __restrict__ out_final,
+    int32_t* __restrict__ out_order) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int li = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (li >= n_lists) return;
+  const int64_t beg = list_off[li], end = list_off[li + 1];
+  for (int64_t ib = beg; ib < end; ib += kWave) {
+    const int64_t i = ib + lane;
+    const double fi =
+        i < end ? egr::ranker_final_score(conf[i], catw[i], support[i], strength[i]) : 0.0;
+    int pos = 0;
+    for (int64_t jb = beg; jb < end; jb += kWave) {
+      const int64_t j = jb + lane;
+      const double fj_own =
+          j < end ? egr::ranker_final_score(conf[j], catw[j], support[j], strength[j]) : 0.0;
+      const int lim = (int)min<int64_t>(kWave, end - jb);
+      for (int p = 0; p < lim; ++p) {
+        const double fj = __shfl(fj_own, p, kWave);
+        const int64_t jj = jb + p;
+        pos += (fj > fi) || (fj == fi && jj < i);
+      }
+    }
+    if (i < end) {
+      out_final[i] = fi;
+      out_order[beg + pos] = (int32_t)(i - beg);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_flags,
+                              const uint32_t* row_vocab, const uint32_t* row_node,
+                              const double* row_err, const int64_t* seg_off, int32_t n_incidents,
+                              const egr_rules_out* out, void* stream) {
+  if (!table || !out || !seg_off || n_incidents < 0)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval: NULL argument");
+  if (table->n_rules < 0 || table->n_rules > EGR_MAX_RULES)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval: n_rules out of range");
+  for (int r = 0; r < table->n_rules; ++r)
+    if (table->rules[r].n_conds < 0 || table->rules[r].n_conds > EGR_MAX_CONDS)
+      return egr::fail(EGR_EINVAL, "egr_rules_eval: n_conds out of range");
+  if (!out->mask || !out->n_hyp || !out->order_conf || !out->order_rank || !out->confidence ||
+      !out->final_score || !out->strength)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval: NULL output");
+  if (n_incidents == 0) return EGR_OK;
+  const dim3 grid((n_incidents + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(rules_eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, *table,
+                     row_flags, row_vocab, row_node, row_err, seg_off, n_incidents, *out);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
+
+extern "C" int egr_rank(const double* confidence, const double* cat_weight, const double* support,
+                        const double* strength, const int64_t* list_off, int32_t n_lists,
+                        double* out_final, int32_t* out_order, void* stream) {
+  if (!list_off || n_lists < 0) return egr::fail(EGR_EINVAL, "egr_rank: bad arguments");
+  if (n_lists == 0) return EGR_OK;
+  const dim3 grid((n_lists + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(rank_kernel, grid, dim3(256), 0, (hipStream_t)stream, confidence,
+                     cat_weight, support, strength, list_off, n_lists, out_final, out_order);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}

@@ -1,0 +1,314 @@
+"""Evidence graph (host MERGE semantics), device snapshot and per-batch propagation plans.
+
+  EvidenceGraph  <- GraphService.create_entities_batch / create_relations_batch
+                    (src/database/neo4j.py:95-113, :145-167); vertex/edge structure lives in
+                    libegraph (C++), properties stay here (SET n += props, last write wins).
+  Snapshot       <- the Neo4j store: symmetric typed CSR resident in HBM.
+  Plan           <- apoc.path.subgraphAll(maxLevel=k) candidate sets (neo4j.py:169-202) plus
+                    the build-defined typed propagation / top-k.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from collections.abc import Iterable, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .device import require_device
+
+# Per relationship type (forward, reverse) propagation weights -- DESIGN.md §A9.
+DEFAULT_WEIGHTS: dict[str, tuple[float, float]] = {
+    "AFFECTS": (1.0, 1.0),
+    "CORRELATES_WITH": (1.0, 1.0),
+    "HAS_RECENT_CHANGE": (0.9, 0.9),
+    "SCHEDULED_ON": (0.6, 0.6),
+    "OWNS": (0.8, 0.8),
+    "SELECTS": (0.7, 0.7),
+    "CALLS": (0.5, 0.5),
+    "HAS_EVENT": (0.9, 0.9),
+    "HAS_LOG_PATTERN": (0.9, 0.9),
+    "HAS_METRIC_ANOMALY": (0.9, 0.9),
+}
+DEFAULT_OTHER_WEIGHT = (0.5, 0.5)
+
+
+def str_blob(strs: Sequence[str]) -> tuple[bytes, np.ndarray]:
+    """UTF-8 blob + int64 offsets [n+1] for the C-ABI string arrays."""
+    enc = [s.encode() for s in strs]
+    off = np.zeros(len(enc) + 1, np.int64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=off[1:])
+    return b"".join(enc), off
+
+
+def _addr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def _field(x, name, default=KeyError):
+    if isinstance(x, dict):
+        return x[name] if default is KeyError else x.get(name, default)
+    return getattr(x, name) if default is KeyError else getattr(x, name, default)
+
+
+class EvidenceGraph:
+    """The evidence graph with the reference's MERGE semantics (host side, C++)."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        L.check(L.lib.egr_graph_create(C.byref(h)), "egr_graph_create")
+        self._h = h
+        self.node_props: dict[tuple[str, str], dict] = {}
+        self.vertex_of: dict[tuple[str, str], int] = {}      # (label, id) -> vertex
+        self.edge_props: dict[tuple[str, str, str], dict] = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and getattr(L, "lib", None) is not None:
+            L.lib.egr_graph_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- writes ---------------------------------------------------------------------------
+    def merge_nodes(self, ids: Sequence[str], labels: Sequence[str]) -> np.ndarray:
+        """MERGE (n:label {id}) for each pair; returns the vertex index of each item."""
+        if len(ids) != len(labels):
+            raise ValueError("ids and labels differ in length")
+        ib, io = str_blob(ids)
+        lb, lo = str_blob(labels)
+        out = np.empty(len(ids), np.int32)
+        L.check(L.lib.egr_graph_merge_nodes(self._h, ib, _addr(io), lb, _addr(lo), len(ids),
+                                            _addr(out)), "egr_graph_merge_nodes")
+        vo = self.vertex_of
+        for i, lab, v in zip(ids, labels, out.tolist()):
+            vo[(lab, i)] = v
+        return out
+
+    def merge_edges(self, src: Sequence[str], dst: Sequence[str], types: Sequence[str]) -> int:
+        """MATCH/MATCH/MERGE per relation; returns the number of edges actually created."""
+        if not (len(src) == len(dst) == len(types)):
+            raise ValueError("src, dst and types differ in length")
+        sb, so = str_blob(src)
+        db, do = str_blob(dst)
+        tb, to = str_blob(types)
+        created = C.c_int64(0)
+        L.check(L.lib.egr_graph_merge_edges(self._h, sb, _addr(so), db, _addr(do), tb, _addr(to),
+                                            len(src), C.byref(created)), "egr_graph_merge_edges")
+        return created.value
+
+    def create_entities_batch(self, entities: Iterable) -> int:
+        """GraphService.create_entities_batch: returns the number of items attempted (:112)."""
+        entities = list(entities)
+        ids = [str(_field(e, "id")) for e in entities]
+        labels = [str(_field(e, "type")) for e in entities]
+        self.merge_nodes(ids, labels)
+        for e, i, lab in zip(entities, ids, labels):
+            props = dict(_field(e, "properties", None) or {})
+            props["id"] = i                                    # neo4j.py:101-102
+            self.node_props.setdefault((lab, i), {}).update(props)
+        return len(entities)
+
+    def create_relations_batch(self, relations: Iterable) -> int:
+        """GraphService.create_relations_batch: returns the number of items attempted (:166)."""
+        relations = list(relations)
+        src = [str(_field(r, "source_id")) for r in relations]
+        dst = [str(_field(r, "target_id")) for r in relations]
+        typ = [str(_field(r, "relation_type")) for r in relations]
+        self.merge_edges(src, dst, typ)
+        known = set(self.vertex_ids_set())
+        for r, s, d, t in zip(relations, src, dst, typ):
+            if s in known and d in known:
+                self.edge_props.setdefault((s, t, d), {}).update(dict(_field(r, "properties", None) or {}))
+        return len(relations)
+
+    # ---- reads ----------------------------------------------------------------------------
+    @property
+    def num_vertices(self) -> int:
+        return int(L.lib.egr_graph_num_vertices(self._h))
+
+    @property
+    def num_edges(self) -> int:
+        return int(L.lib.egr_graph_num_edges(self._h))
+
+    def _names(self, count_fn, name_fn) -> list[str]:
+        out = []
+        for i in range(count_fn(self._h)):
+            n = name_fn(self._h, i, None, 0)
+            buf = C.create_string_buffer(max(int(n), 1))
+            name_fn(self._h, i, buf, n)
+            out.append(buf.raw[:n].decode())
+        return out
+
+    def labels(self) -> list[str]:
+        return self._names(L.lib.egr_graph_num_labels, L.lib.egr_graph_label_name)
+
+    def rel_types(self) -> list[str]:
+        return self._names(L.lib.egr_graph_num_rel_types, L.lib.egr_graph_rel_type_name)
+
+    def vertex_id(self, v: int) -> str:
+        n = L.lib.egr_graph_vertex_id(self._h, v, None, 0)
+        if n < 0:
+            raise IndexError(v)
+        buf = C.create_string_buffer(max(int(n), 1))
+        L.lib.egr_graph_vertex_id(self._h, v, buf, n)
+        return buf.raw[:n].decode()
+
+    def vertex_ids(self) -> list[str]:
+        return [self.vertex_id(v) for v in range(self.num_vertices)]
+
+    def vertex_ids_set(self) -> set[str]:
+        return {i for (_, i) in self.vertex_of}
+
+    def lookup(self, ids: Sequence[str]) -> np.ndarray:
+        """First vertex carrying each id (-1 if none)."""
+        b, o = str_blob(ids)
+        out = np.empty(len(ids), np.int32)
+        L.check(L.lib.egr_graph_lookup(self._h, b, _addr(o), len(ids), _addr(out)), "egr_graph_lookup")
+        return out
+
+    def export(self) -> tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """(vertex_label u8[V], edge_src i32[E], edge_dst i32[E], edge_type u8[E])."""
+        V, E = self.num_vertices, self.num_edges
+        vl = np.empty(V, np.uint8)
+        es, ed = np.empty(E, np.int32), np.empty(E, np.int32)
+        et = np.empty(E, np.uint8)
+        L.check(L.lib.egr_graph_export(self._h, _addr(vl), _addr(es), _addr(ed), _addr(et)),
+                "egr_graph_export")
+        return vl, es, ed, et
+
+    def weight_array(self, weights: dict[str, tuple[float, float]] | None = None) -> np.ndarray:
+        """[n_types*2] fp32 (fwd, rev) weights in this graph's type order."""
+        weights = DEFAULT_WEIGHTS if weights is None else weights
+        names = self.rel_types()
+        w = np.empty(max(2 * len(names), 2), np.float32)
+        for t, name in enumerate(names):
+            w[2 * t: 2 * t + 2] = weights.get(name, DEFAULT_OTHER_WEIGHT)
+        return w
+
+    def csr(self, weights=None) -> dict[str, np.ndarray]:
+        """Host copy of the symmetric typed CSR (exactly what the snapshot uploads)."""
+        V, E = self.num_vertices, self.num_edges
+        w = self.weight_array(weights)
+        row_ptr = np.empty(V + 1, np.uint32)
+        col = np.empty(max(2 * E, 1), np.uint32)
+        meta = np.empty(max(2 * E, 1), np.uint8)
+        val = np.empty(max(2 * E, 1), np.float32)
+        L.check(L.lib.egr_graph_csr(self._h, _addr(w), len(self.rel_types()), _addr(row_ptr),
+                                    _addr(col), _addr(meta), _addr(val)), "egr_graph_csr")
+        return {"row_ptr": row_ptr, "col": col[:2 * E], "meta": meta[:2 * E], "val": val[:2 * E]}
+
+    def snapshot(self, weights=None, device=None) -> "Snapshot":
+        return Snapshot(self, weights, device)
+
+
+class Snapshot:
+    """Typed CSR + vertex labels resident in HBM on one device."""
+
+    def __init__(self, graph: EvidenceGraph, weights=None, device=None):
+        self.dev = require_device(device)
+        w = graph.weight_array(weights)
+        h = C.c_void_p()
+        L.check(L.lib.egr_snapshot_create(graph.handle, _addr(w), len(graph.rel_types()),
+                                          self.dev.index, C.byref(h)), "egr_snapshot_create")
+        self._h = h
+        nv, ne = C.c_int64(), C.c_int64()
+        L.check(L.lib.egr_snapshot_info(h, C.byref(nv), C.byref(ne)), "egr_snapshot_info")
+        self.n_vertices, self.n_entries = nv.value, ne.value
+        self.labels = graph.labels()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and getattr(L, "lib", None) is not None:
+            L.lib.egr_snapshot_free(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def plan(self, n_cols: int, max_seeds: int, k: int = 10) -> "Plan":
+        return Plan(self, n_cols, max_seeds, k)
+
+
+class Plan:
+    """Per-batch device workspace: B incident columns over one snapshot."""
+
+    def __init__(self, snap: Snapshot, n_cols: int, max_seeds: int, k: int = 10):
+        self.snap = snap
+        self.dev = snap.dev
+        self.B, self.k = n_cols, k
+        h = C.c_void_p()
+        L.check(L.lib.egr_plan_create(snap.handle, n_cols, max_seeds, k, C.byref(h)), "egr_plan_create")
+        self._h = h
+        self.tile_width = L.lib.egr_plan_tile_width(h)
+        self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
+        self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and getattr(L, "lib", None) is not None:
+            L.lib.egr_plan_free(h)
+            self._h = None
+
+    def _st(self, stream):
+        return L.stream_handle(self.dev) if stream is None else stream
+
+    def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
+        n = vertex.numel()
+        if not (col.numel() == n == val.numel()):
+            raise ValueError("seed arrays differ in length")
+        L.check(L.lib.egr_plan_set_seeds(self._h, L.ptr(vertex), L.ptr(col), L.ptr(val), n,
+                                         self._st(stream)), "egr_plan_set_seeds")
+
+    def set_sources(self, source_vertex: torch.Tensor, stream=None):
+        if source_vertex.numel() != self.B:
+            raise ValueError(f"need one source vertex per column ({self.B})")
+        L.check(L.lib.egr_plan_set_sources(self._h, L.ptr(source_vertex), self._st(stream)),
+                "egr_plan_set_sources")
+
+    def hop(self, stream=None):
+        L.check(L.lib.egr_plan_hop(self._h, self._st(stream)), "egr_plan_hop")
+
+    def reach_hop(self, stream=None):
+        L.check(L.lib.egr_plan_reach_hop(self._h, self._st(stream)), "egr_plan_reach_hop")
+
+    def topk(self, exclude_label: int = -1, stream=None) -> tuple[torch.Tensor, torch.Tensor]:
+        L.check(L.lib.egr_plan_topk(self._h, exclude_label, L.ptr(self.out_ids),
+                                    L.ptr(self.out_scores), self._st(stream)), "egr_plan_topk")
+        return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
+
+    def run(self, hops: int = 3, exclude_label: int = -1, stream=None):
+        L.check(L.lib.egr_plan_run(self._h, hops, exclude_label, L.ptr(self.out_ids),
+                                   L.ptr(self.out_scores), self._st(stream)), "egr_plan_run")
+        return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
+
+    def read_scores(self, stream=None) -> torch.Tensor:
+        out = torch.empty(self.snap.n_vertices * self.B, dtype=torch.float32, device=self.dev)
+        L.check(L.lib.egr_plan_read_scores(self._h, L.ptr(out), self._st(stream)), "egr_plan_read_scores")
+        return out.view(self.snap.n_vertices, self.B)
+
+    def read_reach(self, stream=None) -> torch.Tensor:
+        W = (self.B + 63) // 64
+        out = torch.empty(W * self.snap.n_vertices, dtype=torch.int64, device=self.dev)
+        L.check(L.lib.egr_plan_read_reach(self._h, L.ptr(out), self._st(stream)), "egr_plan_read_reach")
+        return out.view(W, self.snap.n_vertices)
+
+    def induced_edges(self, col: int, stream=None) -> np.ndarray:
+        """(src, dst, type) rows of the induced subgraph of column `col`'s reach set."""
+        n = C.c_int64(0)
+        L.check(L.lib.egr_plan_induced_edges(self._h, col, None, None, None, 0, C.byref(n),
+                                             self._st(stream)), "egr_plan_induced_edges")
+        cap = n.value
+        src = torch.empty(max(cap, 1), dtype=torch.int32, device=self.dev)
+        dst = torch.empty(max(cap, 1), dtype=torch.int32, device=self.dev)
+        typ = torch.empty(max(cap, 1), dtype=torch.uint8, device=self.dev)
+        L.check(L.lib.egr_plan_induced_edges(self._h, col, L.ptr(src), L.ptr(dst), L.ptr(typ), cap,
+                                             C.byref(n), self._st(stream)), "egr_plan_induced_edges")
+        out = np.stack([src[:cap].cpu().numpy(), dst[:cap].cpu().numpy(),
+                        typ[:cap].cpu().numpy().astype(np.int32)], axis=1)
+        return out[np.lexsort((out[:, 2], out[:, 0], out[:, 1]))] if cap else out.reshape(0, 3)

@@ -1,0 +1,364 @@
+"""Synthetic cluster graphs and collector-shaped incident evidence (BASELINE configs C1-C4).
+
+The reference's simulator applies faulty manifests to a live cluster
+(src/simulator/incident_simulator.py:13-269) and the collectors turn what they observe into
+Evidence / GraphEntity / GraphRelation items.  Offline, this module generates the same shapes:
+
+  * vertices / edges with the collectors' id scheme (kubernetes_collector.py:93-314,
+    deploy_diff_collector.py:246-269) plus the build-side superset Service / Event /
+    LogPattern / MetricAnomaly, laid out namespace by namespace so that
+    neighbouring vertices get neighbouring indices;
+  * per incident ~100 evidence rows whose `data` payloads follow the collectors
+    (kubernetes_collector.py:136-195, :386-485, :512-626; deploy_diff_collector.py:127-183;
+    logs_collector.py:133-164; metrics_collector.py:100-145) and whose signal_strength seeds
+    follow their scoring functions.
+
+All draws come from numpy Generators seeded per config (default 20260821 + config index).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+PROMQL = {  # query names of src/config/promql_queries.yaml used by the metric rows
+    "crashloop": ["restart_count", "container_exit_code"],
+    "oom": ["memory_usage_percentage", "oom_killed_total", "memory_working_set"],
+    "latency": ["p99_latency", "p95_latency"],
+    "hpa": ["hpa_at_max", "hpa_current_replicas", "hpa_max_replicas"],
+    "resource": ["cpu_usage_percentage", "cpu_throttling", "disk_usage"],
+    "deployment": ["deployment_replicas_unavailable", "deployment_generation_mismatch"],
+}
+
+
+@dataclass
+class ClusterConfig:
+    pods: int = 10_000
+    namespaces: int = 20
+    nodes: int = 200
+    deployments: int = 1_000
+    services: int = 1_000
+    calls_per_service: int = 3
+    attach_fraction: float = 0.2      # pods with an Event / LogPattern / MetricAnomaly vertex
+    unhealthy_node_fraction: float = 0.05
+    seed: int = 20260821
+
+
+CONFIGS = {
+    "C2": ClusterConfig(),
+    "C3": ClusterConfig(pods=100_000, namespaces=100, nodes=2_000, deployments=10_000,
+                        services=10_000, attach_fraction=0.35, seed=20260823),
+    "C4": ClusterConfig(pods=400_000, namespaces=400, nodes=8_000, deployments=40_000,
+                        services=40_000, attach_fraction=0.5, seed=20260824),
+}
+
+
+@dataclass
+class Cluster:
+    cfg: ClusterConfig
+    ids: list = field(default_factory=list)
+    labels: list = field(default_factory=list)
+    src: list = field(default_factory=list)
+    dst: list = field(default_factory=list)
+    types: list = field(default_factory=list)
+    ns_names: list = field(default_factory=list)
+    deploy_ns: np.ndarray | None = None        # deployment -> namespace index
+    deploy_name: list = field(default_factory=list)
+    deploy_pods: list = field(default_factory=list)   # deployment -> list of pod names
+    pod_node: dict = field(default_factory=dict)       # pod name -> node name
+    unhealthy_nodes: set = field(default_factory=set)
+    attachments: dict = field(default_factory=dict)    # pod name -> [(label, vertex id)]
+
+    def add_vertex(self, vid: str, label: str) -> None:
+        self.ids.append(vid)
+        self.labels.append(label)
+
+    def add_edge(self, s: str, d: str, t: str) -> None:
+        self.src.append(s)
+        self.dst.append(d)
+        self.types.append(t)
+
+
+def build_cluster(cfg: ClusterConfig) -> Cluster:
+    rng = np.random.default_rng(cfg.seed)
+    c = Cluster(cfg)
+    c.ns_names = [f"ns-{i:03d}" for i in range(cfg.namespaces)]
+    node_names = [f"node-{i:05d}" for i in range(cfg.nodes)]
+    bad = rng.random(cfg.nodes) < cfg.unhealthy_node_fraction
+    c.unhealthy_nodes = {n for n, b in zip(node_names, bad) if b}
+    for n in node_names:
+        c.add_vertex(f"node:{n}", "Node")
+    c.deploy_ns = np.sort(rng.integers(0, cfg.namespaces, cfg.deployments))
+    svc_ns = np.sort(rng.integers(0, cfg.namespaces, cfg.services))
+    pods_per = np.full(cfg.deployments, cfg.pods // cfg.deployments)
+    pods_per[: cfg.pods % cfg.deployments] += 1
+    pod_nodes = rng.integers(0, cfg.nodes, cfg.pods)
+    attach = rng.random((cfg.pods, 3)) < cfg.attach_fraction
+    svc_of_deploy = np.minimum((np.arange(cfg.deployments) * cfg.services) // cfg.deployments,
+                               cfg.services - 1)
+    p = 0
+    d = 0
+    s = 0
+    for ns_i, ns in enumerate(c.ns_names):
+        while s < cfg.services and svc_ns[s] == ns_i:
+            c.add_vertex(f"service:{ns}:svc-{s}", "Service")
+            s += 1
+        while d < cfg.deployments and c.deploy_ns[d] == ns_i:
+            dname = f"app-{d}"
+            c.deploy_name.append(dname)
+            did = f"deployment:{ns}:{dname}"
+            c.add_vertex(did, "Deployment")
+            sv = int(svc_of_deploy[d])
+            c.add_edge(f"service:{c.ns_names[svc_ns[sv]]}:svc-{sv}", did, "SELECTS")
+            pods = []
+            for j in range(int(pods_per[d])):
+                pname = f"{dname}-{j:02d}-{p:06x}"
+                pid = f"pod:{ns}:{pname}"
+                node = node_names[pod_nodes[p]]
+                c.add_vertex(pid, "Pod")
+                c.add_edge(did, pid, "OWNS")
+                c.add_edge(pid, f"node:{node}", "SCHEDULED_ON")
+                c.pod_node[pname] = node
+                att = []
+                for k, (lab, et, pre) in enumerate((("Event", "HAS_EVENT", "event"),
+                                                     ("LogPattern", "HAS_LOG_PATTERN", "logpattern"),
+                                                     ("MetricAnomaly", "HAS_METRIC_ANOMALY", "metric"))):
+                    if attach[p, k]:
+                        vid = f"{pre}:{ns}:{pname}"
+                        c.add_vertex(vid, lab)
+                        c.add_edge(pid, vid, et)
+                        att.append((lab, vid))
+                if att:
+                    c.attachments[pname] = att
+                pods.append(pname)
+                p += 1
+            c.deploy_pods.append(pods)
+            d += 1
+    # service call graph: mostly within the namespace
+    for sv in range(cfg.services):
+        for _ in range(cfg.calls_per_service):
+            if rng.random() < 0.9:
+                lo = np.searchsorted(svc_ns, svc_ns[sv])
+                hi = np.searchsorted(svc_ns, svc_ns[sv], side="right")
+                t = int(rng.integers(lo, hi))
+            else:
+                t = int(rng.integers(0, cfg.services))
+            if t != sv:
+                c.add_edge(f"service:{c.ns_names[svc_ns[sv]]}:svc-{sv}",
+                           f"service:{c.ns_names[svc_ns[t]]}:svc-{t}", "CALLS")
+    return c
+
+
+# ---------------------------------------------------------------------------------------------
+# incidents
+SCENARIOS = ("crashloop_deploy", "crashloop", "oom", "imagepull")
+SCENARIO_P = (0.2, 0.2, 0.3, 0.3)   # BASELINE C2 mix: 40 % CrashLoop (half with deploy), 30/30
+
+
+@dataclass
+class IncidentCase:
+    incident: dict            # Incident model fields
+    scenario: str
+    evidence: list            # evidence dicts (Evidence.model_dump(mode="json") shape)
+    entities: list            # GraphEntity dicts added by this incident
+    relations: list           # GraphRelation dicts added by this incident
+
+
+def _pod_strength(wr, tr, restarts, phase):   # kubernetes_collector.py:255-270
+    if wr in ("CrashLoopBackOff", "ImagePullBackOff", "ErrImagePull"):
+        return 0.95
+    if tr == "OOMKilled":
+        return 0.95
+    if restarts > 3:
+        return 0.8
+    if phase != "Running":
+        return 0.7
+    return 0.3
+
+
+def _metric_strength(name, v):   # metrics_collector.py:246-328
+    if "restart" in name:
+        return 0.9 if v > 5 else 0.7 if v > 2 else 0.5 if v > 0 else 0.3
+    if "error" in name or "5xx" in name:
+        return 0.9 if v > 0.1 else 0.8 if v > 0.05 else 0.6 if v > 0.01 else 0.3
+    if "memory" in name or "usage" in name:
+        return 0.9 if v > 90 else 0.7 if v > 80 else 0.5 if v > 70 else 0.3
+    if "latency" in name:
+        return 0.9 if v > 5 else 0.7 if v > 2 else 0.5 if v > 1 else 0.3
+    if "throttl" in name:
+        return 0.8 if v > 0.5 else 0.6 if v > 0.1 else 0.3
+    if "oom" in name:
+        return 0.95 if v > 0 else 0.3
+    if "hpa" in name:
+        return 0.8 if ("max" in name and v == 1) else 0.3
+    return 0.3
+
+
+def make_incidents(c: Cluster, n: int, seed: int = 7, events_per_incident: int = 60,
+                   scenario: str | None = None) -> list[IncidentCase]:
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        sc = scenario or SCENARIOS[int(rng.choice(len(SCENARIOS), p=SCENARIO_P))]
+        d = int(rng.integers(0, len(c.deploy_name)))
+        ns = c.ns_names[int(c.deploy_ns[d])]
+        dname = c.deploy_name[d]
+        iid = f"00000000-0000-4000-8000-{seed:04x}{i:08x}"
+        inc = {"id": iid, "fingerprint": f"fp-{i}", "title": f"{sc}: {dname}",
+               "severity": "critical", "source": "synthetic", "cluster": "synthetic",
+               "namespace": ns, "service": dname, "started_at": "2026-08-21T00:00:00Z"}
+        ev, ents, rels = [], [], []
+        k = 0
+
+        def row(etype, entity, data, strength, source="kubernetes_api"):
+            nonlocal k
+            k += 1
+            ev.append({"id": f"{iid[-12:]}-{k:04d}", "incident_id": iid, "evidence_type": etype,
+                       "source": source, "entity_name": entity, "entity_namespace": ns,
+                       "data": data, "signal_strength": strength})
+
+        ents.append({"id": f"incident:{iid}", "type": "Incident",
+                     "properties": {"id": iid, "title": inc["title"], "namespace": ns}})
+        pods = c.deploy_pods[d]
+        for pname in pods:
+            restarts = int(rng.geometric(0.3)) - 1
+            wr = tr = None
+            phase = "Running"
+            if sc.startswith("crashloop"):
+                wr = "CrashLoopBackOff" if rng.random() < 0.8 else None
+                tr = "Error" if rng.random() < 0.5 else None
+            elif sc == "oom":
+                tr = "OOMKilled" if rng.random() < 0.7 else None
+            elif sc == "imagepull":
+                wr = ("ImagePullBackOff", "ErrImagePull")[int(rng.integers(0, 2))]
+                phase, restarts = "Pending", 0
+            ready = "True" if (wr is None and tr is None and rng.random() < 0.7) else "False"
+            conds = [{"type": "Ready", "status": ready,
+                      "reason": None if ready == "True" else "ContainersNotReady"}]
+            row("kubernetes_pod", pname,
+                {"name": pname, "namespace": ns, "phase": phase, "node_name": c.pod_node[pname],
+                 "restart_count": restarts, "waiting_reason": wr, "terminated_reason": tr,
+                 "conditions": conds}, _pod_strength(wr, tr, restarts, phase))
+            rels.append({"source_id": f"incident:{iid}", "target_id": f"pod:{ns}:{pname}",
+                         "relation_type": "AFFECTS"})
+        row("kubernetes_deployment", dname,
+            {"name": dname, "namespace": ns, "replicas": len(pods), "ready_replicas": 0,
+             "unavailable_replicas": len(pods)}, 0.8)
+        for j in range(events_per_incident):
+            pname = pods[j % len(pods)]
+            reason = ("BackOff", "Unhealthy", "Failed", "Pulled", "Created")[int(rng.integers(0, 5))]
+            warn = reason in ("BackOff", "Unhealthy", "Failed")
+            row("kubernetes_event", pname,
+                {"type": "Warning" if warn else "Normal", "reason": reason, "message": reason,
+                 "involved_object": {"kind": "Pod", "name": pname, "namespace": ns}, "count": 1},
+                0.9 if warn else 0.4)
+        errors = int(rng.integers(0, 40))
+        pats = ["error"] + (["network"] if rng.random() < 0.3 else []) + \
+            (["oom"] if sc == "oom" else [])
+        row("log_signal", dname, {"total_lines": 500, "error_count": errors, "warning_count": 3,
+                                  "patterns_found": pats},
+            0.9 if errors > 10 else 0.8 if errors > 5 else 0.6 if errors else 0.3, "loki")
+        cats = ["crashloop", "resource", "deployment"] + (["oom"] if sc == "oom" else ["latency", "hpa"])
+        names = [q for cat in cats for q in PROMQL[cat]]
+        for j in range(15):
+            qn = names[j % len(names)]
+            if "memory" in qn:
+                v = float(rng.uniform(0, 100))
+            elif "latency" in qn:
+                v = float(rng.uniform(0, 5))
+            elif "hpa" in qn:
+                v = float(rng.integers(0, 2))
+            else:
+                v = float(rng.uniform(0, 10))
+            st = _metric_strength(qn, v)
+            row("metric_signal", qn, {"query_name": qn, "current_value": v, "is_anomalous": st > 0.7},
+                st, "prometheus")
+        for node in sorted({c.pod_node[p] for p in pods} & c.unhealthy_nodes):
+            row("kubernetes_node", node,
+                {"name": node, "conditions": {"Ready": {"status": "False"},
+                                              "MemoryPressure": {"status": "True"}}}, 0.9)
+        recent = sc in ("crashloop_deploy", "imagepull")
+        row("deploy_change", dname, {"deployment_name": dname, "namespace": ns,
+                                     "is_recent_change": recent, "current_revision": "7"},
+            0.95 if recent else 0.3)
+        if recent:
+            cid = f"change:deployment:{ns}:{dname}:7"
+            ents.append({"id": cid, "type": "ChangeEvent",
+                         "properties": {"deployment": dname, "namespace": ns, "revision": "7"}})
+            rels.append({"source_id": f"deployment:{ns}:{dname}", "target_id": cid,
+                         "relation_type": "HAS_RECENT_CHANGE"})
+            rels.append({"source_id": f"incident:{iid}", "target_id": cid,
+                         "relation_type": "CORRELATES_WITH"})
+            row("image_change", dname, {"deployment": dname, "image_changed": True}, 0.85)
+        out.append(IncidentCase(inc, sc, ev, ents, rels))
+    return out
+
+
+def add_incidents(c: Cluster, cases: list[IncidentCase]) -> None:
+    for case in cases:
+        for e in case.entities:
+            c.add_vertex(e["id"], e["type"])
+        for r in case.relations:
+            c.add_edge(r["source_id"], r["target_id"], r["relation_type"])
+
+
+# ---------------------------------------------------------------------------------------------
+# seeds: evidence row -> graph vertex (DESIGN.md §A9 "attachment")
+def attach_ids(ev: dict) -> list[str]:
+    """Candidate vertex ids of an evidence row, most specific first."""
+    t, ns, name = ev.get("evidence_type"), ev.get("entity_namespace"), ev.get("entity_name")
+    data = ev.get("data") or {}
+    if t == "kubernetes_pod":
+        return [f"pod:{ns}:{name}"]
+    if t in ("kubernetes_deployment", "deploy_change", "image_change"):
+        return [f"deployment:{ns}:{name}"]
+    if t == "kubernetes_node":
+        return [f"node:{name}"]
+    if t == "kubernetes_hpa":
+        return [f"hpa:{ns}:{name}"]
+    if t == "config_change":
+        return [f"configmap:{ns}:{name}"]
+    if t == "kubernetes_event":
+        obj = data.get("involved_object") or {}
+        kind = str(obj.get("kind", "")).lower()
+        ids = [f"event:{ns}:{name}"]
+        if kind == "node":
+            ids.append(f"node:{obj.get('name')}")
+        elif kind:
+            ids.append(f"{kind}:{obj.get('namespace', ns)}:{obj.get('name')}")
+        return ids
+    if t == "log_signal":
+        return [f"logpattern:{ns}:{name}", f"service:{ns}:{name}", f"deployment:{ns}:{name}"]
+    if t == "metric_signal":
+        return [f"metric:{ns}:{name}"]
+    return []
+
+
+def seeds_for_batch(graph, evidence_lists: list[list[dict]]):
+    """(vertex u32, column u32, strength f32) triples for a batch: each row attaches to the
+    first of its candidate ids present in the graph; unattached rows are dropped."""
+    flat, count, col, val = [], [], [], []
+    for b, evs in enumerate(evidence_lists):
+        for ev in evs:
+            ids = attach_ids(ev)
+            s = float(ev.get("signal_strength", 0.5))
+            if not ids or s <= 0:
+                continue
+            flat.extend(ids)
+            count.append(len(ids))
+            col.append(b)
+            val.append(s)
+    if not flat:
+        return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
+    found = graph.lookup(flat)
+    chosen = np.full(len(count), -1, np.int64)
+    pos = 0
+    for r, n in enumerate(count):
+        for v in found[pos:pos + n]:
+            if v >= 0:
+                chosen[r] = v
+                break
+        pos += n
+    keep = chosen >= 0
+    return (chosen[keep].astype(np.uint32), np.asarray(col, np.uint32)[keep],
+            np.asarray(val, np.float32)[keep])

@@ -1,0 +1,135 @@
+"""Drop-in GraphService (reference src/database/neo4j.py:68-202) backed by the GPU snapshot.
+
+Write path: create_entity / create_entities_batch / create_relation / create_relations_batch
+keep the reference's MERGE semantics and return values (attempted counts, :112 / :166).
+Read path: get_incident_graph(incident_id, depth=3) reproduces
+`MATCH (i:Incident {id}) CALL apoc.path.subgraphAll(i, {maxLevel: depth})` (:170-202): the
+vertex set within `depth` undirected hops (egr_plan_reach_hop on the device) and every edge
+among those vertices (egr_plan_induced_edges).  As in the reference, the Incident vertex's id
+property is the GraphEntity id ("incident:<uuid>", neo4j.py:101-102), so a bare UUID matches
+nothing unless `resolve_bare_uuid=True`.
+
+The graph is process-wide, like the Neo4j database the reference talks to; writes invalidate
+the device snapshot, the next read rebuilds it.
+"""
+from __future__ import annotations
+
+import torch
+
+from egraph.graph import EvidenceGraph
+from src.models.evidence import GraphEntity, GraphRelation
+
+
+class GraphService:
+    """Service for Evidence Graph operations (process-wide store)."""
+
+    _graph: EvidenceGraph | None = None
+    _snapshot = None
+    _plans: dict = {}
+    device = None
+
+    @classmethod
+    def graph(cls) -> EvidenceGraph:
+        if cls._graph is None:
+            cls._graph = EvidenceGraph()
+        return cls._graph
+
+    @classmethod
+    def reset(cls) -> None:
+        cls._graph, cls._snapshot, cls._plans = None, None, {}
+
+    @classmethod
+    def _invalidate(cls) -> None:
+        cls._snapshot, cls._plans = None, {}
+
+    @staticmethod
+    async def create_entity(entity: GraphEntity) -> str:
+        GraphService.create_entities_sync([entity])
+        return entity.id
+
+    @staticmethod
+    async def create_entities_batch(entities: list[GraphEntity]) -> int:
+        return GraphService.create_entities_sync(entities)
+
+    @staticmethod
+    async def create_relation(relation: GraphRelation) -> bool:
+        g = GraphService.graph()
+        known = g.lookup([relation.source_id, relation.target_id])
+        GraphService.create_relations_sync([relation])
+        return bool((known >= 0).all())
+
+    @staticmethod
+    async def create_relations_batch(relations: list[GraphRelation]) -> int:
+        return GraphService.create_relations_sync(relations)
+
+    @classmethod
+    def create_entities_sync(cls, entities) -> int:
+        n = cls.graph().create_entities_batch(entities)
+        cls._invalidate()
+        return n
+
+    @classmethod
+    def create_relations_sync(cls, relations) -> int:
+        n = cls.graph().create_relations_batch(relations)
+        cls._invalidate()
+        return n
+
+    @classmethod
+    def _plan(cls, n_cols: int):
+        if cls._snapshot is None:
+            cls._snapshot = cls.graph().snapshot(device=cls.device)
+        if n_cols not in cls._plans:
+            cls._plans[n_cols] = cls._snapshot.plan(n_cols, max_seeds=0, k=1)
+        return cls._plans[n_cols]
+
+    @staticmethod
+    async def get_incident_graph(incident_id: str, depth: int = 3,
+                                 resolve_bare_uuid: bool = False) -> dict:
+        return GraphService.get_incident_graphs([incident_id], depth, resolve_bare_uuid)[0]
+
+    @classmethod
+    def get_incident_graphs(cls, incident_ids: list[str], depth: int = 3,
+                            resolve_bare_uuid: bool = False) -> list[dict]:
+        """Batched get_incident_graph: one reach launch per hop for all incidents."""
+        g = cls.graph()
+        empty = {"nodes": [], "relationships": []}
+        if g.num_vertices == 0 or not incident_ids:
+            return [dict(empty) for _ in incident_ids]
+        keys = []
+        for iid in incident_ids:
+            iid = str(iid)
+            if ("Incident", iid) not in g.vertex_of and resolve_bare_uuid:
+                iid = f"incident:{iid}"
+            keys.append(g.vertex_of.get(("Incident", iid), -1))
+        plan = cls._plan(len(keys))
+        dev = plan.dev
+        # -1 as int32 is EGR_NO_NODE as u32: an empty column
+        src = torch.tensor([k if k >= 0 else -1 for k in keys], dtype=torch.int32, device=dev)
+        plan.set_sources(src)
+        for _ in range(depth):
+            plan.reach_hop()
+        bits = plan.read_reach().cpu().numpy().view("uint64")
+        labels = g.labels()
+        vlabel, _, _, _ = g.export()
+        rtypes = g.rel_types()
+        out = []
+        for b, k in enumerate(keys):
+            if k < 0:
+                out.append(dict(empty))
+                continue
+            word = bits[b // 64]
+            members = [int(v) for v in ((word >> (b % 64)) & 1).nonzero()[0]]
+            nodes = []
+            for v in members:
+                lab = labels[vlabel[v]]
+                vid = g.vertex_id(v)
+                props = dict(g.node_props.get((lab, vid), {"id": vid}))
+                nodes.append({"id": props.get("id"), "labels": [lab], "properties": props})
+            rels = []
+            for s, d, t in plan.induced_edges(b):
+                sid, did = g.vertex_id(int(s)), g.vertex_id(int(d))
+                rt = rtypes[int(t)]
+                rels.append({"type": rt, "source": sid, "target": did,
+                             "properties": dict(g.edge_props.get((sid, rt, did), {}))})
+            out.append({"nodes": nodes, "relationships": rels})
+        return out

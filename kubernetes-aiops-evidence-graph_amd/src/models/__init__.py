@@ -1,0 +1,23 @@
+"""Models on the evidence-graph hot path (reference src/models/__init__.py)."""
+from src.models.evidence import (
+    CollectorResult,
+    Evidence,
+    EvidenceSource,
+    EvidenceType,
+    GraphEntity,
+    GraphRelation,
+)
+from src.models.hypothesis import (
+    DiagnosisRule,
+    Hypothesis,
+    HypothesisCategory,
+    HypothesisSource,
+    RCAResult,
+)
+from src.models.incident import Incident, IncidentSeverity, IncidentSource, IncidentStatus
+
+__all__ = [
+    "CollectorResult", "DiagnosisRule", "Evidence", "EvidenceSource", "EvidenceType",
+    "GraphEntity", "GraphRelation", "Hypothesis", "HypothesisCategory", "HypothesisSource",
+    "Incident", "IncidentSeverity", "IncidentSource", "IncidentStatus", "RCAResult",
+]

@@ -1,0 +1,154 @@
+"""GPU parity of the graph stages: reach (A8), propagation (A9), top-k.
+
+Reach sets are exact against a per-column BFS (oracle) and hand-built known answers of
+APOC subgraphAll semantics; propagated scores are compared BIT-FOR-BIT with the C oracle (both
+accumulate with fmaf in CSR order), which is far inside the north star's 1e-5 relative bar;
+top-k ids and scores are exact.
+"""
+from __future__ import annotations
+
+import asyncio
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_world(B, seed=11, pods=3000):
+    from egraph import synth
+    from egraph.graph import EvidenceGraph
+    cfg = synth.ClusterConfig(pods=pods, namespaces=6, nodes=60, deployments=300, services=200,
+                              attach_fraction=0.3, seed=seed)
+    c = synth.build_cluster(cfg)
+    cases = synth.make_incidents(c, B, seed=seed + 1)
+    synth.add_incidents(c, cases)
+    g = EvidenceGraph()
+    g.merge_nodes(c.ids, c.labels)
+    g.merge_edges(c.src, c.dst, c.types)
+    sv, sc, ss = synth.seeds_for_batch(g, [x.evidence for x in cases])
+    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+    return g, sv, sc, ss, src
+
+
+def _dev(a):
+    from egraph.device import to_device
+    return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
+
+
+@pytest.mark.parametrize("B", [1, 5, 16, 37, 64, 130])
+def test_propagation_reach_topk_equal_oracle(B):
+    g, sv, sc, ss, src = _small_world(B)
+    snap = g.snapshot()
+    plan = snap.plan(B, max_seeds=len(sv), k=10)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    inc_label = g.labels().index("Incident")
+    ids, scores = plan.run(hops=3, exclude_label=inc_label)
+    got_scores = plan.read_scores().cpu().numpy()
+    got_reach = plan.read_reach().cpu().numpy().view(np.uint64)
+    torch.cuda.synchronize()
+    csr = g.csr()
+    exp_scores = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    assert got_scores.tobytes() == exp_scores.tobytes()           # bit-identical
+    exp_reach = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    np.testing.assert_array_equal(got_reach, exp_reach)
+    vl, _, _, _ = g.export()
+    e_ids, e_sc = oracle.topk(exp_scores, exp_reach, vl, inc_label, 10)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids)
+    np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
+
+
+@pytest.mark.parametrize("hops", [1, 2, 4])
+def test_hop_counts(hops):
+    B = 20
+    g, sv, sc, ss, src = _small_world(B, seed=3, pods=1500)
+    plan = g.snapshot().plan(B, max_seeds=len(sv), k=5)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    plan.run(hops=hops)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, hops)
+    assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+    np.testing.assert_array_equal(plan.read_reach().cpu().numpy().view(np.uint64),
+                                  oracle.reach(csr["row_ptr"], csr["col"], src, hops))
+
+
+def test_duplicate_and_invalid_seeds_are_max_combined():
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    g.merge_nodes(["a", "b", "c"], ["Pod", "Pod", "Node"])
+    g.merge_edges(["a", "b"], ["c", "c"], ["SCHEDULED_ON", "SCHEDULED_ON"])
+    sv = np.array([0, 0, 1, 7, 2], np.uint32)          # vertex 7 does not exist: dropped
+    sc = np.array([0, 0, 1, 0, 9], np.uint32)          # column 9 >= B: dropped
+    ss = np.array([0.25, 0.75, 0.5, 1.0, 1.0], np.float32)
+    plan = g.snapshot().plan(2, max_seeds=5, k=3)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(np.array([0, 1], np.uint32)))
+    plan.run(hops=2)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, 2, 2)
+    assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+
+
+def test_reach_known_answers_apoc_semantics():
+    """subgraphAll(maxLevel=3): undirected, all types, start node included, shared pods link
+    incidents (Incident -> Pod <- Incident' -> Pod')."""
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    g.create_entities_batch([
+        {"id": "incident:1", "type": "Incident"}, {"id": "incident:2", "type": "Incident"},
+        {"id": "pod:p1", "type": "Pod"}, {"id": "pod:p2", "type": "Pod"},
+        {"id": "pod:p3", "type": "Pod"}, {"id": "node:n1", "type": "Node"},
+        {"id": "deployment:d", "type": "Deployment"}, {"id": "change:c", "type": "ChangeEvent"}])
+    g.create_relations_batch([
+        {"source_id": "incident:1", "target_id": "pod:p1", "relation_type": "AFFECTS"},
+        {"source_id": "incident:2", "target_id": "pod:p1", "relation_type": "AFFECTS"},
+        {"source_id": "incident:2", "target_id": "pod:p2", "relation_type": "AFFECTS"},
+        {"source_id": "pod:p2", "target_id": "node:n1", "relation_type": "SCHEDULED_ON"},
+        {"source_id": "pod:p3", "target_id": "node:n1", "relation_type": "SCHEDULED_ON"},
+        {"source_id": "deployment:d", "target_id": "change:c", "relation_type": "HAS_RECENT_CHANGE"},
+        {"source_id": "pod:p3", "target_id": "node:missing", "relation_type": "SCHEDULED_ON"}])
+    plan = g.snapshot().plan(2, max_seeds=0, k=1)
+    plan.set_sources(_dev(g.lookup(["incident:1", "incident:2"]).astype(np.uint32)))
+    for _ in range(3):
+        plan.reach_hop()
+    bits = plan.read_reach().cpu().numpy().view(np.uint64)[0]
+    members = lambda b: {g.vertex_id(v) for v in range(g.num_vertices) if bits[v] >> b & 1}  # noqa
+    assert members(0) == {"incident:1", "pod:p1", "incident:2", "pod:p2"}
+    assert members(1) == {"incident:2", "pod:p1", "pod:p2", "incident:1", "node:n1", "pod:p3"}
+
+
+def test_graph_service_get_incident_graph():
+    from src.database import GraphService
+    from src.models import GraphEntity, GraphRelation
+    GraphService.reset()
+    ents = [GraphEntity(id="incident:42", type="Incident", properties={"id": "42", "title": "t"}),
+            GraphEntity(id="pod:ns:a", type="Pod", properties={"phase": "Running"}),
+            GraphEntity(id="node:n", type="Node", properties={"ready": False}),
+            GraphEntity(id="pod:ns:b", type="Pod"), GraphEntity(id="pod:ns:far", type="Pod"),
+            GraphEntity(id="deployment:ns:x", type="Deployment")]
+    rels = [GraphRelation(source_id="incident:42", target_id="pod:ns:a", relation_type="AFFECTS"),
+            GraphRelation(source_id="pod:ns:a", target_id="node:n", relation_type="SCHEDULED_ON",
+                          properties={"w": 1}),
+            GraphRelation(source_id="pod:ns:b", target_id="node:n", relation_type="SCHEDULED_ON"),
+            GraphRelation(source_id="deployment:ns:x", target_id="pod:ns:b", relation_type="OWNS"),
+            GraphRelation(source_id="deployment:ns:x", target_id="pod:ns:far", relation_type="OWNS")]
+    assert asyncio.run(GraphService.create_entities_batch(ents)) == 6
+    assert asyncio.run(GraphService.create_relations_batch(rels)) == 5
+    out = asyncio.run(GraphService.get_incident_graph("incident:42", depth=3))
+    assert {n["id"] for n in out["nodes"]} == {"incident:42", "pod:ns:a", "node:n", "pod:ns:b"}
+    inc = next(n for n in out["nodes"] if n["id"] == "incident:42")
+    assert inc["labels"] == ["Incident"] and inc["properties"]["title"] == "t"
+    assert {(r["type"], r["source"], r["target"]) for r in out["relationships"]} == {
+        ("AFFECTS", "incident:42", "pod:ns:a"), ("SCHEDULED_ON", "pod:ns:a", "node:n"),
+        ("SCHEDULED_ON", "pod:ns:b", "node:n")}
+    assert asyncio.run(GraphService.get_incident_graph("42")) == {"nodes": [], "relationships": []}
+    assert len(asyncio.run(GraphService.get_incident_graph("42", resolve_bare_uuid=True))["nodes"]) == 4
+    d4 = asyncio.run(GraphService.get_incident_graph("incident:42", depth=4))
+    assert {n["id"] for n in d4["nodes"]} == {"incident:42", "pod:ns:a", "node:n", "pod:ns:b",
+                                              "deployment:ns:x"}
+    GraphService.reset()

@@ -1,0 +1,113 @@
+"""Host-side checks of libegraph.so that need no GPU: symbols, exact rounding, MERGE
+semantics and the CSR the snapshot uploads (against the pure-Python restatement)."""
+from __future__ import annotations
+
+import random
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def _header_functions() -> list[str]:
+    text = (REPO / "include" / "egraph.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(egr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from egraph import _lib as L
+    names = _header_functions()
+    assert len(names) >= 30
+    for name in names:
+        assert hasattr(L.lib, name), name
+        assert name in L.SIGNATURES, f"{name} declared in egraph.h but not bound"
+    assert L.lib.egr_version() == 1
+
+
+def test_device_count_is_safe_without_gpu():
+    from egraph import _lib as L
+    assert L.lib.egr_device_count() >= 0
+
+
+def test_exact_python_round_host():
+    from egraph import _lib as L
+    rng = random.Random(3)
+    for _ in range(100000):
+        x = rng.choice([rng.random() * 3, rng.uniform(-5, 5), round(rng.random(), 5),
+                        rng.random() * 1e13, rng.random() * 1e17, rng.random() * 1e-7,
+                        rng.randint(0, 10**6) / 2e4, rng.randint(0, 10**6) / 2e3])
+        nd = rng.choice([0, 1, 2, 3, 4, 6, 9])
+        assert L.lib.egr_py_round(x, nd) == round(x, nd), (x, nd)
+    for x in (float("inf"), -float("inf"), 0.0, -0.0, 2.675, 0.00005, -0.00005, 1e300, 5e-324):
+        r = L.lib.egr_py_round(x, 4)
+        assert r == round(x, 4) and np.signbit(r) == np.signbit(round(x, 4))
+    assert np.isnan(L.lib.egr_py_round(float("nan"), 4))
+
+
+def _random_graph(rng: random.Random, n_ids=30, n_ent=60, n_rel=120):
+    labels = ["Pod", "Node", "Deployment", "Incident", "Service"]
+    types = ["AFFECTS", "SCHEDULED_ON", "OWNS", "CALLS"]
+    ents = [{"id": f"id{rng.randrange(n_ids)}", "type": rng.choice(labels), "properties": {"k": i}}
+            for i in range(n_ent)]
+    rels = [{"source_id": f"id{rng.randrange(n_ids + 5)}", "target_id": f"id{rng.randrange(n_ids + 5)}",
+             "relation_type": rng.choice(types), "properties": {}} for _ in range(n_rel)]
+    return ents, rels
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_merge_semantics_and_csr_match_restatement(seed):
+    import oracle
+    from egraph.graph import EvidenceGraph
+    rng = random.Random(seed)
+    ents, rels = _random_graph(rng)
+    g = EvidenceGraph()
+    # feed in two batches to exercise incremental MERGE
+    g.create_entities_batch(ents[:30])
+    g.create_relations_batch(rels[:50])
+    g.create_entities_batch(ents[30:])
+    g.create_relations_batch(rels[50:])
+    # reference order: node merges then edge merges interleaved the same way
+    verts, _ = oracle.graph_reference(ents, [])
+    _, e1 = oracle.graph_reference(ents[:30], rels[:50])
+    vert_all, _ = oracle.graph_reference(ents, [])
+    vid = {k: i for i, k in enumerate(vert_all)}
+    # edges of batch 1 were matched against the first 30 entities only
+    v30, _ = oracle.graph_reference(ents[:30], [])
+    e_ref = [(vid[v30[s]], vid[v30[d]], t) for s, d, t in e1]
+    _, e_all = oracle.graph_reference(ents, rels[50:])
+    seen = set(e_ref)
+    for s, d, t in e_all:
+        if (s, d, t) not in seen:
+            seen.add((s, d, t))
+            e_ref.append((s, d, t))
+    assert g.num_vertices == len(verts)
+    labels = g.labels()
+    vl, es, ed, et = g.export()
+    assert [(labels[vl[v]], g.vertex_id(v)) for v in range(g.num_vertices)] == verts
+    types = g.rel_types()
+    assert list(zip(es.tolist(), ed.tolist(), [types[t] for t in et])) == e_ref
+    # CSR
+    w = g.weight_array({"AFFECTS": (1.0, 0.5), "OWNS": (0.25, 2.0)})
+    csr = g.csr({"AFFECTS": (1.0, 0.5), "OWNS": (0.25, 2.0)})
+    rp, col, meta, val = oracle.csr_reference(len(verts), e_ref, {t: i for i, t in enumerate(types)}, w)
+    np.testing.assert_array_equal(csr["row_ptr"], rp)
+    np.testing.assert_array_equal(csr["col"], col)
+    np.testing.assert_array_equal(csr["meta"], meta)
+    np.testing.assert_array_equal(csr["val"], val)
+
+
+def test_dangling_edges_dropped_and_counts_are_attempts():
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    assert g.create_entities_batch([{"id": "pod:a", "type": "Pod"}, {"id": "pod:a", "type": "Pod"},
+                                    {"id": "incident:1", "type": "Incident"}]) == 3
+    assert g.num_vertices == 2
+    rels = [{"source_id": "incident:1", "target_id": "pod:a", "relation_type": "AFFECTS"},
+            {"source_id": "incident:1", "target_id": "pod:a", "relation_type": "AFFECTS"},
+            {"source_id": "pod:a", "target_id": "node:healthy", "relation_type": "SCHEDULED_ON"}]
+    assert g.create_relations_batch(rels) == 3          # attempted, like neo4j.py:166
+    assert g.num_edges == 1                              # dedup + dangling SCHEDULED_ON dropped
+    assert g.node_props[("Pod", "pod:a")]["id"] == "pod:a"
