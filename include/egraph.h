@@ -185,7 +185,8 @@ int egr_snapshot_info(const egr_snapshot* s, int64_t* n_vertices, int64_t* n_ent
 /* ------------------------------------------------------------------------------------------
  * Plan: per-batch workspace for B incident columns on a snapshot (all device memory is
  * allocated here, none in the launch functions, so a step can be captured into a hipGraph).
- *   scores: fp32, tiled [B/TW][V][TW] with TW = 64 (B >= 64), 16 or 4.
+ *   scores: fp32, tiled [B/TW][V][TW] with TW = 128 (B >= 128), 64, 16 or 4
+ *           ($EGRAPH_TILE_WIDTH caps TW).
  *   reach : u64 words [ceil(B/64)][V], bit b%64 of word b/64 = vertex within `hops` of the
  *           incident vertex of column b (undirected, all types: apoc.path.subgraphAll).
  * ---------------------------------------------------------------------------------------- */
@@ -204,6 +205,12 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
 int egr_plan_hop(egr_plan* p, void* stream);
 /* One reachability hop over the undirected graph.                                          */
 int egr_plan_reach_hop(egr_plan* p, void* stream);
+/* One hop of both recurrences (fused into a single pass over the CSR when TW >= 64).        */
+int egr_plan_step(egr_plan* p, void* stream);
+/* The last hop: egr_plan_step plus, when TW >= 64, the top-k candidate lists (reached
+ * vertices whose label is not exclude_label), so egr_plan_topk with the same exclude_label
+ * reads only the candidates instead of rescanning every score.                              */
+int egr_plan_final_step(egr_plan* p, int32_t exclude_label, void* stream);
 /* Per column: top-k vertices by final score (desc), vertex id asc on ties, over the reach
  * set excluding vertices whose label is `exclude_label` (-1: none).  Outputs [n_cols*k];
  * unused slots hold EGR_NO_NODE / -inf.                                                     */

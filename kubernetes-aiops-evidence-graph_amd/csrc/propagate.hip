@@ -106,72 +106,192 @@ __device__ __forceinline__ void add_seeds(float4& acc, uint32_t v, uint32_t lo,
   }
 }
 
-// ---- hop from sparse seeds (h = 0 -> 1): gathers s0_u straight from the seed lists ---------
+// ---- propagation hop ---------------------------------------------------------------------
+// One block = ROWS consecutive rows of one column tile.  The block stages its rows' row_ptr,
+// own seed-tile masks, labels and CSR segment (col, val) in LDS with coalesced loads.  Each
+// lane group (G lanes x float4 = the row's TW columns) then walks its rows with a two-row
+// software pipeline: the next row's first NB neighbour gathers (and reach words) are in flight
+// while the current row runs its fmaf chain in CSR order (bit-exact with the oracle).
+//   FROM_SEEDS (h = 0 -> 1): neighbour values come from the sparse seed lists, filtered by a
+//              per-vertex seed-tile mask, so s0 is never materialised densely;
+//   REACH      (TW >= 64): the same walk ORs the neighbours' reach words (one pass per hop);
+//   CAND       (last hop): reached, non-excluded (vertex, column) pairs are appended to the
+//              column's candidate list for the top-k merge, so top-k never rescans the scores.
 template <int G>
-__global__ __launch_bounds__(256) void hop_from_seeds_kernel(
-    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-    const float* __restrict__ val, const uint32_t* __restrict__ seed_ptr,
-    const uint32_t* __restrict__ seed_col, const float* __restrict__ seed_val,
-    float* __restrict__ xout, uint32_t V, uint32_t nrb8) {
-  constexpr int TW = 4 * G;
-  constexpr int ROWS = 256 / G;
-  const uint32_t gl = threadIdx.x % G;
-  const uint32_t tile = blockIdx.x / nrb8;
-  const uint32_t rb = xcd_remap(blockIdx.x % nrb8, nrb8);
-  const uint32_t v = rb * ROWS + threadIdx.x / G;
-  if (v >= V) return;
-  const uint32_t lo = tile * TW + 4 * gl;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  const uint32_t e1 = row_ptr[v + 1];
-  for (uint32_t e = row_ptr[v]; e < e1; ++e) {
-    const uint32_t u = col[e];
-    const uint32_t s0 = seed_ptr[u], s1 = seed_ptr[u + 1];
-    if (s0 == s1) continue;  // contribution w*0: skipping it is exact (acc is never -0.0)
-    const float w = val[e];
-    for (uint32_t s = seed_lower(seed_col, s0, s1, lo); s < s1; ++s) {
-      const uint32_t c = seed_col[s] - lo;
-      if (c >= 4u) break;
-      fma_comp(acc, (int)c, w, seed_val[s]);
-    }
+struct HopGeo {
+  static constexpr int ROWS = G == 1 ? 256 : 128;
+};
+constexpr uint32_t CSR_CAP = 2048;   // staged entries per block (longer segments read global)
+constexpr int NB = 4;                // neighbour gathers per batch
+
+struct HopArgs {
+  const uint32_t* row_ptr;
+  const uint32_t* col;
+  const float* val;
+  const uint32_t* seed_ptr;
+  const uint32_t* seed_col;
+  const float* seed_val;
+  const uint32_t* seed_tiles;
+  const uint8_t* vlabel;
+  const float* xin;
+  float* xout;
+  const uint64_t* rin;
+  uint64_t* rout;
+  uint32_t* cand_count;
+  uint32_t* cand_list;
+  uint32_t V;
+  uint32_t nchunks;
+  int32_t B;
+  int32_t exclude_label;
+};
+
+template <bool SEEDS, bool REACH>
+struct Batch {
+  float4 x[NB];
+  uint64_t rw[NB];
+  uint32_t m[NB];
+  uint32_t u[NB];
+  float w[NB];
+  uint32_t n;
+};
+
+template <int G, bool FROM_SEEDS, bool REACH, bool CAND>
+__global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
+  constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
+  __shared__ uint32_t s_rp[ROWS + 1];
+  __shared__ uint32_t s_mask[ROWS];
+  __shared__ uint8_t s_lab[ROWS];
+  __shared__ uint32_t s_col[CSR_CAP];
+  __shared__ float s_val[CSR_CAP];
+  const uint32_t tid = threadIdx.x, gl = tid % G, grp = tid / G;
+  const uint32_t V = A.V;
+  const uint32_t tile = blockIdx.x / A.nchunks;
+  const uint32_t v0 = (blockIdx.x % A.nchunks) * ROWS;
+  if (v0 >= V) return;  // block-uniform, before any barrier
+  const uint32_t nrows = min((uint32_t)ROWS, V - v0);
+  for (uint32_t i = tid; i <= nrows; i += 256) s_rp[i] = A.row_ptr[v0 + i];
+  for (uint32_t i = tid; i < nrows; i += 256) {
+    s_mask[i] = A.seed_tiles[v0 + i];
+    if constexpr (CAND) s_lab[i] = A.vlabel[v0 + i];
   }
-  add_seeds(acc, v, lo, seed_ptr, seed_col, seed_val);
-  reinterpret_cast<float4*>(xout + (size_t)tile * V * TW)[(size_t)v * G + gl] = acc;
+  __syncthreads();
+  const uint32_t e0 = s_rp[0];
+  const uint32_t nst = min(s_rp[nrows] - e0, CSR_CAP);
+  for (uint32_t i = tid; i < nst; i += 256) {
+    s_col[i] = A.col[e0 + i];
+    s_val[i] = A.val[e0 + i];
+  }
+  __syncthreads();
+  uint32_t r = grp;
+  if (r >= nrows) return;  // no barrier below
+
+  const uint32_t lo = tile * TW + 4 * gl;  // first column of this lane
+  const uint32_t tbit = tile & 31u;
+  const size_t toff = (size_t)tile * V * TW;
+  const float4* __restrict__ X = reinterpret_cast<const float4*>(A.xin + toff);
+  const uint32_t word = lo >> 6;
+  const uint64_t* __restrict__ R = A.rin + (size_t)word * V;
+
+  auto issue = [&](uint32_t ja, uint32_t jb, Batch<FROM_SEEDS, REACH>& bt) {
+    bt.n = jb > ja ? min(jb - ja, (uint32_t)NB) : 0u;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const uint32_t jj = ja + t;
+      const bool ok = (uint32_t)t < bt.n;
+      uint32_t u = 0u;
+      float w = 0.f;
+      if (ok) {
+        u = jj < CSR_CAP ? s_col[jj] : A.col[e0 + jj];
+        w = jj < CSR_CAP ? s_val[jj] : A.val[e0 + jj];
+      }
+      bt.u[t] = u;
+      bt.w[t] = w;
+      if constexpr (FROM_SEEDS) {
+        bt.m[t] = ok ? A.seed_tiles[u] : 0u;
+      } else {
+        bt.x[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) bt.x[t] = X[(size_t)u * G + gl];
+      }
+      if constexpr (REACH) bt.rw[t] = ok ? R[u] : 0ull;
+    }
+  };
+  auto consume = [&](const Batch<FROM_SEEDS, REACH>& bt, float4& acc, uint64_t& rr) {
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      if ((uint32_t)t < bt.n) {
+        if constexpr (FROM_SEEDS) {
+          if ((bt.m[t] >> tbit) & 1u) {  // w * 0 otherwise: skipping the fmaf is exact
+            const uint32_t u = bt.u[t];
+            const uint32_t s1 = A.seed_ptr[u + 1];
+            for (uint32_t q = seed_lower(A.seed_col, A.seed_ptr[u], s1, lo); q < s1; ++q) {
+              const uint32_t c = A.seed_col[q] - lo;
+              if (c >= 4u) break;
+              fma_comp(acc, (int)c, bt.w[t], A.seed_val[q]);
+            }
+          }
+        } else {
+          fma4(bt.w[t], bt.x[t], acc);
+        }
+        if constexpr (REACH) rr |= bt.rw[t];
+      }
+    }
+  };
+
+  Batch<FROM_SEEDS, REACH> cur, nxt;
+  issue(s_rp[r] - e0, s_rp[r + 1] - e0, cur);
+  uint64_t own = 0;
+  if constexpr (REACH) own = R[v0 + r];
+  while (true) {
+    const uint32_t rn = r + GROUPS;
+    const bool more = rn < nrows;
+    uint64_t own_n = 0;
+    if (more) {
+      issue(s_rp[rn] - e0, s_rp[rn + 1] - e0, nxt);
+      if constexpr (REACH) own_n = R[v0 + rn];
+    }
+    const uint32_t v = v0 + r;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint64_t rr = own;
+    consume(cur, acc, rr);
+    const uint32_t b = s_rp[r + 1] - e0;
+    for (uint32_t j = s_rp[r] - e0 + NB; j < b; j += NB) {  // rows longer than NB
+      Batch<FROM_SEEDS, REACH> tail;
+      issue(j, b, tail);
+      consume(tail, acc, rr);
+    }
+    if ((s_mask[r] >> tbit) & 1u) add_seeds(acc, v, lo, A.seed_ptr, A.seed_col, A.seed_val);
+    reinterpret_cast<float4*>(A.xout + toff)[(size_t)v * G + gl] = acc;
+    if constexpr (REACH) {
+      if ((lo & 63u) == 0u) A.rout[(size_t)word * V + v] = rr;
+    }
+    if constexpr (CAND) {
+      const uint32_t bits = (uint32_t)(rr >> (lo & 63u)) & 0xFu;
+      if (bits && !(A.exclude_label >= 0 && s_lab[r] == (uint8_t)A.exclude_label)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t bcol = lo + i;
+          if (((bits >> i) & 1u) && bcol < (uint32_t)A.B) {
+            const uint32_t slot = atomicAdd(&A.cand_count[bcol], 1u);
+            A.cand_list[(size_t)bcol * V + slot] = v;
+          }
+        }
+      }
+    }
+    if (!more) break;
+    cur = nxt;
+    own = own_n;
+    r = rn;
+  }
 }
 
-// ---- dense hop (h >= 1): pull-gather TW-wide neighbour rows, 4 entries in flight ----------
-template <int G>
-__global__ __launch_bounds__(256) void hop_kernel(
-    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ col,
-    const float* __restrict__ val, const uint32_t* __restrict__ seed_ptr,
-    const uint32_t* __restrict__ seed_col, const float* __restrict__ seed_val,
-    const float* __restrict__ xin, float* __restrict__ xout, uint32_t V, uint32_t nrb8) {
-  constexpr int TW = 4 * G;
-  constexpr int ROWS = 256 / G;
-  const uint32_t gl = threadIdx.x % G;
-  const uint32_t tile = blockIdx.x / nrb8;
-  const uint32_t rb = xcd_remap(blockIdx.x % nrb8, nrb8);
-  const uint32_t v = rb * ROWS + threadIdx.x / G;
-  if (v >= V) return;
-  const size_t toff = (size_t)tile * V * TW;
-  const float4* __restrict__ X = reinterpret_cast<const float4*>(xin + toff);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  uint32_t e = row_ptr[v];
-  const uint32_t e1 = row_ptr[v + 1];
-  for (; e + 4 <= e1; e += 4) {
-    const uint32_t u0 = col[e], u1 = col[e + 1], u2 = col[e + 2], u3 = col[e + 3];
-    const float w0 = val[e], w1 = val[e + 1], w2 = val[e + 2], w3 = val[e + 3];
-    const float4 a0 = X[(size_t)u0 * G + gl];
-    const float4 a1 = X[(size_t)u1 * G + gl];
-    const float4 a2 = X[(size_t)u2 * G + gl];
-    const float4 a3 = X[(size_t)u3 * G + gl];
-    fma4(w0, a0, acc);
-    fma4(w1, a1, acc);
-    fma4(w2, a2, acc);
-    fma4(w3, a3, acc);
-  }
-  for (; e < e1; ++e) fma4(val[e], X[(size_t)col[e] * G + gl], acc);
-  add_seeds(acc, v, tile * TW + 4 * gl, seed_ptr, seed_col, seed_val);
-  reinterpret_cast<float4*>(xout + toff)[(size_t)v * G + gl] = acc;
+__global__ void seed_tiles_kernel(const uint64_t* __restrict__ ukeys,
+                                  const uint32_t* __restrict__ n_unique, uint32_t Bpad,
+                                  uint32_t TW, uint32_t* seed_tiles) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_unique) return;
+  const uint64_t k = ukeys[i];
+  const uint32_t v = (uint32_t)(k / Bpad), tile = (uint32_t)(k % Bpad) / TW;
+  atomicOr(&seed_tiles[v], 1u << (tile & 31u));
 }
 
 // ---- reachability ----------------------------------------------------------------------------
@@ -284,70 +404,11 @@ __device__ __forceinline__ void list_insert(float (&Ls)[KMAX], uint32_t (&Lv)[KM
   }
 }
 
-__global__ __launch_bounds__(256) void topk_partial_kernel(
-    const float* __restrict__ X, const uint64_t* __restrict__ R,
-    const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, int TW, int B,
-    int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v) {
-  const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int ntiles = (B + TW - 1) / TW;
-  if (wid >= ntiles * n_chunks) return;
-  const int tile = wid / n_chunks, ch = wid % n_chunks;
-  const int c = lane % TW, rp = lane / TW, rps = 64 / TW;
-  const int b = tile * TW + c;
-  float Ls[KMAX];
-  uint32_t Lv[KMAX];
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    Ls[i] = -INFINITY;
-    Lv[i] = NO_NODE;
-  }
-  if (b < B) {
-    const float* Xt = X + (size_t)tile * V * TW;
-    const uint64_t* Rw = R + (size_t)(b >> 6) * V;
-    const uint64_t bit = 1ull << (b & 63);
-    const uint32_t v0 = (uint32_t)ch * TOPK_CHUNK;
-    const uint32_t v1 = min(V, v0 + TOPK_CHUNK);
-    for (uint32_t v = v0 + rp; v < v1; v += rps) {
-      if (!(Rw[v] & bit)) continue;
-      if (exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label) continue;
-      list_insert(Ls, Lv, Xt[(size_t)v * TW + c], v);
-    }
-  }
-  const size_t o = ((size_t)wid * 64 + lane) * KMAX;
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    part_s[o + i] = Ls[i];
-    part_v[o + i] = Lv[i];
-  }
-}
-
-__global__ __launch_bounds__(256) void topk_merge_kernel(
-    const float* __restrict__ part_s, const uint32_t* __restrict__ part_v, int TW, int B,
-    int n_chunks, int k, uint32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const int tile = b / TW, c = b % TW, rps = 64 / TW;
-  float Ls[KMAX];
-  uint32_t Lv[KMAX];
-#pragma unroll
-  for (int i = 0; i < KMAX; ++i) {
-    Ls[i] = -INFINITY;
-    Lv[i] = NO_NODE;
-  }
-  // candidate lists of column b: chunks x (lanes with lane % TW == c), KMAX entries each
-  const int n_lists = n_chunks * rps;
-  for (int li = lane; li < n_lists; li += 64) {
-    const int ch = li / rps, rp = li % rps;
-    const size_t o = (((size_t)(tile * n_chunks + ch)) * 64 + rp * TW + c) * KMAX;
-    for (int i = 0; i < k; ++i) {
-      const uint32_t v = part_v[o + i];
-      if (v == NO_NODE) break;
-      list_insert(Ls, Lv, part_s[o + i], v);
-    }
-  }
-  // k rounds of a wave-wide arg-best over the list heads
+// k rounds of a wave-wide arg-best over the per-lane list heads; lane 0 writes the result.
+// Every vertex appears in at most one lane's list, so (score desc, id asc) is a strict order
+// and all lanes agree on each round's winner.
+__device__ __forceinline__ void wave_emit_topk(float (&Ls)[KMAX], uint32_t (&Lv)[KMAX], int k,
+                                               int lane, uint32_t* out_ids, float* out_scores) {
   for (int q = 0; q < k; ++q) {
     float bs = Ls[0];
     uint32_t bv = Lv[0];
@@ -364,8 +425,8 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
       }
     }
     if (lane == 0) {
-      out_ids[(size_t)b * k + q] = bv;
-      out_scores[(size_t)b * k + q] = bv == NO_NODE ? -INFINITY : bs;
+      out_ids[q] = bv;
+      out_scores[q] = bv == NO_NODE ? -INFINITY : bs;
     }
     if (bv != NO_NODE && lane == bl) {
 #pragma unroll
@@ -377,6 +438,127 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
       Lv[KMAX - 1] = NO_NODE;
     }
   }
+}
+
+// A wave covers CW = min(TW, 64) columns of one tile: lane -> (column c, row phase rp); the
+// wave index enumerates (tile, 64-column slice, row chunk).
+__global__ __launch_bounds__(256) void topk_partial_kernel(
+    const float* __restrict__ X, const uint64_t* __restrict__ R,
+    const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, int TW, int B,
+    int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int CW = TW < 64 ? TW : 64, nsub = TW / CW;
+  const int ntiles = (B + TW - 1) / TW;
+  if (wid >= ntiles * nsub * n_chunks) return;
+  const int ch = wid % n_chunks, ts = wid / n_chunks, tile = ts / nsub, sub = ts % nsub;
+  const int c = lane % CW, rp = lane / CW, rps = 64 / CW;
+  const int b = tile * TW + sub * CW + c;
+  const int cx = sub * CW + c;   // column inside the tile
+  float Ls[KMAX];
+  uint32_t Lv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    Ls[i] = -INFINITY;
+    Lv[i] = NO_NODE;
+  }
+  if (b < B) {
+    const float* Xt = X + (size_t)tile * V * TW;
+    const uint64_t* Rw = R + (size_t)(b >> 6) * V;
+    const uint64_t bit = 1ull << (b & 63);
+    const uint32_t v0 = (uint32_t)ch * TOPK_CHUNK;
+    const uint32_t v1 = min(V, v0 + TOPK_CHUNK);
+    // eight rows per step: all reach words and labels, then the reached scores, are loaded
+    // before any insertion, so a wave keeps 8-16 loads in flight instead of one
+    for (uint32_t vb = v0 + rp; vb < v1; vb += 8u * rps) {
+      uint64_t wd[8];
+      uint8_t lab[8];
+      float xs[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t v = vb + t * rps;
+        wd[t] = v < v1 ? Rw[v] : 0ull;
+        lab[t] = v < v1 ? vlabel[v] : 0;
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t v = vb + t * rps;
+        const bool cand = (wd[t] & bit) && !(exclude_label >= 0 && lab[t] == (uint8_t)exclude_label);
+        wd[t] = cand;
+        xs[t] = cand ? Xt[(size_t)v * TW + cx] : 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        if (wd[t]) list_insert(Ls, Lv, xs[t], vb + t * rps);
+    }
+  }
+  const size_t o = ((size_t)wid * 64 + lane) * KMAX;
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    part_s[o + i] = Ls[i];
+    part_v[o + i] = Lv[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void topk_merge_kernel(
+    const float* __restrict__ part_s, const uint32_t* __restrict__ part_v, int TW, int B,
+    int n_chunks, int k, uint32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int CW = TW < 64 ? TW : 64, nsub = TW / CW;
+  const int tile = b / TW, sub = (b % TW) / CW, c = b % CW, rps = 64 / CW;
+  float Ls[KMAX];
+  uint32_t Lv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    Ls[i] = -INFINITY;
+    Lv[i] = NO_NODE;
+  }
+  // candidate lists of column b: chunks x (lanes with lane % CW == c), KMAX entries each
+  const int n_lists = n_chunks * rps;
+  for (int li = lane; li < n_lists; li += 64) {
+    const int ch = li / rps, rp = li % rps;
+    const size_t o = (((size_t)((tile * nsub + sub) * n_chunks + ch)) * 64 + rp * CW + c) * KMAX;
+    for (int i = 0; i < k; ++i) {
+      const uint32_t v = part_v[o + i];
+      if (v == NO_NODE) break;
+      list_insert(Ls, Lv, part_s[o + i], v);
+    }
+  }
+  wave_emit_topk(Ls, Lv, k, lane, out_ids + (size_t)b * k, out_scores + (size_t)b * k);
+}
+
+// top-k from the candidate lists the CAND hop appended: one wave per column
+__global__ __launch_bounds__(256) void topk_cand_kernel(
+    const float* __restrict__ X, const uint32_t* __restrict__ cand_count,
+    const uint32_t* __restrict__ cand_list, uint32_t V, int TW, int B, int k,
+    uint32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float Ls[KMAX];
+  uint32_t Lv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    Ls[i] = -INFINITY;
+    Lv[i] = NO_NODE;
+  }
+  const uint32_t n = min(cand_count[b], V);
+  const float* __restrict__ Xc = X + (size_t)(b / TW) * V * TW + (b % TW);
+  const uint32_t* __restrict__ Lb = cand_list + (size_t)b * V;
+  for (uint32_t i0 = lane; i0 < n; i0 += 64u * 4u) {
+    uint32_t vv[4];
+    float ss[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) vv[t] = i0 + t * 64u < n ? Lb[i0 + t * 64u] : NO_NODE;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ss[t] = vv[t] != NO_NODE ? Xc[(size_t)vv[t] * TW] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (vv[t] != NO_NODE) list_insert(Ls, Lv, ss[t], vv[t]);
+  }
+  wave_emit_topk(Ls, Lv, k, lane, out_ids + (size_t)b * k, out_scores + (size_t)b * k);
 }
 
 __global__ void scores_rowmajor_kernel(const float* __restrict__ X, uint32_t V, int TW, int B,
@@ -414,28 +596,34 @@ __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
 struct egr_plan {
   const egr_snapshot* s = nullptr;
   int B = 0, TW = 0, Bpad = 0, ntiles = 0, W = 0, k = 0;
+  int Wa = 0;                // reach words allocated: padded columns of 128-wide tiles too
   int64_t max_seeds = 0;
-  int n_chunks = 0;
-  uint32_t nrb8_hop = 0, nrb8_reach = 0;
+  int n_chunks = 0;          // top-k full-scan chunks
+  uint32_t nchunks = 0;      // hop row chunks per tile
+  uint32_t nrb8_reach = 0;
   float* x[2] = {nullptr, nullptr};
   int xcur = 0;
   uint64_t* reach[2] = {nullptr, nullptr};
   int rcur = 0;
   int reach_hops = -1;  // -1: sources not set
+  int hops_done = -1;   // -1: seeds not set
+  bool sources_set = false;
   // seeds
   uint64_t *skeys_in = nullptr, *skeys = nullptr, *ukeys = nullptr;
   float *svals_in = nullptr, *svals = nullptr, *uval = nullptr;
   uint32_t *head = nullptr, *pos = nullptr, *ucol = nullptr, *seed_ptr = nullptr,
-           *n_unique = nullptr;
+           *n_unique = nullptr, *seed_tiles = nullptr;
   void* cub_tmp = nullptr;
   size_t cub_tmp_bytes = 0;
   int end_bit = 64;
-  // top-k partials
+  // top-k: full-scan partials, and the candidate lists of the fused last hop
   float* part_s = nullptr;
   uint32_t* part_v = nullptr;
+  uint32_t* cand_count = nullptr;
+  uint32_t* cand_list = nullptr;
+  bool cand_valid = false;
+  int cand_exclude = -1;
   unsigned long long* counter = nullptr;
-  int hops_done = -1;  // -1: seeds not set
-  bool sources_set = false;
 };
 
 namespace {
@@ -457,11 +645,105 @@ void dfree(T*& p) {
   p = nullptr;
 }
 
-#define EGR_TRY(x)              \
-  do {                          \
-    int rc_ = (x);              \
+#define EGR_TRY(x)                 \
+  do {                             \
+    int rc_ = (x);                 \
     if (rc_ != EGR_OK) return rc_; \
   } while (0)
+
+int choose_tile_width(int n_cols) {
+  // 128-wide tiles (512-B gathers, two reach words) unless overridden; a tile must not
+  // exceed the batch by more than padding, so narrow batches use narrower tiles
+  int cap = 128;
+  if (const char* e = getenv("EGRAPH_TILE_WIDTH")) {
+    const int t = atoi(e);
+    if (t == 4 || t == 16 || t == 64 || t == 128) cap = t;
+  }
+  int tw = n_cols >= 128 ? 128 : (n_cols >= 64 ? 64 : (n_cols >= 16 ? 16 : 4));
+  return tw < cap ? tw : cap;
+}
+
+uint32_t hop_rows(int TW) {
+  switch (TW) {
+    case 128: return HopGeo<32>::ROWS;
+    case 64: return HopGeo<16>::ROWS;
+    case 16: return HopGeo<4>::ROWS;
+    default: return HopGeo<1>::ROWS;
+  }
+}
+
+template <int G, bool SEEDS, bool REACH, bool CAND>
+void launch_hop_t(const HopArgs& a, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((hop_kernel<G, SEEDS, REACH, CAND>), grid, dim3(256), 0, st, a);
+}
+
+template <int G>
+void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool reach, bool cand) {
+  if constexpr (G >= 16) {
+    if (seeds) {
+      if (cand) launch_hop_t<G, true, true, true>(a, grid, st);
+      else if (reach) launch_hop_t<G, true, true, false>(a, grid, st);
+      else launch_hop_t<G, true, false, false>(a, grid, st);
+    } else {
+      if (cand) launch_hop_t<G, false, true, true>(a, grid, st);
+      else if (reach) launch_hop_t<G, false, true, false>(a, grid, st);
+      else launch_hop_t<G, false, false, false>(a, grid, st);
+    }
+  } else {
+    if (seeds) launch_hop_t<G, true, false, false>(a, grid, st);
+    else launch_hop_t<G, false, false, false>(a, grid, st);
+  }
+}
+
+// One propagation hop.  reach: also one reachability hop in the same pass (TW >= 64);
+// cand: also append the top-k candidates of this (last) hop.
+int plan_hop(egr_plan* p, void* stream, bool reach, bool cand, int exclude_label) {
+  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_hop: NULL plan");
+  if (p->hops_done < 0) return egr::fail(EGR_ESTATE, "egr_plan_hop: seeds not set");
+  if ((reach || cand) && (p->TW < 64 || !p->sources_set))
+    return egr::fail(EGR_ESTATE, "fused reach needs TW >= 64 and sources set");
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const egr_snapshot* s = p->s;
+  const bool seeds = p->hops_done == 0;
+  if (cand) EGR_HIP(hipMemsetAsync(p->cand_count, 0, (size_t)p->Bpad * 4, st));
+  HopArgs a;
+  a.row_ptr = s->row_ptr;
+  a.col = s->col;
+  a.val = s->val;
+  a.seed_ptr = p->seed_ptr;
+  a.seed_col = p->ucol;
+  a.seed_val = p->uval;
+  a.seed_tiles = p->seed_tiles;
+  a.vlabel = s->vlabel;
+  a.xin = seeds ? nullptr : p->x[p->xcur];
+  a.xout = p->x[seeds ? 0 : 1 - p->xcur];
+  a.rin = p->reach[p->rcur];
+  a.rout = p->reach[1 - p->rcur];
+  a.cand_count = p->cand_count;
+  a.cand_list = p->cand_list;
+  a.V = (uint32_t)s->V;
+  a.nchunks = p->nchunks;
+  a.B = p->B;
+  a.exclude_label = exclude_label;
+  const dim3 grid(p->nchunks * p->ntiles);
+  switch (p->TW) {
+    case 128: launch_hop_g<32>(a, grid, st, seeds, reach, cand); break;
+    case 64: launch_hop_g<16>(a, grid, st, seeds, reach, cand); break;
+    case 16: launch_hop_g<4>(a, grid, st, seeds, false, false); break;
+    default: launch_hop_g<1>(a, grid, st, seeds, false, false); break;
+  }
+  EGR_CHECK_LAUNCH();
+  p->xcur = seeds ? 0 : 1 - p->xcur;
+  ++p->hops_done;
+  if (reach || cand) {
+    p->rcur = 1 - p->rcur;
+    ++p->reach_hops;
+  }
+  p->cand_valid = cand;
+  p->cand_exclude = exclude_label;
+  return EGR_OK;
+}
 
 }  // namespace
 
@@ -533,15 +815,16 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   auto* p = new egr_plan();
   p->s = s;
   p->B = n_cols;
-  p->TW = n_cols >= 64 ? 64 : (n_cols >= 16 ? 16 : 4);
+  p->TW = choose_tile_width(n_cols);
   p->Bpad = (n_cols + p->TW - 1) / p->TW * p->TW;
   p->ntiles = p->Bpad / p->TW;
   p->W = (n_cols + 63) / 64;
+  p->Wa = std::max(p->W, p->Bpad / 64);
   p->k = k;
   p->max_seeds = max_seeds;
   const uint32_t V = (uint32_t)s->V;
-  const uint32_t rows_per_block = 256 / (p->TW / 4);
-  p->nrb8_hop = ((V + rows_per_block - 1) / rows_per_block + 7) / 8 * 8;
+  const uint32_t rows = hop_rows(p->TW);
+  p->nchunks = (V + rows - 1) / rows;
   p->nrb8_reach = ((V + 255) / 256 + 7) / 8 * 8;
   p->n_chunks = (int)((V + TOPK_CHUNK - 1) / TOPK_CHUNK);
   const uint64_t keyspace = (uint64_t)V * p->Bpad;
@@ -550,14 +833,18 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
   int rc = EGR_OK;
   const size_t xs = (size_t)V * p->Bpad;
-  const size_t parts = (size_t)p->ntiles * p->n_chunks * 64 * KMAX;
+  const size_t parts = (size_t)p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks * 64 * KMAX;
+  const bool fused = p->TW >= 64;
   if ((rc = dalloc(&p->x[0], xs)) || (rc = dalloc(&p->x[1], xs)) ||
-      (rc = dalloc(&p->reach[0], (size_t)p->W * V)) || (rc = dalloc(&p->reach[1], (size_t)p->W * V)) ||
+      (rc = dalloc(&p->reach[0], (size_t)p->Wa * V)) || (rc = dalloc(&p->reach[1], (size_t)p->Wa * V)) ||
       (rc = dalloc(&p->skeys_in, ms)) || (rc = dalloc(&p->skeys, ms)) || (rc = dalloc(&p->ukeys, ms)) ||
       (rc = dalloc(&p->svals_in, ms)) || (rc = dalloc(&p->svals, ms)) || (rc = dalloc(&p->uval, ms)) ||
       (rc = dalloc(&p->head, ms)) || (rc = dalloc(&p->pos, ms)) || (rc = dalloc(&p->ucol, ms)) ||
       (rc = dalloc(&p->seed_ptr, (size_t)V + 1)) || (rc = dalloc(&p->n_unique, 1)) ||
+      (rc = dalloc(&p->seed_tiles, (size_t)V)) ||
       (rc = dalloc(&p->part_s, parts)) || (rc = dalloc(&p->part_v, parts)) ||
+      (rc = dalloc(&p->cand_count, (size_t)p->Bpad)) ||
+      (rc = dalloc(&p->cand_list, fused ? (size_t)V * p->B : 1)) ||
       (rc = dalloc(&p->counter, 1))) {
     egr_plan_free(p);
     return rc;
@@ -581,8 +868,7 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
 void egr_plan_free(egr_plan* p) {
   if (!p) return;
   DeviceGuard guard(p->s->device);
-  dfree(p->x[0]);
-  dfree(p->x[1]);
+  for (auto* q : {&p->x[0], &p->x[1]}) dfree(*q);
   dfree(p->reach[0]);
   dfree(p->reach[1]);
   dfree(p->skeys_in);
@@ -596,8 +882,11 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->ucol);
   dfree(p->seed_ptr);
   dfree(p->n_unique);
+  dfree(p->seed_tiles);
   dfree(p->part_s);
   dfree(p->part_v);
+  dfree(p->cand_count);
+  dfree(p->cand_list);
   dfree(p->counter);
   if (p->cub_tmp) (void)hipFree(p->cub_tmp);
   delete p;
@@ -614,6 +903,8 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
   const uint32_t V = (uint32_t)p->s->V;
   p->hops_done = 0;
   p->xcur = 0;
+  p->cand_valid = false;
+  EGR_HIP(hipMemsetAsync(p->seed_tiles, 0, (size_t)V * 4, st));
   if (n_seeds == 0) {
     hipLaunchKernelGGL(zero_seed_ptr_kernel, dim3((V + 256) / 256), dim3(256), 0, st, p->seed_ptr, V);
     EGR_CHECK_LAUNCH();
@@ -625,9 +916,9 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
                      (int64_t)n, V, p->B, (uint32_t)p->Bpad, p->skeys_in, p->svals_in);
   EGR_CHECK_LAUNCH();
   size_t tb = p->cub_tmp_bytes;
+  // invalid keys (~0) sort last: their low end_bit bits are all ones, above every valid key
   EGR_HIP(hipcub::DeviceRadixSort::SortPairs(p->cub_tmp, tb, p->skeys_in, p->skeys, p->svals_in,
                                              p->svals, n, 0, p->end_bit, st));
-  // invalid keys (~0) sort last only if their low end_bit bits are all ones, which they are
   hipLaunchKernelGGL(seed_head_kernel, g1, dim3(256), 0, st, p->skeys, (int64_t)n, p->head);
   EGR_CHECK_LAUNCH();
   tb = p->cub_tmp_bytes;
@@ -639,6 +930,9 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
   hipLaunchKernelGGL(seed_ptr_kernel, dim3((V + 256) / 256), dim3(256), 0, st, p->ukeys,
                      p->n_unique, V, (uint32_t)p->Bpad, p->seed_ptr);
   EGR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(seed_tiles_kernel, g1, dim3(256), 0, st, p->ukeys, p->n_unique,
+                     (uint32_t)p->Bpad, (uint32_t)p->TW, p->seed_tiles);
+  EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
 
@@ -648,7 +942,8 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
   hipStream_t st = (hipStream_t)stream;
   const uint32_t V = (uint32_t)p->s->V;
   p->rcur = 0;
-  EGR_HIP(hipMemsetAsync(p->reach[0], 0, (size_t)p->W * V * 8, st));
+  p->cand_valid = false;
+  EGR_HIP(hipMemsetAsync(p->reach[0], 0, (size_t)p->Wa * V * 8, st));
   hipLaunchKernelGGL(reach_sources_kernel, dim3((p->B + 255) / 256), dim3(256), 0, st,
                      source_vertex, p->B, p->reach[0], V);
   EGR_CHECK_LAUNCH();
@@ -657,39 +952,7 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
   return EGR_OK;
 }
 
-int egr_plan_hop(egr_plan* p, void* stream) {
-  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_hop: NULL plan");
-  if (p->hops_done < 0) return egr::fail(EGR_ESTATE, "egr_plan_hop: seeds not set");
-  DeviceGuard guard(p->s->device);
-  hipStream_t st = (hipStream_t)stream;
-  const egr_snapshot* s = p->s;
-  const uint32_t V = (uint32_t)s->V;
-  const dim3 grid(p->nrb8_hop * p->ntiles), block(256);
-  float* xo = p->x[p->hops_done == 0 ? 0 : 1 - p->xcur];
-  if (p->hops_done == 0) {
-#define LAUNCH_SEED_HOP(G)                                                                   \
-  hipLaunchKernelGGL(hop_from_seeds_kernel<G>, grid, block, 0, st, s->row_ptr, s->col, s->val, \
-                     p->seed_ptr, p->ucol, p->uval, xo, V, p->nrb8_hop)
-    if (p->TW == 64) LAUNCH_SEED_HOP(16);
-    else if (p->TW == 16) LAUNCH_SEED_HOP(4);
-    else LAUNCH_SEED_HOP(1);
-#undef LAUNCH_SEED_HOP
-    p->xcur = 0;
-  } else {
-    const float* xi = p->x[p->xcur];
-#define LAUNCH_HOP(G)                                                                          \
-  hipLaunchKernelGGL(hop_kernel<G>, grid, block, 0, st, s->row_ptr, s->col, s->val, p->seed_ptr, \
-                     p->ucol, p->uval, xi, xo, V, p->nrb8_hop)
-    if (p->TW == 64) LAUNCH_HOP(16);
-    else if (p->TW == 16) LAUNCH_HOP(4);
-    else LAUNCH_HOP(1);
-#undef LAUNCH_HOP
-    p->xcur = 1 - p->xcur;
-  }
-  EGR_CHECK_LAUNCH();
-  ++p->hops_done;
-  return EGR_OK;
-}
+int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream, false, false, -1); }
 
 int egr_plan_reach_hop(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_reach_hop: NULL plan");
@@ -702,7 +965,23 @@ int egr_plan_reach_hop(egr_plan* p, void* stream) {
   EGR_CHECK_LAUNCH();
   p->rcur = 1 - p->rcur;
   ++p->reach_hops;
+  p->cand_valid = false;
   return EGR_OK;
+}
+
+int egr_plan_step(egr_plan* p, void* stream) {
+  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_step: NULL plan");
+  if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_step: sources not set");
+  if (p->TW >= 64) return plan_hop(p, stream, true, false, -1);
+  EGR_TRY(plan_hop(p, stream, false, false, -1));
+  return egr_plan_reach_hop(p, stream);
+}
+
+int egr_plan_final_step(egr_plan* p, int32_t exclude_label, void* stream) {
+  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_final_step: NULL plan");
+  if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_final_step: sources not set");
+  if (p->TW >= 64) return plan_hop(p, stream, true, true, exclude_label);
+  return egr_plan_step(p, stream);
 }
 
 int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* out_scores,
@@ -713,7 +992,13 @@ int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* 
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const uint32_t V = (uint32_t)p->s->V;
-  const int waves = p->ntiles * p->n_chunks;
+  if (p->cand_valid && p->cand_exclude == exclude_label) {
+    hipLaunchKernelGGL(topk_cand_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->x[p->xcur],
+                       p->cand_count, p->cand_list, V, p->TW, p->B, p->k, out_ids, out_scores);
+    EGR_CHECK_LAUNCH();
+    return EGR_OK;
+  }
+  const int waves = p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks;
   hipLaunchKernelGGL(topk_partial_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
                      p->x[p->xcur], p->reach[p->rcur], p->s->vlabel, exclude_label, V, p->TW,
                      p->B, p->n_chunks, p->part_s, p->part_v);
@@ -729,10 +1014,8 @@ int egr_plan_run(egr_plan* p, int32_t hops, int32_t exclude_label, uint32_t* out
   if (!p || hops < 1) return egr::fail(EGR_EINVAL, "egr_plan_run: need hops >= 1");
   if (p->hops_done != 0 || p->reach_hops != 0)
     return egr::fail(EGR_ESTATE, "egr_plan_run: set seeds and sources first");
-  for (int h = 0; h < hops; ++h) {
-    EGR_TRY(egr_plan_hop(p, stream));
-    EGR_TRY(egr_plan_reach_hop(p, stream));
-  }
+  for (int h = 0; h + 1 < hops; ++h) EGR_TRY(egr_plan_step(p, stream));
+  EGR_TRY(egr_plan_final_step(p, exclude_label, stream));
   return egr_plan_topk(p, exclude_label, out_ids, out_scores, stream);
 }
 

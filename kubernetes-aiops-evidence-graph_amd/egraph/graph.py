@@ -274,6 +274,15 @@ class Plan:
     def hop(self, stream=None):
         L.check(L.lib.egr_plan_hop(self._h, self._st(stream)), "egr_plan_hop")
 
+    def step(self, stream=None):
+        """One hop of propagation and reachability (one fused pass when TW == 64)."""
+        L.check(L.lib.egr_plan_step(self._h, self._st(stream)), "egr_plan_step")
+
+    def final_step(self, exclude_label: int = -1, stream=None):
+        """The last hop: step() plus the top-k candidate lists for topk(exclude_label)."""
+        L.check(L.lib.egr_plan_final_step(self._h, exclude_label, self._st(stream)),
+                "egr_plan_final_step")
+
     def reach_hop(self, stream=None):
         L.check(L.lib.egr_plan_reach_hop(self._h, self._st(stream)), "egr_plan_reach_hop")
 

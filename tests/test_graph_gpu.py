@@ -62,6 +62,81 @@ def test_propagation_reach_topk_equal_oracle(B):
     np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
 
 
+@pytest.mark.parametrize("tw", [4, 16, 64, 128])
+def test_tile_width_override(tw, monkeypatch):
+    B = 200
+    monkeypatch.setenv("EGRAPH_TILE_WIDTH", str(tw))
+    g, sv, sc, ss, src = _small_world(B, seed=31, pods=1500)
+    plan = g.snapshot().plan(B, max_seeds=len(sv), k=6)
+    assert plan.tile_width == tw
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    inc = g.labels().index("Incident")
+    ids, scores = plan.run(hops=3, exclude_label=inc)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    np.testing.assert_array_equal(plan.read_reach().cpu().numpy().view(np.uint64), er)
+    vl, _, _, _ = g.export()
+    eids, esc = oracle.topk(exp, er, vl, inc, 6)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), eids)
+    np.testing.assert_array_equal(scores.cpu().numpy(), esc)
+    # the full-scan top-k path (no candidate lists) must agree too
+    ids2, sc2 = plan.topk(exclude_label=-1)
+    eids2, esc2 = oracle.topk(exp, er, vl, -1, 6)
+    np.testing.assert_array_equal(ids2.cpu().numpy().view(np.uint32), eids2)
+    np.testing.assert_array_equal(sc2.cpu().numpy(), esc2)
+
+
+@pytest.mark.parametrize("B", [64, 128])
+def test_unfused_and_fused_steps_agree(B):
+    g, sv, sc, ss, src = _small_world(B, seed=21, pods=2000)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    exp_r = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    snap = g.snapshot()
+    for fused in (False, True):
+        plan = snap.plan(B, max_seeds=len(sv), k=4)
+        plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+        plan.set_sources(_dev(src))
+        for _ in range(3):
+            if fused:
+                plan.step()
+            else:
+                plan.hop()
+                plan.reach_hop()
+        assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+        np.testing.assert_array_equal(plan.read_reach().cpu().numpy().view(np.uint64), exp_r)
+
+
+def test_hub_rows_longer_than_the_lds_stage():
+    """A vertex whose CSR row exceeds the 2048 staged entries takes the global-read path."""
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    n = 5000
+    g.merge_nodes([f"p{i}" for i in range(n)] + ["hub", "inc"], ["Pod"] * n + ["Node", "Incident"])
+    g.merge_edges([f"p{i}" for i in range(n)] + ["inc"], ["hub"] * n + ["p0"],
+                  ["SCHEDULED_ON"] * n + ["AFFECTS"])
+    B = 64
+    rng = np.random.default_rng(0)
+    sv = rng.integers(0, n, 3000).astype(np.uint32)
+    sc = rng.integers(0, B, 3000).astype(np.uint32)
+    ss = rng.random(3000).astype(np.float32)
+    src = np.full(B, n + 1, np.uint32)
+    plan = g.snapshot().plan(B, max_seeds=len(sv), k=8)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    ids, _ = plan.run(hops=3)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    vl, _, _, _ = g.export()
+    eids, _ = oracle.topk(exp, er, vl, -1, 8)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), eids)
+
+
 @pytest.mark.parametrize("hops", [1, 2, 4])
 def test_hop_counts(hops):
     B = 20
