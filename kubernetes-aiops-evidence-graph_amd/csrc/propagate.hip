@@ -23,6 +23,7 @@
 struct egr_snapshot {
   int device = 0;
   int64_t V = 0, NE = 0;
+  std::vector<uint32_t> row_ptr_host;   // for the per-plan chunk tables
   uint32_t* row_ptr = nullptr;
   uint32_t* col = nullptr;
   uint8_t* meta = nullptr;
@@ -107,42 +108,43 @@ __device__ __forceinline__ void add_seeds(float4& acc, uint32_t v, uint32_t lo,
 }
 
 // ---- propagation hop ---------------------------------------------------------------------
-// One block = ROWS consecutive rows of one column tile.  The block stages its rows' row_ptr,
-// own seed-tile masks, labels and CSR segment (col, val) in LDS with coalesced loads.  Each
-// lane group (G lanes x float4 = the row's TW columns) then walks its rows with a two-row
-// software pipeline: the next row's first NB neighbour gathers (and reach words) are in flight
-// while the current row runs its fmaf chain in CSR order (bit-exact with the oracle).
+// One block = one row chunk of one column tile.  Chunks come from a per-plan table built so
+// that a chunk's CSR segment fits the LDS stage (CSR_CAP entries; only a lone row longer than
+// that spills, into the cold tail loop).  The block stages row_ptr and (col, val) in LDS with
+// all loads issued before the first wait, then every lane group (G lanes x float4 = the row's
+// TW columns) walks its rows with a two-buffer software pipeline: the next row's NB gathers
+// (and reach words) are in flight while the current row runs its fmaf chain in CSR order.
+// The hot loop is branch-free: a row with fewer than NB entries fills the batch with its own
+// last neighbour at weight 0 (fmaf(0, x, acc) == acc exactly: acc is never -0.0), so the
+// compiler's vmcnt accounting keeps the next row's loads in flight.
 //   FROM_SEEDS (h = 0 -> 1): neighbour values come from the sparse seed lists, filtered by a
 //              per-vertex seed-tile mask, so s0 is never materialised densely;
-//   REACH      (TW >= 64): the same walk ORs the neighbours' reach words (one pass per hop);
-//   CAND       (last hop): reached, non-excluded (vertex, column) pairs are appended to the
-//              column's candidate list for the top-k merge, so top-k never rescans the scores.
+//   REACH      (TW >= 64): the same walk ORs the neighbours' reach words (one pass per hop).
+// The own-row seed term s0_v is added afterwards by seed_add_kernel (out = acc + s0, the same
+// single rounding as the oracle).
+constexpr uint32_t CSR_CAP = 2048;
+constexpr int NB = 4;
+
 template <int G>
 struct HopGeo {
-  static constexpr int ROWS = G == 1 ? 256 : 128;
+  static constexpr int ROWS = G == 1 ? 256 : 128;   // max rows per chunk
 };
-constexpr uint32_t CSR_CAP = 2048;   // staged entries per block (longer segments read global)
-constexpr int NB = 4;                // neighbour gathers per batch
 
 struct HopArgs {
   const uint32_t* row_ptr;
   const uint32_t* col;
   const float* val;
+  const uint32_t* chunk_start;
   const uint32_t* seed_ptr;
   const uint32_t* seed_col;
   const float* seed_val;
   const uint32_t* seed_tiles;
-  const uint8_t* vlabel;
   const float* xin;
   float* xout;
   const uint64_t* rin;
   uint64_t* rout;
-  uint32_t* cand_count;
-  uint32_t* cand_list;
   uint32_t V;
   uint32_t nchunks;
-  int32_t B;
-  int32_t exclude_label;
 };
 
 template <bool SEEDS, bool REACH>
@@ -152,135 +154,206 @@ struct Batch {
   uint32_t m[NB];
   uint32_t u[NB];
   float w[NB];
+  uint64_t own;
   uint32_t n;
 };
 
-template <int G, bool FROM_SEEDS, bool REACH, bool CAND>
+template <int G, bool FROM_SEEDS, bool REACH>
 __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
+  constexpr int PER = CSR_CAP / 256;
   __shared__ uint32_t s_rp[ROWS + 1];
-  __shared__ uint32_t s_mask[ROWS];
-  __shared__ uint8_t s_lab[ROWS];
   __shared__ uint32_t s_col[CSR_CAP];
   __shared__ float s_val[CSR_CAP];
   const uint32_t tid = threadIdx.x, gl = tid % G, grp = tid / G;
   const uint32_t V = A.V;
-  const uint32_t tile = blockIdx.x / A.nchunks;
-  const uint32_t v0 = (blockIdx.x % A.nchunks) * ROWS;
-  if (v0 >= V) return;  // block-uniform, before any barrier
-  const uint32_t nrows = min((uint32_t)ROWS, V - v0);
-  for (uint32_t i = tid; i <= nrows; i += 256) s_rp[i] = A.row_ptr[v0 + i];
-  for (uint32_t i = tid; i < nrows; i += 256) {
-    s_mask[i] = A.seed_tiles[v0 + i];
-    if constexpr (CAND) s_lab[i] = A.vlabel[v0 + i];
+  const uint32_t tile = blockIdx.x / A.nchunks, chunk = blockIdx.x % A.nchunks;
+  const uint32_t v0 = A.chunk_start[chunk], v1 = A.chunk_start[chunk + 1];
+  const uint32_t nrows = v1 - v0;
+  const uint32_t e0 = A.row_ptr[v0], e1 = A.row_ptr[v1];
+  const uint32_t nst = min(e1 - e0, CSR_CAP);
+  uint32_t rp_t = 0;
+  if (tid < nrows) rp_t = A.row_ptr[v0 + tid];
+  uint32_t cc[PER];
+  float ww[PER];
+  if (nst > 0) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = min(tid + k * 256u, nst - 1u);
+      cc[k] = A.col[e0 + i];
+      ww[k] = A.val[e0 + i];
+    }
+  }
+  if (tid < nrows) s_rp[tid] = rp_t - e0;   // entries relative to the chunk
+  if (tid == 0) s_rp[nrows] = e1 - e0;       // nrows may equal the block size (G = 1)
+  if (nst > 0) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = tid + k * 256u;
+      if (i < nst) {
+        s_col[i] = cc[k];
+        s_val[i] = ww[k];
+      }
+    }
   }
   __syncthreads();
-  const uint32_t e0 = s_rp[0];
-  const uint32_t nst = min(s_rp[nrows] - e0, CSR_CAP);
-  for (uint32_t i = tid; i < nst; i += 256) {
-    s_col[i] = A.col[e0 + i];
-    s_val[i] = A.val[e0 + i];
-  }
-  __syncthreads();
-  uint32_t r = grp;
-  if (r >= nrows) return;  // no barrier below
+  if (grp >= nrows) return;  // no barrier below
 
   const uint32_t lo = tile * TW + 4 * gl;  // first column of this lane
   const uint32_t tbit = tile & 31u;
   const size_t toff = (size_t)tile * V * TW;
   const float4* __restrict__ X = reinterpret_cast<const float4*>(A.xin + toff);
+  float4* __restrict__ Y = reinterpret_cast<float4*>(A.xout + toff);
   const uint32_t word = lo >> 6;
   const uint64_t* __restrict__ R = A.rin + (size_t)word * V;
 
-  auto issue = [&](uint32_t ja, uint32_t jb, Batch<FROM_SEEDS, REACH>& bt) {
-    bt.n = jb > ja ? min(jb - ja, (uint32_t)NB) : 0u;
+  // NB entries of row r; slots past the row's end repeat its last neighbour at weight 0
+  auto issue = [&](uint32_t r, Batch<FROM_SEEDS, REACH>& bt) {
+    const uint32_t a = s_rp[r], b = s_rp[r + 1];
+    const uint32_t n = b - a;
+    bt.n = n;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-      const uint32_t jj = ja + t;
-      const bool ok = (uint32_t)t < bt.n;
-      uint32_t u = 0u;
-      float w = 0.f;
-      if (ok) {
-        u = jj < CSR_CAP ? s_col[jj] : A.col[e0 + jj];
-        w = jj < CSR_CAP ? s_val[jj] : A.val[e0 + jj];
-      }
+      const uint32_t jj = a + min((uint32_t)t, n > 0u ? n - 1u : 0u);
+      const uint32_t u = n > 0u ? s_col[min(jj, CSR_CAP - 1u)] : v0 + r;
       bt.u[t] = u;
-      bt.w[t] = w;
-      if constexpr (FROM_SEEDS) {
-        bt.m[t] = ok ? A.seed_tiles[u] : 0u;
-      } else {
-        bt.x[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok) bt.x[t] = X[(size_t)u * G + gl];
-      }
-      if constexpr (REACH) bt.rw[t] = ok ? R[u] : 0ull;
+      bt.w[t] = (uint32_t)t < n ? s_val[min(jj, CSR_CAP - 1u)] : 0.f;
+      if constexpr (FROM_SEEDS) bt.m[t] = A.seed_tiles[u];
+      else bt.x[t] = X[(size_t)u * G + gl];
+      if constexpr (REACH) bt.rw[t] = R[u];
+    }
+    if constexpr (REACH) bt.own = R[v0 + r];
+  };
+  auto seed_gather = [&](uint32_t u, float w, float4& acc) {
+    const uint32_t s1 = A.seed_ptr[u + 1];
+    for (uint32_t q = seed_lower(A.seed_col, A.seed_ptr[u], s1, lo); q < s1; ++q) {
+      const uint32_t c = A.seed_col[q] - lo;
+      if (c >= 4u) break;
+      fma_comp(acc, (int)c, w, A.seed_val[q]);
     }
   };
-  auto consume = [&](const Batch<FROM_SEEDS, REACH>& bt, float4& acc, uint64_t& rr) {
-#pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      if ((uint32_t)t < bt.n) {
-        if constexpr (FROM_SEEDS) {
-          if ((bt.m[t] >> tbit) & 1u) {  // w * 0 otherwise: skipping the fmaf is exact
-            const uint32_t u = bt.u[t];
-            const uint32_t s1 = A.seed_ptr[u + 1];
-            for (uint32_t q = seed_lower(A.seed_col, A.seed_ptr[u], s1, lo); q < s1; ++q) {
-              const uint32_t c = A.seed_col[q] - lo;
-              if (c >= 4u) break;
-              fma_comp(acc, (int)c, bt.w[t], A.seed_val[q]);
-            }
-          }
-        } else {
-          fma4(bt.w[t], bt.x[t], acc);
-        }
-        if constexpr (REACH) rr |= bt.rw[t];
-      }
-    }
-  };
-
-  Batch<FROM_SEEDS, REACH> cur, nxt;
-  issue(s_rp[r] - e0, s_rp[r + 1] - e0, cur);
-  uint64_t own = 0;
-  if constexpr (REACH) own = R[v0 + r];
-  while (true) {
-    const uint32_t rn = r + GROUPS;
-    const bool more = rn < nrows;
-    uint64_t own_n = 0;
-    if (more) {
-      issue(s_rp[rn] - e0, s_rp[rn + 1] - e0, nxt);
-      if constexpr (REACH) own_n = R[v0 + rn];
-    }
+  auto process = [&](uint32_t r, const Batch<FROM_SEEDS, REACH>& bt) {
     const uint32_t v = v0 + r;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint64_t rr = own;
-    consume(cur, acc, rr);
-    const uint32_t b = s_rp[r + 1] - e0;
-    for (uint32_t j = s_rp[r] - e0 + NB; j < b; j += NB) {  // rows longer than NB
-      Batch<FROM_SEEDS, REACH> tail;
-      issue(j, b, tail);
-      consume(tail, acc, rr);
+    uint64_t rr = 0;
+    if constexpr (REACH) rr = bt.own;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      if constexpr (FROM_SEEDS) {
+        // w * 0 unless the neighbour has a seed in this tile: skipping the fmaf is exact
+        if ((uint32_t)t < bt.n && ((bt.m[t] >> tbit) & 1u)) seed_gather(bt.u[t], bt.w[t], acc);
+      } else {
+        fma4(bt.w[t], bt.x[t], acc);
+      }
+      if constexpr (REACH) rr |= bt.rw[t];
     }
-    if ((s_mask[r] >> tbit) & 1u) add_seeds(acc, v, lo, A.seed_ptr, A.seed_col, A.seed_val);
-    reinterpret_cast<float4*>(A.xout + toff)[(size_t)v * G + gl] = acc;
+    // tail of rows with more than NB entries, NT gathers per batch (deployments, services,
+    // Node hubs); slots past the end repeat the last entry at weight 0
+    constexpr int NT = 4;
+    const uint32_t b = s_rp[r + 1];
+    for (uint32_t j = s_rp[r] + NB; j < b; j += NT) {
+      uint32_t u[NT];
+      float w[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const uint32_t jj = min(j + t, b - 1u);
+        u[t] = jj < CSR_CAP ? s_col[jj] : A.col[e0 + jj];
+        w[t] = j + t < b ? (jj < CSR_CAP ? s_val[jj] : A.val[e0 + jj]) : 0.f;
+      }
+      if constexpr (FROM_SEEDS) {
+        uint32_t m[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) m[t] = A.seed_tiles[u[t]];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (j + t < b && ((m[t] >> tbit) & 1u)) seed_gather(u[t], w[t], acc);
+      } else {
+        float4 x[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) x[t] = X[(size_t)u[t] * G + gl];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) fma4(w[t], x[t], acc);
+      }
+      if constexpr (REACH) {
+        uint64_t rw[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) rw[t] = R[u[t]];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) rr |= rw[t];
+      }
+    }
+    Y[(size_t)v * G + gl] = acc;
     if constexpr (REACH) {
       if ((lo & 63u) == 0u) A.rout[(size_t)word * V + v] = rr;
     }
-    if constexpr (CAND) {
-      const uint32_t bits = (uint32_t)(rr >> (lo & 63u)) & 0xFu;
-      if (bits && !(A.exclude_label >= 0 && s_lab[r] == (uint8_t)A.exclude_label)) {
+  };
+
+  Batch<FROM_SEEDS, REACH> ba, bb;
+  uint32_t r = grp;
+  issue(r, ba);
+  while (true) {
+    const uint32_t r1 = r + GROUPS;
+    issue(r1 < nrows ? r1 : r, bb);           // unconditional: keeps vmcnt exact
+    process(r, ba);
+    if (r1 >= nrows) break;
+    const uint32_t r2 = r1 + GROUPS;
+    issue(r2 < nrows ? r2 : r1, ba);
+    process(r1, bb);
+    if (r2 >= nrows) break;
+    r = r2;
+  }
+}
+
+// out[v, b] = acc + s0[v, b] for every unique seed (after the hop wrote acc)
+__global__ void seed_add_kernel(const uint64_t* __restrict__ ukeys,
+                                const float* __restrict__ uval,
+                                const uint32_t* __restrict__ n_unique, uint32_t Bpad,
+                                uint32_t TW, uint32_t V, float* __restrict__ X) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_unique) return;
+  const uint64_t k = ukeys[i];
+  const uint32_t v = (uint32_t)(k / Bpad), b = (uint32_t)(k % Bpad);
+  float* p = X + ((size_t)(b / TW) * V + v) * TW + (b % TW);
+  *p = *p + uval[i];
+}
+
+// Top-k candidates of the final reach words.  A wave owns 64 rows (lane = row) of one word:
+// ballots give every column's count (lane c keeps column c's), ONE atomicAdd instruction
+// reserves all 64 columns' slots at once, then the rows write their ids.  Only columns present
+// in the wave are visited.  Order inside a list is irrelevant: the merge applies the strict
+// (score desc, id asc) order.
+__global__ __launch_bounds__(256) void cand_extract_kernel(
+    const uint64_t* __restrict__ R, const uint8_t* __restrict__ vlabel, int exclude_label,
+    uint32_t V, int B, uint32_t nrb, uint32_t* __restrict__ cand_count,
+    uint32_t* __restrict__ cand_list) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t w = wave / nrb;
+  const uint32_t v = (wave % nrb) * 64 + lane;
+  if (w * 64 >= (uint32_t)B) return;
+  uint64_t word = 0;
+  if (v < V && !(exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label)) word = R[(size_t)w * V + v];
+  const int cmax = min(64, B - (int)w * 64);
+  if (cmax < 64) word &= (1ull << cmax) - 1ull;
+  uint64_t cols = word;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t bcol = lo + i;
-          if (((bits >> i) & 1u) && bcol < (uint32_t)A.B) {
-            const uint32_t slot = atomicAdd(&A.cand_count[bcol], 1u);
-            A.cand_list[(size_t)bcol * V + slot] = v;
-          }
-        }
-      }
-    }
-    if (!more) break;
-    cur = nxt;
-    own = own_n;
-    r = rn;
+  for (int off = 32; off > 0; off >>= 1) cols |= __shfl_xor(cols, off, 64);
+  if (!cols) return;
+  uint32_t mycnt = 0;
+  for (uint64_t m = cols; m; m &= m - 1) {
+    const int c = __ffsll((long long)m) - 1;
+    const uint32_t n = (uint32_t)__popcll(__ballot((word >> c) & 1ull));
+    if (lane == c) mycnt = n;
+  }
+  uint32_t mybase = 0;
+  if (mycnt) mybase = atomicAdd(&cand_count[w * 64 + lane], mycnt);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint64_t m = cols; m; m &= m - 1) {
+    const int c = __ffsll((long long)m) - 1;
+    const uint64_t bits = __ballot((word >> c) & 1ull);
+    const uint32_t base = __shfl(mybase, c, 64);
+    if ((word >> c) & 1ull)
+      cand_list[(size_t)(w * 64 + c) * V + base + __popcll(bits & lt)] = v;
   }
 }
 
@@ -600,6 +673,7 @@ struct egr_plan {
   int64_t max_seeds = 0;
   int n_chunks = 0;          // top-k full-scan chunks
   uint32_t nchunks = 0;      // hop row chunks per tile
+  uint32_t* chunk_start = nullptr;
   uint32_t nrb8_reach = 0;
   float* x[2] = {nullptr, nullptr};
   int xcur = 0;
@@ -672,76 +746,91 @@ uint32_t hop_rows(int TW) {
   }
 }
 
-template <int G, bool SEEDS, bool REACH, bool CAND>
+// Row chunks of at most max_rows rows whose CSR segment fits CSR_CAP entries; a row longer
+// than CSR_CAP forms a chunk of its own (its excess is read by the kernel's tail loop).
+std::vector<uint32_t> build_chunks(const std::vector<uint32_t>& rp, uint32_t V, uint32_t max_rows) {
+  std::vector<uint32_t> cs{0};
+  uint32_t v = 0;
+  while (v < V) {
+    const uint32_t start = v;
+    uint32_t ents = 0;
+    while (v < V && v - start < max_rows) {
+      const uint32_t d = rp[v + 1] - rp[v];
+      if (v > start && ents + d > CSR_CAP) break;
+      ents += d;
+      ++v;
+    }
+    cs.push_back(v);
+  }
+  return cs;
+}
+
+template <int G, bool SEEDS, bool REACH>
 void launch_hop_t(const HopArgs& a, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((hop_kernel<G, SEEDS, REACH, CAND>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((hop_kernel<G, SEEDS, REACH>), grid, dim3(256), 0, st, a);
 }
 
 template <int G>
-void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool reach, bool cand) {
+void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool reach) {
   if constexpr (G >= 16) {
     if (seeds) {
-      if (cand) launch_hop_t<G, true, true, true>(a, grid, st);
-      else if (reach) launch_hop_t<G, true, true, false>(a, grid, st);
-      else launch_hop_t<G, true, false, false>(a, grid, st);
+      if (reach) launch_hop_t<G, true, true>(a, grid, st);
+      else launch_hop_t<G, true, false>(a, grid, st);
     } else {
-      if (cand) launch_hop_t<G, false, true, true>(a, grid, st);
-      else if (reach) launch_hop_t<G, false, true, false>(a, grid, st);
-      else launch_hop_t<G, false, false, false>(a, grid, st);
+      if (reach) launch_hop_t<G, false, true>(a, grid, st);
+      else launch_hop_t<G, false, false>(a, grid, st);
     }
   } else {
-    if (seeds) launch_hop_t<G, true, false, false>(a, grid, st);
-    else launch_hop_t<G, false, false, false>(a, grid, st);
+    if (seeds) launch_hop_t<G, true, false>(a, grid, st);
+    else launch_hop_t<G, false, false>(a, grid, st);
   }
 }
 
-// One propagation hop.  reach: also one reachability hop in the same pass (TW >= 64);
-// cand: also append the top-k candidates of this (last) hop.
-int plan_hop(egr_plan* p, void* stream, bool reach, bool cand, int exclude_label) {
+// One propagation hop (+ its own-row seed add); with `reach` (TW >= 64) also one
+// reachability hop in the same pass.
+int plan_hop(egr_plan* p, void* stream, bool reach) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_hop: NULL plan");
   if (p->hops_done < 0) return egr::fail(EGR_ESTATE, "egr_plan_hop: seeds not set");
-  if ((reach || cand) && (p->TW < 64 || !p->sources_set))
+  if (reach && (p->TW < 64 || !p->sources_set))
     return egr::fail(EGR_ESTATE, "fused reach needs TW >= 64 and sources set");
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const egr_snapshot* s = p->s;
   const bool seeds = p->hops_done == 0;
-  if (cand) EGR_HIP(hipMemsetAsync(p->cand_count, 0, (size_t)p->Bpad * 4, st));
   HopArgs a;
   a.row_ptr = s->row_ptr;
   a.col = s->col;
   a.val = s->val;
+  a.chunk_start = p->chunk_start;
   a.seed_ptr = p->seed_ptr;
   a.seed_col = p->ucol;
   a.seed_val = p->uval;
   a.seed_tiles = p->seed_tiles;
-  a.vlabel = s->vlabel;
   a.xin = seeds ? nullptr : p->x[p->xcur];
   a.xout = p->x[seeds ? 0 : 1 - p->xcur];
   a.rin = p->reach[p->rcur];
   a.rout = p->reach[1 - p->rcur];
-  a.cand_count = p->cand_count;
-  a.cand_list = p->cand_list;
   a.V = (uint32_t)s->V;
   a.nchunks = p->nchunks;
-  a.B = p->B;
-  a.exclude_label = exclude_label;
   const dim3 grid(p->nchunks * p->ntiles);
   switch (p->TW) {
-    case 128: launch_hop_g<32>(a, grid, st, seeds, reach, cand); break;
-    case 64: launch_hop_g<16>(a, grid, st, seeds, reach, cand); break;
-    case 16: launch_hop_g<4>(a, grid, st, seeds, false, false); break;
-    default: launch_hop_g<1>(a, grid, st, seeds, false, false); break;
+    case 128: launch_hop_g<32>(a, grid, st, seeds, reach); break;
+    case 64: launch_hop_g<16>(a, grid, st, seeds, reach); break;
+    case 16: launch_hop_g<4>(a, grid, st, seeds, false); break;
+    default: launch_hop_g<1>(a, grid, st, seeds, false); break;
   }
+  EGR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
+                     dim3(256), 0, st, p->ukeys, p->uval, p->n_unique, (uint32_t)p->Bpad,
+                     (uint32_t)p->TW, (uint32_t)s->V, a.xout);
   EGR_CHECK_LAUNCH();
   p->xcur = seeds ? 0 : 1 - p->xcur;
   ++p->hops_done;
-  if (reach || cand) {
+  if (reach) {
     p->rcur = 1 - p->rcur;
     ++p->reach_hops;
   }
-  p->cand_valid = cand;
-  p->cand_exclude = exclude_label;
+  p->cand_valid = false;
   return EGR_OK;
 }
 
@@ -784,6 +873,7 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
     egr_snapshot_free(s);
     return egr::fail(EGR_EDEVICE, std::string("snapshot upload: ") + hipGetErrorString(e));
   }
+  s->row_ptr_host = std::move(row_ptr);
   *out = s;
   return EGR_OK;
 }
@@ -823,8 +913,8 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   p->k = k;
   p->max_seeds = max_seeds;
   const uint32_t V = (uint32_t)s->V;
-  const uint32_t rows = hop_rows(p->TW);
-  p->nchunks = (V + rows - 1) / rows;
+  const std::vector<uint32_t> chunks = build_chunks(s->row_ptr_host, V, hop_rows(p->TW));
+  p->nchunks = (uint32_t)chunks.size() - 1;
   p->nrb8_reach = ((V + 255) / 256 + 7) / 8 * 8;
   p->n_chunks = (int)((V + TOPK_CHUNK - 1) / TOPK_CHUNK);
   const uint64_t keyspace = (uint64_t)V * p->Bpad;
@@ -845,9 +935,13 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
       (rc = dalloc(&p->part_s, parts)) || (rc = dalloc(&p->part_v, parts)) ||
       (rc = dalloc(&p->cand_count, (size_t)p->Bpad)) ||
       (rc = dalloc(&p->cand_list, fused ? (size_t)V * p->B : 1)) ||
-      (rc = dalloc(&p->counter, 1))) {
+      (rc = dalloc(&p->counter, 1)) || (rc = dalloc(&p->chunk_start, chunks.size()))) {
     egr_plan_free(p);
     return rc;
+  }
+  if (hipMemcpy(p->chunk_start, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    egr_plan_free(p);
+    return egr::fail(EGR_EDEVICE, "chunk table upload failed");
   }
   size_t b1 = 0, b2 = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, b1, p->skeys_in, p->skeys, p->svals_in, p->svals,
@@ -888,6 +982,7 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->cand_count);
   dfree(p->cand_list);
   dfree(p->counter);
+  dfree(p->chunk_start);
   if (p->cub_tmp) (void)hipFree(p->cub_tmp);
   delete p;
 }
@@ -905,6 +1000,7 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
   p->xcur = 0;
   p->cand_valid = false;
   EGR_HIP(hipMemsetAsync(p->seed_tiles, 0, (size_t)V * 4, st));
+  EGR_HIP(hipMemsetAsync(p->n_unique, 0, 4, st));
   if (n_seeds == 0) {
     hipLaunchKernelGGL(zero_seed_ptr_kernel, dim3((V + 256) / 256), dim3(256), 0, st, p->seed_ptr, V);
     EGR_CHECK_LAUNCH();
@@ -952,7 +1048,7 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
   return EGR_OK;
 }
 
-int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream, false, false, -1); }
+int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream, false); }
 
 int egr_plan_reach_hop(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_reach_hop: NULL plan");
@@ -972,16 +1068,29 @@ int egr_plan_reach_hop(egr_plan* p, void* stream) {
 int egr_plan_step(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_step: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_step: sources not set");
-  if (p->TW >= 64) return plan_hop(p, stream, true, false, -1);
-  EGR_TRY(plan_hop(p, stream, false, false, -1));
+  if (p->TW >= 64) return plan_hop(p, stream, true);
+  EGR_TRY(plan_hop(p, stream, false));
   return egr_plan_reach_hop(p, stream);
 }
 
 int egr_plan_final_step(egr_plan* p, int32_t exclude_label, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_final_step: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_final_step: sources not set");
-  if (p->TW >= 64) return plan_hop(p, stream, true, true, exclude_label);
-  return egr_plan_step(p, stream);
+  EGR_TRY(egr_plan_step(p, stream));
+  if (p->TW < 64) return EGR_OK;   // no candidate lists: top-k scans the scores
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t V = (uint32_t)p->s->V;
+  const uint32_t nrb = (V + 63) / 64;
+  EGR_HIP(hipMemsetAsync(p->cand_count, 0, (size_t)p->Bpad * 4, st));
+  const uint32_t waves = nrb * (uint32_t)p->W;
+  hipLaunchKernelGGL(cand_extract_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
+                     p->reach[p->rcur], p->s->vlabel, exclude_label, V, p->B, nrb, p->cand_count,
+                     p->cand_list);
+  EGR_CHECK_LAUNCH();
+  p->cand_valid = true;
+  p->cand_exclude = exclude_label;
+  return EGR_OK;
 }
 
 int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* out_scores,
