@@ -68,6 +68,25 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device):
                 evidence=evidence)
 
 
+def step_unfused(ctx, hops: int, ev=None):
+    """A/B variant: propagation and reachability as separate passes over the CSR."""
+    plan = ctx["plan"]
+    ctx["rules"].launch()
+    plan.set_seeds(*ctx["seeds"])
+    plan.set_sources(ctx["sources"])
+    for h in range(hops):
+        if ev is not None and h > 0:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            plan.hop()
+            b.record()
+            ev.append((a, b))
+        else:
+            plan.hop()
+        plan.reach_hop()
+    plan.topk(ctx["inc_label"])
+
+
 def step(ctx, hops: int, ev=None):
     """One pass; `ev` (list) collects (start, end) events around the dense hop launches."""
     plan = ctx["plan"]
@@ -135,6 +154,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--unfused", action="store_true", help="A/B: reach as its own pass")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,8 +170,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     ctx = setup(args.config, args.batch, args.k, rank, dev)
+    run_step = step_unfused if args.unfused else step
     for _ in range(args.warmup):
-        step(ctx, args.hops)
+        run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
 
     events: list = []
@@ -160,7 +181,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(ctx, args.hops, events)
+        run_step(ctx, args.hops, events)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
