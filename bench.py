@@ -3,8 +3,8 @@
 One step = one pass of the hot path over one batch of B incidents whose inputs are already
 resident in HBM (encoded evidence rows, seed triples, incident vertices), on one stream:
   egr_rules_eval (A1-A6, fused ranker)  ->  egr_plan_set_seeds (radix sort + max-combine)
-  ->  egr_plan_set_sources  ->  2 x egr_plan_step (hop + reach, one fused pass each)
-  ->  egr_plan_final_step (3rd hop + top-k candidates)  ->  egr_plan_topk.
+  ->  egr_plan_set_sources  ->  3 x (egr_plan_hop + egr_plan_reach_hop)
+  ->  egr_plan_candidates (top-k candidate lists)  ->  egr_plan_topk.
 Workload: BASELINE.json configs[2] (C3: 100k pods / 100 namespaces / 2k nodes / 10k
 deployments / 10k services, Event/LogPattern/MetricAnomaly vertices; synthetic, seeded).
 Multi-GPU (torchrun): every rank holds the snapshot and ranks its own B incidents -- incidents
@@ -68,14 +68,14 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device):
                 evidence=evidence)
 
 
-def step_unfused(ctx, hops: int, ev=None):
-    """A/B variant: propagation and reachability as separate passes over the CSR."""
+def step(ctx, hops: int, ev=None):
+    """One pass; `ev` (list) collects (start, end) events around the dense hop launches."""
     plan = ctx["plan"]
     ctx["rules"].launch()
     plan.set_seeds(*ctx["seeds"])
     plan.set_sources(ctx["sources"])
     for h in range(hops):
-        if ev is not None and h > 0:
+        if ev is not None and h > 0:                      # dense (non-seed) hops are timed
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             plan.hop()
@@ -84,27 +84,8 @@ def step_unfused(ctx, hops: int, ev=None):
         else:
             plan.hop()
         plan.reach_hop()
-    plan.topk(ctx["inc_label"])
-
-
-def step(ctx, hops: int, ev=None):
-    """One pass; `ev` (list) collects (start, end) events around the dense hop launches."""
-    plan = ctx["plan"]
-    ctx["rules"].launch()
-    plan.set_seeds(*ctx["seeds"])
-    plan.set_sources(ctx["sources"])
-    # propagation + reach: one fused pass per hop; the last one also appends the top-k
-    # candidates, so top-k reads only the reached vertices
-    for h in range(hops - 1):
-        if ev is not None and h > 0:                      # dense (non-seed) hops are timed
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            plan.step()
-            b.record()
-            ev.append((a, b))
-        else:
-            plan.step()
-    plan.final_step(ctx["inc_label"])
+    # candidate lists from the final reach sets, so top-k reads only the reached vertices
+    plan.candidates(ctx["inc_label"])
     plan.topk(ctx["inc_label"])
 
 
@@ -154,7 +135,6 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--unfused", action="store_true", help="A/B: reach as its own pass")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +150,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     ctx = setup(args.config, args.batch, args.k, rank, dev)
-    run_step = step_unfused if args.unfused else step
+    run_step = step
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
@@ -195,9 +175,9 @@ def main():
     nnz = ctx["snap"].n_entries
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    W = (B + 63) // 64
-    # SURVEY §8d compulsory bytes of one fused hop: CSR once + scores read/write + reach words
-    hop_bytes = nnz * 5 + (V + 1) * 4 + 2 * V * B * 4 + 2 * V * W * 8
+    # SURVEY §8d compulsory bytes of one propagation hop: CSR (col + type) once, row_ptr,
+    # scores read once and written once; gathers beyond the one compulsory read are not counted
+    hop_bytes = nnz * 5 + (V + 1) * 4 + 2 * V * B * 4
     achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
     traffic = None
     pmc = REPO / "profiles" / "pmc_hop.json"
@@ -225,8 +205,8 @@ def main():
             "evidence_rows_per_gpu": ctx["enc"].n_rows, "seeds_per_gpu": int(len(ctx["seed_host"][0])),
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
         },
-        "roofline": {"bound": "hbm", "kernel": f"hop_kernel<{ctx['plan'].tile_width // 4},false,true,false> "
-                               "(dense propagation hop + fused reach)",
+        "roofline": {"bound": "hbm", "kernel": f"hop_kernel<{ctx['plan'].tile_width // 4},false> "
+                               "(dense propagation hop + seed_add)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes},

@@ -187,10 +187,13 @@ int egr_snapshot_info(const egr_snapshot* s, int64_t* n_vertices, int64_t* n_ent
  * allocated here, none in the launch functions, so a step can be captured into a hipGraph).
  *   scores: fp32, tiled [B/TW][V][TW] with TW = 128 (B >= 128), 64, 16 or 4
  *           ($EGRAPH_TILE_WIDTH caps TW).
- *   reach : u64 words [ceil(B/64)][V], bit b%64 of word b/64 = vertex within `hops` of the
- *           incident vertex of column b (undirected, all types: apoc.path.subgraphAll).
+ *   reach : u64 bitsets, bit b%64 of word b/64 of vertex v = v within `hops` of the
+ *           incident vertex of column b (undirected, all types: apoc.path.subgraphAll);
+ *           held row-major (one vertex's words contiguous), exported as [ceil(B/64)][V].
+ * n_cols <= EGR_MAX_COLS.
  * ---------------------------------------------------------------------------------------- */
 typedef struct egr_plan egr_plan;
+#define EGR_MAX_COLS 8192
 
 int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
                     egr_plan** out);
@@ -205,12 +208,16 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
 int egr_plan_hop(egr_plan* p, void* stream);
 /* One reachability hop over the undirected graph.                                          */
 int egr_plan_reach_hop(egr_plan* p, void* stream);
-/* One hop of both recurrences (fused into a single pass over the CSR when TW >= 64).        */
+/* One hop of both recurrences (egr_plan_hop then egr_plan_reach_hop).                       */
 int egr_plan_step(egr_plan* p, void* stream);
-/* The last hop: egr_plan_step plus, when TW >= 64, the top-k candidate lists (reached
- * vertices whose label is not exclude_label), so egr_plan_topk with the same exclude_label
- * reads only the candidates instead of rescanning every score.                              */
+/* The last hop: egr_plan_step plus the top-k candidate lists (reached vertices whose label
+ * is not exclude_label, per column, in vertex order), so egr_plan_topk with the same
+ * exclude_label reads only the candidates instead of rescanning every score.  (Plans whose
+ * worst-case lists, V*n_cols*4 B, exceed 16 GiB skip the lists and top-k rescans.)          */
 int egr_plan_final_step(egr_plan* p, int32_t exclude_label, void* stream);
+/* The candidate lists of egr_plan_final_step alone, from the current reach sets (for callers
+ * that run the hops themselves).                                                            */
+int egr_plan_candidates(egr_plan* p, int32_t exclude_label, void* stream);
 /* Per column: top-k vertices by final score (desc), vertex id asc on ties, over the reach
  * set excluding vertices whose label is `exclude_label` (-1: none).  Outputs [n_cols*k];
  * unused slots hold EGR_NO_NODE / -inf.                                                     */

@@ -7,12 +7,13 @@
 //       topk   : per incident, top-k vertices of the final scores over its reach set, score
 //                descending, vertex id ascending on ties.
 //
-// Layout: scores are tiled [B/TW][V][TW] fp32 (TW = 64/16/4 columns), so a
-// pull-gather of one neighbour row is TW*4 contiguous bytes (256 B at TW = 64) served by G = TW/4
-// lanes with one float4 each, and the whole gather working set of a launch is one tile
-// (V*TW*4 B = 64 MB at 250k vertices), which the 256 MB Infinity Cache holds while the grid,
-// ordered tile-major, sweeps it.  Row blocks are remapped so that each XCD streams a contiguous
-// vertex range (its L2 sees the namespace locality of the snapshot's vertex order).
+// Layout: scores are tiled [B/TW][V][TW] fp32 (TW = 128/64/16/4 columns), so a
+// pull-gather of one neighbour row is TW*4 contiguous bytes (512 B at TW = 128) served by
+// G = TW/4 lanes with one float4 each, and the gather working set of one tile sweep
+// (V*TW*4 B = 117 MB at 229k vertices) fits the 256 MB Infinity Cache.  Reach words are
+// row-major [V][RS] u64 (RS = 2*RG words, RG a power of two): a vertex's words for all
+// incidents are one contiguous row, so a reach hop is the same staged gather as a propagation
+// hop at 1/32 of its bytes (RG lanes x 16 B per row).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -48,14 +49,6 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
-
-// Contiguous row ranges per XCD: workgroups are dealt round-robin over the 8 XCDs, so block l
-// of a tile (nrb padded to a multiple of 8) runs on XCD l % 8; give that XCD the (l/8)-th block
-// of its own contiguous eighth.  Speed only -- any placement gives the same result.
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t l, uint32_t nrb8) {
-  const uint32_t per = nrb8 >> 3;
-  return (l & 7u) * per + (l >> 3);
-}
 
 __device__ __forceinline__ void fma4(float w, const float4& x, float4& a) {
   a.x = fmaf(w, x.x, a.x);
@@ -113,15 +106,15 @@ __device__ __forceinline__ void add_seeds(float4& acc, uint32_t v, uint32_t lo,
 // that spills, into the cold tail loop).  The block stages row_ptr and (col, val) in LDS with
 // all loads issued before the first wait, then every lane group (G lanes x float4 = the row's
 // TW columns) walks its rows with a two-buffer software pipeline: the next row's NB gathers
-// (and reach words) are in flight while the current row runs its fmaf chain in CSR order.
+// are in flight while the current row runs its fmaf chain in CSR order.
 // The hot loop is branch-free: a row with fewer than NB entries fills the batch with its own
 // last neighbour at weight 0 (fmaf(0, x, acc) == acc exactly: acc is never -0.0), so the
 // compiler's vmcnt accounting keeps the next row's loads in flight.
 //   FROM_SEEDS (h = 0 -> 1): neighbour values come from the sparse seed lists, filtered by a
-//              per-vertex seed-tile mask, so s0 is never materialised densely;
-//   REACH      (TW >= 64): the same walk ORs the neighbours' reach words (one pass per hop).
+//              per-vertex seed-tile mask, so s0 is never materialised densely.
 // The own-row seed term s0_v is added afterwards by seed_add_kernel (out = acc + s0, the same
-// single rounding as the oracle).
+// single rounding as the oracle).  Reachability is a separate pass (reach_kernel): folding
+// its words into this walk costs more TA cycles than the reach pass itself (PMC, round 1).
 constexpr uint32_t CSR_CAP = 2048;
 constexpr int NB = 4;
 
@@ -141,27 +134,60 @@ struct HopArgs {
   const uint32_t* seed_tiles;
   const float* xin;
   float* xout;
-  const uint64_t* rin;
-  uint64_t* rout;
   uint32_t V;
   uint32_t nchunks;
 };
 
-template <bool SEEDS, bool REACH>
+template <bool SEEDS>
 struct Batch {
   float4 x[NB];
-  uint64_t rw[NB];
   uint32_t m[NB];
   uint32_t u[NB];
   float w[NB];
-  uint64_t own;
   uint32_t n;
 };
 
-template <int G, bool FROM_SEEDS, bool REACH>
+// Stage a chunk's row offsets (relative to its first entry) and up to CSR_CAP column ids (and
+// values) in LDS: every global load is issued before the first LDS store.
+template <int ROWS, bool VAL>
+__device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr,
+                                            const uint32_t* __restrict__ col,
+                                            const float* __restrict__ val, uint32_t v0,
+                                            uint32_t nrows, uint32_t e0, uint32_t e1,
+                                            uint32_t* s_rp, uint32_t* s_col, float* s_val) {
+  constexpr int PER = CSR_CAP / 256;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nst = min(e1 - e0, CSR_CAP);
+  uint32_t rp_t = 0;
+  if (tid < nrows) rp_t = row_ptr[v0 + tid];
+  uint32_t cc[PER];
+  float ww[PER];
+  if (nst > 0) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = min(tid + k * 256u, nst - 1u);
+      cc[k] = col[e0 + i];
+      if constexpr (VAL) ww[k] = val[e0 + i];
+    }
+  }
+  if (tid < nrows) s_rp[tid] = rp_t - e0;
+  if (tid == 0) s_rp[nrows] = e1 - e0;       // nrows may equal the block size
+  if (nst > 0) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t i = tid + k * 256u;
+      if (i < nst) {
+        s_col[i] = cc[k];
+        if constexpr (VAL) s_val[i] = ww[k];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int G, bool FROM_SEEDS>
 __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
-  constexpr int PER = CSR_CAP / 256;
   __shared__ uint32_t s_rp[ROWS + 1];
   __shared__ uint32_t s_col[CSR_CAP];
   __shared__ float s_val[CSR_CAP];
@@ -171,32 +197,7 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   const uint32_t v0 = A.chunk_start[chunk], v1 = A.chunk_start[chunk + 1];
   const uint32_t nrows = v1 - v0;
   const uint32_t e0 = A.row_ptr[v0], e1 = A.row_ptr[v1];
-  const uint32_t nst = min(e1 - e0, CSR_CAP);
-  uint32_t rp_t = 0;
-  if (tid < nrows) rp_t = A.row_ptr[v0 + tid];
-  uint32_t cc[PER];
-  float ww[PER];
-  if (nst > 0) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t i = min(tid + k * 256u, nst - 1u);
-      cc[k] = A.col[e0 + i];
-      ww[k] = A.val[e0 + i];
-    }
-  }
-  if (tid < nrows) s_rp[tid] = rp_t - e0;   // entries relative to the chunk
-  if (tid == 0) s_rp[nrows] = e1 - e0;       // nrows may equal the block size (G = 1)
-  if (nst > 0) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t i = tid + k * 256u;
-      if (i < nst) {
-        s_col[i] = cc[k];
-        s_val[i] = ww[k];
-      }
-    }
-  }
-  __syncthreads();
+  stage_chunk<ROWS, true>(A.row_ptr, A.col, A.val, v0, nrows, e0, e1, s_rp, s_col, s_val);
   if (grp >= nrows) return;  // no barrier below
 
   const uint32_t lo = tile * TW + 4 * gl;  // first column of this lane
@@ -204,11 +205,9 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   const size_t toff = (size_t)tile * V * TW;
   const float4* __restrict__ X = reinterpret_cast<const float4*>(A.xin + toff);
   float4* __restrict__ Y = reinterpret_cast<float4*>(A.xout + toff);
-  const uint32_t word = lo >> 6;
-  const uint64_t* __restrict__ R = A.rin + (size_t)word * V;
 
   // NB entries of row r; slots past the row's end repeat its last neighbour at weight 0
-  auto issue = [&](uint32_t r, Batch<FROM_SEEDS, REACH>& bt) {
+  auto issue = [&](uint32_t r, Batch<FROM_SEEDS>& bt) {
     const uint32_t a = s_rp[r], b = s_rp[r + 1];
     const uint32_t n = b - a;
     bt.n = n;
@@ -220,9 +219,7 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       bt.w[t] = (uint32_t)t < n ? s_val[min(jj, CSR_CAP - 1u)] : 0.f;
       if constexpr (FROM_SEEDS) bt.m[t] = A.seed_tiles[u];
       else bt.x[t] = X[(size_t)u * G + gl];
-      if constexpr (REACH) bt.rw[t] = R[u];
     }
-    if constexpr (REACH) bt.own = R[v0 + r];
   };
   auto seed_gather = [&](uint32_t u, float w, float4& acc) {
     const uint32_t s1 = A.seed_ptr[u + 1];
@@ -232,11 +229,9 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       fma_comp(acc, (int)c, w, A.seed_val[q]);
     }
   };
-  auto process = [&](uint32_t r, const Batch<FROM_SEEDS, REACH>& bt) {
+  auto process = [&](uint32_t r, const Batch<FROM_SEEDS>& bt) {
     const uint32_t v = v0 + r;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint64_t rr = 0;
-    if constexpr (REACH) rr = bt.own;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
       if constexpr (FROM_SEEDS) {
@@ -245,7 +240,6 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       } else {
         fma4(bt.w[t], bt.x[t], acc);
       }
-      if constexpr (REACH) rr |= bt.rw[t];
     }
     // tail of rows with more than NB entries, NT gathers per batch (deployments, services,
     // Node hubs); slots past the end repeat the last entry at weight 0
@@ -274,21 +268,11 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) fma4(w[t], x[t], acc);
       }
-      if constexpr (REACH) {
-        uint64_t rw[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) rw[t] = R[u[t]];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) rr |= rw[t];
-      }
     }
     Y[(size_t)v * G + gl] = acc;
-    if constexpr (REACH) {
-      if ((lo & 63u) == 0u) A.rout[(size_t)word * V + v] = rr;
-    }
   };
 
-  Batch<FROM_SEEDS, REACH> ba, bb;
+  Batch<FROM_SEEDS> ba, bb;
   uint32_t r = grp;
   issue(r, ba);
   while (true) {
@@ -317,46 +301,6 @@ __global__ void seed_add_kernel(const uint64_t* __restrict__ ukeys,
   *p = *p + uval[i];
 }
 
-// Top-k candidates of the final reach words.  A wave owns 64 rows (lane = row) of one word:
-// ballots give every column's count (lane c keeps column c's), ONE atomicAdd instruction
-// reserves all 64 columns' slots at once, then the rows write their ids.  Only columns present
-// in the wave are visited.  Order inside a list is irrelevant: the merge applies the strict
-// (score desc, id asc) order.
-__global__ __launch_bounds__(256) void cand_extract_kernel(
-    const uint64_t* __restrict__ R, const uint8_t* __restrict__ vlabel, int exclude_label,
-    uint32_t V, int B, uint32_t nrb, uint32_t* __restrict__ cand_count,
-    uint32_t* __restrict__ cand_list) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t w = wave / nrb;
-  const uint32_t v = (wave % nrb) * 64 + lane;
-  if (w * 64 >= (uint32_t)B) return;
-  uint64_t word = 0;
-  if (v < V && !(exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label)) word = R[(size_t)w * V + v];
-  const int cmax = min(64, B - (int)w * 64);
-  if (cmax < 64) word &= (1ull << cmax) - 1ull;
-  uint64_t cols = word;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cols |= __shfl_xor(cols, off, 64);
-  if (!cols) return;
-  uint32_t mycnt = 0;
-  for (uint64_t m = cols; m; m &= m - 1) {
-    const int c = __ffsll((long long)m) - 1;
-    const uint32_t n = (uint32_t)__popcll(__ballot((word >> c) & 1ull));
-    if (lane == c) mycnt = n;
-  }
-  uint32_t mybase = 0;
-  if (mycnt) mybase = atomicAdd(&cand_count[w * 64 + lane], mycnt);
-  const uint64_t lt = (1ull << lane) - 1ull;
-  for (uint64_t m = cols; m; m &= m - 1) {
-    const int c = __ffsll((long long)m) - 1;
-    const uint64_t bits = __ballot((word >> c) & 1ull);
-    const uint32_t base = __shfl(mybase, c, 64);
-    if ((word >> c) & 1ull)
-      cand_list[(size_t)(w * 64 + c) * V + base + __popcll(bits & lt)] = v;
-  }
-}
-
 __global__ void seed_tiles_kernel(const uint64_t* __restrict__ ukeys,
                                   const uint32_t* __restrict__ n_unique, uint32_t Bpad,
                                   uint32_t TW, uint32_t* seed_tiles) {
@@ -368,27 +312,178 @@ __global__ void seed_tiles_kernel(const uint64_t* __restrict__ ukeys,
 }
 
 // ---- reachability ----------------------------------------------------------------------------
+// R is row-major [V][RS] u64, RS = 2 * RG: word b/64 of row v holds incident b's bit.
 __global__ void reach_sources_kernel(const uint32_t* __restrict__ src, int B, uint64_t* R,
-                                     uint32_t V) {
+                                     uint32_t V, uint32_t RS) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint32_t v = src[b];
-  if (v < V) atomicOr((unsigned long long*)&R[(size_t)(b >> 6) * V + v], 1ull << (b & 63));
+  if (v < V) atomicOr((unsigned long long*)&R[(size_t)v * RS + (b >> 6)], 1ull << (b & 63));
 }
 
-__global__ __launch_bounds__(256) void reach_hop_kernel(const uint32_t* __restrict__ row_ptr,
-                                                        const uint32_t* __restrict__ col,
-                                                        const uint64_t* __restrict__ rin,
-                                                        uint64_t* __restrict__ rout, uint32_t V,
-                                                        uint32_t nrb8) {
-  const uint32_t w = blockIdx.x / nrb8;
-  const uint32_t v = xcd_remap(blockIdx.x % nrb8, nrb8) * 256 + threadIdx.x;
-  if (v >= V) return;
-  const uint64_t* R = rin + (size_t)w * V;
-  uint64_t acc = R[v];
-  const uint32_t e1 = row_ptr[v + 1];
-  for (uint32_t e = row_ptr[v]; e < e1; ++e) acc |= R[col[e]];
-  rout[(size_t)w * V + v] = acc;
+template <int RG>
+struct ReachGeo {
+  static constexpr int ROWS = RG == 1 ? 256 : 128;
+};
+
+__device__ __forceinline__ uint4 or4(uint4 a, const uint4& b) {
+  a.x |= b.x;
+  a.y |= b.y;
+  a.z |= b.z;
+  a.w |= b.w;
+  return a;
+}
+
+// One reach hop R' = R | A R over one row chunk: the chunk's columns are staged in LDS like
+// hop_kernel's, each lane group (RG lanes x 16 B = the row's RS words) ORs its rows' neighbour
+// rows with the same two-buffer, branch-free pipeline (a short row repeats its last neighbour:
+// OR is idempotent).
+template <int RG>
+__global__ __launch_bounds__(256) void reach_kernel(const uint32_t* __restrict__ row_ptr,
+                                                    const uint32_t* __restrict__ col,
+                                                    const uint32_t* __restrict__ chunk_start,
+                                                    const uint4* __restrict__ rin,
+                                                    uint4* __restrict__ rout) {
+  constexpr int GROUPS = 256 / RG, ROWS = ReachGeo<RG>::ROWS;
+  __shared__ uint32_t s_rp[ROWS + 1];
+  __shared__ uint32_t s_col[CSR_CAP];
+  const uint32_t tid = threadIdx.x, gl = tid % RG, grp = tid / RG;
+  const uint32_t v0 = chunk_start[blockIdx.x], v1 = chunk_start[blockIdx.x + 1];
+  const uint32_t nrows = v1 - v0;
+  const uint32_t e0 = row_ptr[v0], e1 = row_ptr[v1];
+  stage_chunk<ROWS, false>(row_ptr, col, nullptr, v0, nrows, e0, e1, s_rp, s_col, nullptr);
+  if (grp >= nrows) return;  // no barrier below
+
+  struct RB {
+    uint4 x[NB];
+    uint4 own;
+  };
+  auto issue = [&](uint32_t r, RB& bt) {
+    const uint32_t a = s_rp[r], n = s_rp[r + 1] - a;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const uint32_t jj = a + min((uint32_t)t, n > 0u ? n - 1u : 0u);
+      const uint32_t u = n > 0u ? s_col[min(jj, CSR_CAP - 1u)] : v0 + r;
+      bt.x[t] = rin[(size_t)u * RG + gl];
+    }
+    bt.own = rin[(size_t)(v0 + r) * RG + gl];
+  };
+  auto process = [&](uint32_t r, const RB& bt) {
+    uint4 acc = bt.own;
+#pragma unroll
+    for (int t = 0; t < NB; ++t) acc = or4(acc, bt.x[t]);
+    constexpr int NT = 4;
+    const uint32_t b = s_rp[r + 1];
+    for (uint32_t j = s_rp[r] + NB; j < b; j += NT) {
+      uint4 x[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const uint32_t jj = min(j + t, b - 1u);
+        const uint32_t u = jj < CSR_CAP ? s_col[jj] : col[e0 + jj];
+        x[t] = rin[(size_t)u * RG + gl];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc = or4(acc, x[t]);
+    }
+    rout[(size_t)(v0 + r) * RG + gl] = acc;
+  };
+
+  RB ba, bb;
+  uint32_t r = grp;
+  issue(r, ba);
+  while (true) {
+    const uint32_t r1 = r + GROUPS;
+    issue(r1 < nrows ? r1 : r, bb);
+    process(r, ba);
+    if (r1 >= nrows) break;
+    const uint32_t r2 = r1 + GROUPS;
+    issue(r2 < nrows ? r2 : r1, ba);
+    process(r1, bb);
+    if (r2 >= nrows) break;
+    r = r2;
+  }
+}
+
+// ---- top-k candidates: deterministic count -> scan -> fill over the final reach rows --------
+// A wave owns 64 vertices (lane = row) of group g.  For each word, ballots over the columns
+// present in the wave give every column's count; lane c stores column (64w + c)'s count at
+// cnt[col * NG + g].  One exclusive scan over cnt (column-major) yields each (column, group)
+// slot, so every column's candidates end up contiguous and in vertex order, with no atomics.
+// Excluded-label vertices (Incident) are never candidates.
+__device__ __forceinline__ uint64_t cand_word(const uint64_t* __restrict__ R, uint32_t RS,
+                                              uint32_t v, bool ok, int w, int B) {
+  uint64_t word = ok ? R[(size_t)v * RS + w] : 0ull;
+  const int cmax = min(64, B - w * 64);
+  if (cmax < 64) word &= (1ull << cmax) - 1ull;
+  return word;
+}
+
+__device__ __forceinline__ uint64_t wave_or(uint64_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x |= __shfl_xor(x, off, 64);
+  return x;
+}
+
+__global__ __launch_bounds__(256) void cand_count_kernel(
+    const uint64_t* __restrict__ R, uint32_t RS, const uint8_t* __restrict__ vlabel,
+    int exclude_label, uint32_t V, int B, uint32_t NG, uint32_t* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= NG) return;
+  const uint32_t v = g * 64 + lane;
+  const bool ok = v < V && !(exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label);
+  const int W = (B + 63) / 64;
+  for (int w0 = 0; w0 < W; w0 += 4) {
+    uint64_t wd[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wd[t] = w0 + t < W ? cand_word(R, RS, v, ok, w0 + t, B) : 0ull;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int w = w0 + t;
+      if (w >= W) break;
+      uint32_t mycnt = 0;
+      for (uint64_t m = wave_or(wd[t]); m; m &= m - 1) {
+        const int c = __ffsll((long long)m) - 1;
+        const uint32_t n = (uint32_t)__popcll(__ballot((wd[t] >> c) & 1ull));
+        if (lane == c) mycnt = n;
+      }
+      if (lane < min(64, B - w * 64)) cnt[(size_t)(w * 64 + lane) * NG + g] = mycnt;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cand_fill_kernel(
+    const uint64_t* __restrict__ R, uint32_t RS, const uint8_t* __restrict__ vlabel,
+    int exclude_label, uint32_t V, int B, uint32_t NG, const uint32_t* __restrict__ off,
+    uint32_t* __restrict__ cand_list) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= NG) return;
+  const uint32_t v = g * 64 + lane;
+  const bool ok = v < V && !(exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int W = (B + 63) / 64;
+  for (int w = 0; w < W; ++w) {
+    const uint64_t word = cand_word(R, RS, v, ok, w, B);
+    const uint64_t cols = wave_or(word);
+    if (!cols) continue;
+    const uint32_t mybase = lane < min(64, B - w * 64) ? off[(size_t)(w * 64 + lane) * NG + g] : 0u;
+    for (uint64_t m = cols; m; m &= m - 1) {
+      const int c = __ffsll((long long)m) - 1;
+      const uint64_t bits = __ballot((word >> c) & 1ull);
+      const uint32_t base = __shfl(mybase, c, 64);
+      if ((word >> c) & 1ull) cand_list[base + __popcll(bits & lt)] = v;
+    }
+  }
+}
+
+// [V][RS] -> [W][V] for egr_plan_read_reach (the header's layout)
+__global__ void reach_export_kernel(const uint64_t* __restrict__ R, uint32_t RS, uint32_t V,
+                                    int W, uint64_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * V) return;
+  const uint32_t w = (uint32_t)(i / V), v = (uint32_t)(i % V);
+  out[i] = R[(size_t)v * RS + w];
 }
 
 // ---- seeds: (vertex, column, value) triples -> unique per-vertex lists (max-combined) ----------
@@ -516,7 +611,7 @@ __device__ __forceinline__ void wave_emit_topk(float (&Ls)[KMAX], uint32_t (&Lv)
 // A wave covers CW = min(TW, 64) columns of one tile: lane -> (column c, row phase rp); the
 // wave index enumerates (tile, 64-column slice, row chunk).
 __global__ __launch_bounds__(256) void topk_partial_kernel(
-    const float* __restrict__ X, const uint64_t* __restrict__ R,
+    const float* __restrict__ X, const uint64_t* __restrict__ R, uint32_t RS,
     const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, int TW, int B,
     int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v) {
   const int lane = threadIdx.x & 63;
@@ -537,7 +632,7 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(
   }
   if (b < B) {
     const float* Xt = X + (size_t)tile * V * TW;
-    const uint64_t* Rw = R + (size_t)(b >> 6) * V;
+    const uint64_t* Rw = R + (b >> 6);
     const uint64_t bit = 1ull << (b & 63);
     const uint32_t v0 = (uint32_t)ch * TOPK_CHUNK;
     const uint32_t v1 = min(V, v0 + TOPK_CHUNK);
@@ -550,7 +645,7 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const uint32_t v = vb + t * rps;
-        wd[t] = v < v1 ? Rw[v] : 0ull;
+        wd[t] = v < v1 ? Rw[(size_t)v * RS] : 0ull;
         lab[t] = v < v1 ? vlabel[v] : 0;
       }
 #pragma unroll
@@ -602,9 +697,9 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   wave_emit_topk(Ls, Lv, k, lane, out_ids + (size_t)b * k, out_scores + (size_t)b * k);
 }
 
-// top-k from the candidate lists the CAND hop appended: one wave per column
+// top-k over each column's candidate list (cand_fill_kernel): one wave per column
 __global__ __launch_bounds__(256) void topk_cand_kernel(
-    const float* __restrict__ X, const uint32_t* __restrict__ cand_count,
+    const float* __restrict__ X, const uint32_t* __restrict__ off, uint32_t NG,
     const uint32_t* __restrict__ cand_list, uint32_t V, int TW, int B, int k,
     uint32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
   const int lane = threadIdx.x & 63;
@@ -617,9 +712,10 @@ __global__ __launch_bounds__(256) void topk_cand_kernel(
     Ls[i] = -INFINITY;
     Lv[i] = NO_NODE;
   }
-  const uint32_t n = min(cand_count[b], V);
+  const uint32_t s0 = off[(size_t)b * NG];
+  const uint32_t n = min(off[(size_t)(b + 1) * NG] - s0, V);
   const float* __restrict__ Xc = X + (size_t)(b / TW) * V * TW + (b % TW);
-  const uint32_t* __restrict__ Lb = cand_list + (size_t)b * V;
+  const uint32_t* __restrict__ Lb = cand_list + s0;
   for (uint32_t i0 = lane; i0 < n; i0 += 64u * 4u) {
     uint32_t vv[4];
     float ss[4];
@@ -645,16 +741,16 @@ __global__ void scores_rowmajor_kernel(const float* __restrict__ X, uint32_t V, 
 
 __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
                                const uint32_t* __restrict__ col, const uint8_t* __restrict__ meta,
-                               const uint64_t* __restrict__ Rw, uint64_t bit, uint32_t V,
+                               const uint64_t* __restrict__ Rw, uint32_t RS, uint64_t bit, uint32_t V,
                                uint32_t* osrc, uint32_t* odst, uint8_t* otype, int64_t cap,
                                unsigned long long* counter) {
   const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V || !(Rw[v] & bit)) return;
+  if (v >= V || !(Rw[(size_t)v * RS] & bit)) return;
   for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e) {
     const uint8_t m = meta[e];
     if (m & 1u) continue;  // dir 1 duplicates: each edge is listed once, in its target's row
     const uint32_t u = col[e];
-    if (!(Rw[u] & bit)) continue;
+    if (!(Rw[(size_t)u * RS] & bit)) continue;
     const unsigned long long slot = atomicAdd(counter, 1ull);
     if ((int64_t)slot < cap) {
       osrc[slot] = u;
@@ -669,12 +765,13 @@ __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
 struct egr_plan {
   const egr_snapshot* s = nullptr;
   int B = 0, TW = 0, Bpad = 0, ntiles = 0, W = 0, k = 0;
-  int Wa = 0;                // reach words allocated: padded columns of 128-wide tiles too
+  int RG = 0, RS = 0;        // reach: RG lanes x 16 B per row, RS = 2*RG words per row
   int64_t max_seeds = 0;
   int n_chunks = 0;          // top-k full-scan chunks
   uint32_t nchunks = 0;      // hop row chunks per tile
   uint32_t* chunk_start = nullptr;
-  uint32_t nrb8_reach = 0;
+  uint32_t rnchunks = 0;     // reach row chunks
+  uint32_t* rchunk_start = nullptr;
   float* x[2] = {nullptr, nullptr};
   int xcur = 0;
   uint64_t* reach[2] = {nullptr, nullptr};
@@ -690,11 +787,14 @@ struct egr_plan {
   void* cub_tmp = nullptr;
   size_t cub_tmp_bytes = 0;
   int end_bit = 64;
-  // top-k: full-scan partials, and the candidate lists of the fused last hop
+  // top-k: full-scan partials, and the candidate lists of the final reach
   float* part_s = nullptr;
   uint32_t* part_v = nullptr;
-  uint32_t* cand_count = nullptr;
-  uint32_t* cand_list = nullptr;
+  uint32_t NG = 0;                  // 64-vertex groups
+  uint32_t* cand_cnt = nullptr;     // [B*NG + 1] per (column, group) counts
+  uint32_t* cand_off = nullptr;     // exclusive scan of cand_cnt
+  uint32_t* cand_list = nullptr;    // all columns' candidates, column-contiguous
+  bool cand_enabled = false;
   bool cand_valid = false;
   int cand_exclude = -1;
   unsigned long long* counter = nullptr;
@@ -765,34 +865,25 @@ std::vector<uint32_t> build_chunks(const std::vector<uint32_t>& rp, uint32_t V, 
   return cs;
 }
 
-template <int G, bool SEEDS, bool REACH>
-void launch_hop_t(const HopArgs& a, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((hop_kernel<G, SEEDS, REACH>), grid, dim3(256), 0, st, a);
-}
-
 template <int G>
-void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool reach) {
-  if constexpr (G >= 16) {
-    if (seeds) {
-      if (reach) launch_hop_t<G, true, true>(a, grid, st);
-      else launch_hop_t<G, true, false>(a, grid, st);
-    } else {
-      if (reach) launch_hop_t<G, false, true>(a, grid, st);
-      else launch_hop_t<G, false, false>(a, grid, st);
-    }
-  } else {
-    if (seeds) launch_hop_t<G, true, false>(a, grid, st);
-    else launch_hop_t<G, false, false>(a, grid, st);
-  }
+void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds) {
+  if (seeds) hipLaunchKernelGGL((hop_kernel<G, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((hop_kernel<G, false>), grid, dim3(256), 0, st, a);
 }
 
-// One propagation hop (+ its own-row seed add); with `reach` (TW >= 64) also one
-// reachability hop in the same pass.
-int plan_hop(egr_plan* p, void* stream, bool reach) {
+template <int RG>
+void launch_reach_g(const egr_plan* p, hipStream_t st) {
+  hipLaunchKernelGGL((reach_kernel<RG>), dim3(p->rnchunks), dim3(256), 0, st, p->s->row_ptr,
+                     p->s->col, p->rchunk_start, reinterpret_cast<const uint4*>(p->reach[p->rcur]),
+                     reinterpret_cast<uint4*>(p->reach[1 - p->rcur]));
+}
+
+uint32_t reach_rows(int RG) { return RG == 1 ? ReachGeo<1>::ROWS : ReachGeo<2>::ROWS; }
+
+// One propagation hop (+ its own-row seed add).
+int plan_hop(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_hop: NULL plan");
   if (p->hops_done < 0) return egr::fail(EGR_ESTATE, "egr_plan_hop: seeds not set");
-  if (reach && (p->TW < 64 || !p->sources_set))
-    return egr::fail(EGR_ESTATE, "fused reach needs TW >= 64 and sources set");
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const egr_snapshot* s = p->s;
@@ -808,16 +899,14 @@ int plan_hop(egr_plan* p, void* stream, bool reach) {
   a.seed_tiles = p->seed_tiles;
   a.xin = seeds ? nullptr : p->x[p->xcur];
   a.xout = p->x[seeds ? 0 : 1 - p->xcur];
-  a.rin = p->reach[p->rcur];
-  a.rout = p->reach[1 - p->rcur];
   a.V = (uint32_t)s->V;
   a.nchunks = p->nchunks;
   const dim3 grid(p->nchunks * p->ntiles);
   switch (p->TW) {
-    case 128: launch_hop_g<32>(a, grid, st, seeds, reach); break;
-    case 64: launch_hop_g<16>(a, grid, st, seeds, reach); break;
-    case 16: launch_hop_g<4>(a, grid, st, seeds, false); break;
-    default: launch_hop_g<1>(a, grid, st, seeds, false); break;
+    case 128: launch_hop_g<32>(a, grid, st, seeds); break;
+    case 64: launch_hop_g<16>(a, grid, st, seeds); break;
+    case 16: launch_hop_g<4>(a, grid, st, seeds); break;
+    default: launch_hop_g<1>(a, grid, st, seeds); break;
   }
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
@@ -826,10 +915,6 @@ int plan_hop(egr_plan* p, void* stream, bool reach) {
   EGR_CHECK_LAUNCH();
   p->xcur = seeds ? 0 : 1 - p->xcur;
   ++p->hops_done;
-  if (reach) {
-    p->rcur = 1 - p->rcur;
-    ++p->reach_hops;
-  }
   p->cand_valid = false;
   return EGR_OK;
 }
@@ -898,8 +983,9 @@ int egr_snapshot_info(const egr_snapshot* s, int64_t* n_vertices, int64_t* n_ent
 
 int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
                     egr_plan** out) {
-  if (!s || !out || n_cols <= 0 || max_seeds < 0 || k < 1 || k > KMAX)
-    return egr::fail(EGR_EINVAL, "egr_plan_create: bad arguments (need n_cols > 0, 1 <= k <= 16)");
+  if (!s || !out || n_cols <= 0 || n_cols > EGR_MAX_COLS || max_seeds < 0 || k < 1 || k > KMAX)
+    return egr::fail(EGR_EINVAL,
+                     "egr_plan_create: bad arguments (need 0 < n_cols <= 8192, 1 <= k <= 16)");
   *out = nullptr;
   DeviceGuard guard(s->device);
   auto* p = new egr_plan();
@@ -909,13 +995,21 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   p->Bpad = (n_cols + p->TW - 1) / p->TW * p->TW;
   p->ntiles = p->Bpad / p->TW;
   p->W = (n_cols + 63) / 64;
-  p->Wa = std::max(p->W, p->Bpad / 64);
+  p->RG = 1;
+  while (2 * p->RG < p->W) p->RG *= 2;
+  p->RS = 2 * p->RG;
   p->k = k;
   p->max_seeds = max_seeds;
   const uint32_t V = (uint32_t)s->V;
   const std::vector<uint32_t> chunks = build_chunks(s->row_ptr_host, V, hop_rows(p->TW));
   p->nchunks = (uint32_t)chunks.size() - 1;
-  p->nrb8_reach = ((V + 255) / 256 + 7) / 8 * 8;
+  const std::vector<uint32_t> rchunks = build_chunks(s->row_ptr_host, V, reach_rows(p->RG));
+  p->rnchunks = (uint32_t)rchunks.size() - 1;
+  p->NG = (V + 63) / 64;
+  // candidate lists: worst case every vertex for every column (4 B each)
+  p->cand_enabled = (uint64_t)V * p->B <= (1ull << 32) - 1 &&
+                    (uint64_t)V * p->B * 4 <= (16ull << 30);
+  const size_t ncnt = p->cand_enabled ? (size_t)p->B * p->NG + 1 : 1;
   p->n_chunks = (int)((V + TOPK_CHUNK - 1) / TOPK_CHUNK);
   const uint64_t keyspace = (uint64_t)V * p->Bpad;
   p->end_bit = 1;
@@ -924,33 +1018,37 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   int rc = EGR_OK;
   const size_t xs = (size_t)V * p->Bpad;
   const size_t parts = (size_t)p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks * 64 * KMAX;
-  const bool fused = p->TW >= 64;
   if ((rc = dalloc(&p->x[0], xs)) || (rc = dalloc(&p->x[1], xs)) ||
-      (rc = dalloc(&p->reach[0], (size_t)p->Wa * V)) || (rc = dalloc(&p->reach[1], (size_t)p->Wa * V)) ||
+      (rc = dalloc(&p->reach[0], (size_t)p->RS * V)) || (rc = dalloc(&p->reach[1], (size_t)p->RS * V)) ||
       (rc = dalloc(&p->skeys_in, ms)) || (rc = dalloc(&p->skeys, ms)) || (rc = dalloc(&p->ukeys, ms)) ||
       (rc = dalloc(&p->svals_in, ms)) || (rc = dalloc(&p->svals, ms)) || (rc = dalloc(&p->uval, ms)) ||
       (rc = dalloc(&p->head, ms)) || (rc = dalloc(&p->pos, ms)) || (rc = dalloc(&p->ucol, ms)) ||
       (rc = dalloc(&p->seed_ptr, (size_t)V + 1)) || (rc = dalloc(&p->n_unique, 1)) ||
       (rc = dalloc(&p->seed_tiles, (size_t)V)) ||
       (rc = dalloc(&p->part_s, parts)) || (rc = dalloc(&p->part_v, parts)) ||
-      (rc = dalloc(&p->cand_count, (size_t)p->Bpad)) ||
-      (rc = dalloc(&p->cand_list, fused ? (size_t)V * p->B : 1)) ||
-      (rc = dalloc(&p->counter, 1)) || (rc = dalloc(&p->chunk_start, chunks.size()))) {
+      (rc = dalloc(&p->cand_cnt, ncnt)) || (rc = dalloc(&p->cand_off, ncnt)) ||
+      (rc = dalloc(&p->cand_list, p->cand_enabled ? (size_t)V * p->B : 1)) ||
+      (rc = dalloc(&p->counter, 1)) || (rc = dalloc(&p->chunk_start, chunks.size())) ||
+      (rc = dalloc(&p->rchunk_start, rchunks.size()))) {
     egr_plan_free(p);
     return rc;
   }
-  if (hipMemcpy(p->chunk_start, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+  // the count pass never writes cand_cnt[B*NG], so the scan's last slot is the grand total
+  if (hipMemcpy(p->chunk_start, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->rchunk_start, rchunks.data(), rchunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(p->cand_cnt, 0, ncnt * 4) != hipSuccess) {
     egr_plan_free(p);
-    return egr::fail(EGR_EDEVICE, "chunk table upload failed");
+    return egr::fail(EGR_EDEVICE, "plan table upload failed");
   }
-  size_t b1 = 0, b2 = 0;
+  size_t b1 = 0, b2 = 0, b3 = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, b1, p->skeys_in, p->skeys, p->svals_in, p->svals,
                                          (int)ms, 0, p->end_bit) != hipSuccess ||
-      hipcub::DeviceScan::ExclusiveSum(nullptr, b2, p->head, p->pos, (int)ms) != hipSuccess) {
+      hipcub::DeviceScan::ExclusiveSum(nullptr, b2, p->head, p->pos, (int)ms) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, b3, p->cand_cnt, p->cand_off, (int)ncnt) != hipSuccess) {
     egr_plan_free(p);
     return egr::fail(EGR_EDEVICE, "hipcub temp-size query failed");
   }
-  p->cub_tmp_bytes = std::max(b1, b2);
+  p->cub_tmp_bytes = std::max({b1, b2, b3});
   if (hipMalloc(&p->cub_tmp, p->cub_tmp_bytes) != hipSuccess) {
     egr_plan_free(p);
     return egr::fail(EGR_ENOMEM, "hipMalloc (hipcub temp) failed");
@@ -979,10 +1077,12 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->seed_tiles);
   dfree(p->part_s);
   dfree(p->part_v);
-  dfree(p->cand_count);
+  dfree(p->cand_cnt);
+  dfree(p->cand_off);
   dfree(p->cand_list);
   dfree(p->counter);
   dfree(p->chunk_start);
+  dfree(p->rchunk_start);
   if (p->cub_tmp) (void)hipFree(p->cub_tmp);
   delete p;
 }
@@ -1039,25 +1139,31 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
   const uint32_t V = (uint32_t)p->s->V;
   p->rcur = 0;
   p->cand_valid = false;
-  EGR_HIP(hipMemsetAsync(p->reach[0], 0, (size_t)p->Wa * V * 8, st));
+  EGR_HIP(hipMemsetAsync(p->reach[0], 0, (size_t)p->RS * V * 8, st));
   hipLaunchKernelGGL(reach_sources_kernel, dim3((p->B + 255) / 256), dim3(256), 0, st,
-                     source_vertex, p->B, p->reach[0], V);
+                     source_vertex, p->B, p->reach[0], V, (uint32_t)p->RS);
   EGR_CHECK_LAUNCH();
   p->sources_set = true;
   p->reach_hops = 0;
   return EGR_OK;
 }
 
-int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream, false); }
+int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream); }
 
 int egr_plan_reach_hop(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_reach_hop: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_reach_hop: sources not set");
   DeviceGuard guard(p->s->device);
-  const uint32_t V = (uint32_t)p->s->V;
-  hipLaunchKernelGGL(reach_hop_kernel, dim3(p->nrb8_reach * p->W), dim3(256), 0,
-                     (hipStream_t)stream, p->s->row_ptr, p->s->col, p->reach[p->rcur],
-                     p->reach[1 - p->rcur], V, p->nrb8_reach);
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->RG) {
+    case 1: launch_reach_g<1>(p, st); break;
+    case 2: launch_reach_g<2>(p, st); break;
+    case 4: launch_reach_g<4>(p, st); break;
+    case 8: launch_reach_g<8>(p, st); break;
+    case 16: launch_reach_g<16>(p, st); break;
+    case 32: launch_reach_g<32>(p, st); break;
+    default: launch_reach_g<64>(p, st); break;
+  }
   EGR_CHECK_LAUNCH();
   p->rcur = 1 - p->rcur;
   ++p->reach_hops;
@@ -1068,8 +1174,7 @@ int egr_plan_reach_hop(egr_plan* p, void* stream) {
 int egr_plan_step(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_step: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_step: sources not set");
-  if (p->TW >= 64) return plan_hop(p, stream, true);
-  EGR_TRY(plan_hop(p, stream, false));
+  EGR_TRY(plan_hop(p, stream));
   return egr_plan_reach_hop(p, stream);
 }
 
@@ -1077,16 +1182,26 @@ int egr_plan_final_step(egr_plan* p, int32_t exclude_label, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_final_step: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_final_step: sources not set");
   EGR_TRY(egr_plan_step(p, stream));
-  if (p->TW < 64) return EGR_OK;   // no candidate lists: top-k scans the scores
+  return egr_plan_candidates(p, exclude_label, stream);
+}
+
+int egr_plan_candidates(egr_plan* p, int32_t exclude_label, void* stream) {
+  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_candidates: NULL plan");
+  if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_candidates: sources not set");
+  if (!p->cand_enabled) return EGR_OK;   // no candidate lists: top-k scans the scores
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const uint32_t V = (uint32_t)p->s->V;
-  const uint32_t nrb = (V + 63) / 64;
-  EGR_HIP(hipMemsetAsync(p->cand_count, 0, (size_t)p->Bpad * 4, st));
-  const uint32_t waves = nrb * (uint32_t)p->W;
-  hipLaunchKernelGGL(cand_extract_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
-                     p->reach[p->rcur], p->s->vlabel, exclude_label, V, p->B, nrb, p->cand_count,
-                     p->cand_list);
+  const dim3 grid((p->NG + 3) / 4);
+  const uint64_t* R = p->reach[p->rcur];
+  hipLaunchKernelGGL(cand_count_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS,
+                     p->s->vlabel, exclude_label, V, p->B, p->NG, p->cand_cnt);
+  EGR_CHECK_LAUNCH();
+  size_t tb = p->cub_tmp_bytes;
+  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->cub_tmp, tb, p->cand_cnt, p->cand_off,
+                                           (int)((size_t)p->B * p->NG + 1), st));
+  hipLaunchKernelGGL(cand_fill_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS, p->s->vlabel,
+                     exclude_label, V, p->B, p->NG, p->cand_off, p->cand_list);
   EGR_CHECK_LAUNCH();
   p->cand_valid = true;
   p->cand_exclude = exclude_label;
@@ -1103,13 +1218,13 @@ int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* 
   const uint32_t V = (uint32_t)p->s->V;
   if (p->cand_valid && p->cand_exclude == exclude_label) {
     hipLaunchKernelGGL(topk_cand_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->x[p->xcur],
-                       p->cand_count, p->cand_list, V, p->TW, p->B, p->k, out_ids, out_scores);
+                       p->cand_off, p->NG, p->cand_list, V, p->TW, p->B, p->k, out_ids, out_scores);
     EGR_CHECK_LAUNCH();
     return EGR_OK;
   }
   const int waves = p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks;
   hipLaunchKernelGGL(topk_partial_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
-                     p->x[p->xcur], p->reach[p->rcur], p->s->vlabel, exclude_label, V, p->TW,
+                     p->x[p->xcur], p->reach[p->rcur], (uint32_t)p->RS, p->s->vlabel, exclude_label, V, p->TW,
                      p->B, p->n_chunks, p->part_s, p->part_v);
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->part_s,
@@ -1143,8 +1258,11 @@ int egr_plan_read_reach(const egr_plan* p, uint64_t* out, void* stream) {
   if (!p || !out) return egr::fail(EGR_EINVAL, "egr_plan_read_reach: NULL argument");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_read_reach: sources not set");
   DeviceGuard guard(p->s->device);
-  EGR_HIP(hipMemcpyAsync(out, p->reach[p->rcur], (size_t)p->W * p->s->V * 8,
-                         hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  const size_t n = (size_t)p->W * p->s->V;
+  hipLaunchKernelGGL(reach_export_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, p->reach[p->rcur], (uint32_t)p->RS, (uint32_t)p->s->V,
+                     p->W, out);
+  EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
 
@@ -1158,7 +1276,7 @@ int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, ui
   const uint32_t V = (uint32_t)p->s->V;
   EGR_HIP(hipMemsetAsync(p->counter, 0, sizeof(unsigned long long), st));
   hipLaunchKernelGGL(induced_kernel, dim3((V + 255) / 256), dim3(256), 0, st, p->s->row_ptr,
-                     p->s->col, p->s->meta, p->reach[p->rcur] + (size_t)(col >> 6) * V,
+                     p->s->col, p->s->meta, p->reach[p->rcur] + (col >> 6), (uint32_t)p->RS,
                      1ull << (col & 63), V, out_src, out_dst, out_type, cap, p->counter);
   EGR_CHECK_LAUNCH();
   unsigned long long n = 0;

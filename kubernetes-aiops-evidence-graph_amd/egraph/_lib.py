@@ -105,6 +105,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_plan_reach_hop": (C.c_int, [P, P]),
     "egr_plan_step": (C.c_int, [P, P]),
     "egr_plan_final_step": (C.c_int, [P, I32, P]),
+    "egr_plan_candidates": (C.c_int, [P, I32, P]),
     "egr_plan_topk": (C.c_int, [P, I32, P, P, P]),
     "egr_plan_run": (C.c_int, [P, I32, I32, P, P, P]),
     "egr_plan_read_scores": (C.c_int, [P, P, P]),

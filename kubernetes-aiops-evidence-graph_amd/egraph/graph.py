@@ -275,13 +275,18 @@ class Plan:
         L.check(L.lib.egr_plan_hop(self._h, self._st(stream)), "egr_plan_hop")
 
     def step(self, stream=None):
-        """One hop of propagation and reachability (one fused pass when TW == 64)."""
+        """One hop of propagation and one of reachability (egr_plan_step)."""
         L.check(L.lib.egr_plan_step(self._h, self._st(stream)), "egr_plan_step")
 
     def final_step(self, exclude_label: int = -1, stream=None):
         """The last hop: step() plus the top-k candidate lists for topk(exclude_label)."""
         L.check(L.lib.egr_plan_final_step(self._h, exclude_label, self._st(stream)),
                 "egr_plan_final_step")
+
+    def candidates(self, exclude_label: int = -1, stream=None):
+        """Top-k candidate lists from the current reach sets (no hop)."""
+        L.check(L.lib.egr_plan_candidates(self._h, exclude_label, self._st(stream)),
+                "egr_plan_candidates")
 
     def reach_hop(self, stream=None):
         L.check(L.lib.egr_plan_reach_hop(self._h, self._st(stream)), "egr_plan_reach_hop")

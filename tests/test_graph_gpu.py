@@ -39,9 +39,10 @@ def _dev(a):
     return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
 
 
-@pytest.mark.parametrize("B", [1, 5, 16, 37, 64, 130])
+# B spans every reach row width: RG = 1 (B <= 128), 2, 4, 8, 16, 32 and 64 lanes x 16 B
+@pytest.mark.parametrize("B", [1, 5, 16, 37, 64, 130, 257, 600, 1100, 2100, 4200])
 def test_propagation_reach_topk_equal_oracle(B):
-    g, sv, sc, ss, src = _small_world(B)
+    g, sv, sc, ss, src = _small_world(B, pods=3000 if B <= 600 else 800)
     snap = g.snapshot()
     plan = snap.plan(B, max_seeds=len(sv), k=10)
     plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
@@ -90,7 +91,7 @@ def test_tile_width_override(tw, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [64, 128])
-def test_unfused_and_fused_steps_agree(B):
+def test_step_equals_hop_plus_reach_hop(B):
     g, sv, sc, ss, src = _small_world(B, seed=21, pods=2000)
     csr = g.csr()
     exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
@@ -108,6 +109,36 @@ def test_unfused_and_fused_steps_agree(B):
                 plan.reach_hop()
         assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
         np.testing.assert_array_equal(plan.read_reach().cpu().numpy().view(np.uint64), exp_r)
+
+
+@pytest.mark.parametrize("exclude", [-1, "Incident", "Pod"])
+def test_candidates_entry_point_and_exclusions(exclude):
+    """hop/reach_hop driven by the caller, then candidates() + topk(): same as the oracle for
+    every exclusion (candidate lists are rebuilt when the exclusion changes)."""
+    B = 150
+    g, sv, sc, ss, src = _small_world(B, seed=41, pods=1200)
+    ex = g.labels().index(exclude) if isinstance(exclude, str) else exclude
+    plan = g.snapshot().plan(B, max_seeds=len(sv), k=7)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    for _ in range(3):
+        plan.hop()
+        plan.reach_hop()
+    plan.candidates(ex)
+    ids, scores = plan.topk(ex)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    vl, _, _, _ = g.export()
+    eids, esc = oracle.topk(exp, er, vl, ex, 7)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), eids)
+    np.testing.assert_array_equal(scores.cpu().numpy(), esc)
+    # a different exclusion than the lists were built for falls back to the full scan
+    other = -1 if ex != -1 else g.labels().index("Incident")
+    ids2, sc2 = plan.topk(other)
+    eids2, esc2 = oracle.topk(exp, er, vl, other, 7)
+    np.testing.assert_array_equal(ids2.cpu().numpy().view(np.uint32), eids2)
+    np.testing.assert_array_equal(sc2.cpu().numpy(), esc2)
 
 
 def test_hub_rows_longer_than_the_lds_stage():
