@@ -2,9 +2,16 @@
 
 One step = one pass of the hot path over one batch of B incidents whose inputs are already
 resident in HBM (encoded evidence rows, seed triples, incident vertices), on one stream:
-  egr_rules_eval (A1-A6, fused ranker)  ->  egr_plan_set_seeds (radix sort + max-combine)
-  ->  egr_plan_set_sources  ->  3 x (egr_plan_hop + egr_plan_reach_hop)
-  ->  egr_plan_candidates (top-k candidate lists)  ->  egr_plan_topk.
+  --engine frontier (default):
+    egr_rules_eval (A1-A6, fused ranker)  ->  egr_frontier_set_seeds (radix sort by (column,
+    vertex) + max-combine)  ->  egr_frontier_run (per column: 3-hop reach + 3-hop propagation
+    + top-k in one workgroup, LDS hash table; overflow columns in the global-memory variant)
+  --engine dense:
+    egr_rules_eval  ->  egr_plan_set_seeds  ->  egr_plan_set_sources
+    ->  3 x (egr_plan_hop + egr_plan_reach_hop)  ->  egr_plan_candidates  ->  egr_plan_topk.
+Both engines produce bit-identical scores, reach sets and top-k (tests/test_frontier_gpu.py).
+The default run also times a few dense steps after the timed region and reports them under
+"dense_engine" (with the dense hop kernel's HBM roofline) for comparison.
 Workload: BASELINE.json configs[2] (C3: 100k pods / 100 namespaces / 2k nodes / 10k
 deployments / 10k services, Event/LogPattern/MetricAnomaly vertices; synthetic, seeded).
 Multi-GPU (torchrun): every rank holds the snapshot and ranks its own B incidents -- incidents
@@ -58,14 +65,30 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device):
     with torch.cuda.device(dev):
         snap = g.snapshot(device=dev)
         plan = snap.plan(B, max_seeds=len(sv), k=k)
+        fr = snap.frontier(B, max_seeds=len(sv), k=k)
         rules = RulesDeviceBatch(enc, catalog.default(), dev)
         seeds = tuple(to_device(a, dev) for a in (sv, sc, ss))
         sources = to_device(src, dev)
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
-    return dict(graph=g, snap=snap, plan=plan, rules=rules, seeds=seeds, sources=sources,
+    return dict(graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence)
+
+
+def step_frontier(ctx, hops: int, ev=None):
+    """One pass; `ev` (list) collects (start, end) events around the frontier run."""
+    fr = ctx["frontier"]
+    ctx["rules"].launch()
+    fr.set_seeds(*ctx["seeds"])
+    if ev is not None:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fr.run(ctx["sources"], hops, ctx["inc_label"])
+        b.record()
+        ev.append((a, b))
+    else:
+        fr.run(ctx["sources"], hops, ctx["inc_label"])
 
 
 def step(ctx, hops: int, ev=None):
@@ -124,6 +147,58 @@ def cpu_baseline(ctx, hops: int, k: int, threads: int):
                                             "HypothesisRanker; the reference's CPU path)"}}
 
 
+def _traffic(name: str):
+    """HBM bytes per launch from a committed PMC summary (scripts/pmc_passes.sh), if any."""
+    pmc = REPO / "profiles" / f"pmc_{name}.json"
+    if pmc.is_file():
+        return json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+    return None
+
+
+def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
+    # SURVEY §8d compulsory bytes of one propagation hop: CSR (col + type) once, row_ptr,
+    # scores read once and written once; gathers beyond the one compulsory read are not counted
+    hop_bytes = nnz * 5 + (V + 1) * 4 + 2 * V * B * 4
+    achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": f"hop_kernel<{ctx['plan'].tile_width // 4},false> "
+                                      "(dense propagation hop + seed_add)",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("hop"),
+            "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes}
+
+
+def frontier_roofline(ctx, run_ms: float, B: int, k: int) -> tuple[dict, dict]:
+    """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
+    (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
+    (8 B), the unique seeds (vertex + value, 8 B), the member pool written (vertex, score,
+    depth: 9 B) and the top-k output (8 B per slot)."""
+    work = ctx["frontier"].stats()
+    n_seeds = work["unique_seeds"]
+    nbytes = (8 * work["pull_entries"] + 4 * work["expand_entries"] + 8 * work["rows"]
+              + 8 * n_seeds + 9 * work["members"] + 8 * B * k)
+    achieved = nbytes / (run_ms * 1e-3) / 1e9
+    return ({"bound": "hbm", "kernel": "frontier_lds_kernel + frontier_global_kernel "
+                                       "(egr_frontier_run: reach + propagation + top-k)",
+             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("frontier"),
+             "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes}, work)
+
+
+def time_dense(ctx, hops: int, steps: int, B: int, V: int, nnz: int, dev) -> dict:
+    """A few dense-engine steps after the timed region, for comparison (not `value`)."""
+    step(ctx, hops)
+    torch.cuda.synchronize(dev)
+    ev: list = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(ctx, hops, ev)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    hop_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return {"ms_per_step": ms, "incidents_per_sec": B / (ms * 1e-3), "steps": steps,
+            "roofline": dense_roofline(ctx, hop_ms, B, V, nnz)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +210,9 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--engine", default="frontier", choices=["frontier", "dense"])
+    ap.add_argument("--dense-steps", type=int, default=5,
+                    help="dense-engine steps timed after the main run for comparison (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,7 +228,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     ctx = setup(args.config, args.batch, args.k, rank, dev)
-    run_step = step
+    run_step = step_frontier if args.engine == "frontier" else step
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
@@ -174,15 +252,11 @@ def main():
     B, V = args.batch, ctx["snap"].n_vertices
     nnz = ctx["snap"].n_entries
     ms = elapsed / args.steps * 1e3
-    hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    # SURVEY §8d compulsory bytes of one propagation hop: CSR (col + type) once, row_ptr,
-    # scores read once and written once; gathers beyond the one compulsory read are not counted
-    hop_bytes = nnz * 5 + (V + 1) * 4 + 2 * V * B * 4
-    achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = REPO / "profiles" / "pmc_hop.json"
-    if pmc.is_file():
-        traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if args.engine == "frontier":
+        roof, work = frontier_roofline(ctx, launch_ms, B, args.k)
+    else:
+        roof, work = dense_roofline(ctx, launch_ms, B, V, nnz), None
     out = {
         "metric": METRIC,
         "value": world * B / (ms * 1e-3),
@@ -196,21 +270,26 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
+        # edge = one directed CSR entry processed in one hop for one column
+        # (dense-equivalent, 3*nnz*B per step); edges_traversed_per_sec counts the CSR entries
+        # the engine actually read
         "edges_per_sec": world * args.hops * nnz * B / (ms * 1e-3),
         "config": {
             "workload": f"{args.config}: 100k-pod multi-namespace graph, full rule set + "
                         f"{args.hops}-hop typed propagation + reach + top-{args.k}, "
                         f"{B} incidents per GPU per step",
+            "engine": args.engine,
             "vertices": V, "csr_entries": nnz, "incidents_per_gpu": B,
             "evidence_rows_per_gpu": ctx["enc"].n_rows, "seeds_per_gpu": int(len(ctx["seed_host"][0])),
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
         },
-        "roofline": {"bound": "hbm", "kernel": f"hop_kernel<{ctx['plan'].tile_width // 4},false> "
-                               "(dense propagation hop + seed_add)",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes},
+        "roofline": roof,
     }
+    if work is not None:
+        out["edges_traversed_per_sec"] = world * (work["pull_entries"] + work["expand_entries"]) / (ms * 1e-3)
+        out["frontier_work"] = work
+    if args.engine == "frontier" and args.dense_steps > 0:
+        out["dense_engine"] = time_dense(ctx, args.hops, args.dense_steps, B, V, nnz, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
         out["cpu_baseline"] = cpu_baseline(ctx, args.hops, args.k, threads)

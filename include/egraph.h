@@ -237,6 +237,49 @@ int egr_plan_read_reach(const egr_plan* p, uint64_t* out, void* stream);
 int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, uint32_t* out_dst,
                            uint8_t* out_type, int64_t cap, int64_t* out_n, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Frontier engine: the same A8 + A9 + top-k results as a plan's egr_plan_run, computed per
+ * incident column over only the vertices the column touches (one workgroup per column, the
+ * column's state in an LDS hash table).  Scores, reach sets and top-k are
+ * bit-identical to the dense plan's.  Replaces, like the plan, apoc.path.subgraphAll
+ * (neo4j.py:169-202) plus the build-defined propagation / top-k.
+ *   egr_frontier_create : pool_entries = capacity of the member pool that keeps every
+ *                         column's (vertex, score, depth) for the read functions; 0 picks
+ *                         n_cols*4096 + 4V.  Columns that do not fit are still ranked.
+ *   egr_frontier_run    : one pass; sources [n_cols] device; outputs [n_cols*k] as
+ *                         egr_plan_topk (EGR_NO_NODE / -inf in unused slots).
+ *   egr_frontier_stats  : synchronous; out[8] of the last run = CSR entries gathered by
+ *                         pulls (col + val read), CSR entries read by expansions (col only),
+ *                         rows walked (row_ptr pairs), members, columns that overflowed the
+ *                         LDS table (redone by the global-memory variant), pool entries
+ *                         used, unique seeds, 0.
+ *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
+ *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
+ *                         members did not fit the pool reads as all zero.
+ *   egr_frontier_members: one column's members (unordered); depth = hops from the incident
+ *                         vertex + 1, 0 = not reached.  Synchronous.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct egr_frontier egr_frontier;
+
+int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
+                        int64_t pool_entries, egr_frontier** out);
+void egr_frontier_free(egr_frontier* f);
+int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const uint32_t* seed_col,
+                           const float* seed_val, int64_t n_seeds, void* stream);
+int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hops,
+                     int32_t exclude_label, uint32_t* out_ids, float* out_scores, void* stream);
+int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream);
+int egr_frontier_read_scores(const egr_frontier* f, float* out, void* stream);
+/* Diagnostics: with $EGRAPH_FRONTIER_PROFILE set when the frontier was created, each column's
+ * workgroup stamps s_memrealtime (100 MHz) at its phase boundaries: per column and slot, the
+ * stamp after the barrier then each wave's stamp before it.  Copies [n_cols][slots][1+waves]
+ * (0 = unused) into out (cap entries) and returns the int64 count per column (0: off).    */
+int egr_frontier_phase_times(const egr_frontier* f, int64_t* out, int64_t cap, void* stream);
+int egr_frontier_read_reach(const egr_frontier* f, uint64_t* out, void* stream);
+int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_vertex,
+                         float* out_score, uint8_t* out_depth, int64_t cap, int64_t* out_n,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

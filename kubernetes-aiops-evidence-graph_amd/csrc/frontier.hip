@@ -1,0 +1,994 @@
+// Frontier engine: the whole graph stage of one incident column -- apoc-style k-hop reach
+// (A8, src/database/neo4j.py:169-202), typed k-hop propagation (A9) and the
+// per-incident top-k -- in ONE workgroup, with the incident's state in an LDS hash table.
+//
+// Why: a column's scores are non-zero only within `hops` hops of its seeds.  On the 100k-pod
+// graph that is ~1.9k of 229k vertices after 3 hops (0.8 %), so the dense [V x B] sweep of
+// propagate.hip spends >99 % of its HBM bytes on exact zeros.  Here a workgroup keeps only the
+// touched vertices: key = vertex id, s = current score, fl = reach depth + 1 (0 = not reached).
+//
+// Exactness (bit-identical to the dense plan and to oracle/egraph_oracle.c): for every member
+// v the pull  s'[v] = sum_{e in row v, CSR order} fmaf(val_e, s[col_e], acc)  then  s'[v] + s0[v]
+// is the dense recurrence with the terms of non-members skipped; a non-member's dense value is
+// exactly +0 and fmaf(w, +0, acc) == acc for finite w and acc != -0 (acc starts at +0 and can
+// never become -0 under round-to-nearest), so skipping them changes no bit.  Members are
+// (seeds) U (N(u) for every member u with s[u] != 0) U (reach set), which contains every
+// vertex whose dense value can be non-zero.
+//
+// Work layout: a hop is two phases over the member list, GROW (the reach level and the
+// expansion of the non-zero members insert their neighbours) and PULL (the members an
+// expansion touched recompute their score).  A wave takes 64 members at a time: a row of <= 16
+// entries is one lane's, which loads and probes all its entries at once and runs the in-order
+// fmaf chain in registers; a longer (hub) row is taken by the whole wave, 64 entries per round,
+// with the chain run over v_readlane operands.  Top-k packs (score, vertex) into one u64 key:
+// each wave extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
+//
+// Capacity: the LDS table holds 6144 slots (keys, scores, depths, member list: ~70 KB, two
+// workgroups per CU); a column with more than 4608 members is flagged and redone by the
+// global-memory variant of the same code (a table of >= 2V slots per resident workgroup, never
+// overflows), launched unconditionally right after (it drains an empty work list at once).
+#include <algorithm>
+#include <type_traits>
+#include <vector>
+
+#include "graph_dev.h"
+
+using egr::DeviceGuard;
+using egr::dalloc;
+using egr::dfree;
+
+namespace {
+
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t NO_NODE = EGR_NO_NODE;
+constexpr int FT = 512;                     // threads per workgroup (8 waves)
+constexpr int NWAVES = FT / 64;
+constexpr uint32_t LCAP = 6144;             // LDS table slots
+constexpr uint32_t LLIMIT = 4608;           // members before a column overflows (load 0.75)
+constexpr int LPPT = LCAP / FT;             // slots cleared per thread
+constexpr int LMAX = 16;                    // rows up to this many entries run one lane per row
+constexpr int LB = 4;                       // keys probed together per lane
+constexpr uint32_t BLOOM_WORDS = 2048;      // 64 Kbit filter: rejects absent keys in one read
+constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
+constexpr int KMAXF = 16;
+constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
+constexpr int MAX_HOPS = 60;
+constexpr int PROF_SLOTS = 32;
+constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
+
+
+struct FArgs {
+  const uint32_t* row_ptr;
+  const uint2* cv;             // (col, val bits) per CSR entry
+  const uint8_t* vlabel;
+  uint32_t V;
+  int B, hops, k, exclude;
+  const uint32_t* seed_ptr;    // [B+1] per column
+  const uint32_t* seed_vert;   // unique vertices, ascending within a column
+  const float* seed_val;       // max-combined s0
+  const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
+  uint32_t* out_ids;           // [B*k]
+  float* out_scores;
+  // member pool: every column's (vertex, score, depth+1) after the last hop
+  uint32_t* pool_v;
+  float* pool_s;
+  uint8_t* pool_d;
+  unsigned long long pool_cap;
+  unsigned long long* pool_ctr;
+  unsigned long long* mem_off;  // [B]
+  uint32_t* mem_cnt;            // [B], EGR_NO_NODE = not kept (pool full)
+  // overflow work list
+  uint32_t* ovf_list;
+  uint32_t* ovf_n;
+  uint32_t* ovf_next;
+  float* lsnew;                 // [B][LLIMIT] pull results of the LDS variant (by member index)
+  // global tables (one per resident workgroup of the fallback kernel)
+  uint32_t* gkeys;              // [nbig][gcap]
+  float* gs;                    // [nbig][gcap]
+  uint8_t* gfl;                 // [nbig][gcap]
+  uint8_t* gneed;               // [nbig][gcap]
+  uint32_t* gmlist;             // [nbig][V]
+  float* gsnew;                 // [nbig][V]
+  uint32_t gcap;
+  unsigned long long* prof;     // [B][PROF_SLOTS] wall-clock stamps per phase, or nullptr
+  // [0] CSR entries gathered by pulls (col + val), [1] entries read by expansions (col),
+  // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed
+  unsigned long long* stats;
+};
+
+// The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
+// insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
+// index.
+template <bool GT>
+struct Tab {
+  using MT = typename std::conditional<GT, uint32_t, uint16_t>::type;
+  uint32_t* keys;
+  float* s;
+  uint8_t* fl;
+  uint8_t* need;    // touched by an expansion this hop: pulled
+  MT* mlist;
+  float* snew;
+  uint32_t cap, limit;
+  uint32_t* count;  // LDS
+  uint32_t* ovf;    // LDS
+  uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
+};
+
+// Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
+// insert CASes the lowest empty slot it sees and moves on only when that slot is taken, so a
+// bucket with an empty slot ends every probe sequence that passes through it.
+__device__ __forceinline__ uint32_t hbucket(uint32_t v, uint32_t nb) {
+  return __umulhi(v * 0x9E3779B1u, nb);    // multiplicative hash, range-reduced to [0, nb)
+}
+
+__device__ __forceinline__ uint4 read_bucket(const uint32_t* keys, uint32_t bk) {
+  return reinterpret_cast<const uint4*>(keys)[bk];
+}
+
+// outcome of one bucket read for key v: slot (>= 0), -1 = absent, -2 = continue probing
+__device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_t bk) {
+  if (kk.x == v) return (int)(4 * bk);
+  if (kk.y == v) return (int)(4 * bk + 1);
+  if (kk.z == v) return (int)(4 * bk + 2);
+  if (kk.w == v) return (int)(4 * bk + 3);
+  if (kk.w == EMPTY) return -1;            // slots fill in order: an empty last slot ends it
+  return -2;
+}
+
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) { return (v * 0x85EBCA6Bu) >> 16; }
+
+// slot of v, inserting it if absent (-1: table full)
+template <bool GT>
+__device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk = hbucket(v, nb);
+  for (uint32_t n = 0; n < nb; ++n) {
+    uint4 kk = read_bucket(t.keys, bk);
+    uint32_t ks[4] = {kk.x, kk.y, kk.z, kk.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ks[j] == v) return (int)(4 * bk + j);
+      if (ks[j] == EMPTY) {
+        const uint32_t p = 4 * bk + j;
+        const uint32_t old = atomicCAS(&t.keys[p], EMPTY, v);
+        if (old == EMPTY) {
+          if constexpr (!GT) {
+            const uint32_t h = bloom_hash(v);
+            atomicOr(&t.bloom[h >> 5], 1u << (h & 31u));
+          }
+          const uint32_t c = atomicAdd(t.count, 1u);
+          if (c < t.limit) t.mlist[c] = (typename Tab<GT>::MT)p;
+          else *t.ovf = 1u;
+          return (int)p;
+        }
+        if (old == v) return (int)p;
+        // taken by another key: look at the next slot
+      }
+    }
+    bk = bk + 1 == nb ? 0 : bk + 1;
+  }
+  *t.ovf = 1u;
+  return -1;
+}
+
+// slot of v or -1 (only called while no insertion is in flight)
+template <bool GT>
+__device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
+  if constexpr (!GT) {
+    const uint32_t h = bloom_hash(v);
+    if (!((t.bloom[h >> 5] >> (h & 31u)) & 1u)) return -1;
+  }
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk = hbucket(v, nb);
+  for (uint32_t n = 0; n < nb; ++n) {
+    const int r = bucket_match(read_bucket(t.keys, bk), v, bk);
+    if (r != -2) return r;
+    bk = bk + 1 == nb ? 0 : bk + 1;
+  }
+  return -1;
+}
+
+struct Work {
+  uint32_t pull = 0, expand = 0, rows = 0;
+};
+
+// diagnostics: per-wave sums of sub-step times (profiling builds of a phase only)
+struct Ticker {
+  bool on = false;
+  uint64_t t0 = 0;
+  uint64_t sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void tick(int k) {
+    if (on) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t t1 = wall_clock64();
+      sub[k] += t1 - t0;
+      t0 = t1;
+    }
+  }
+};
+
+enum Phase { GROW, PULL };
+
+// Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
+// still unresolved, so a lane's NQ probe sequences share round trips.
+template <bool GT, int NQ>
+__device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
+                                           int (&q)[NQ]) {
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk[NQ];
+  uint32_t pend = 0;
+#pragma unroll
+  for (int x = 0; x < NQ; ++x) {
+    bk[x] = hbucket(key[x], nb);
+    q[x] = -1;
+    if ((uint32_t)x < nq) pend |= 1u << x;
+  }
+  if constexpr (!GT) {
+    // the filter: a key whose bit is clear is not a member (most pulled neighbours are not)
+    uint32_t bw[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      bw[x] = (pend & (1u << x)) ? t.bloom[bloom_hash(key[x]) >> 5] : ~0u;
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      if (!((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u)) pend &= ~(1u << x);
+  }
+  for (uint32_t n = 0; n < nb && __any(pend != 0); ++n) {
+    uint4 kk[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      if (pend & (1u << x)) kk[x] = read_bucket(t.keys, bk[x]);
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) {
+      if (pend & (1u << x)) {
+        const int r = bucket_match(kk[x], key[x], bk[x]);
+        if (r != -2) {
+          q[x] = r;
+          pend &= ~(1u << x);
+        } else {
+          bk[x] = bk[x] + 1 == nb ? 0 : bk[x] + 1;
+        }
+      }
+    }
+  }
+}
+
+// Pull (PULL) or neighbour insertion (GROW) of a row of dl <= LMAX entries, one lane per row:
+// every entry is loaded in one round trip, then probed LB keys at a time (lockstep), and the
+// in-order fmaf chain runs in registers.
+template <bool GT, Phase PH>
+__device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
+                                          uint32_t kind, int level, float& acc, Ticker& tk) {
+  uint32_t c[LMAX];
+  float w[LMAX];
+#pragma unroll
+  for (int x = 0; x < LMAX; ++x) {
+    uint2 ce = make_uint2(0u, 0u);
+    if ((uint32_t)x < dl) ce = A.cv[e0 + x];
+    c[x] = ce.x;
+    w[x] = __uint_as_float(ce.y);
+  }
+  tk.tick(4);
+#pragma unroll
+  for (int sb = 0; sb < LMAX / LB; ++sb) {
+    if (!__any(dl > (uint32_t)(sb * LB))) continue;   // (continue, not break: keeps it unrolled)
+    const uint32_t nq = dl > (uint32_t)(sb * LB) ? min(dl - sb * LB, (uint32_t)LB) : 0u;
+    uint32_t key[LB];
+#pragma unroll
+    for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
+    int q[LB];
+    find_batch<GT, LB>(t, key, nq, q);
+    tk.tick(5);
+    if constexpr (PH == PULL) {
+      float xs[LB];
+#pragma unroll
+      for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
+#pragma unroll
+      for (int x = 0; x < LB; ++x)
+        if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
+      tk.tick(6);
+    } else {
+#pragma unroll
+      for (int x = 0; x < LB; ++x) {
+        if ((uint32_t)x < nq) {
+          const int qq = q[x] >= 0 ? q[x] : tab_insert<GT>(t, key[x]);
+          if (qq >= 0) {
+            if ((kind & 1u) && t.fl[qq] == 0) t.fl[qq] = (uint8_t)(level + 1);
+            if (kind & 2u) t.need[qq] = 1;
+          }
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// The rows of the selected members of [0, n): a wave takes 64 members at a time.
+//   GROW (hop h, reach level l = h + 1): members at reach depth l and members with s != 0
+//         insert their neighbours; a neighbour of a depth-l member without a depth gets l + 1,
+//         a neighbour of a non-zero member is marked `need` (it is pulled at this hop).
+//   PULL: every `need` member's sum over its row, CSR order, of val * s[neighbour]
+//         (non-members skipped: exact, see the file comment) -> snew[member index].
+// Rows of <= LMAX entries run one lane per row (light_row); longer rows (hubs) run one at a
+// time across the whole wave: 64 entries loaded and probed per round, then the fmaf chain in
+// order over v_readlane operands (every lane computes the same chain; the owner keeps it).
+template <bool GT, Phase PH>
+__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int level, Work& work,
+                          int b = -1) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
+  Ticker tk;
+  tk.on = A.prof && b >= 0;
+  if (tk.on) tk.t0 = wall_clock64();
+  // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
+  // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves
+  for (uint32_t k0 = 0; k0 * FT < n; ++k0) {
+    const uint32_t i = wave + NWAVES * (lane + 64u * k0);
+    uint32_t v = 0, e0 = 0, deg = 0, kind = 0;   // kind: bit 0 reach frontier, bit 1 non-zero
+    if (i < n) {
+      const uint32_t p = t.mlist[i];
+      v = t.keys[p];
+      if constexpr (PH == GROW) {
+        kind = (t.fl[p] == (uint8_t)level ? 1u : 0u) | (t.s[p] != 0.f ? 2u : 0u);
+      } else {
+        kind = t.need[p];
+      }
+    }
+    if (kind) {
+      e0 = A.row_ptr[v];
+      deg = A.row_ptr[v + 1] - e0;
+      ++work.rows;
+      if constexpr (PH == PULL) work.pull += deg;
+      else work.expand += deg;
+    }
+    tk.tick(0);
+    const bool light = deg <= (uint32_t)LMAX;
+    float acc = 0.f;
+    light_row<GT, PH>(A, t, e0, light ? deg : 0u, kind, level, acc, tk);
+    tk.tick(1);
+    uint64_t heavy = __ballot(!light);
+    while (heavy) {
+      const int m = __ffsll((long long)heavy) - 1;
+      heavy &= heavy - 1;
+      const uint32_t he0 = __builtin_amdgcn_readlane(e0, m);
+      const uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
+      const uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
+      float hacc = 0.f;
+      for (uint32_t base = 0; base < hdeg; base += 64) {
+        const uint32_t j = base + lane;
+        const bool act = j < hdeg;
+        const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
+        const uint32_t u = ce.x;
+        if constexpr (PH == PULL) {
+          const float w = __uint_as_float(ce.y);
+          float x = 0.f;
+          bool found = false;
+          if (act) {
+            const int q = tab_find<GT>(t, u);
+            found = q >= 0;
+            if (found) x = t.s[q];
+          }
+          // the chain runs over the present entries only, in lane (= CSR) order
+          for (uint64_t fm = __ballot(found); fm; fm &= fm - 1) {
+            const int y = __ffsll((long long)fm) - 1;
+            hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
+          }
+        } else if (act) {
+          const int q = tab_insert<GT>(t, u);
+          if (q >= 0) {
+            if ((hkind & 1u) && t.fl[q] == 0) t.fl[q] = (uint8_t)(level + 1);
+            if (hkind & 2u) t.need[q] = 1;
+          }
+        }
+      }
+      if (lane == m) acc = hacc;
+    }
+    tk.tick(2);
+    if constexpr (PH == PULL) {
+      if (kind) t.snew[i] = acc;
+    }
+    tk.tick(3);
+  }
+  if (tk.on && lane == 0)
+    for (int k = 0; k < 8; ++k)
+      A.prof[((size_t)b * PROF_SLOTS + 24 + k) * PROF_W + 1 + wave] = tk.sub[k];
+}
+
+// ---- top-k keys: (score desc, vertex asc) as one u64, larger = better, 0 = none -----------
+__device__ __forceinline__ uint64_t topk_key(float s, uint32_t v) {
+  const uint32_t f = __float_as_uint(s);
+  const uint32_t o = (f & 0x80000000u) ? ~f : (f | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)~v;
+}
+
+__device__ __forceinline__ void topk_unkey(uint64_t k, float& s, uint32_t& v) {
+  if (k == 0) {
+    s = -INFINITY;
+    v = NO_NODE;
+    return;
+  }
+  const uint32_t o = (uint32_t)(k >> 32);
+  s = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+  v = ~(uint32_t)k;
+}
+
+#define EGR_DPP_MAX64(CTRL, RM)                                                            \
+  {                                                                                        \
+    const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, RM, \
+                                                               0xF, false);                \
+    const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, RM, \
+                                                               0xF, false);                \
+    if (ohi > hi || (ohi == hi && olo > lo)) {                                             \
+      hi = ohi;                                                                            \
+      lo = olo;                                                                            \
+    }                                                                                      \
+  }
+
+// wave-wide max of a u64 with DPP row ops (quad perms, half / full row mirror, row
+// broadcasts 15 and 31); every lane gets the result
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  EGR_DPP_MAX64(0xB1, 0xF)    // quad_perm [1,0,3,2]
+  EGR_DPP_MAX64(0x4E, 0xF)    // quad_perm [2,3,0,1]
+  EGR_DPP_MAX64(0x141, 0xF)   // row_half_mirror
+  EGR_DPP_MAX64(0x140, 0xF)   // row_mirror
+  EGR_DPP_MAX64(0x142, 0xA)   // row_bcast:15
+  EGR_DPP_MAX64(0x143, 0xC)   // row_bcast:31
+  lo = __builtin_amdgcn_readlane(lo, 63);
+  hi = __builtin_amdgcn_readlane(hi, 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+struct Shared {
+  uint32_t count, ovf, item;
+  unsigned long long base;
+  uint64_t top[NWAVES][KMAXF];
+  uint32_t w_pull, w_expand, w_rows;
+};
+
+// candidate key of member slot p: reached within `hops`, not carrying the excluded label
+template <bool GT>
+__device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, uint32_t p,
+                                             uint8_t maxd) {
+  const uint8_t f = t.fl[p];
+  if (f < 1 || f > maxd) return 0;
+  const uint32_t v = t.keys[p];
+  if (A.exclude >= 0 && A.vlabel[v] == (uint8_t)A.exclude) return 0;
+  return topk_key(t.s[p], v);
+}
+
+// This thread's best candidate key strictly below `bound` (global variant: rescans).
+template <bool GT>
+__device__ __forceinline__ uint64_t rescan_best(const FArgs& A, const Tab<GT>& t, uint32_t n,
+                                                uint8_t maxd, uint64_t bound) {
+  uint64_t b = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += FT) {
+    const uint64_t kk = cand_key<GT>(A, t, t.mlist[i], maxd);
+    if (kk < bound && kk > b) b = kk;
+  }
+  return b;
+}
+
+// Per-wave top-k into sh.top[wave][0..k) (k wave-wide max rounds, no block barrier).
+template <bool GT>
+__device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shared& sh, uint32_t n,
+                                          uint8_t maxd) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if constexpr (!GT) {
+    uint64_t kk[MPT];
+#pragma unroll
+    for (int j = 0; j < MPT; ++j) {
+      const uint32_t i = threadIdx.x + j * FT;
+      kk[j] = i < n ? cand_key<GT>(A, t, t.mlist[i], maxd) : 0ull;
+    }
+    auto best = [&]() {
+      uint64_t b = 0;
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) b = kk[j] > b ? kk[j] : b;
+      return b;
+    };
+    uint64_t lb = best();
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t wb = wave_max_u64(lb);
+      if (lane == 0) sh.top[wave][q] = wb;
+      if (wb == 0) {                         // uniform: no candidate left in this wave
+        for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+        break;
+      }
+      if (lb == wb) {
+#pragma unroll
+        for (int j = 0; j < MPT; ++j)
+          if (kk[j] == wb) kk[j] = 0;
+        lb = best();
+      }
+    }
+  } else {
+    uint64_t lb = rescan_best<GT>(A, t, n, maxd, ~0ull);
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t wb = wave_max_u64(lb);
+      if (lane == 0) sh.top[wave][q] = wb;
+      if (wb == 0) {
+        for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+        break;
+      }
+      if (lb == wb) lb = rescan_best<GT>(A, t, n, maxd, wb);
+    }
+  }
+}
+
+// One column end to end.  Returns false (uniformly) if the table overflowed.
+template <bool GT>
+__device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b) {
+  const uint32_t tid = threadIdx.x;
+  const int hops = A.hops;
+  Work work;
+  // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
+  // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
+  int slot = 0;
+  auto stamp = [&]() {
+    if (A.prof && tid == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
+    ++slot;
+  };
+  auto wstamp = [&]() {
+    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
+  };
+  stamp();
+  // seeds (s = s0) and the incident vertex (depth 0)
+  const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_insert<GT>(t, A.seed_vert[i]);
+    if (q >= 0) t.s[q] = A.seed_val[i];
+  }
+  if (tid == 0) {
+    const uint32_t src = A.sources[b];
+    if (src < A.V) {
+      const int q = tab_insert<GT>(t, src);
+      if (q >= 0) t.fl[q] = 1;
+    }
+  }
+  wstamp();
+  __syncthreads();
+  stamp();
+  if (sh.ovf) return false;
+  // hop h: grow (reach level h + 1 and the expansion of the non-zero members), then pull
+  for (int h = 0; h < hops; ++h) {
+    row_phase<GT, GROW>(A, t, sh.count, h + 1, work, -1);
+    wstamp();
+    __syncthreads();
+    stamp();
+    if (sh.ovf) return false;
+    const uint32_t n = sh.count;
+    row_phase<GT, PULL>(A, t, n, 0, work, h == hops - 1 ? b : -1);
+    wstamp();
+    __syncthreads();
+    stamp();
+    // members no expansion touched have no non-zero neighbour: their new value is exactly +0
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      t.s[p] = t.need[p] ? t.snew[i] : 0.f;
+      t.need[p] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = sb + tid; i < se; i += FT) {
+      const int q = tab_find<GT>(t, A.seed_vert[i]);
+      if (q >= 0) t.s[q] = t.s[q] + A.seed_val[i];
+    }
+    __syncthreads();
+    stamp();
+  }
+  const uint32_t n = sh.count;
+  // top-k over the reach set: each wave its own k best, then wave 0 merges the NWAVES lists
+  const int lane = tid & 63, wave = tid >> 6;
+  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1));
+  wstamp();
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t c[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int cc = lane + 64 * y, w = cc / KMAXF, r = cc % KMAXF;
+      c[y] = (w < NWAVES && r < A.k) ? sh.top[w][r] : 0ull;
+    }
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t mine = c[0] > c[1] ? c[0] : c[1];
+      const uint64_t wb = wave_max_u64(mine);
+      if (lane == 0) {
+        float sc;
+        uint32_t v;
+        topk_unkey(wb, sc, v);
+        A.out_ids[(size_t)b * A.k + q] = v;
+        A.out_scores[(size_t)b * A.k + q] = sc;
+      }
+      if (wb != 0) {
+        if (c[0] == wb) c[0] = 0;
+        if (c[1] == wb) c[1] = 0;
+      }
+    }
+  }
+  stamp();
+  // members -> pool (coalesced by member index)
+  if (tid == 0) sh.base = atomicAdd(A.pool_ctr, (unsigned long long)n);
+  atomicAdd(&sh.w_pull, work.pull);
+  atomicAdd(&sh.w_expand, work.expand);
+  atomicAdd(&sh.w_rows, work.rows);
+  __syncthreads();
+  const unsigned long long base = sh.base;
+  const bool keep = base + n <= A.pool_cap;
+  if (keep) {
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      A.pool_v[base + i] = t.keys[p];
+      A.pool_s[base + i] = t.s[p];
+      A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
+    }
+  }
+  if (tid == 0) {
+    A.mem_off[b] = base;
+    A.mem_cnt[b] = keep ? n : NO_NODE;
+    atomicAdd(&A.stats[0], (unsigned long long)sh.w_pull);
+    atomicAdd(&A.stats[1], (unsigned long long)sh.w_expand);
+    atomicAdd(&A.stats[2], (unsigned long long)sh.w_rows);
+    atomicAdd(&A.stats[3], (unsigned long long)n);
+  }
+  stamp();
+  return true;
+}
+
+__global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
+  __shared__ uint32_t keys[LCAP];
+  __shared__ float s[LCAP];
+  __shared__ uint8_t fl[LCAP];
+  __shared__ uint8_t need[LCAP];
+  __shared__ uint16_t mlist[LLIMIT];
+  __shared__ uint32_t bloom[BLOOM_WORDS];
+  __shared__ Shared sh;
+  const uint32_t tid = threadIdx.x;
+  const int b = blockIdx.x;
+  for (uint32_t i = tid; i < BLOOM_WORDS; i += FT) bloom[i] = 0;
+#pragma unroll
+  for (int i = 0; i < LPPT; ++i) {
+    keys[tid + i * FT] = EMPTY;
+    s[tid + i * FT] = 0.f;
+    fl[tid + i * FT] = 0;
+    need[tid + i * FT] = 0;
+  }
+  if (tid == 0) {
+    sh.count = 0;
+    sh.ovf = 0;
+    sh.w_pull = sh.w_expand = sh.w_rows = 0;
+  }
+  __syncthreads();
+  Tab<false> t{keys, s, fl, need, mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count,
+               &sh.ovf, bloom};
+  if (!run_column<false>(A, t, sh, b) && tid == 0) {
+    A.ovf_list[atomicAdd(A.ovf_n, 1u)] = (uint32_t)b;
+    atomicAdd(&A.stats[4], 1ull);
+  }
+}
+
+// Persistent fallback: each workgroup owns one global table and drains the overflow list.
+__global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
+  __shared__ Shared sh;
+  const uint32_t tid = threadIdx.x;
+  const size_t cap = A.gcap;
+  Tab<true> t{A.gkeys + blockIdx.x * cap, A.gs + blockIdx.x * cap, A.gfl + blockIdx.x * cap,
+              A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
+              A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr};
+  const uint32_t n_items = *A.ovf_n;
+  for (;;) {
+    if (tid == 0) {
+      sh.item = atomicAdd(A.ovf_next, 1u);
+      sh.count = 0;
+      sh.ovf = 0;
+      sh.w_pull = sh.w_expand = sh.w_rows = 0;
+    }
+    __syncthreads();
+    const uint32_t item = sh.item;
+    if (item >= n_items) break;
+    const int b = (int)A.ovf_list[item];
+    if (!run_column<true>(A, t, sh, b)) {   // cannot happen: members <= V
+      for (int q = tid; q < A.k; q += FT) {
+        A.out_ids[(size_t)b * A.k + q] = NO_NODE;
+        A.out_scores[(size_t)b * A.k + q] = -INFINITY;
+      }
+      if (tid == 0) A.mem_cnt[b] = NO_NODE;
+    }
+    __syncthreads();
+    // reset the slots this column used (the table starts clean: memset at creation)
+    const uint32_t n = min(sh.count, A.V);
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      t.keys[p] = EMPTY;
+      t.s[p] = 0.f;
+      t.fl[p] = 0;
+      t.need[p] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
+__global__ void scatter_scores_kernel(const uint32_t* __restrict__ pool_v,
+                                      const float* __restrict__ pool_s,
+                                      const unsigned long long* __restrict__ mem_off,
+                                      const uint32_t* __restrict__ mem_cnt, int B,
+                                      float* __restrict__ out) {
+  const int b = blockIdx.x;
+  const uint32_t n = mem_cnt[b];
+  if (n == NO_NODE) return;
+  const unsigned long long o = mem_off[b];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    out[(size_t)pool_v[o + i] * B + b] = pool_s[o + i];
+}
+
+__global__ void scatter_reach_kernel(const uint32_t* __restrict__ pool_v,
+                                     const uint8_t* __restrict__ pool_d,
+                                     const unsigned long long* __restrict__ mem_off,
+                                     const uint32_t* __restrict__ mem_cnt, uint32_t V,
+                                     unsigned long long* __restrict__ out) {
+  const int b = blockIdx.x;
+  const uint32_t n = mem_cnt[b];
+  if (n == NO_NODE) return;
+  const unsigned long long o = mem_off[b];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (pool_d[o + i]) atomicOr(&out[(size_t)(b >> 6) * V + pool_v[o + i]], 1ull << (b & 63));
+}
+
+}  // namespace
+
+struct egr_frontier {
+  const egr_snapshot* s = nullptr;
+  int B = 0, k = 0, nbig = 0;
+  int64_t max_seeds = 0;
+  uint32_t gcap = 0;
+  egr::SeedPrep sp;
+  uint32_t* seed_ptr = nullptr;   // [B+1]
+  uint32_t* pool_v = nullptr;
+  float* pool_s = nullptr;
+  uint8_t* pool_d = nullptr;
+  unsigned long long pool_cap = 0;
+  unsigned long long* ctr = nullptr;   // [0] pool, [1..5] stats
+  unsigned long long* mem_off = nullptr;
+  uint32_t* mem_cnt = nullptr;
+  uint32_t* ovf = nullptr;             // [0] n, [1] next, [2..] list (B)
+  uint32_t* gkeys = nullptr;
+  float* gs = nullptr;
+  float* gsnew = nullptr;
+  float* lsnew = nullptr;
+  unsigned long long* prof = nullptr;   // [B][PROF_SLOTS] when $EGRAPH_FRONTIER_PROFILE is set
+  uint8_t* gfl = nullptr;
+  uint8_t* gneed = nullptr;
+  uint32_t* gmlist = nullptr;
+  bool seeds_set = false;
+  bool ran = false;
+};
+
+extern "C" {
+
+int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
+                        int64_t pool_entries, egr_frontier** out) {
+  if (!s || !out || n_cols <= 0 || n_cols > (1 << 20) || max_seeds < 0 || k < 1 || k > KMAXF ||
+      pool_entries < 0)
+    return egr::fail(EGR_EINVAL,
+                     "egr_frontier_create: bad arguments (need 0 < n_cols <= 2^20, 1 <= k <= 16)");
+  *out = nullptr;
+  DeviceGuard guard(s->device);
+  auto* f = new egr_frontier();
+  f->s = s;
+  f->B = n_cols;
+  f->k = k;
+  f->max_seeds = max_seeds;
+  const uint32_t V = (uint32_t)s->V;
+  // fallback table: 2 x nextpow2(V) slots, never more than half full
+  size_t gcap = 2 * LCAP;
+  while (gcap < 2ull * V) gcap *= 2;
+  f->gcap = (uint32_t)gcap;
+  f->nbig = std::min(n_cols, 32);
+  f->pool_cap = pool_entries > 0 ? (unsigned long long)pool_entries
+                                 : (unsigned long long)n_cols * 4096ull + 4ull * V;
+  int rc = EGR_OK;
+  if ((rc = f->sp.alloc(max_seeds, (uint64_t)n_cols * V, 1)) ||
+      (rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) ||
+      (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
+      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 6)) ||
+      (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
+      (rc = dalloc(&f->ovf, (size_t)n_cols + 2)) ||
+      (rc = dalloc(&f->gkeys, gcap * f->nbig)) || (rc = dalloc(&f->gs, gcap * f->nbig)) ||
+      (rc = dalloc(&f->gfl, gcap * f->nbig)) || (rc = dalloc(&f->gneed, gcap * f->nbig)) || (rc = dalloc(&f->gsnew, (size_t)V * f->nbig)) ||
+      (rc = dalloc(&f->gmlist, (size_t)V * f->nbig)) ||
+      (rc = dalloc(&f->lsnew, (size_t)n_cols * LLIMIT))) {
+    egr_frontier_free(f);
+    return rc;
+  }
+  if (getenv("EGRAPH_FRONTIER_PROFILE") &&
+      (rc = dalloc(&f->prof, (size_t)n_cols * PROF_SLOTS * PROF_W))) {
+    egr_frontier_free(f);
+    return rc;
+  }
+  if (hipMemset(f->gkeys, 0xFF, gcap * f->nbig * 4) != hipSuccess ||
+      hipMemset(f->gs, 0, gcap * f->nbig * 4) != hipSuccess ||
+      hipMemset(f->gfl, 0, gcap * f->nbig) != hipSuccess ||
+      hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
+      hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
+      hipMemset(f->ctr, 0, 6 * 8) != hipSuccess) {
+    egr_frontier_free(f);
+    return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
+  }
+  *out = f;
+  return EGR_OK;
+}
+
+void egr_frontier_free(egr_frontier* f) {
+  if (!f) return;
+  DeviceGuard guard(f->s->device);
+  f->sp.free_all();
+  dfree(f->seed_ptr);
+  dfree(f->pool_v);
+  dfree(f->pool_s);
+  dfree(f->pool_d);
+  dfree(f->ctr);
+  dfree(f->mem_off);
+  dfree(f->mem_cnt);
+  dfree(f->ovf);
+  dfree(f->gkeys);
+  dfree(f->gs);
+  dfree(f->gsnew);
+  dfree(f->lsnew);
+  dfree(f->prof);
+  dfree(f->gfl);
+  dfree(f->gneed);
+  dfree(f->gmlist);
+  delete f;
+}
+
+int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const uint32_t* seed_col,
+                           const float* seed_val, int64_t n_seeds, void* stream) {
+  if (!f || n_seeds < 0 || n_seeds > f->max_seeds ||
+      (n_seeds > 0 && (!seed_vertex || !seed_col || !seed_val)))
+    return egr::fail(EGR_EINVAL,
+                     "egr_frontier_set_seeds: bad arguments (n_seeds above capacity?)");
+  DeviceGuard guard(f->s->device);
+  const uint32_t V = (uint32_t)f->s->V;
+  EGR_TRY(f->sp.run(seed_vertex, seed_col, seed_val, n_seeds, V, f->B, true, (uint64_t)V,
+                    (uint32_t)f->B, f->seed_ptr, (hipStream_t)stream));
+  f->seeds_set = true;
+  return EGR_OK;
+}
+
+int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hops,
+                     int32_t exclude_label, uint32_t* out_ids, float* out_scores, void* stream) {
+  if (!f || !source_vertex || !out_ids || !out_scores || hops < 1 || hops > MAX_HOPS)
+    return egr::fail(EGR_EINVAL, "egr_frontier_run: bad arguments (need 1 <= hops <= 60)");
+  if (!f->seeds_set) return egr::fail(EGR_ESTATE, "egr_frontier_run: seeds not set");
+  DeviceGuard guard(f->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const egr_snapshot* s = f->s;
+  EGR_HIP(hipMemsetAsync(f->ctr, 0, 6 * 8, st));
+  EGR_HIP(hipMemsetAsync(f->ovf, 0, 2 * 4, st));
+  FArgs a;
+  a.row_ptr = s->row_ptr;
+  a.cv = s->cv;
+  a.vlabel = s->vlabel;
+  a.V = (uint32_t)s->V;
+  a.B = f->B;
+  a.hops = hops;
+  a.k = f->k;
+  a.exclude = exclude_label;
+  a.seed_ptr = f->seed_ptr;
+  a.seed_vert = f->sp.uminor;
+  a.seed_val = f->sp.uval;
+  a.sources = source_vertex;
+  a.out_ids = out_ids;
+  a.out_scores = out_scores;
+  a.pool_v = f->pool_v;
+  a.pool_s = f->pool_s;
+  a.pool_d = f->pool_d;
+  a.pool_cap = f->pool_cap;
+  a.pool_ctr = f->ctr;
+  a.mem_off = f->mem_off;
+  a.mem_cnt = f->mem_cnt;
+  a.ovf_n = f->ovf;
+  a.ovf_next = f->ovf + 1;
+  a.ovf_list = f->ovf + 2;
+  a.gkeys = f->gkeys;
+  a.gs = f->gs;
+  a.gsnew = f->gsnew;
+  a.gfl = f->gfl;
+  a.gneed = f->gneed;
+  a.gmlist = f->gmlist;
+  a.gcap = f->gcap;
+  a.lsnew = f->lsnew;
+  a.prof = f->prof;
+  if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * PROF_W * 8, st));
+  a.stats = f->ctr + 1;
+  hipLaunchKernelGGL(frontier_lds_kernel, dim3(f->B), dim3(FT), 0, st, a);
+  EGR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(frontier_global_kernel, dim3(f->nbig), dim3(FT), 0, st, a);
+  EGR_CHECK_LAUNCH();
+  f->ran = true;
+  return EGR_OK;
+}
+
+int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
+  if (!f || !out8) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
+  if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_stats: not run yet");
+  DeviceGuard guard(f->s->device);
+  unsigned long long h[6];
+  uint32_t nu = 0;
+  EGR_HIP(hipMemcpyAsync(h, f->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  EGR_HIP(hipMemcpyAsync(&nu, f->sp.n_unique, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
+  out8[5] = (int64_t)h[0];
+  out8[6] = (int64_t)nu;
+  out8[7] = 0;
+  return EGR_OK;
+}
+
+int egr_frontier_phase_times(const egr_frontier* f, int64_t* out, int64_t cap, void* stream) {
+  if (!f || (cap > 0 && !out) || cap < 0)
+    return egr::fail(EGR_EINVAL, "egr_frontier_phase_times: bad arguments");
+  if (!f->prof) return 0;
+  DeviceGuard guard(f->s->device);
+  const int64_t n = std::min<int64_t>(cap, (int64_t)f->B * PROF_SLOTS * PROF_W);
+  if (n > 0) {
+    EGR_HIP(hipMemcpyAsync(out, f->prof, n * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  }
+  return PROF_SLOTS * PROF_W;
+}
+
+int egr_frontier_read_scores(const egr_frontier* f, float* out, void* stream) {
+  if (!f || !out) return egr::fail(EGR_EINVAL, "egr_frontier_read_scores: NULL argument");
+  if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_read_scores: not run yet");
+  DeviceGuard guard(f->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  EGR_HIP(hipMemsetAsync(out, 0, (size_t)f->s->V * f->B * 4, st));
+  hipLaunchKernelGGL(scatter_scores_kernel, dim3(f->B), dim3(256), 0, st, f->pool_v, f->pool_s,
+                     f->mem_off, f->mem_cnt, f->B, out);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
+
+int egr_frontier_read_reach(const egr_frontier* f, uint64_t* out, void* stream) {
+  if (!f || !out) return egr::fail(EGR_EINVAL, "egr_frontier_read_reach: NULL argument");
+  if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_read_reach: not run yet");
+  DeviceGuard guard(f->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  EGR_HIP(hipMemsetAsync(out, 0, (size_t)((f->B + 63) / 64) * f->s->V * 8, st));
+  hipLaunchKernelGGL(scatter_reach_kernel, dim3(f->B), dim3(256), 0, st, f->pool_v, f->pool_d,
+                     f->mem_off, f->mem_cnt, (uint32_t)f->s->V,
+                     reinterpret_cast<unsigned long long*>(out));
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
+
+int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_vertex,
+                         float* out_score, uint8_t* out_depth, int64_t cap, int64_t* out_n,
+                         void* stream) {
+  if (!f || !out_n || col < 0 || col >= f->B || cap < 0)
+    return egr::fail(EGR_EINVAL, "egr_frontier_members: bad arguments");
+  if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_members: not run yet");
+  DeviceGuard guard(f->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  unsigned long long off = 0;
+  uint32_t n = 0;
+  EGR_HIP(hipMemcpyAsync(&off, f->mem_off + col, 8, hipMemcpyDeviceToHost, st));
+  EGR_HIP(hipMemcpyAsync(&n, f->mem_cnt + col, 4, hipMemcpyDeviceToHost, st));
+  EGR_HIP(hipStreamSynchronize(st));
+  if (n == NO_NODE) return egr::fail(EGR_ESTATE, "egr_frontier_members: member pool was full");
+  *out_n = n;
+  const size_t m = std::min<int64_t>(cap, n);
+  if (m && out_vertex) EGR_HIP(hipMemcpyAsync(out_vertex, f->pool_v + off, m * 4, hipMemcpyDefault, st));
+  if (m && out_score) EGR_HIP(hipMemcpyAsync(out_score, f->pool_s + off, m * 4, hipMemcpyDefault, st));
+  if (m && out_depth) EGR_HIP(hipMemcpyAsync(out_depth, f->pool_d + off, m, hipMemcpyDefault, st));
+  EGR_HIP(hipStreamSynchronize(st));
+  return EGR_OK;
+}
+
+}  // extern "C"

@@ -14,41 +14,20 @@
 // row-major [V][RS] u64 (RS = 2*RG words, RG a power of two): a vertex's words for all
 // incidents are one contiguous row, so a reach hop is the same staged gather as a propagation
 // hop at 1/32 of its bytes (RG lanes x 16 B per row).
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <vector>
 
-#include "egr_internal.h"
+#include "graph_dev.h"
 
-struct egr_snapshot {
-  int device = 0;
-  int64_t V = 0, NE = 0;
-  std::vector<uint32_t> row_ptr_host;   // for the per-plan chunk tables
-  uint32_t* row_ptr = nullptr;
-  uint32_t* col = nullptr;
-  uint8_t* meta = nullptr;
-  float* val = nullptr;
-  uint8_t* vlabel = nullptr;
-};
+using egr::DeviceGuard;
+using egr::dalloc;
+using egr::dfree;
 
 namespace {
 
 constexpr int KMAX = 16;              // top-k capacity per list
 constexpr int TOPK_CHUNK = 1024;      // rows per wave in top-k phase 1
 constexpr uint32_t NO_NODE = EGR_NO_NODE;
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 __device__ __forceinline__ void fma4(float w, const float4& x, float4& a) {
   a.x = fmaf(w, x.x, a.x);
@@ -486,64 +465,6 @@ __global__ void reach_export_kernel(const uint64_t* __restrict__ R, uint32_t RS,
   out[i] = R[(size_t)v * RS + w];
 }
 
-// ---- seeds: (vertex, column, value) triples -> unique per-vertex lists (max-combined) ----------
-__global__ void seed_keys_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
-                                 const float* __restrict__ sval, int64_t n, uint32_t V, int B,
-                                 uint32_t Bpad, uint64_t* keys, float* vals) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t v = sv[i], c = sc[i];
-  const bool ok = v < V && c < (uint32_t)B;
-  keys[i] = ok ? (uint64_t)v * Bpad + c : ~0ull;
-  vals[i] = sval[i];
-}
-
-__global__ void seed_head_kernel(const uint64_t* __restrict__ keys, int64_t n, uint32_t* head) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t k = keys[i];
-  head[i] = (k != ~0ull && (i == 0 || keys[i - 1] != k)) ? 1u : 0u;
-}
-
-__global__ void seed_compact_kernel(const uint64_t* __restrict__ keys,
-                                    const float* __restrict__ vals,
-                                    const uint32_t* __restrict__ head,
-                                    const uint32_t* __restrict__ pos, int64_t n, uint32_t Bpad,
-                                    uint64_t* ukeys, uint32_t* ucol, float* uval,
-                                    uint32_t* n_unique) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (i == n - 1) *n_unique = pos[i] + head[i];
-  if (!head[i]) return;
-  const uint64_t k = keys[i];
-  float m = vals[i];
-  for (int64_t j = i + 1; j < n && keys[j] == k; ++j) m = fmaxf(m, vals[j]);
-  const uint32_t p = pos[i];
-  ukeys[p] = k;
-  ucol[p] = (uint32_t)(k % Bpad);
-  uval[p] = m;
-}
-
-__global__ void seed_ptr_kernel(const uint64_t* __restrict__ ukeys,
-                                const uint32_t* __restrict__ n_unique, uint32_t V, uint32_t Bpad,
-                                uint32_t* seed_ptr) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v > V) return;
-  const uint64_t target = (uint64_t)v * Bpad;
-  uint32_t lo = 0, hi = *n_unique;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (ukeys[mid] < target) lo = mid + 1;
-    else hi = mid;
-  }
-  seed_ptr[v] = lo;
-}
-
-__global__ void zero_seed_ptr_kernel(uint32_t* seed_ptr, uint32_t V) {
-  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v <= V) seed_ptr[v] = 0;
-}
-
 // ---- top-k -----------------------------------------------------------------------------------
 struct Cand {
   float s;
@@ -779,14 +700,9 @@ struct egr_plan {
   int reach_hops = -1;  // -1: sources not set
   int hops_done = -1;   // -1: seeds not set
   bool sources_set = false;
-  // seeds
-  uint64_t *skeys_in = nullptr, *skeys = nullptr, *ukeys = nullptr;
-  float *svals_in = nullptr, *svals = nullptr, *uval = nullptr;
-  uint32_t *head = nullptr, *pos = nullptr, *ucol = nullptr, *seed_ptr = nullptr,
-           *n_unique = nullptr, *seed_tiles = nullptr;
-  void* cub_tmp = nullptr;
-  size_t cub_tmp_bytes = 0;
-  int end_bit = 64;
+  // seeds: unique (vertex, column) keys and per-vertex lists
+  egr::SeedPrep sp;
+  uint32_t *seed_ptr = nullptr, *seed_tiles = nullptr;
   // top-k: full-scan partials, and the candidate lists of the final reach
   float* part_s = nullptr;
   uint32_t* part_v = nullptr;
@@ -801,29 +717,6 @@ struct egr_plan {
 };
 
 namespace {
-
-template <typename T>
-int dalloc(T** p, size_t count) {
-  if (count == 0) count = 1;
-  if (hipMalloc((void**)p, count * sizeof(T)) != hipSuccess) {
-    (void)hipGetLastError();
-    *p = nullptr;
-    return egr::fail(EGR_ENOMEM, "hipMalloc failed (" + std::to_string(count * sizeof(T)) + " B)");
-  }
-  return EGR_OK;
-}
-
-template <typename T>
-void dfree(T*& p) {
-  if (p) (void)hipFree((void*)p);
-  p = nullptr;
-}
-
-#define EGR_TRY(x)                 \
-  do {                             \
-    int rc_ = (x);                 \
-    if (rc_ != EGR_OK) return rc_; \
-  } while (0)
 
 int choose_tile_width(int n_cols) {
   // 128-wide tiles (512-B gathers, two reach words) unless overridden; a tile must not
@@ -894,8 +787,8 @@ int plan_hop(egr_plan* p, void* stream) {
   a.val = s->val;
   a.chunk_start = p->chunk_start;
   a.seed_ptr = p->seed_ptr;
-  a.seed_col = p->ucol;
-  a.seed_val = p->uval;
+  a.seed_col = p->sp.uminor;
+  a.seed_val = p->sp.uval;
   a.seed_tiles = p->seed_tiles;
   a.xin = seeds ? nullptr : p->x[p->xcur];
   a.xout = p->x[seeds ? 0 : 1 - p->xcur];
@@ -910,7 +803,7 @@ int plan_hop(egr_plan* p, void* stream) {
   }
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
-                     dim3(256), 0, st, p->ukeys, p->uval, p->n_unique, (uint32_t)p->Bpad,
+                     dim3(256), 0, st, p->sp.ukeys, p->sp.uval, p->sp.n_unique, (uint32_t)p->Bpad,
                      (uint32_t)p->TW, (uint32_t)s->V, a.xout);
   EGR_CHECK_LAUNCH();
   p->xcur = seeds ? 0 : 1 - p->xcur;
@@ -945,7 +838,7 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
   int rc = EGR_OK;
   if ((rc = dalloc(&s->row_ptr, V + 1)) || (rc = dalloc(&s->col, 2 * E)) ||
       (rc = dalloc(&s->meta, 2 * E)) || (rc = dalloc(&s->val, 2 * E)) ||
-      (rc = dalloc(&s->vlabel, V))) {
+      (rc = dalloc(&s->cv, 2 * E)) || (rc = dalloc(&s->vlabel, V))) {
     egr_snapshot_free(s);
     return rc;
   }
@@ -953,6 +846,15 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
   if (e == hipSuccess && E) e = hipMemcpy(s->col, col.data(), 2 * E * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess && E) e = hipMemcpy(s->meta, meta.data(), 2 * E, hipMemcpyHostToDevice);
   if (e == hipSuccess && E) e = hipMemcpy(s->val, val.data(), 2 * E * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && E) {
+    std::vector<uint2> cv(2 * E);
+    for (int64_t i = 0; i < 2 * E; ++i) {
+      uint32_t vb;
+      std::memcpy(&vb, &val[i], 4);
+      cv[i] = make_uint2(col[i], vb);
+    }
+    e = hipMemcpy(s->cv, cv.data(), 2 * E * 8, hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemcpy(s->vlabel, vlabel.data(), V, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     egr_snapshot_free(s);
@@ -970,6 +872,7 @@ void egr_snapshot_free(egr_snapshot* s) {
   dfree(s->col);
   dfree(s->meta);
   dfree(s->val);
+  dfree(s->cv);
   dfree(s->vlabel);
   delete s;
 }
@@ -1011,19 +914,13 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
                     (uint64_t)V * p->B * 4 <= (16ull << 30);
   const size_t ncnt = p->cand_enabled ? (size_t)p->B * p->NG + 1 : 1;
   p->n_chunks = (int)((V + TOPK_CHUNK - 1) / TOPK_CHUNK);
-  const uint64_t keyspace = (uint64_t)V * p->Bpad;
-  p->end_bit = 1;
-  while (p->end_bit < 64 && (1ull << p->end_bit) <= keyspace) ++p->end_bit;
-  const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
   int rc = EGR_OK;
   const size_t xs = (size_t)V * p->Bpad;
   const size_t parts = (size_t)p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks * 64 * KMAX;
   if ((rc = dalloc(&p->x[0], xs)) || (rc = dalloc(&p->x[1], xs)) ||
       (rc = dalloc(&p->reach[0], (size_t)p->RS * V)) || (rc = dalloc(&p->reach[1], (size_t)p->RS * V)) ||
-      (rc = dalloc(&p->skeys_in, ms)) || (rc = dalloc(&p->skeys, ms)) || (rc = dalloc(&p->ukeys, ms)) ||
-      (rc = dalloc(&p->svals_in, ms)) || (rc = dalloc(&p->svals, ms)) || (rc = dalloc(&p->uval, ms)) ||
-      (rc = dalloc(&p->head, ms)) || (rc = dalloc(&p->pos, ms)) || (rc = dalloc(&p->ucol, ms)) ||
-      (rc = dalloc(&p->seed_ptr, (size_t)V + 1)) || (rc = dalloc(&p->n_unique, 1)) ||
+      (rc = p->sp.alloc(max_seeds, (uint64_t)V * p->Bpad, ncnt)) ||
+      (rc = dalloc(&p->seed_ptr, (size_t)V + 1)) ||
       (rc = dalloc(&p->seed_tiles, (size_t)V)) ||
       (rc = dalloc(&p->part_s, parts)) || (rc = dalloc(&p->part_v, parts)) ||
       (rc = dalloc(&p->cand_cnt, ncnt)) || (rc = dalloc(&p->cand_off, ncnt)) ||
@@ -1040,19 +937,6 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
     egr_plan_free(p);
     return egr::fail(EGR_EDEVICE, "plan table upload failed");
   }
-  size_t b1 = 0, b2 = 0, b3 = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, b1, p->skeys_in, p->skeys, p->svals_in, p->svals,
-                                         (int)ms, 0, p->end_bit) != hipSuccess ||
-      hipcub::DeviceScan::ExclusiveSum(nullptr, b2, p->head, p->pos, (int)ms) != hipSuccess ||
-      hipcub::DeviceScan::ExclusiveSum(nullptr, b3, p->cand_cnt, p->cand_off, (int)ncnt) != hipSuccess) {
-    egr_plan_free(p);
-    return egr::fail(EGR_EDEVICE, "hipcub temp-size query failed");
-  }
-  p->cub_tmp_bytes = std::max({b1, b2, b3});
-  if (hipMalloc(&p->cub_tmp, p->cub_tmp_bytes) != hipSuccess) {
-    egr_plan_free(p);
-    return egr::fail(EGR_ENOMEM, "hipMalloc (hipcub temp) failed");
-  }
   *out = p;
   return EGR_OK;
 }
@@ -1063,17 +947,8 @@ void egr_plan_free(egr_plan* p) {
   for (auto* q : {&p->x[0], &p->x[1]}) dfree(*q);
   dfree(p->reach[0]);
   dfree(p->reach[1]);
-  dfree(p->skeys_in);
-  dfree(p->skeys);
-  dfree(p->ukeys);
-  dfree(p->svals_in);
-  dfree(p->svals);
-  dfree(p->uval);
-  dfree(p->head);
-  dfree(p->pos);
-  dfree(p->ucol);
+  p->sp.free_all();
   dfree(p->seed_ptr);
-  dfree(p->n_unique);
   dfree(p->seed_tiles);
   dfree(p->part_s);
   dfree(p->part_v);
@@ -1083,7 +958,6 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->counter);
   dfree(p->chunk_start);
   dfree(p->rchunk_start);
-  if (p->cub_tmp) (void)hipFree(p->cub_tmp);
   delete p;
 }
 
@@ -1100,33 +974,11 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
   p->xcur = 0;
   p->cand_valid = false;
   EGR_HIP(hipMemsetAsync(p->seed_tiles, 0, (size_t)V * 4, st));
-  EGR_HIP(hipMemsetAsync(p->n_unique, 0, 4, st));
-  if (n_seeds == 0) {
-    hipLaunchKernelGGL(zero_seed_ptr_kernel, dim3((V + 256) / 256), dim3(256), 0, st, p->seed_ptr, V);
-    EGR_CHECK_LAUNCH();
-    return EGR_OK;
-  }
-  const int n = (int)n_seeds;
-  const dim3 g1((n + 255) / 256);
-  hipLaunchKernelGGL(seed_keys_kernel, g1, dim3(256), 0, st, seed_vertex, seed_col, seed_val,
-                     (int64_t)n, V, p->B, (uint32_t)p->Bpad, p->skeys_in, p->svals_in);
-  EGR_CHECK_LAUNCH();
-  size_t tb = p->cub_tmp_bytes;
-  // invalid keys (~0) sort last: their low end_bit bits are all ones, above every valid key
-  EGR_HIP(hipcub::DeviceRadixSort::SortPairs(p->cub_tmp, tb, p->skeys_in, p->skeys, p->svals_in,
-                                             p->svals, n, 0, p->end_bit, st));
-  hipLaunchKernelGGL(seed_head_kernel, g1, dim3(256), 0, st, p->skeys, (int64_t)n, p->head);
-  EGR_CHECK_LAUNCH();
-  tb = p->cub_tmp_bytes;
-  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->cub_tmp, tb, p->head, p->pos, n, st));
-  hipLaunchKernelGGL(seed_compact_kernel, g1, dim3(256), 0, st, p->skeys, p->svals, p->head,
-                     p->pos, (int64_t)n, (uint32_t)p->Bpad, p->ukeys, p->ucol, p->uval,
-                     p->n_unique);
-  EGR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(seed_ptr_kernel, dim3((V + 256) / 256), dim3(256), 0, st, p->ukeys,
-                     p->n_unique, V, (uint32_t)p->Bpad, p->seed_ptr);
-  EGR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(seed_tiles_kernel, g1, dim3(256), 0, st, p->ukeys, p->n_unique,
+  EGR_TRY(p->sp.run(seed_vertex, seed_col, seed_val, n_seeds, V, p->B, false,
+                    (uint64_t)p->Bpad, V, p->seed_ptr, st));
+  if (n_seeds == 0) return EGR_OK;
+  const dim3 g1((unsigned)((n_seeds + 255) / 256));
+  hipLaunchKernelGGL(seed_tiles_kernel, g1, dim3(256), 0, st, p->sp.ukeys, p->sp.n_unique,
                      (uint32_t)p->Bpad, (uint32_t)p->TW, p->seed_tiles);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
@@ -1197,8 +1049,8 @@ int egr_plan_candidates(egr_plan* p, int32_t exclude_label, void* stream) {
   hipLaunchKernelGGL(cand_count_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS,
                      p->s->vlabel, exclude_label, V, p->B, p->NG, p->cand_cnt);
   EGR_CHECK_LAUNCH();
-  size_t tb = p->cub_tmp_bytes;
-  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->cub_tmp, tb, p->cand_cnt, p->cand_off,
+  size_t tb = p->sp.tmp_bytes;
+  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sp.tmp, tb, p->cand_cnt, p->cand_off,
                                            (int)((size_t)p->B * p->NG + 1), st));
   hipLaunchKernelGGL(cand_fill_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS, p->s->vlabel,
                      exclude_label, V, p->B, p->NG, p->cand_off, p->cand_list);

@@ -234,6 +234,9 @@ class Snapshot:
     def plan(self, n_cols: int, max_seeds: int, k: int = 10) -> "Plan":
         return Plan(self, n_cols, max_seeds, k)
 
+    def frontier(self, n_cols: int, max_seeds: int, k: int = 10, pool_entries: int = 0) -> "Frontier":
+        return Frontier(self, n_cols, max_seeds, k, pool_entries)
+
 
 class Plan:
     """Per-batch device workspace: B incident columns over one snapshot."""
@@ -326,3 +329,91 @@ class Plan:
         out = np.stack([src[:cap].cpu().numpy(), dst[:cap].cpu().numpy(),
                         typ[:cap].cpu().numpy().astype(np.int32)], axis=1)
         return out[np.lexsort((out[:, 2], out[:, 0], out[:, 1]))] if cap else out.reshape(0, 3)
+
+
+class Frontier:
+    """Per-batch frontier engine (egr_frontier_*): the same seeds / sources / top-k contract as
+    Plan.run, computed per incident column over only the vertices that column touches."""
+
+    def __init__(self, snap: Snapshot, n_cols: int, max_seeds: int, k: int = 10,
+                 pool_entries: int = 0):
+        self.snap = snap
+        self.dev = snap.dev
+        self.B, self.k = n_cols, k
+        h = C.c_void_p()
+        L.check(L.lib.egr_frontier_create(snap.handle, n_cols, max_seeds, k, pool_entries,
+                                          C.byref(h)), "egr_frontier_create")
+        self._h = h
+        self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
+        self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and getattr(L, "lib", None) is not None:
+            L.lib.egr_frontier_free(h)
+            self._h = None
+
+    def _st(self, stream):
+        return L.stream_handle(self.dev) if stream is None else stream
+
+    def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
+        n = vertex.numel()
+        if not (col.numel() == n == val.numel()):
+            raise ValueError("seed arrays differ in length")
+        L.check(L.lib.egr_frontier_set_seeds(self._h, L.ptr(vertex), L.ptr(col), L.ptr(val), n,
+                                             self._st(stream)), "egr_frontier_set_seeds")
+
+    def run(self, sources: torch.Tensor, hops: int = 3, exclude_label: int = -1, stream=None):
+        if sources.numel() != self.B:
+            raise ValueError(f"need one source vertex per column ({self.B})")
+        L.check(L.lib.egr_frontier_run(self._h, L.ptr(sources), hops, exclude_label,
+                                       L.ptr(self.out_ids), L.ptr(self.out_scores),
+                                       self._st(stream)), "egr_frontier_run")
+        return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
+
+    STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",
+             "unique_seeds")
+
+    def stats(self, stream=None) -> dict:
+        """Work counters of the last run (synchronous)."""
+        out = np.zeros(8, np.int64)
+        L.check(L.lib.egr_frontier_stats(self._h, _addr(out), self._st(stream)),
+                "egr_frontier_stats")
+        return dict(zip(self.STATS, out.tolist()))
+
+    def phase_times(self, stream=None) -> np.ndarray | None:
+        """[B, slots, 1 + waves] s_memrealtime stamps (100 MHz): per phase boundary the stamp
+        after the barrier, then each wave's stamp before it; None when the frontier was
+        created without $EGRAPH_FRONTIER_PROFILE."""
+        cap = self.B * 32 * 64
+        out = np.zeros(cap, np.int64)
+        slots = L.lib.egr_frontier_phase_times(self._h, _addr(out), cap, self._st(stream))
+        if slots < 0:
+            L.check(slots, "egr_frontier_phase_times")
+        return out[: self.B * slots].reshape(self.B, 32, -1) if slots > 0 else None
+
+    def read_scores(self, stream=None) -> torch.Tensor:
+        out = torch.empty(self.snap.n_vertices * self.B, dtype=torch.float32, device=self.dev)
+        L.check(L.lib.egr_frontier_read_scores(self._h, L.ptr(out), self._st(stream)),
+                "egr_frontier_read_scores")
+        return out.view(self.snap.n_vertices, self.B)
+
+    def read_reach(self, stream=None) -> torch.Tensor:
+        W = (self.B + 63) // 64
+        out = torch.empty(W * self.snap.n_vertices, dtype=torch.int64, device=self.dev)
+        L.check(L.lib.egr_frontier_read_reach(self._h, L.ptr(out), self._st(stream)),
+                "egr_frontier_read_reach")
+        return out.view(W, self.snap.n_vertices)
+
+    def members(self, col: int, stream=None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(vertex, score, depth+1) of one column's members, sorted by vertex."""
+        n = C.c_int64(0)
+        L.check(L.lib.egr_frontier_members(self._h, col, None, None, None, 0, C.byref(n),
+                                           self._st(stream)), "egr_frontier_members")
+        v = np.empty(n.value, np.uint32)
+        s = np.empty(n.value, np.float32)
+        d = np.empty(n.value, np.uint8)
+        L.check(L.lib.egr_frontier_members(self._h, col, _addr(v), _addr(s), _addr(d), n.value,
+                                           C.byref(n), self._st(stream)), "egr_frontier_members")
+        o = np.argsort(v, kind="stable")
+        return v[o], s[o], d[o]

@@ -1,0 +1,89 @@
+"""Per-phase timing of the frontier kernel on the bench workload (diagnostic, GPU box).
+
+Creates the frontier with $EGRAPH_FRONTIER_PROFILE=1 so every column's workgroup stamps
+s_memrealtime (100 MHz) at its phase boundaries, runs the bench's C3 batch a few times and
+prints the mean / p50 / p99 duration of each phase and the spread of column start times.
+Usage: python scripts/frontier_profile.py [--config C3] [--batch 1024]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+os.environ["EGRAPH_FRONTIER_PROFILE"] = "1"
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "kubernetes-aiops-evidence-graph_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--hops", type=int, default=3)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ctx = bench.setup(args.config, args.batch, 10, 0, dev)
+    for _ in range(3):
+        bench.step_frontier(ctx, args.hops)
+    torch.cuda.synchronize()
+    full = ctx["frontier"].phase_times().astype(np.float64) * 10.0 / 1000.0   # -> us
+    t = full[:, :, 0]
+    wv = full[:, :, 1:]
+    H = args.hops
+    names = ["seeds"]
+    for h in range(H):
+        names += [f"grow{h}", f"pull{h}", f"copy+seed{h}"]
+    names += ["exclude", "topk", "pool"]
+    used = int((t[0, :24] > 0).sum())
+    d = np.diff(t[:, : used], axis=1)
+    rep = {}
+    for i in range(used - 1):
+        nm = names[i] if i < len(names) else f"slot{i}"
+        col = d[:, i]
+        rep[nm] = {"mean_us": float(col.mean()), "p50_us": float(np.percentile(col, 50)),
+                   "p99_us": float(np.percentile(col, 99)), "max_us": float(col.max())}
+        print(f"{nm:>12}: mean {col.mean():8.2f}  p50 {np.percentile(col, 50):8.2f}  "
+              f"p99 {np.percentile(col, 99):8.2f}  max {col.max():8.2f} us")
+    # per phase: spread of the waves' finish times before the barrier (imbalance) and the
+    # barrier's own latency after the last wave
+    print("wave finish spread (max - min over waves) / last-wave-to-barrier-exit:")
+    for i in range(1, used):
+        w = wv[:, i, :]
+        if (w > 0).all():
+            spread = w.max(1) - w.min(1)
+            exitlat = t[:, i] - w.max(1)
+            nm = names[i - 1] if i - 1 < len(names) else f"slot{i}"
+            print(f"{nm:>12}: spread mean {spread.mean():7.2f} p99 {np.percentile(spread, 99):7.2f}"
+                  f"  barrier-exit mean {exitlat.mean():6.2f} us")
+    sub = wv[:, 24:32, :]
+    if (sub > 0).any():
+        print("last pull, per-wave sums (us): member+row_ptr / light rows (rest) / hub rows / "
+              "store / light loads / light probes / light chain:",
+              " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(7)))
+    total = t[:, used - 1] - t[:, 0]
+    start = t[:, 0] - t[:, 0].min()
+    end = t[:, used - 1] - t[:, 0].min()
+    print(f"column total: mean {total.mean():.1f} p50 {np.percentile(total, 50):.1f} "
+          f"max {total.max():.1f} us; starts span {start.max():.1f} us; last end {end.max():.1f} us")
+    rep["column_total"] = {"mean_us": float(total.mean()), "max_us": float(total.max())}
+    rep["start_span_us"] = float(start.max())
+    rep["makespan_us"] = float(end.max())
+    rep["work"] = ctx["frontier"].stats()
+    print(json.dumps(rep["work"]))
+    if args.out:
+        Path(args.out).write_text(json.dumps(rep, indent=1))
+
+
+if __name__ == "__main__":
+    main()

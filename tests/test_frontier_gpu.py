@@ -1,0 +1,182 @@
+"""GPU parity of the frontier engine (egr_frontier_*, csrc/frontier.hip).
+
+The frontier engine must give exactly what the dense plan gives: scores bit-identical to the
+C oracle's dense recurrence (oracle/egraph_oracle.c orc_propagate, fmaf in CSR order), reach
+sets equal to the per-column BFS (orc_reach), top-k ids and scores equal to orc_topk.  Cases
+cover the LDS table, the global-memory fallback (columns whose members overflow the LDS table),
+both mixed in one batch, empty / invalid sources and seeds, duplicate seeds (max-combined), a
+member pool too small to keep every column, and several hop counts.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+NO_NODE = 0xFFFFFFFF
+
+
+def _dev(a):
+    from egraph.device import to_device
+    return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
+
+
+def _world(B, seed=11, pods=3000, nodes=60):
+    from egraph import synth
+    from egraph.graph import EvidenceGraph
+    cfg = synth.ClusterConfig(pods=pods, namespaces=6, nodes=nodes, deployments=pods // 10,
+                              services=pods // 15, attach_fraction=0.3, seed=seed)
+    c = synth.build_cluster(cfg)
+    cases = synth.make_incidents(c, B, seed=seed + 1)
+    synth.add_incidents(c, cases)
+    g = EvidenceGraph()
+    g.merge_nodes(c.ids, c.labels)
+    g.merge_edges(c.src, c.dst, c.types)
+    sv, sc, ss = synth.seeds_for_batch(g, [x.evidence for x in cases])
+    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+    return g, sv, sc, ss, src
+
+
+def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, scores=True):
+    fr = g.snapshot().frontier(B, max_seeds=max(len(sv), 1), k=k, pool_entries=pool_entries)
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    inc = g.labels().index("Incident") if exclude is None else exclude
+    ids, sco = fr.run(_dev(src), hops=hops, exclude_label=inc)
+    got_ids = ids.cpu().numpy().view(np.uint32).copy()
+    got_sc = sco.cpu().numpy().copy()
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, hops)
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, hops)
+    vl, _, _, _ = g.export()
+    e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)
+    np.testing.assert_array_equal(got_ids, e_ids)
+    np.testing.assert_array_equal(got_sc, e_sc)
+    if scores:
+        assert fr.read_scores().cpu().numpy().tobytes() == exp.tobytes()     # bit-identical
+        np.testing.assert_array_equal(fr.read_reach().cpu().numpy().view(np.uint64), er)
+    return fr
+
+
+@pytest.mark.parametrize("B", [1, 7, 64, 130, 600])
+def test_frontier_equals_oracle(B):
+    g, sv, sc, ss, src = _world(B)
+    fr = _check(g, sv, sc, ss, src, B)
+    st = fr.stats()
+    assert st["overflowed"] == 0 and st["members"] > 0 and st["pull_entries"] > 0
+
+
+@pytest.mark.parametrize("hops", [1, 2, 4])
+def test_frontier_hops(hops):
+    g, sv, sc, ss, src = _world(40, seed=21, pods=1500)
+    _check(g, sv, sc, ss, src, 40, hops=hops, k=7)
+
+
+@pytest.mark.parametrize("k", [1, 16])
+def test_frontier_k_and_no_exclusion(k):
+    g, sv, sc, ss, src = _world(33, seed=23, pods=1200)
+    _check(g, sv, sc, ss, src, 33, k=k, exclude=-1)
+
+
+def test_frontier_matches_dense_plan():
+    B = 300
+    g, sv, sc, ss, src = _world(B, seed=5, pods=6000, nodes=100)
+    snap = g.snapshot()
+    inc = g.labels().index("Incident")
+    plan = snap.plan(B, max_seeds=len(sv), k=10)
+    plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    plan.set_sources(_dev(src))
+    d_ids, d_sc = plan.run(hops=3, exclude_label=inc)
+    fr = snap.frontier(B, max_seeds=len(sv), k=10)
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    f_ids, f_sc = fr.run(_dev(src), hops=3, exclude_label=inc)
+    assert torch.equal(d_ids, f_ids) and torch.equal(d_sc, f_sc)
+    assert torch.equal(plan.read_scores(), fr.read_scores())
+    assert torch.equal(plan.read_reach(), fr.read_reach())
+
+
+def _hub_world(n_leaves=9000, n_cols=6):
+    """A star (hub + leaves, each leaf with a private tail vertex) plus a small ring: a column
+    seeded at the hub touches every vertex (> the LDS table's 6144 members) and takes the
+    global-memory fallback; a column seeded on the ring stays in LDS."""
+    from egraph.graph import EvidenceGraph
+    ids = ["hub"] + [f"leaf{i}" for i in range(n_leaves)] + [f"tail{i}" for i in range(n_leaves)]
+    ids += [f"ring{i}" for i in range(50)] + [f"inc{c}" for c in range(n_cols)]
+    labels = ["Node"] + ["Pod"] * (2 * n_leaves) + ["Service"] * 50 + ["Incident"] * n_cols
+    src = ["hub"] * n_leaves + [f"leaf{i}" for i in range(n_leaves)]
+    dst = [f"leaf{i}" for i in range(n_leaves)] + [f"tail{i}" for i in range(n_leaves)]
+    typ = ["SCHEDULED_ON"] * n_leaves + ["HAS_EVENT"] * n_leaves
+    src += [f"ring{i}" for i in range(50)]
+    dst += [f"ring{(i + 1) % 50}" for i in range(50)]
+    typ += ["CALLS"] * 50
+    for c in range(n_cols):
+        src.append(f"inc{c}")
+        dst.append("hub" if c % 2 == 0 else f"ring{c}")
+        typ.append("AFFECTS")
+    g = EvidenceGraph()
+    g.merge_nodes(ids, labels)
+    g.merge_edges(src, dst, typ)
+    look = g.lookup
+    sv = np.concatenate([look(["hub", "leaf3", "tail7"]), look(["ring1", "ring2"]),
+                         look(["hub"]), look(["ring5"])]).astype(np.uint32)
+    sc = np.array([0, 0, 0, 1, 1, 2, 3], np.uint32)
+    ss = np.array([0.9, 0.5, 0.7, 0.8, 0.6, 0.95, 0.4], np.float32)
+    srcv = look([f"inc{c}" for c in range(n_cols)]).astype(np.uint32)
+    return g, sv, sc, ss, srcv
+
+
+def test_frontier_overflow_fallback_mixed():
+    g, sv, sc, ss, src = _hub_world()
+    fr = _check(g, sv, sc, ss, src, len(src), k=12)
+    st = fr.stats()
+    assert st["overflowed"] >= 1             # the hub columns went through the fallback
+    assert st["overflowed"] < len(src)       # the ring columns did not
+
+
+def test_frontier_edge_inputs():
+    """Empty column (no source), out-of-range seeds and columns, duplicate seeds."""
+    g, sv, sc, ss, src = _world(20, seed=41, pods=1000)
+    V = g.num_vertices
+    src = src.copy()
+    src[3] = NO_NODE
+    src[7] = V + 5                                  # out of range: no reach set
+    sv = np.concatenate([sv, [V + 1, 0, sv[0], sv[0]]]).astype(np.uint32)
+    sc = np.concatenate([sc, [0, 25, sc[0], sc[0]]]).astype(np.uint32)        # col 25 >= B
+    ss = np.concatenate([ss, [0.5, 0.5, 0.01, 0.99]]).astype(np.float32)      # max-combined
+    fr = _check(g, sv, sc, ss, src, 20)
+    ids = fr.out_ids.view(20, 10).cpu().numpy().view(np.uint32)
+    assert (ids[3] == NO_NODE).all() and (ids[7] == NO_NODE).all()
+
+
+def test_frontier_no_seeds():
+    g, sv, sc, ss, src = _world(9, seed=43, pods=800)
+    e = np.zeros(0, np.uint32)
+    _check(g, e, e, np.zeros(0, np.float32), src, 9)
+
+
+def test_frontier_small_pool_still_ranks():
+    """A pool too small for every column's members: top-k stays exact."""
+    g, sv, sc, ss, src = _world(50, seed=47, pods=2000)
+    fr = _check(g, sv, sc, ss, src, 50, pool_entries=3000, scores=False)
+    assert fr.stats()["pool_used"] > 3000
+
+
+def test_frontier_bad_arguments():
+    g, sv, sc, ss, src = _world(4, seed=49, pods=400)
+    snap = g.snapshot()
+    with pytest.raises(ValueError):
+        snap.frontier(0, 10)
+    with pytest.raises(ValueError):
+        snap.frontier(4, 10, k=17)
+    fr = snap.frontier(4, max_seeds=len(sv), k=3)
+    with pytest.raises(RuntimeError):          # seeds not set (EGR_ESTATE)
+        fr.run(_dev(src))
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    with pytest.raises(ValueError):
+        fr.run(_dev(src), hops=0)
+    with pytest.raises(ValueError):
+        fr.set_seeds(_dev(np.zeros(len(sv) + 1, np.uint32)), _dev(np.zeros(len(sv) + 1, np.uint32)),
+                     _dev(np.zeros(len(sv) + 1, np.float32)))
