@@ -52,6 +52,7 @@ constexpr uint32_t BLOOM_WORDS = 2048;      // 64 Kbit filter: rejects absent ke
 constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
 constexpr int KMAXF = 16;
 constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
+constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
 constexpr int MAX_HOPS = 60;
 constexpr int PROF_SLOTS = 32;
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
@@ -207,7 +208,6 @@ struct Ticker {
   }
 };
 
-enum Phase { GROW, PULL };
 
 // Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
 // still unresolved, so a lane's NQ probe sequences share round trips.
@@ -253,12 +253,39 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
   }
 }
 
-// Pull (PULL) or neighbour insertion (GROW) of a row of dl <= LMAX entries, one lane per row:
-// every entry is loaded in one round trip, then probed LB keys at a time (lockstep), and the
-// in-order fmaf chain runs in registers.
-template <bool GT, Phase PH>
+// Row kinds of a phase: K_REACH = reach frontier (insert neighbours, give new ones the next
+// depth), K_PULL = recompute the row's score, K_PROP = expansion for the next hop (insert
+// neighbours and mark them `need` for it).
+constexpr uint32_t K_REACH = 1u, K_PULL = 2u, K_PROP = 4u;
+
+enum Phase { SEEDS, PULL };
+
+// `need` bits: bit (h & 1) marks the members pulled at hop h; set with a 32-bit LDS / global
+// atomic OR because the other parity's bit of the same byte is read concurrently
+template <bool GT>
+__device__ __forceinline__ void set_need(const Tab<GT>& t, uint32_t q, uint32_t par) {
+  atomicOr(reinterpret_cast<uint32_t*>(t.need) + (q >> 2), (1u << par) << ((q & 3u) * 8u));
+}
+
+// Insertion side of a row entry (after its probe): q = the slot if present, else insert.
+template <bool GT>
+__device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q, uint32_t kind,
+                                           int h) {
+  const int qq = q >= 0 ? q : tab_insert<GT>(t, key);
+  if (qq < 0) return;
+  if (kind & K_REACH) {
+    const uint8_t fo = t.fl[qq];
+    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 2);   // every writer writes this
+  }
+  if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
+}
+
+// One row of dl <= LMAX entries, one lane per row: every entry is loaded in one round trip,
+// probed LB keys at a time (lockstep), then the in-order fmaf chain runs in registers (K_PULL)
+// and the absent neighbours are inserted (K_REACH / K_PROP).
+template <bool GT>
 __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
-                                          uint32_t kind, int level, float& acc, Ticker& tk) {
+                                          uint32_t kind, int h, float& acc, Ticker& tk) {
   uint32_t c[LMAX];
   float w[LMAX];
 #pragma unroll
@@ -279,26 +306,21 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     int q[LB];
     find_batch<GT, LB>(t, key, nq, q);
     tk.tick(5);
-    if constexpr (PH == PULL) {
+    if (kind & K_PULL) {
       float xs[LB];
 #pragma unroll
       for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
 #pragma unroll
       for (int x = 0; x < LB; ++x)
         if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
-      tk.tick(6);
-    } else {
-#pragma unroll
-      for (int x = 0; x < LB; ++x) {
-        if ((uint32_t)x < nq) {
-          const int qq = q[x] >= 0 ? q[x] : tab_insert<GT>(t, key[x]);
-          if (qq >= 0) {
-            if ((kind & 1u) && t.fl[qq] == 0) t.fl[qq] = (uint8_t)(level + 1);
-            if (kind & 2u) t.need[qq] = 1;
-          }
-        }
-      }
     }
+    tk.tick(6);
+    if (kind & (K_REACH | K_PROP)) {
+#pragma unroll
+      for (int x = 0; x < LB; ++x)
+        if ((uint32_t)x < nq) grow_entry<GT>(t, key[x], q[x], kind, h);
+    }
+    tk.tick(7);
   }
 }
 
@@ -306,48 +328,56 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 
-// The rows of the selected members of [0, n): a wave takes 64 members at a time.
-//   GROW (hop h, reach level l = h + 1): members at reach depth l and members with s != 0
-//         insert their neighbours; a neighbour of a depth-l member without a depth gets l + 1,
-//         a neighbour of a non-zero member is marked `need` (it is pulled at this hop).
-//   PULL: every `need` member's sum over its row, CSR order, of val * s[neighbour]
-//         (non-members skipped: exact, see the file comment) -> snew[member index].
+// One pass over the members [0, n) present when it starts, a wave taking 64 at a time.
+//   SEEDS (before hop 0): the seeds insert their neighbours and mark them `need` for hop 0.
+//   PULL (hop h): a member pulled at h (`need` bit h & 1, or a seed) recomputes its score:
+//         its sum over its row, CSR order, of val * s[neighbour] (non-members skipped: exact,
+//         see the file comment) -> snew[member index]; unless h is the last hop it also
+//         inserts its neighbours and marks them `need` for h + 1 (a superset of the expansion
+//         of the non-zero members: harmless).  Members at reach depth h + 1 insert their
+//         neighbours with depth h + 2 in the same walk.  Insertions during the pass are exact:
+//         a new member's score is +0, so a pull that sees it or not reads the same term.
 // Rows of <= LMAX entries run one lane per row (light_row); longer rows (hubs) run one at a
-// time across the whole wave: 64 entries loaded and probed per round, then the fmaf chain in
-// order over v_readlane operands (every lane computes the same chain; the owner keeps it).
+// time across the whole wave: 64 entries loaded and probed per round, the fmaf chain over the
+// present entries in lane (= CSR) order with v_readlane operands (every lane computes the
+// same chain; the owner keeps it).
 template <bool GT, Phase PH>
-__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int level, Work& work,
-                          int b = -1) {
+__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int h, Work& work,
+                                          int b = -1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
   Ticker tk;
   tk.on = A.prof && b >= 0;
   if (tk.on) tk.t0 = wall_clock64();
+  const bool prop_next = h + 1 < A.hops;
+  const uint32_t par = (uint32_t)h & 1u;
   // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
   // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves
   for (uint32_t k0 = 0; k0 * FT < n; ++k0) {
     const uint32_t i = wave + NWAVES * (lane + 64u * k0);
-    uint32_t v = 0, e0 = 0, deg = 0, kind = 0;   // kind: bit 0 reach frontier, bit 1 non-zero
+    uint32_t v = 0, e0 = 0, deg = 0, kind = 0;
     if (i < n) {
       const uint32_t p = t.mlist[i];
       v = t.keys[p];
-      if constexpr (PH == GROW) {
-        kind = (t.fl[p] == (uint8_t)level ? 1u : 0u) | (t.s[p] != 0.f ? 2u : 0u);
+      const uint8_t f = t.fl[p];
+      if constexpr (PH == SEEDS) {
+        kind = (f & FL_SEED) ? K_PROP : 0u;
       } else {
-        kind = t.need[p];
+        if ((f & FL_DEPTH) == (uint32_t)(h + 1)) kind |= K_REACH;
+        if (((t.need[p] >> par) & 1u) || (f & FL_SEED)) kind |= K_PULL | (prop_next ? K_PROP : 0u);
       }
     }
     if (kind) {
       e0 = A.row_ptr[v];
       deg = A.row_ptr[v + 1] - e0;
       ++work.rows;
-      if constexpr (PH == PULL) work.pull += deg;
+      if (kind & K_PULL) work.pull += deg;
       else work.expand += deg;
     }
     tk.tick(0);
     const bool light = deg <= (uint32_t)LMAX;
     float acc = 0.f;
-    light_row<GT, PH>(A, t, e0, light ? deg : 0u, kind, level, acc, tk);
+    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
     tk.tick(1);
     uint64_t heavy = __ballot(!light);
     while (heavy) {
@@ -362,33 +392,23 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         const bool act = j < hdeg;
         const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
         const uint32_t u = ce.x;
-        if constexpr (PH == PULL) {
+        const int q = act ? tab_find<GT>(t, u) : -1;
+        if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
-          float x = 0.f;
-          bool found = false;
-          if (act) {
-            const int q = tab_find<GT>(t, u);
-            found = q >= 0;
-            if (found) x = t.s[q];
-          }
+          const float x = q >= 0 ? t.s[q] : 0.f;
           // the chain runs over the present entries only, in lane (= CSR) order
-          for (uint64_t fm = __ballot(found); fm; fm &= fm - 1) {
+          for (uint64_t fm = __ballot(q >= 0); fm; fm &= fm - 1) {
             const int y = __ffsll((long long)fm) - 1;
             hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
           }
-        } else if (act) {
-          const int q = tab_insert<GT>(t, u);
-          if (q >= 0) {
-            if ((hkind & 1u) && t.fl[q] == 0) t.fl[q] = (uint8_t)(level + 1);
-            if (hkind & 2u) t.need[q] = 1;
-          }
         }
+        if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
       }
       if (lane == m) acc = hacc;
     }
     tk.tick(2);
     if constexpr (PH == PULL) {
-      if (kind) t.snew[i] = acc;
+      if (kind & K_PULL) t.snew[i] = acc;
     }
     tk.tick(3);
   }
@@ -453,7 +473,7 @@ struct Shared {
 template <bool GT>
 __device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, uint32_t p,
                                              uint8_t maxd) {
-  const uint8_t f = t.fl[p];
+  const uint8_t f = t.fl[p] & FL_DEPTH;
   if (f < 1 || f > maxd) return 0;
   const uint32_t v = t.keys[p];
   if (A.exclude >= 0 && A.vlabel[v] == (uint8_t)A.exclude) return 0;
@@ -538,40 +558,49 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   stamp();
-  // seeds (s = s0) and the incident vertex (depth 0)
+  // seeds (s = s0), then the incident vertex (depth 0; after a barrier: it may be a seed)
   const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
   for (uint32_t i = sb + tid; i < se; i += FT) {
     const int q = tab_insert<GT>(t, A.seed_vert[i]);
-    if (q >= 0) t.s[q] = A.seed_val[i];
+    if (q >= 0) {
+      t.s[q] = A.seed_val[i];
+      t.fl[q] = FL_SEED;
+    }
   }
+  __syncthreads();
   if (tid == 0) {
     const uint32_t src = A.sources[b];
     if (src < A.V) {
       const int q = tab_insert<GT>(t, src);
-      if (q >= 0) t.fl[q] = 1;
+      if (q >= 0) t.fl[q] |= 1;
     }
   }
   wstamp();
   __syncthreads();
   stamp();
   if (sh.ovf) return false;
-  // hop h: grow (reach level h + 1 and the expansion of the non-zero members), then pull
+  // the seeds' neighbours are the members pulled at hop 0
+  row_phase<GT, SEEDS>(A, t, sh.count, -1, work, -1);
+  wstamp();
+  __syncthreads();
+  stamp();
+  if (sh.ovf) return false;
   for (int h = 0; h < hops; ++h) {
-    row_phase<GT, GROW>(A, t, sh.count, h + 1, work, -1);
+    // pull hop h (+ the expansion for hop h + 1 and reach level h + 1, in the same walk)
+    const uint32_t n0 = sh.count;
+    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
     wstamp();
     __syncthreads();
     stamp();
     if (sh.ovf) return false;
-    const uint32_t n = sh.count;
-    row_phase<GT, PULL>(A, t, n, 0, work, h == hops - 1 ? b : -1);
-    wstamp();
-    __syncthreads();
-    stamp();
-    // members no expansion touched have no non-zero neighbour: their new value is exactly +0
+    // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
+    const uint32_t n = sh.count, bit = 1u << ((uint32_t)h & 1u);
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
-      t.s[p] = t.need[p] ? t.snew[i] : 0.f;
-      t.need[p] = 0;
+      const uint8_t nd = t.need[p];
+      const bool pulled = i < n0 && ((nd & bit) || (t.fl[p] & FL_SEED));
+      t.s[p] = pulled ? t.snew[i] : 0.f;
+      if (nd & bit) t.need[p] = nd & ~bit;
     }
     __syncthreads();
     for (uint32_t i = sb + tid; i < se; i += FT) {
@@ -643,7 +672,7 @@ __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
   __shared__ uint32_t keys[LCAP];
   __shared__ float s[LCAP];
   __shared__ uint8_t fl[LCAP];
-  __shared__ uint8_t need[LCAP];
+  __shared__ uint32_t needw[LCAP / 4];
   __shared__ uint16_t mlist[LLIMIT];
   __shared__ uint32_t bloom[BLOOM_WORDS];
   __shared__ Shared sh;
@@ -655,15 +684,15 @@ __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
     keys[tid + i * FT] = EMPTY;
     s[tid + i * FT] = 0.f;
     fl[tid + i * FT] = 0;
-    need[tid + i * FT] = 0;
   }
+  for (uint32_t i = tid; i < LCAP / 4; i += FT) needw[i] = 0;
   if (tid == 0) {
     sh.count = 0;
     sh.ovf = 0;
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
-  Tab<false> t{keys, s, fl, need, mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count,
+  Tab<false> t{keys, s, fl, reinterpret_cast<uint8_t*>(needw), mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count,
                &sh.ovf, bloom};
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     A.ovf_list[atomicAdd(A.ovf_n, 1u)] = (uint32_t)b;

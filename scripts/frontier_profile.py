@@ -41,10 +41,10 @@ def main():
     t = full[:, :, 0]
     wv = full[:, :, 1:]
     H = args.hops
-    names = ["seeds"]
+    names = ["seeds", "seed-grow"]
     for h in range(H):
-        names += [f"grow{h}", f"pull{h}", f"copy+seed{h}"]
-    names += ["exclude", "topk", "pool"]
+        names += [f"pull{h}", f"copy+seed{h}"]
+    names += ["topk(wave)", "merge+pool", "end"]
     used = int((t[0, :24] > 0).sum())
     d = np.diff(t[:, : used], axis=1)
     rep = {}
@@ -69,8 +69,8 @@ def main():
     sub = wv[:, 24:32, :]
     if (sub > 0).any():
         print("last pull, per-wave sums (us): member+row_ptr / light rows (rest) / hub rows / "
-              "store / light loads / light probes / light chain:",
-              " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(7)))
+              "store / light loads / light probes / light chain / light inserts:",
+              " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(8)))
     total = t[:, used - 1] - t[:, 0]
     start = t[:, 0] - t[:, 0].min()
     end = t[:, used - 1] - t[:, 0].min()
