@@ -9,14 +9,22 @@ among those vertices (egr_plan_induced_edges).  As in the reference, the Inciden
 property is the GraphEntity id ("incident:<uuid>", neo4j.py:101-102), so a bare UUID matches
 nothing unless `resolve_bare_uuid=True`.
 
+Root-cause ranking (build-defined): rank_root_causes runs
+the frontier engine (egr_frontier_*) -- per incident, 3-hop typed propagation of the evidence
+rows' signal strengths over the graph, ranked over the incident's 3-hop reach set.
+
 The graph is process-wide, like the Neo4j database the reference talks to; writes invalidate
 the device snapshot, the next read rebuilds it.
 """
 from __future__ import annotations
 
+import asyncio
+
 import torch
 
+from egraph.device import to_device
 from egraph.graph import EvidenceGraph
+from egraph.seeds import seeds_for_batch
 from src.models.evidence import GraphEntity, GraphRelation
 
 
@@ -26,6 +34,7 @@ class GraphService:
     _graph: EvidenceGraph | None = None
     _snapshot = None
     _plans: dict = {}
+    _frontiers: dict = {}
     device = None
 
     @classmethod
@@ -36,11 +45,11 @@ class GraphService:
 
     @classmethod
     def reset(cls) -> None:
-        cls._graph, cls._snapshot, cls._plans = None, None, {}
+        cls._graph, cls._snapshot, cls._plans, cls._frontiers = None, None, {}, {}
 
     @classmethod
     def _invalidate(cls) -> None:
-        cls._snapshot, cls._plans = None, {}
+        cls._snapshot, cls._plans, cls._frontiers = None, {}, {}
 
     @staticmethod
     async def create_entity(entity: GraphEntity) -> str:
@@ -76,11 +85,73 @@ class GraphService:
 
     @classmethod
     def _plan(cls, n_cols: int):
+        if n_cols not in cls._plans:
+            cls._plans[n_cols] = cls._snap().plan(n_cols, max_seeds=0, k=1)
+        return cls._plans[n_cols]
+
+    @classmethod
+    def _snap(cls):
         if cls._snapshot is None:
             cls._snapshot = cls.graph().snapshot(device=cls.device)
-        if n_cols not in cls._plans:
-            cls._plans[n_cols] = cls._snapshot.plan(n_cols, max_seeds=0, k=1)
-        return cls._plans[n_cols]
+        return cls._snapshot
+
+    @classmethod
+    def _frontier(cls, n_cols: int, n_seeds: int, k: int):
+        """A frontier for n_cols columns, reused while its seed capacity suffices."""
+        fr = cls._frontiers.get((n_cols, k))
+        if fr is None or fr.max_seeds < n_seeds:
+            fr = cls._snap().frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k)
+            cls._frontiers[(n_cols, k)] = fr
+        return fr
+
+    @staticmethod
+    async def rank_root_causes(incident_ids: list[str], evidence_lists: list[list[dict]],
+                               hops: int = 3, k: int = 10) -> list[list[dict]]:
+        # the launch + completion wait run off the event loop (the worker is never blocked)
+        return await asyncio.to_thread(GraphService.rank_root_causes_sync, incident_ids,
+                                       evidence_lists, hops, k)
+
+    @classmethod
+    def rank_root_causes_sync(cls, incident_ids: list[str], evidence_lists: list[list[dict]],
+                              hops: int = 3, k: int = 10) -> list[list[dict]]:
+        """Per incident, the top-k graph entities by propagated evidence score, over the
+        entities within `hops` undirected hops of the incident (Incident entities excluded):
+        [{"id", "labels", "score", "rank"}], score descending, entity order on ties.
+        Incidents are matched like get_incident_graph: by Incident id, or "incident:<id>"."""
+        if len(incident_ids) != len(evidence_lists):
+            raise ValueError("incident_ids and evidence_lists differ in length")
+        if not incident_ids:
+            return []
+        g = cls.graph()
+        if g.num_vertices == 0:
+            return [[] for _ in incident_ids]
+        keys = []
+        for iid in incident_ids:
+            iid = str(iid)
+            v = g.vertex_of.get(("Incident", iid), g.vertex_of.get(("Incident", f"incident:{iid}"), -1))
+            keys.append(v)
+        sv, sc, ss = seeds_for_batch(g, evidence_lists)
+        fr = cls._frontier(len(keys), len(sv), k)
+        dev = fr.dev
+        fr.set_seeds(to_device(sv, dev), to_device(sc, dev), to_device(ss, dev))
+        src = torch.tensor(keys, dtype=torch.int32, device=dev)   # -1 = EGR_NO_NODE: no column
+        labels = g.labels()
+        inc = labels.index("Incident") if "Incident" in labels else -1
+        ids, scores = fr.run(src, hops=hops, exclude_label=inc)
+        ids = ids.cpu().numpy().view("uint32")
+        scores = scores.cpu().numpy()
+        vlabel, _, _, _ = g.export()
+        out = []
+        for b in range(len(keys)):
+            row = []
+            for r in range(k):
+                v = int(ids[b, r])
+                if v == 0xFFFFFFFF:
+                    break
+                row.append({"id": g.vertex_id(v), "labels": [labels[vlabel[v]]],
+                            "score": float(scores[b, r]), "rank": r + 1})
+            out.append(row)
+        return out
 
     @staticmethod
     async def get_incident_graph(incident_id: str, depth: int = 3,

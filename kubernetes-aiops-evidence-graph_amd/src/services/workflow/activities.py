@@ -1,5 +1,6 @@
 """The three workflow activities on the hot path (reference
-src/services/workflow/activities.py:94-170), same names, argument shapes and results.
+src/services/workflow/activities.py:94-170), same names, argument shapes and results, plus
+additive batch / root-cause activities.
 
 They stay drop-in sockets for IncidentWorkflow (incident_workflow.py:96-139): JSON-shaped
 dicts in and out.  When temporalio is installed they are registered with @activity.defn,
@@ -59,3 +60,22 @@ async def generate_and_rank_batch(data: list[dict]) -> list[list[dict]]:
     incidents = [Incident(**d["incident"]) for d in data]
     evidence = [d["evidence"].get("evidence", []) for d in data]
     return await RulesEngine().rank_incidents_batch(incidents, evidence)
+
+
+@_defn
+async def rank_root_causes(data: dict) -> list[dict]:
+    """Additive (build-defined): the incident's top-k root-cause graph entities
+    by 3-hop evidence propagation, same input dict as generate_hypotheses (+ optional "k")."""
+    inc = data["incident"]
+    ev = data["evidence"].get("evidence", [])
+    out = await GraphService.rank_root_causes([str(inc["id"])], [ev], k=int(data.get("k", 10)))
+    return out[0]
+
+
+@_defn
+async def rank_root_causes_batch(data: list[dict]) -> list[list[dict]]:
+    """Additive: rank_root_causes for many incidents in one frontier launch."""
+    ids = [str(d["incident"]["id"]) for d in data]
+    ev = [d["evidence"].get("evidence", []) for d in data]
+    k = int(data[0].get("k", 10)) if data else 10
+    return await GraphService.rank_root_causes(ids, ev, k=k)

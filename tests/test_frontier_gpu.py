@@ -180,3 +180,49 @@ def test_frontier_bad_arguments():
     with pytest.raises(ValueError):
         fr.set_seeds(_dev(np.zeros(len(sv) + 1, np.uint32)), _dev(np.zeros(len(sv) + 1, np.uint32)),
                      _dev(np.zeros(len(sv) + 1, np.float32)))
+
+
+def test_graph_service_rank_root_causes():
+    """GraphService.rank_root_causes (drop-in API, entities / relations as the collectors emit
+    them) against the oracle's propagation + reach + top-k over the same graph."""
+    import asyncio
+
+    from egraph import synth
+    from egraph.seeds import seeds_for_batch
+    from src.database import GraphService
+    from src.services.workflow import activities
+    cfg = synth.ClusterConfig(pods=1500, namespaces=5, nodes=40, deployments=150, services=100,
+                              attach_fraction=0.3, seed=61)
+    c = synth.build_cluster(cfg)
+    cases = synth.make_incidents(c, 12, seed=62)
+    synth.add_incidents(c, cases)
+    GraphService.reset()
+    try:
+        ents = [{"id": i, "type": lab} for i, lab in zip(c.ids, c.labels)]
+        rels = [{"source_id": s, "target_id": d, "relation_type": t}
+                for s, d, t in zip(c.src, c.dst, c.types)]
+        from src.models import GraphEntity, GraphRelation
+        asyncio.run(GraphService.create_entities_batch([GraphEntity(**e) for e in ents]))
+        asyncio.run(GraphService.create_relations_batch([GraphRelation(**r) for r in rels]))
+        ids = [x.incident["id"] for x in cases]
+        evs = [x.evidence for x in cases]
+        got = asyncio.run(GraphService.rank_root_causes(ids, evs, hops=3, k=5))
+        g = GraphService.graph()
+        sv, sc, ss = seeds_for_batch(g, evs)
+        src = g.lookup([f"incident:{i}" for i in ids]).astype(np.uint32)
+        csr = g.csr()
+        exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, len(ids), 3)
+        er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+        vl, _, _, _ = g.export()
+        e_ids, e_sc = oracle.topk(exp, er, vl, g.labels().index("Incident"), 5)
+        for b in range(len(ids)):
+            want = [(g.vertex_id(int(v)), float(s)) for v, s in zip(e_ids[b], e_sc[b])
+                    if v != NO_NODE]
+            assert [(r["id"], r["score"]) for r in got[b]] == want
+            assert [r["rank"] for r in got[b]] == list(range(1, len(want) + 1))
+        # the additive activity returns the same list for one incident
+        one = asyncio.run(activities.rank_root_causes(
+            {"incident": cases[3].incident, "evidence": {"evidence": evs[3]}, "k": 5}))
+        assert one == got[3]
+    finally:
+        GraphService.reset()
