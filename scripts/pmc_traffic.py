@@ -1,0 +1,42 @@
+"""Per-launch HBM traffic of the bench's dominant kernels from the pmc_traffic.sh passes.
+
+traffic = 2 * FETCH_SIZE + WRITE_SIZE (bytes, FETCH_SIZE/WRITE_SIZE in KiB as rocprofv3 derives
+them; the x2 is the guide's gfx950 correction for 16-B/lane reads, exact for the dense hop's
+float4 gathers and uncalibrated for the frontier's 8-B / 4-B gathers -- both raw values are
+kept).  Writes profiles/pmc_frontier.json and profiles/pmc_hop.json, which bench.py reads.
+Usage: python scripts/pmc_traffic.py <pmc output dir>"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+root = Path(sys.argv[1])
+REPO = Path(__file__).resolve().parents[1]
+KERNELS = {"frontier": "frontier_lds_kernel", "hop": "hop_kernel<32, false>"}
+vals = defaultdict(lambda: defaultdict(list))
+for f in sorted(root.rglob("*counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        for key, pat in KERNELS.items():
+            if pat in r.get("Kernel_Name", ""):
+                vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for key in KERNELS:
+    v = vals[key]
+    if not v.get("FETCH_SIZE") or not v.get("WRITE_SIZE"):
+        print(f"{key}: counters missing")
+        continue
+    mean = {c: sum(x) / len(x) for c, x in v.items()}
+    fetch_b = mean["FETCH_SIZE"] * 1024.0
+    write_b = mean["WRITE_SIZE"] * 1024.0
+    rep = {
+        "kernel": KERNELS[key],
+        "dispatches": len(v["FETCH_SIZE"]),
+        "fetch_size_kib_per_launch": mean["FETCH_SIZE"],
+        "write_size_kib_per_launch": mean["WRITE_SIZE"],
+        "tcc_ea0_rdreq_per_launch": mean.get("TCC_EA0_RDREQ_sum"),
+        "tcc_ea0_wrreq_per_launch": mean.get("TCC_EA0_WRREQ_sum"),
+        "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
+        "correction": "2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section) + WRITE_SIZE",
+    }
+    (REPO / "profiles" / f"pmc_{key}.json").write_text(json.dumps(rep, indent=1))
+    print(key, json.dumps(rep))
