@@ -352,24 +352,39 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   const bool prop_next = h + 1 < A.hops;
   const uint32_t par = (uint32_t)h & 1u;
   // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
-  // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves
-  for (uint32_t k0 = 0; k0 * FT < n; ++k0) {
-    const uint32_t i = wave + NWAVES * (lane + 64u * k0);
-    uint32_t v = 0, e0 = 0, deg = 0, kind = 0;
-    if (i < n) {
-      const uint32_t p = t.mlist[i];
+  // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves.
+  // The next chunk's selection and row_ptr loads are issued before the current chunk is walked
+  // (a member's kind cannot change during the pass: see the comment above).
+  struct Chunk {
+    uint32_t i, kind, e0, e1;
+  };
+  auto fetch = [&](uint32_t k0) {
+    Chunk c{wave + NWAVES * (lane + 64u * k0), 0u, 0u, 0u};
+    uint32_t v = 0;
+    if (c.i < n) {
+      const uint32_t p = t.mlist[c.i];
       v = t.keys[p];
       const uint8_t f = t.fl[p];
       if constexpr (PH == SEEDS) {
-        kind = (f & FL_SEED) ? K_PROP : 0u;
+        c.kind = (f & FL_SEED) ? K_PROP : 0u;
       } else {
-        if ((f & FL_DEPTH) == (uint32_t)(h + 1)) kind |= K_REACH;
-        if (((t.need[p] >> par) & 1u) || (f & FL_SEED)) kind |= K_PULL | (prop_next ? K_PROP : 0u);
+        if ((f & FL_DEPTH) == (uint32_t)(h + 1)) c.kind |= K_REACH;
+        if (((t.need[p] >> par) & 1u) || (f & FL_SEED)) c.kind |= K_PULL | (prop_next ? K_PROP : 0u);
       }
     }
+    if (c.kind) {
+      c.e0 = A.row_ptr[v];
+      c.e1 = A.row_ptr[v + 1];
+    }
+    return c;
+  };
+  const uint32_t nk = (n + FT - 1) / FT;
+  Chunk nxt = nk ? fetch(0) : Chunk{0u, 0u, 0u, 0u};
+  for (uint32_t k0 = 0; k0 < nk; ++k0) {
+    const Chunk cur = nxt;
+    if (k0 + 1 < nk) nxt = fetch(k0 + 1);
+    const uint32_t i = cur.i, kind = cur.kind, e0 = cur.e0, deg = cur.e1 - cur.e0;
     if (kind) {
-      e0 = A.row_ptr[v];
-      deg = A.row_ptr[v + 1] - e0;
       ++work.rows;
       if (kind & K_PULL) work.pull += deg;
       else work.expand += deg;
@@ -435,31 +450,24 @@ __device__ __forceinline__ void topk_unkey(uint64_t k, float& s, uint32_t& v) {
   v = ~(uint32_t)k;
 }
 
-#define EGR_DPP_MAX64(CTRL, RM)                                                            \
-  {                                                                                        \
-    const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, RM, \
-                                                               0xF, false);                \
-    const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, RM, \
-                                                               0xF, false);                \
-    if (ohi > hi || (ohi == hi && olo > lo)) {                                             \
-      hi = ohi;                                                                            \
-      lo = olo;                                                                            \
-    }                                                                                      \
-  }
+// wave-wide max of a u32 with DPP row ops (quad perms, half / full row mirror, row broadcasts
+// 15 and 31), result from lane 63; every lane gets it
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x141, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x140, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
 
-// wave-wide max of a u64 with DPP row ops (quad perms, half / full row mirror, row
-// broadcasts 15 and 31); every lane gets the result
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  EGR_DPP_MAX64(0xB1, 0xF)    // quad_perm [1,0,3,2]
-  EGR_DPP_MAX64(0x4E, 0xF)    // quad_perm [2,3,0,1]
-  EGR_DPP_MAX64(0x141, 0xF)   // row_half_mirror
-  EGR_DPP_MAX64(0x140, 0xF)   // row_mirror
-  EGR_DPP_MAX64(0x142, 0xA)   // row_bcast:15
-  EGR_DPP_MAX64(0x143, 0xC)   // row_bcast:31
-  lo = __builtin_amdgcn_readlane(lo, 63);
-  hi = __builtin_amdgcn_readlane(hi, 63);
-  return ((uint64_t)hi << 32) | lo;
+// wave-wide max of a u64 key: the max high word, then the max low word among its holders
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+  const uint32_t hi = (uint32_t)(k >> 32);
+  const uint32_t mh = wave_max_u32(hi);
+  const uint32_t ml = wave_max_u32(hi == mh ? (uint32_t)k : 0u);
+  return ((uint64_t)mh << 32) | ml;
 }
 
 struct Shared {
