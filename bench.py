@@ -170,10 +170,10 @@ def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
 def frontier_roofline(ctx, run_ms: float, B: int, k: int) -> tuple[dict, dict]:
     """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
     (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
-    (8 B), the unique seeds (vertex + value, 8 B), the member pool written (vertex, score,
+    (8 B), the seed entries (vertex + value, 8 B), the member pool written (vertex, score,
     depth: 9 B) and the top-k output (8 B per slot)."""
     work = ctx["frontier"].stats()
-    n_seeds = work["unique_seeds"]
+    n_seeds = work["seed_entries"]
     nbytes = (8 * work["pull_entries"] + 4 * work["expand_entries"] + 8 * work["rows"]
               + 8 * n_seeds + 9 * work["members"] + 8 * B * k)
     achieved = nbytes / (run_ms * 1e-3) / 1e9

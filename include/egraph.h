@@ -252,7 +252,7 @@ int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, ui
  *                         pulls (col + val read), CSR entries read by expansions (col only),
  *                         rows walked (row_ptr pairs), members, columns that overflowed the
  *                         LDS table (redone by the global-memory variant), pool entries
- *                         used, unique seeds, 0.
+ *                         used, valid seed entries, 0.
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.

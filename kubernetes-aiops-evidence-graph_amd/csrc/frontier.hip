@@ -53,6 +53,7 @@ constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candida
 constexpr int KMAXF = 16;
 constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
 constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
+constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
 constexpr int MAX_HOPS = 60;
 constexpr int PROF_SLOTS = 32;
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
@@ -65,8 +66,9 @@ struct FArgs {
   uint32_t V;
   int B, hops, k, exclude;
   const uint32_t* seed_ptr;    // [B+1] per column
-  const uint32_t* seed_vert;   // unique vertices, ascending within a column
-  const float* seed_val;       // max-combined s0
+  const uint32_t* seed_vert;   // grouped by column, any order, duplicates allowed
+  const float* seed_val;       // (duplicates are max-combined in the kernel, as fmaxf)
+  uint2* seed_rep;             // per seed entry: (slot, s0 bits) of a vertex's representative
   const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
   uint32_t* out_ids;           // [B*k]
   float* out_scores;
@@ -566,14 +568,41 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   stamp();
-  // seeds (s = s0), then the incident vertex (depth 0; after a barrier: it may be a seed)
+  // seeds: insert (s = -inf), max-combine duplicates (fmaxf, like the dense plan's seed prep),
+  // then one entry per vertex claims it and records (slot, s0) for the per-hop seed add
   const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
   for (uint32_t i = sb + tid; i < se; i += FT) {
     const int q = tab_insert<GT>(t, A.seed_vert[i]);
     if (q >= 0) {
-      t.s[q] = A.seed_val[i];
+      t.s[q] = -INFINITY;               // every writer writes the same
       t.fl[q] = FL_SEED;
     }
+  }
+  __syncthreads();
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_find<GT>(t, A.seed_vert[i]);
+    if (q < 0) continue;
+    unsigned int* sp = reinterpret_cast<unsigned int*>(&t.s[q]);
+    unsigned int old = *sp;
+    for (;;) {
+      const float m = fmaxf(__uint_as_float(old), A.seed_val[i]);
+      if (__float_as_uint(m) == old) break;
+      const unsigned int got = atomicCAS(sp, old, __float_as_uint(m));
+      if (got == old) break;
+      old = got;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_find<GT>(t, A.seed_vert[i]);
+    uint2 r = make_uint2(NO_NODE, 0u);
+    if (q >= 0) {
+      const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
+      const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
+                                    (uint32_t)FL_CLAIM << sh8);
+      if (!((old >> sh8) & FL_CLAIM)) r = make_uint2((uint32_t)q, __float_as_uint(t.s[q]));
+    }
+    A.seed_rep[i] = r;
   }
   __syncthreads();
   if (tid == 0) {
@@ -612,8 +641,8 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     }
     __syncthreads();
     for (uint32_t i = sb + tid; i < se; i += FT) {
-      const int q = tab_find<GT>(t, A.seed_vert[i]);
-      if (q >= 0) t.s[q] = t.s[q] + A.seed_val[i];
+      const uint2 r = A.seed_rep[i];
+      if (r.x != NO_NODE) t.s[r.x] = t.s[r.x] + __uint_as_float(r.y);
     }
     __syncthreads();
     stamp();
@@ -679,7 +708,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
 __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
   __shared__ uint32_t keys[LCAP];
   __shared__ float s[LCAP];
-  __shared__ uint8_t fl[LCAP];
+  __shared__ uint32_t flw[LCAP / 4];
   __shared__ uint32_t needw[LCAP / 4];
   __shared__ uint16_t mlist[LLIMIT];
   __shared__ uint32_t bloom[BLOOM_WORDS];
@@ -691,8 +720,8 @@ __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
   for (int i = 0; i < LPPT; ++i) {
     keys[tid + i * FT] = EMPTY;
     s[tid + i * FT] = 0.f;
-    fl[tid + i * FT] = 0;
   }
+  for (uint32_t i = tid; i < LCAP / 4; i += FT) flw[i] = 0;
   for (uint32_t i = tid; i < LCAP / 4; i += FT) needw[i] = 0;
   if (tid == 0) {
     sh.count = 0;
@@ -700,7 +729,7 @@ __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
-  Tab<false> t{keys, s, fl, reinterpret_cast<uint8_t*>(needw), mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count,
+  Tab<false> t{keys, s, reinterpret_cast<uint8_t*>(flw), reinterpret_cast<uint8_t*>(needw), mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count,
                &sh.ovf, bloom};
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     A.ovf_list[atomicAdd(A.ovf_n, 1u)] = (uint32_t)b;
@@ -776,6 +805,84 @@ __global__ void scatter_reach_kernel(const uint32_t* __restrict__ pool_v,
     if (pool_d[o + i]) atomicOr(&out[(size_t)(b >> 6) * V + pool_v[o + i]], 1ull << (b & 63));
 }
 
+// seeds grouped by column without a sort: count, one-block scan, scatter.  Seeds usually arrive
+// grouped by column, so a wave's lanes form runs of equal columns: one atomic per run (the run's
+// first lane adds the run length; the others take their rank in the run).
+struct SeedRun {
+  bool ok;
+  uint32_t col, leader, rank, len;
+};
+
+__device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
+                                            const uint32_t* __restrict__ sc, int64_t n, uint32_t V,
+                                            int B) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  SeedRun r;
+  r.ok = i < n && sv[i] < V && sc[i] < (uint32_t)B;
+  r.col = r.ok ? sc[i] : 0xFFFFFFFFu;
+  const uint32_t prev = __shfl_up(r.col, 1, 64);
+  const bool start = r.ok && (lane == 0 || prev != r.col);
+  const uint64_t starts = __ballot(start);
+  const uint64_t below = starts & ((2ull << lane) - 1ull);          // starts at lanes <= lane
+  r.leader = below ? 63u - (uint32_t)__clzll((long long)below) : 0u;
+  r.rank = (uint32_t)lane - r.leader;
+  const uint64_t above = starts & ~((2ull << lane) - 1ull);          // starts at lanes > lane
+  const uint32_t next = above ? (uint32_t)__ffsll((long long)above) - 1u : 64u;
+  // a run ends at the next start or at the first invalid lane
+  const uint64_t okm = __ballot(r.ok);
+  const uint64_t bad_above = ~okm & ~((2ull << lane) - 1ull);
+  const uint32_t nbad = bad_above ? (uint32_t)__ffsll((long long)bad_above) - 1u : 64u;
+  r.len = min(next, nbad) - r.leader;
+  return r;
+}
+
+__global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
+                                  int64_t n, uint32_t V, int B, uint32_t* cnt) {
+  const SeedRun r = seed_run(sv, sc, n, V, B);
+  if (r.ok && r.rank == 0) atomicAdd(&cnt[r.col], r.len);
+}
+
+// ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]).  One block of
+// 1024 threads, each owning a contiguous run of columns.
+__global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr) {
+  __shared__ uint32_t part[1024];
+  const int tid = threadIdx.x;
+  const int per = (B + 1023) / 1024;
+  const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
+  uint32_t sum = 0;
+  for (int c = c0; c < c1; ++c) sum += cnt[c];
+  part[tid] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan of the run sums
+    const uint32_t x = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += x;
+    __syncthreads();
+  }
+  uint32_t run = tid ? part[tid - 1] : 0u;
+  for (int c = c0; c < c1; ++c) {
+    const uint32_t x = cnt[c];
+    ptr[c] = run;
+    cnt[c] = run;
+    run += x;
+  }
+  if (tid == 1023) ptr[B] = part[1023];
+}
+
+__global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
+                                    const float* __restrict__ sval, int64_t n, uint32_t V, int B,
+                                    uint32_t* cursor, uint32_t* out_v, float* out_s) {
+  const SeedRun r = seed_run(sv, sc, n, V, B);
+  uint32_t base = 0;
+  if (r.ok && r.rank == 0) base = atomicAdd(&cursor[r.col], r.len);
+  base = __shfl(base, (int)r.leader, 64);
+  if (!r.ok) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  out_v[base + r.rank] = sv[i];
+  out_s[base + r.rank] = sval[i];
+}
+
 }  // namespace
 
 struct egr_frontier {
@@ -783,8 +890,12 @@ struct egr_frontier {
   int B = 0, k = 0, nbig = 0;
   int64_t max_seeds = 0;
   uint32_t gcap = 0;
-  egr::SeedPrep sp;
-  uint32_t* seed_ptr = nullptr;   // [B+1]
+  int64_t n_seeds = 0;
+  uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
+  uint32_t* seed_cnt = nullptr;   // [B] per-column counts, then scatter cursors
+  uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
+  float* seed_s = nullptr;
+  uint2* seed_rep = nullptr;
   uint32_t* pool_v = nullptr;
   float* pool_s = nullptr;
   uint8_t* pool_d = nullptr;
@@ -829,8 +940,10 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   f->pool_cap = pool_entries > 0 ? (unsigned long long)pool_entries
                                  : (unsigned long long)n_cols * 4096ull + 4ull * V;
   int rc = EGR_OK;
-  if ((rc = f->sp.alloc(max_seeds, (uint64_t)n_cols * V, 1)) ||
-      (rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) ||
+  const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
+  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, (size_t)n_cols)) ||
+      (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
+      (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
       (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 6)) ||
       (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
@@ -863,8 +976,11 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
 void egr_frontier_free(egr_frontier* f) {
   if (!f) return;
   DeviceGuard guard(f->s->device);
-  f->sp.free_all();
   dfree(f->seed_ptr);
+  dfree(f->seed_cnt);
+  dfree(f->seed_v);
+  dfree(f->seed_s);
+  dfree(f->seed_rep);
   dfree(f->pool_v);
   dfree(f->pool_s);
   dfree(f->pool_d);
@@ -891,8 +1007,24 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
                      "egr_frontier_set_seeds: bad arguments (n_seeds above capacity?)");
   DeviceGuard guard(f->s->device);
   const uint32_t V = (uint32_t)f->s->V;
-  EGR_TRY(f->sp.run(seed_vertex, seed_col, seed_val, n_seeds, V, f->B, true, (uint64_t)V,
-                    (uint32_t)f->B, f->seed_ptr, (hipStream_t)stream));
+  hipStream_t st = (hipStream_t)stream;
+  // counting sort by column: count, one-block exclusive scan, scatter (order within a column
+  // is arbitrary; the kernel max-combines duplicates).  Invalid triples are dropped.
+  EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 4, st));
+  const unsigned g = (unsigned)((std::max<int64_t>(n_seeds, 1) + 255) / 256);
+  if (n_seeds > 0) {
+    hipLaunchKernelGGL(seed_count_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
+                       n_seeds, V, f->B, f->seed_cnt);
+    EGR_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(1024), 0, st, f->seed_cnt, f->B, f->seed_ptr);
+  EGR_CHECK_LAUNCH();
+  if (n_seeds > 0) {
+    hipLaunchKernelGGL(seed_scatter_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
+                       seed_val, n_seeds, V, f->B, f->seed_cnt, f->seed_v, f->seed_s);
+    EGR_CHECK_LAUNCH();
+  }
+  f->n_seeds = n_seeds;
   f->seeds_set = true;
   return EGR_OK;
 }
@@ -917,8 +1049,9 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.k = f->k;
   a.exclude = exclude_label;
   a.seed_ptr = f->seed_ptr;
-  a.seed_vert = f->sp.uminor;
-  a.seed_val = f->sp.uval;
+  a.seed_vert = f->seed_v;
+  a.seed_val = f->seed_s;
+  a.seed_rep = f->seed_rep;
   a.sources = source_vertex;
   a.out_ids = out_ids;
   a.out_scores = out_scores;
@@ -958,7 +1091,7 @@ int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
   unsigned long long h[6];
   uint32_t nu = 0;
   EGR_HIP(hipMemcpyAsync(h, f->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
-  EGR_HIP(hipMemcpyAsync(&nu, f->sp.n_unique, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  EGR_HIP(hipMemcpyAsync(&nu, f->seed_ptr + f->B, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
   for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
   out8[5] = (int64_t)h[0];

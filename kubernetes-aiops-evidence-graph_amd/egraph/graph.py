@@ -372,7 +372,7 @@ class Frontier:
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",
-             "unique_seeds")
+             "seed_entries")
 
     def stats(self, stream=None) -> dict:
         """Work counters of the last run (synchronous)."""
