@@ -120,8 +120,15 @@ struct Tab {
 // Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
 // insert CASes the lowest empty slot it sees and moves on only when that slot is taken, so a
 // bucket with an empty slot ends every probe sequence that passes through it.
+// Hashes use only full-rate 24-bit multiplies (a 32-bit v_mul_lo / v_mul_hi is quarter rate,
+// and every probed key pays for its hashes): the id is folded to 24 bits, multiplied by an odd
+// 24-bit constant, and 16 mixed bits are range-reduced to [0, nb) by a second 24-bit multiply.
+__device__ __forceinline__ uint32_t mix24(uint32_t v, uint32_t c) {
+  return __umul24((v ^ (v >> 24)) & 0xFFFFFFu, c);
+}
+
 __device__ __forceinline__ uint32_t hbucket(uint32_t v, uint32_t nb) {
-  return __umulhi(v * 0x9E3779B1u, nb);    // multiplicative hash, range-reduced to [0, nb)
+  return __umul24((mix24(v, 0x9E3779u) >> 8) & 0xFFFFu, nb) >> 16;
 }
 
 __device__ __forceinline__ uint4 read_bucket(const uint32_t* keys, uint32_t bk) {
@@ -138,7 +145,9 @@ __device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_
   return -2;
 }
 
-__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) { return (v * 0x85EBCA6Bu) >> 16; }
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // 16 bits
+  return (mix24(v, 0xB5297Au | 1u) >> 8) & 0xFFFFu;
+}
 
 // slot of v, inserting it if absent (-1: table full)
 template <bool GT>
