@@ -238,6 +238,29 @@ int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, ui
                            uint8_t* out_type, int64_t cap, int64_t* out_n, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Partitioned graphs (egraph/shard.py).  A rank's snapshot is built from its
+ * local CSR: owned vertices first (their full rows, entries remapped to local ids, CSR order
+ * kept so every row's fmaf chain is the unpartitioned one), then halo vertices (empty rows).
+ * Per hop the owners' fresh rows of the exported vertices are packed, exchanged (RCCL
+ * all-gather, done by the caller) and unpacked into the halo rows.
+ *   egr_snapshot_from_csr : host arrays row_ptr [V+1], col/meta/val [row_ptr[V]], vlabel [V].
+ *   egr_plan_set_owned    : rows [0, n_owned) are the only top-k candidates.
+ *   egr_plan_pack_*       : out[i] = row rows[i] of the current scores ([n][Bpad] fp32, column
+ *                           b at b) / reach ([n][ceil(n_cols/64)] u64).
+ *   egr_plan_unpack_*     : row rows[i] = in[src[i]] (same layouts).
+ * ---------------------------------------------------------------------------------------- */
+int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* meta,
+                          const float* val, const uint8_t* vlabel, int64_t n_vertices,
+                          int32_t device, egr_snapshot** out);
+int egr_plan_set_owned(egr_plan* p, int64_t n_owned);
+int egr_plan_pack_scores(const egr_plan* p, const uint32_t* rows, int64_t n, float* out, void* stream);
+int egr_plan_unpack_scores(egr_plan* p, const uint32_t* rows, const uint32_t* src, int64_t n,
+                           const float* in, void* stream);
+int egr_plan_pack_reach(const egr_plan* p, const uint32_t* rows, int64_t n, uint64_t* out, void* stream);
+int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src, int64_t n,
+                          const uint64_t* in, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Frontier engine: the same A8 + A9 + top-k results as a plan's egr_plan_run, computed per
  * incident column over only the vertices the column touches (one workgroup per column, the
  * column's state in an LDS hash table).  Scores, reach sets and top-k are

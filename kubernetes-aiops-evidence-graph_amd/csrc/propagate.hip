@@ -533,7 +533,7 @@ __device__ __forceinline__ void wave_emit_topk(float (&Ls)[KMAX], uint32_t (&Lv)
 // wave index enumerates (tile, 64-column slice, row chunk).
 __global__ __launch_bounds__(256) void topk_partial_kernel(
     const float* __restrict__ X, const uint64_t* __restrict__ R, uint32_t RS,
-    const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, int TW, int B,
+    const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, uint32_t VC, int TW, int B,
     int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v) {
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(
     const uint64_t* Rw = R + (b >> 6);
     const uint64_t bit = 1ull << (b & 63);
     const uint32_t v0 = (uint32_t)ch * TOPK_CHUNK;
-    const uint32_t v1 = min(V, v0 + TOPK_CHUNK);
+    const uint32_t v1 = min(VC, v0 + TOPK_CHUNK);   // rows >= VC (halo) are never candidates
     // eight rows per step: all reach words and labels, then the reached scores, are loaded
     // before any insertion, so a wave keeps 8-16 loads in flight instead of one
     for (uint32_t vb = v0 + rp; vb < v1; vb += 8u * rps) {
@@ -681,6 +681,38 @@ __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
   }
 }
 
+// ---- halo exchange of a partitioned graph (egraph/shard.py): rows of the tiled scores and of
+// the row-major reach words to / from dense [n][Bpad] / [n][W] buffers.  One block per row.
+__global__ void pack_scores_kernel(const float* __restrict__ X, uint32_t V, int TW, int Bpad,
+                                   const uint32_t* __restrict__ rows, float* __restrict__ out) {
+  const uint32_t v = rows[blockIdx.x];
+  for (int b = threadIdx.x; b < Bpad; b += blockDim.x)
+    out[(size_t)blockIdx.x * Bpad + b] = X[((size_t)(b / TW) * V + v) * TW + (b % TW)];
+}
+
+__global__ void unpack_scores_kernel(float* __restrict__ X, uint32_t V, int TW, int Bpad,
+                                     const uint32_t* __restrict__ rows,
+                                     const uint32_t* __restrict__ src, const float* __restrict__ in) {
+  const uint32_t v = rows[blockIdx.x];
+  const size_t o = (size_t)src[blockIdx.x] * Bpad;
+  for (int b = threadIdx.x; b < Bpad; b += blockDim.x)
+    X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = in[o + b];
+}
+
+__global__ void pack_reach_kernel(const uint64_t* __restrict__ R, uint32_t RS, int W,
+                                  const uint32_t* __restrict__ rows, uint64_t* __restrict__ out) {
+  const uint32_t v = rows[blockIdx.x];
+  for (int w = threadIdx.x; w < W; w += blockDim.x) out[(size_t)blockIdx.x * W + w] = R[(size_t)v * RS + w];
+}
+
+__global__ void unpack_reach_kernel(uint64_t* __restrict__ R, uint32_t RS, int W,
+                                    const uint32_t* __restrict__ rows,
+                                    const uint32_t* __restrict__ src, const uint64_t* __restrict__ in) {
+  const uint32_t v = rows[blockIdx.x];
+  const size_t o = (size_t)src[blockIdx.x] * W;
+  for (int w = threadIdx.x; w < W; w += blockDim.x) R[(size_t)v * RS + w] = in[o + w];
+}
+
 }  // namespace
 
 struct egr_plan {
@@ -713,6 +745,7 @@ struct egr_plan {
   bool cand_enabled = false;
   bool cand_valid = false;
   int cand_exclude = -1;
+  uint32_t owned = 0;               // rows [0, owned) are top-k candidates (partition: no halo)
   unsigned long long* counter = nullptr;
 };
 
@@ -898,6 +931,7 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   p->Bpad = (n_cols + p->TW - 1) / p->TW * p->TW;
   p->ntiles = p->Bpad / p->TW;
   p->W = (n_cols + 63) / 64;
+  p->owned = (uint32_t)s->V;
   p->RG = 1;
   while (2 * p->RG < p->W) p->RG *= 2;
   p->RS = 2 * p->RG;
@@ -1046,14 +1080,15 @@ int egr_plan_candidates(egr_plan* p, int32_t exclude_label, void* stream) {
   const uint32_t V = (uint32_t)p->s->V;
   const dim3 grid((p->NG + 3) / 4);
   const uint64_t* R = p->reach[p->rcur];
+  (void)V;
   hipLaunchKernelGGL(cand_count_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS,
-                     p->s->vlabel, exclude_label, V, p->B, p->NG, p->cand_cnt);
+                     p->s->vlabel, exclude_label, p->owned, p->B, p->NG, p->cand_cnt);
   EGR_CHECK_LAUNCH();
   size_t tb = p->sp.tmp_bytes;
   EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sp.tmp, tb, p->cand_cnt, p->cand_off,
                                            (int)((size_t)p->B * p->NG + 1), st));
   hipLaunchKernelGGL(cand_fill_kernel, grid, dim3(256), 0, st, R, (uint32_t)p->RS, p->s->vlabel,
-                     exclude_label, V, p->B, p->NG, p->cand_off, p->cand_list);
+                     exclude_label, p->owned, p->B, p->NG, p->cand_off, p->cand_list);
   EGR_CHECK_LAUNCH();
   p->cand_valid = true;
   p->cand_exclude = exclude_label;
@@ -1076,7 +1111,8 @@ int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* 
   }
   const int waves = p->ntiles * (p->TW > 64 ? p->TW / 64 : 1) * p->n_chunks;
   hipLaunchKernelGGL(topk_partial_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
-                     p->x[p->xcur], p->reach[p->rcur], (uint32_t)p->RS, p->s->vlabel, exclude_label, V, p->TW,
+                     p->x[p->xcur], p->reach[p->rcur], (uint32_t)p->RS, p->s->vlabel, exclude_label, V,
+                     p->owned, p->TW,
                      p->B, p->n_chunks, p->part_s, p->part_v);
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->part_s,
@@ -1135,6 +1171,117 @@ int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, ui
   EGR_HIP(hipMemcpyAsync(&n, p->counter, sizeof(n), hipMemcpyDeviceToHost, st));
   EGR_HIP(hipStreamSynchronize(st));
   *out_n = (int64_t)n;
+  return EGR_OK;
+}
+
+int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const uint8_t* meta,
+                          const float* val, const uint8_t* vlabel, int64_t n_vertices,
+                          int32_t device, egr_snapshot** out) {
+  if (!row_ptr || !out || n_vertices <= 0 || n_vertices >= (int64_t)EGR_NO_NODE || !vlabel)
+    return egr::fail(EGR_EINVAL, "egr_snapshot_from_csr: bad arguments");
+  *out = nullptr;
+  const int64_t V = n_vertices, NE = row_ptr[V];
+  if (row_ptr[0] != 0 || (NE > 0 && (!col || !meta || !val)))
+    return egr::fail(EGR_EINVAL, "egr_snapshot_from_csr: row_ptr must start at 0");
+  for (int64_t v = 0; v < V; ++v)
+    if (row_ptr[v + 1] < row_ptr[v])
+      return egr::fail(EGR_EINVAL, "egr_snapshot_from_csr: row_ptr not monotone");
+  for (int64_t e = 0; e < NE; ++e)
+    if (col[e] >= (uint64_t)V) return egr::fail(EGR_EINVAL, "egr_snapshot_from_csr: col out of range");
+  int ndev = 0;
+  EGR_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return egr::fail(EGR_EINVAL, "egr_snapshot_from_csr: bad device");
+  DeviceGuard guard(device);
+  auto* s = new egr_snapshot();
+  s->device = device;
+  s->V = V;
+  s->NE = NE;
+  int rc = EGR_OK;
+  if ((rc = dalloc(&s->row_ptr, V + 1)) || (rc = dalloc(&s->col, NE)) || (rc = dalloc(&s->meta, NE)) ||
+      (rc = dalloc(&s->val, NE)) || (rc = dalloc(&s->cv, NE)) || (rc = dalloc(&s->vlabel, V))) {
+    egr_snapshot_free(s);
+    return rc;
+  }
+  hipError_t e = hipMemcpy(s->row_ptr, row_ptr, (V + 1) * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && NE) e = hipMemcpy(s->col, col, NE * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && NE) e = hipMemcpy(s->meta, meta, NE, hipMemcpyHostToDevice);
+  if (e == hipSuccess && NE) e = hipMemcpy(s->val, val, NE * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && NE) {
+    std::vector<uint2> cv(NE);
+    for (int64_t i = 0; i < NE; ++i) {
+      uint32_t vb;
+      std::memcpy(&vb, &val[i], 4);
+      cv[i] = make_uint2(col[i], vb);
+    }
+    e = hipMemcpy(s->cv, cv.data(), NE * 8, hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) e = hipMemcpy(s->vlabel, vlabel, V, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    egr_snapshot_free(s);
+    return egr::fail(EGR_EDEVICE, std::string("snapshot upload: ") + hipGetErrorString(e));
+  }
+  s->row_ptr_host.assign(row_ptr, row_ptr + V + 1);
+  *out = s;
+  return EGR_OK;
+}
+
+int egr_plan_set_owned(egr_plan* p, int64_t n_owned) {
+  if (!p || n_owned <= 0 || n_owned > p->s->V)
+    return egr::fail(EGR_EINVAL, "egr_plan_set_owned: need 0 < n_owned <= n_vertices");
+  p->owned = (uint32_t)n_owned;
+  p->cand_valid = false;
+  return EGR_OK;
+}
+
+int egr_plan_pack_scores(const egr_plan* p, const uint32_t* rows, int64_t n, float* out, void* stream) {
+  if (!p || n < 0 || (n > 0 && (!rows || !out))) return egr::fail(EGR_EINVAL, "egr_plan_pack_scores: bad arguments");
+  if (p->hops_done < 0) return egr::fail(EGR_ESTATE, "egr_plan_pack_scores: seeds not set");
+  if (n == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  const float* X = p->hops_done == 0 ? nullptr : p->x[p->xcur];
+  if (!X) return egr::fail(EGR_ESTATE, "egr_plan_pack_scores: run a hop first");
+  hipLaunchKernelGGL(pack_scores_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, X,
+                     (uint32_t)p->s->V, p->TW, p->Bpad, rows, out);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
+
+int egr_plan_unpack_scores(egr_plan* p, const uint32_t* rows, const uint32_t* src, int64_t n,
+                           const float* in, void* stream) {
+  if (!p || n < 0 || (n > 0 && (!rows || !src || !in)))
+    return egr::fail(EGR_EINVAL, "egr_plan_unpack_scores: bad arguments");
+  if (p->hops_done < 1) return egr::fail(EGR_ESTATE, "egr_plan_unpack_scores: run a hop first");
+  if (n == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipLaunchKernelGGL(unpack_scores_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                     p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->Bpad, rows, src, in);
+  EGR_CHECK_LAUNCH();
+  p->cand_valid = false;
+  return EGR_OK;
+}
+
+int egr_plan_pack_reach(const egr_plan* p, const uint32_t* rows, int64_t n, uint64_t* out, void* stream) {
+  if (!p || n < 0 || (n > 0 && (!rows || !out))) return egr::fail(EGR_EINVAL, "egr_plan_pack_reach: bad arguments");
+  if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_pack_reach: sources not set");
+  if (n == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipLaunchKernelGGL(pack_reach_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream,
+                     p->reach[p->rcur], (uint32_t)p->RS, p->W, rows, out);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
+
+int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src, int64_t n,
+                          const uint64_t* in, void* stream) {
+  if (!p || n < 0 || (n > 0 && (!rows || !src || !in)))
+    return egr::fail(EGR_EINVAL, "egr_plan_unpack_reach: bad arguments");
+  if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_unpack_reach: sources not set");
+  if (n == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipLaunchKernelGGL(unpack_reach_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream,
+                     p->reach[p->rcur], (uint32_t)p->RS, p->W, rows, src, in);
+  EGR_CHECK_LAUNCH();
+  p->cand_valid = false;
   return EGR_OK;
 }
 

@@ -111,6 +111,12 @@ SIGNATURES: dict[str, tuple] = {
     "egr_plan_read_scores": (C.c_int, [P, P, P]),
     "egr_plan_read_reach": (C.c_int, [P, P, P]),
     "egr_plan_induced_edges": (C.c_int, [P, I32, P, P, P, I64, PI64, P]),
+    "egr_snapshot_from_csr": (C.c_int, [P, P, P, P, P, I64, I32, C.POINTER(P)]),
+    "egr_plan_set_owned": (C.c_int, [P, I64]),
+    "egr_plan_pack_scores": (C.c_int, [P, P, I64, P, P]),
+    "egr_plan_unpack_scores": (C.c_int, [P, P, P, I64, P, P]),
+    "egr_plan_pack_reach": (C.c_int, [P, P, I64, P, P]),
+    "egr_plan_unpack_reach": (C.c_int, [P, P, P, I64, P, P]),
     "egr_frontier_create": (C.c_int, [P, I32, I64, I32, I64, C.POINTER(P)]),
     "egr_frontier_free": (None, [P]),
     "egr_frontier_set_seeds": (C.c_int, [P, P, P, P, I64, P]),

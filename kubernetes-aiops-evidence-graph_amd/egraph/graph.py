@@ -209,17 +209,34 @@ class EvidenceGraph:
 class Snapshot:
     """Typed CSR + vertex labels resident in HBM on one device."""
 
-    def __init__(self, graph: EvidenceGraph, weights=None, device=None):
+    def __init__(self, graph: EvidenceGraph | None, weights=None, device=None, _handle=None,
+                 _labels=None):
         self.dev = require_device(device)
-        w = graph.weight_array(weights)
-        h = C.c_void_p()
-        L.check(L.lib.egr_snapshot_create(graph.handle, _addr(w), len(graph.rel_types()),
-                                          self.dev.index, C.byref(h)), "egr_snapshot_create")
+        if _handle is None:
+            w = graph.weight_array(weights)
+            h = C.c_void_p()
+            L.check(L.lib.egr_snapshot_create(graph.handle, _addr(w), len(graph.rel_types()),
+                                              self.dev.index, C.byref(h)), "egr_snapshot_create")
+        else:
+            h = _handle
         self._h = h
         nv, ne = C.c_int64(), C.c_int64()
         L.check(L.lib.egr_snapshot_info(h, C.byref(nv), C.byref(ne)), "egr_snapshot_info")
         self.n_vertices, self.n_entries = nv.value, ne.value
-        self.labels = graph.labels()
+        self.labels = graph.labels() if graph is not None else list(_labels or [])
+
+    @classmethod
+    def from_csr(cls, row_ptr, col, meta, val, vlabel, labels=None, device=None) -> "Snapshot":
+        """A snapshot of raw CSR arrays (host numpy), e.g. a partition's local graph
+        (egraph.shard.LocalGraph): egr_snapshot_from_csr."""
+        dev = require_device(device)
+        arrs = [np.ascontiguousarray(row_ptr, np.uint32), np.ascontiguousarray(col, np.uint32),
+                np.ascontiguousarray(meta, np.uint8), np.ascontiguousarray(val, np.float32),
+                np.ascontiguousarray(vlabel, np.uint8)]
+        h = C.c_void_p()
+        L.check(L.lib.egr_snapshot_from_csr(*[_addr(a) for a in arrs], len(arrs[0]) - 1,
+                                            dev.index, C.byref(h)), "egr_snapshot_from_csr")
+        return cls(None, device=dev, _handle=h, _labels=labels)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -260,6 +277,31 @@ class Plan:
 
     def _st(self, stream):
         return L.stream_handle(self.dev) if stream is None else stream
+
+    @property
+    def padded_cols(self) -> int:
+        """Columns padded to the tile width (row length of the pack/unpack buffers)."""
+        return (self.B + self.tile_width - 1) // self.tile_width * self.tile_width
+
+    def set_owned(self, n_owned: int):
+        """Rows [0, n_owned) are the only top-k candidates (a partition's owned vertices)."""
+        L.check(L.lib.egr_plan_set_owned(self._h, n_owned), "egr_plan_set_owned")
+
+    def pack_scores(self, rows: torch.Tensor, out: torch.Tensor, stream=None):
+        L.check(L.lib.egr_plan_pack_scores(self._h, L.ptr(rows), rows.numel(), L.ptr(out),
+                                           self._st(stream)), "egr_plan_pack_scores")
+
+    def unpack_scores(self, rows: torch.Tensor, src: torch.Tensor, inp: torch.Tensor, stream=None):
+        L.check(L.lib.egr_plan_unpack_scores(self._h, L.ptr(rows), L.ptr(src), rows.numel(),
+                                             L.ptr(inp), self._st(stream)), "egr_plan_unpack_scores")
+
+    def pack_reach(self, rows: torch.Tensor, out: torch.Tensor, stream=None):
+        L.check(L.lib.egr_plan_pack_reach(self._h, L.ptr(rows), rows.numel(), L.ptr(out),
+                                          self._st(stream)), "egr_plan_pack_reach")
+
+    def unpack_reach(self, rows: torch.Tensor, src: torch.Tensor, inp: torch.Tensor, stream=None):
+        L.check(L.lib.egr_plan_unpack_reach(self._h, L.ptr(rows), L.ptr(src), rows.numel(),
+                                            L.ptr(inp), self._st(stream)), "egr_plan_unpack_reach")
 
     def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
         n = vertex.numel()

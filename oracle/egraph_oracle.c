@@ -258,6 +258,21 @@ int orc_propagate(const uint32_t* row_ptr, const uint32_t* col, const float* val
   return 0;
 }
 
+/* one hop of the same recurrence on given inputs (the partitioned-graph protocol tests):
+ * out[v][b] = fmaf-chain over row v of val_e * xin[col_e][b], then + s0[v][b]              */
+int orc_hop_step(const uint32_t* row_ptr, const uint32_t* col, const float* val, int64_t V,
+                 int32_t B, const float* xin, const float* s0, float* out) {
+  for (int64_t v = 0; v < V; ++v) {
+    for (int32_t b = 0; b < B; ++b) {
+      float acc = 0.0f;
+      for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e)
+        acc = fmaf(val[e], xin[(size_t)col[e] * B + b], acc);
+      out[(size_t)v * B + b] = acc + s0[(size_t)v * B + b];
+    }
+  }
+  return 0;
+}
+
 typedef struct { float s; uint32_t v; } cand;
 
 static int cand_cmp(const void* a, const void* b) {

@@ -26,7 +26,8 @@ def _load() -> C.CDLL:
     lib = C.CDLL(str(LIB))
     lib.orc_round.restype = C.c_double
     lib.orc_round.argtypes = [C.c_double, C.c_int]
-    for name in ("orc_rules_eval", "orc_rank", "orc_reach", "orc_propagate", "orc_topk"):
+    for name in ("orc_rules_eval", "orc_rank", "orc_reach", "orc_propagate", "orc_topk",
+                 "orc_hop_step"):
         getattr(lib, name).restype = C.c_int
     return lib
 
@@ -135,3 +136,13 @@ def csr_reference(n_vertices, edges, type_index, weights):
         row_ptr.append(len(col))
     return (np.array(row_ptr, np.uint32), np.array(col, np.uint32), np.array(meta, np.uint8),
             np.array(val, np.float32))
+
+
+def hop_step(row_ptr, col, val, xin, s0):
+    """One hop of the A9 recurrence on given scores (partitioned-protocol tests)."""
+    V, B = xin.shape
+    out = np.zeros((V, B), np.float32)
+    lib.orc_hop_step(_p(row_ptr), _p(col), _p(val), C.c_int64(V), C.c_int32(B),
+                     _p(np.ascontiguousarray(xin, np.float32)),
+                     _p(np.ascontiguousarray(s0, np.float32)), _p(out))
+    return out
