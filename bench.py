@@ -17,6 +17,12 @@ deployments / 10k services, Event/LogPattern/MetricAnomaly vertices; synthetic, 
 Multi-GPU (torchrun): every rank holds the snapshot and ranks its own B incidents -- incidents
 are independent, so there is no collective on the data path (weak scaling); the barrier and
 the max-over-ranks timing are the only communication.
+
+--shard graph (BASELINE configs[3], C4: the 1M-vertex graph edge-cut across the ranks,
+egraph/shard.py): each rank owns a partition (local snapshot + dense plan) and the whole job
+ranks ONE batch of B incidents per step; per hop the boundary rows are exchanged point-to-point
+(RCCL all_to_all_single over xGMI), the candidate lists are all-gathered and merged (strong
+scaling).  `--partitions P` on one GPU runs P partitions in one process (device-copy exchange).
 """
 from __future__ import annotations
 
@@ -199,6 +205,157 @@ def time_dense(ctx, hops: int, steps: int, B: int, V: int, nnz: int, dev) -> dic
             "roofline": dense_roofline(ctx, hop_ms, B, V, nnz)}
 
 
+class _TimedPlan:
+    """Delegates to a Plan, recording HIP events around the non-seed propagation hops."""
+
+    def __init__(self, plan, ev):
+        self._p, self._ev, self._h = plan, ev, 0
+
+    def __getattr__(self, name):
+        return getattr(self._p, name)
+
+    def hop(self):
+        if self._ev is not None and self._h > 0:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            self._p.hop()
+            b.record()
+            self._ev.append((a, b))
+        else:
+            self._p.hop()
+        self._h += 1
+
+
+def shard_setup(args, world: int, rank: int, dev: torch.device):
+    from egraph import catalog, shard, synth
+    from egraph.device import to_device
+    from egraph.encode import encode_batch
+    from egraph.graph import EvidenceGraph, Snapshot
+    from egraph.rca import RulesDeviceBatch
+    t0 = time.time()
+    B = args.batch
+    cl = synth.build_cluster(synth.CONFIGS[args.config])
+    cases = synth.make_incidents(cl, B, seed=1000)       # one global batch, same on every rank
+    synth.add_incidents(cl, cases)
+    g = EvidenceGraph()
+    g.merge_nodes(cl.ids, cl.labels)
+    g.merge_edges(cl.src, cl.dst, cl.types)
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    V = g.num_vertices
+    evidence = [x.evidence for x in cases]
+    sv, sc, ss = synth.seeds_for_batch(g, evidence)
+    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+    P = world if world > 1 else max(args.partitions, 1)
+    mine = [rank] if world > 1 else list(range(P))
+    owner = shard.partition_vertices(csr["row_ptr"], vl, g.labels(), P)
+    # rules: each rank evaluates its slice of the batch (incidents are independent)
+    lo, hi = rank * B // world, (rank + 1) * B // world
+    enc = encode_batch(evidence[lo:hi], catalog.default())
+    runs, plans = [], []
+    with torch.cuda.device(dev):
+        rules = RulesDeviceBatch(enc, catalog.default(), dev)
+        for r in mine:
+            lg = shard.build_local(csr, vl, owner, r, P)
+            snap = Snapshot.from_csr(lg.row_ptr, lg.col, lg.meta, lg.val, lg.vlabel, g.labels(), dev)
+            lv, lc, ls = shard.local_seeds(lg, V, sv, sc, ss)
+            plan = snap.plan(B, max_seeds=max(len(lv), 1), k=args.k)
+            seeds = tuple(to_device(np.ascontiguousarray(a), dev) for a in (lv, lc, ls))
+            sources = to_device(shard.local_sources(lg, V, src), dev)
+            runs.append(shard.RankRun(lg, plan, dev))
+            runs[-1].snap = snap
+            plans.append((plan, seeds, sources))
+        torch.cuda.synchronize(dev)
+    comm = shard.TorchComm() if world > 1 else shard.LocalComm()
+    log(f"[rank {rank}] built {args.config}: V={V} entries={len(csr['col'])} P={P} "
+        f"owned={[r.lg.n_owned for r in runs]} halo={[len(r.lg.halo_rows) for r in runs]} "
+        f"in {time.time() - t0:.1f}s")
+    return dict(graph=g, csr=csr, vl=vl, runs=runs, plans=plans, comm=comm, rules=rules, P=P,
+                inc_label=g.labels().index("Incident"), seed_host=(sv, sc, ss), src_host=src,
+                enc_full=encode_batch(evidence, catalog.default()), evidence=evidence, V=V)
+
+
+def shard_step(ctx, hops: int, k: int, ev=None):
+    from egraph import shard
+    ctx["rules"].launch()
+    for run, (plan, seeds, sources) in zip(ctx["runs"], ctx["plans"]):
+        plan.set_seeds(*seeds)
+        plan.set_sources(sources)
+        run.eng = _TimedPlan(plan, ev)
+    return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k)
+
+
+def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
+    ctx = shard_setup(args, world, rank, dev)
+    for _ in range(args.warmup):
+        shard_step(ctx, args.hops, args.k)
+    torch.cuda.synchronize(dev)
+    events: list = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        shard_step(ctx, args.hops, args.k, events)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    B = args.batch
+    ms = elapsed / args.steps * 1e3
+    hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    # the dense hop kernel of the largest local partition (SURVEY §8d bytes, local sizes)
+    big = max(ctx["runs"], key=lambda r: len(r.lg.gid))
+    Vl, nnzl = len(big.lg.gid), len(big.lg.col)
+    hop_bytes = nnzl * 5 + (Vl + 1) * 4 + 2 * Vl * B * 4
+    achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
+    nnz = len(ctx["csr"]["col"])
+    halo = max(r.halo_bytes_per_hop for r in ctx["runs"])
+    out = {
+        "metric": METRIC, "value": B / (ms * 1e-3), "unit": "incidents/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "edges_per_sec": args.hops * nnz * B / (ms * 1e-3),
+        "config": {
+            "workload": f"{args.config}: {ctx['V']}-vertex graph edge-cut into {ctx['P']} "
+                        f"partitions, {args.hops}-hop typed propagation + reach + top-{args.k}, "
+                        f"one batch of {B} incidents per step (whole job)",
+            "engine": "dense (partitioned)", "vertices": ctx["V"], "csr_entries": nnz,
+            "partitions": ctx["P"], "incidents": B, "hops": args.hops, "k": args.k,
+            "parallelism": f"edge-cut x{ctx['P']}" + (" (one process)" if world == 1 else ""),
+            "local_vertices": [len(r.lg.gid) for r in ctx["runs"]],
+            "halo_bytes_per_hop_max_rank": halo,
+        },
+        "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_launch_ms": hop_ms,
+                     "algorithmic_bytes_per_launch": hop_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "oracle"))
+        import oracle
+        from egraph import catalog
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        csr, enc = ctx["csr"], ctx["enc_full"]
+        sv, sc, ss = ctx["seed_host"]
+        t0 = time.perf_counter()
+        oracle.rules_eval(catalog.default().table, enc.flags, enc.vocab, enc.node, enc.err, enc.seg_off)
+        scores = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, args.hops, threads)
+        reach = oracle.reach(csr["row_ptr"], csr["col"], ctx["src_host"], args.hops, threads)
+        oracle.topk(scores, reach, ctx["vl"], ctx["inc_label"], args.k)
+        t1 = time.perf_counter()
+        out["cpu_baseline"] = {"value": B / (t1 - t0), "unit": "incidents/s", "cores": threads,
+                               "kind": "port", "sample": f"one full step of the same batch (B={B}) "
+                               f"on the unpartitioned graph by oracle/egraph_oracle.c, OpenMP "
+                               f"{threads} threads"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -213,6 +370,11 @@ def main():
     ap.add_argument("--engine", default="frontier", choices=["frontier", "dense"])
     ap.add_argument("--dense-steps", type=int, default=5,
                     help="dense-engine steps timed after the main run for comparison (0: skip)")
+    ap.add_argument("--shard", default="incidents", choices=["incidents", "graph"],
+                    help="incidents: replicated snapshot, incident-sharded (default); graph: "
+                         "edge-cut partitioned graph with halo exchange (C4)")
+    ap.add_argument("--partitions", type=int, default=1,
+                    help="--shard graph on one process: partitions run on this GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,6 +389,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.shard == "graph":
+        shard_main(args, world, rank, dev, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     ctx = setup(args.config, args.batch, args.k, rank, dev)
     run_step = step_frontier if args.engine == "frontier" else step
     for _ in range(args.warmup):

@@ -303,6 +303,51 @@ int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_verte
                          float* out_score, uint8_t* out_depth, int64_t cap, int64_t* out_n,
                          void* stream);
 
+/* ---- Alert-storm front end: fingerprints + TTL dedup table (csrc/alerts.hip) ---------------
+ * egr_fingerprint   replaces AlertNormalizer._generate_fingerprint
+ *                   (src/services/ingestion/normalizer.py:208-218) for a batch: key i is
+ *                   blob[offsets[i] .. offsets[i+1]) (device arrays; the caller formats
+ *                   f"{source}:{alertname}:{namespace}:{service}"), out16[i] = first 16 bytes
+ *                   of its SHA-256, out_hex (optional, n*32 chars, no NULs) = the reference's
+ *                   hexdigest()[:32].
+ * egr_dedup_*       replace AlertDeduplicator (src/services/ingestion/deduplicator.py:41-140,
+ *                   Redis with EX) on device: a key is live while now_ms < expiry.
+ *   _ingest         the webhook loop (src/services/ingestion/main.py:141-170 with the
+ *                   registration in create_incident, :392) for a batch in order: an alert whose
+ *                   fingerprint is live is a duplicate of that incident (out_dup 1); the first
+ *                   alert of a non-live fingerprint opens incident first_id + (its rank among
+ *                   the batch's new incidents), registered with expiry now+ttl (out_dup 0);
+ *                   later alerts of that fingerprint in the batch are its duplicates.
+ *                   out_counts (device, 2 u32) = {alerts dropped because the table is full
+ *                   (they fail open: not duplicates, incident EGR_NO_NODE), new incidents}.
+ *   _lookup         check_duplicate (:41-71) for a batch.
+ *   _register       register_fingerprint (:73-104): SET EX for a batch (last write of a
+ *                   repeated key wins); out_full (device u32) = keys dropped (table full).
+ *   _remove         remove_fingerprint (:106-118).
+ *   _extend         extend_fingerprint (:120-140): new expiry for live keys only; out_ok
+ *                   (optional) = was live.
+ *   _stats          out3 = {slots holding a key, live keys, slots}.  Synchronous.
+ *   _compact        rebuild with the live keys only, sized for max(capacity, live).  Synchronous.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct egr_dedup egr_dedup;
+
+int egr_fingerprint(const uint8_t* blob, const int64_t* offsets, int64_t n, uint8_t* out16,
+                    char* out_hex, void* stream);
+int egr_dedup_create(int32_t device, int64_t capacity, egr_dedup** out);
+void egr_dedup_free(egr_dedup* d);
+int egr_dedup_ingest(egr_dedup* d, const uint8_t* fp16, int64_t n, int64_t now_ms, int64_t ttl_ms,
+                     uint32_t first_id, uint8_t* out_dup, uint32_t* out_incident,
+                     uint32_t* out_counts, void* stream);
+int egr_dedup_lookup(const egr_dedup* d, const uint8_t* fp16, int64_t n, int64_t now_ms,
+                     uint8_t* out_dup, uint32_t* out_incident, void* stream);
+int egr_dedup_register(egr_dedup* d, const uint8_t* fp16, int64_t n, int64_t now_ms, int64_t ttl_ms,
+                       const uint32_t* incident, uint32_t* out_full, void* stream);
+int egr_dedup_remove(egr_dedup* d, const uint8_t* fp16, int64_t n, void* stream);
+int egr_dedup_extend(egr_dedup* d, const uint8_t* fp16, int64_t n, int64_t now_ms, int64_t ttl_ms,
+                     uint8_t* out_ok, void* stream);
+int egr_dedup_stats(const egr_dedup* d, int64_t now_ms, int64_t* out3);
+int egr_dedup_compact(egr_dedup* d, int64_t now_ms, int64_t capacity);
+
 #ifdef __cplusplus
 }
 #endif

@@ -126,6 +126,16 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_phase_times": (C.c_int, [P, P, I64, P]),
     "egr_frontier_read_reach": (C.c_int, [P, P, P]),
     "egr_frontier_members": (C.c_int, [P, I32, P, P, P, I64, PI64, P]),
+    "egr_fingerprint": (C.c_int, [P, P, I64, P, P, P]),
+    "egr_dedup_create": (C.c_int, [I32, I64, C.POINTER(P)]),
+    "egr_dedup_free": (None, [P]),
+    "egr_dedup_ingest": (C.c_int, [P, P, I64, I64, I64, U32, P, P, P, P]),
+    "egr_dedup_lookup": (C.c_int, [P, P, I64, I64, P, P, P]),
+    "egr_dedup_register": (C.c_int, [P, P, I64, I64, I64, P, P, P]),
+    "egr_dedup_remove": (C.c_int, [P, P, I64, P]),
+    "egr_dedup_extend": (C.c_int, [P, P, I64, I64, I64, P, P]),
+    "egr_dedup_stats": (C.c_int, [P, I64, PI64]),
+    "egr_dedup_compact": (C.c_int, [P, I64, I64]),
 }
 
 

@@ -30,7 +30,10 @@ def to_device(a, dev: torch.device) -> torch.Tensor:
         a = a.view(np.int32)
     elif a.dtype == np.uint64:
         a = a.view(np.int64)
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:     # e.g. np.frombuffer over bytes
+        a = a.copy()
+    t = torch.from_numpy(a)
     if t.numel() == 0:
         return torch.empty(t.shape, dtype=t.dtype, device=dev)
     return t.pin_memory().to(dev, non_blocking=True)

@@ -10,12 +10,12 @@ whole namespaces and only the cross-namespace edges (CALLS, SCHEDULED_ON) are cu
 Local graph of rank r.  Owned vertices first, in global order, with their FULL rows (entries
 remapped to local ids, CSR order kept, so every row's fmaf chain is exactly the unpartitioned
 one); then the halo (non-owned neighbours of owned vertices), in global order, with empty rows.
-Exports of r = owned vertices with a neighbour owned elsewhere.
+Rank r sends q the r-owned rows that q's rows read.
 
-Per hop (RankRun.run): the engine computes its rows; the owners' fresh export rows are packed,
-all-gathered (RCCL over xGMI: torch.distributed all_gather_into_tensor on device buffers,
-[P * max_export][Bpad] fp32 for scores and [..][ceil(B/64)] u64 for reach) and unpacked into the
-halo rows.  After the last hop each rank ranks its owned candidates; the (score, global id)
+Per hop (run_partitioned): the engine computes its rows; the fresh rows other ranks read are
+packed (one contiguous segment per reader), exchanged point-to-point (RCCL over xGMI:
+torch.distributed all_to_all_single with per-peer row counts; [rows][Bpad] fp32 for scores and
+[rows][ceil(B/64)] u64 for reach) and unpacked into the halo rows.  After the last hop each rank ranks its owned candidates; the (score, global id)
 lists are all-gathered and merged (score desc, global id asc) -- the unpartitioned top-k.
 Scores, reach sets and top-k are bit-identical to the single-GPU plan (tests/test_shard*.py).
 """
@@ -60,28 +60,30 @@ class LocalGraph:
     meta: np.ndarray
     val: np.ndarray
     vlabel: np.ndarray
-    export_rows: np.ndarray  # local ids (owned) this rank sends, in global order
+    send_rows: np.ndarray    # local ids (owned) sent each hop, grouped by destination rank
+    send_counts: list        # rows sent to rank q (send_rows[sum(send_counts[:q]):...])
+    recv_counts: list        # rows received from rank q
     halo_rows: np.ndarray    # local ids of the halo rows
-    halo_src: np.ndarray     # per halo row: index into the all-gathered export rows
-    max_export: int
+    halo_src: np.ndarray     # per halo row: its row in the received buffer
 
 
 def build_local(csr: dict, vlabel: np.ndarray, owner: np.ndarray, rank: int, P: int) -> LocalGraph:
-    """Rank `rank`'s local CSR and exchange maps from the global host CSR (graph.csr())."""
+    """Rank `rank`'s local CSR and exchange maps from the global host CSR (graph.csr()).
+
+    The halo exchange is point-to-point (all-to-all): rank r sends rank q exactly the rows of
+    r-owned vertices that q's rows read, in global id order, and q receives them grouped by
+    sender -- so each boundary row crosses xGMI once per reader instead of once per rank."""
     rp = csr["row_ptr"].astype(np.int64)
     col = csr["col"].astype(np.int64)
     V = len(rp) - 1
     deg = np.diff(rp)
     src_of = np.repeat(np.arange(V, dtype=np.int64), deg)
-    cross = owner[src_of] != owner[col]         # entry (v -> u) across ranks: u is v's halo
-    # exports of every rank (all ranks compute all of them: max_export must agree)
-    exp_mask = np.zeros(V, bool)
-    exp_mask[col[cross]] = True                 # u has a neighbour owned elsewhere
-    exports = [np.flatnonzero(exp_mask & (owner == r)) for r in range(P)]
-    max_export = max([len(e) for e in exports] + [1])
+    cross = owner[src_of] != owner[col]         # entry (v -> u) across ranks: u is in v's halo
+    # (reader rank, vertex) pairs, unique, sorted by reader then vertex id
+    pairs = np.unique(owner[src_of[cross]].astype(np.int64) * V + col[cross])
+    reader, vert = pairs // V, pairs % V
     owned = np.flatnonzero(owner == rank)
-    mine = owner[src_of] == rank
-    halo = np.unique(col[mine & cross])
+    halo = vert[reader == rank]                 # sorted by global id
     gid = np.concatenate([owned, halo]).astype(np.int64)
     g2l = np.full(V, -1, np.int64)
     g2l[gid] = np.arange(len(gid))
@@ -93,19 +95,24 @@ def build_local(csr: dict, vlabel: np.ndarray, owner: np.ndarray, rank: int, P: 
     l_rp[len(owned) + 1:] = l_rp[len(owned)]
     take = np.concatenate([np.arange(s, e) for s, e in zip(starts, ends)]) if len(owned) else \
         np.zeros(0, np.int64)
-    pos_in_export = np.full(V, -1, np.int64)
-    for r in range(P):
-        pos_in_export[exports[r]] = np.arange(len(exports[r]))
-    halo_src = owner[halo].astype(np.int64) * max_export + pos_in_export[halo]
-    assert (pos_in_export[halo] >= 0).all()
+    # sends: pairs whose vertex this rank owns, grouped by reader (already sorted that way)
+    mine = owner[vert] == rank
+    send_v = vert[mine]
+    send_counts = np.bincount(reader[mine], minlength=P).astype(np.int64).tolist()
+    # receives: the halo grouped by owner, vertex order within a group
+    h_owner = owner[halo].astype(np.int64)
+    recv_order = np.lexsort((halo, h_owner))
+    recv_counts = np.bincount(h_owner, minlength=P).astype(np.int64).tolist()
+    halo_src = np.empty(len(halo), np.int64)
+    halo_src[recv_order] = np.arange(len(halo))
     return LocalGraph(
         rank=rank, P=P, gid=gid, n_owned=len(owned),
         row_ptr=l_rp.astype(np.uint32), col=g2l[col[take]].astype(np.uint32),
         meta=csr["meta"][take].astype(np.uint8), val=csr["val"][take].astype(np.float32),
         vlabel=vlabel[gid].astype(np.uint8),
-        export_rows=g2l[exports[rank]].astype(np.uint32),
+        send_rows=g2l[send_v].astype(np.uint32), send_counts=send_counts, recv_counts=recv_counts,
         halo_rows=np.arange(len(owned), len(gid), dtype=np.uint32),
-        halo_src=halo_src.astype(np.uint32), max_export=max_export)
+        halo_src=halo_src.astype(np.uint32))
 
 
 def local_seeds(lg: LocalGraph, V: int, sv: np.ndarray, sc: np.ndarray, ss: np.ndarray):
@@ -128,9 +135,10 @@ def local_sources(lg: LocalGraph, V: int, src: np.ndarray) -> np.ndarray:
 
 
 class TorchComm:
-    """All-gather across the process group: RCCL all_gather_into_tensor on device buffers (the
-    production path, one process per GPU); under gloo (CPU tests, or several processes sharing
-    one GPU, which RCCL refuses) the buffers are staged through host memory."""
+    """Collectives across the process group.  RCCL on device buffers is the production path (one
+    process per GPU): all_to_all_single with per-peer row counts for the halo, all_gather for the
+    candidate lists.  Under gloo (CPU tests, or several processes sharing one GPU, which RCCL
+    refuses) the buffers are staged through host memory."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -151,14 +159,39 @@ class TorchComm:
         self.dist.all_gather_into_tensor(out, x, group=self.group)
         return [out]
 
+    def all_to_all(self, items: list) -> None:
+        """items = [(send, send_counts, recv, recv_counts)] for this process's one rank; rows
+        send[off_q : off_q + send_counts[q]] go to rank q, recv is filled grouped by sender."""
+        ((send, sc, recv, rc),) = items
+        if self.gloo:
+            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+            self.dist.all_to_all_single(hr, hs, output_split_sizes=rc, input_split_sizes=sc,
+                                        group=self.group)
+            recv.copy_(hr)
+            return
+        self.dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
+                                    group=self.group)
+
 
 class LocalComm:
-    """All ranks in one process (tests, and a multi-partition single-GPU run): the gather is a
-    concatenation of the ranks' buffers."""
+    """All ranks in one process (tests, and a multi-partition single-GPU run): gathers are
+    concatenations, the all-to-all copies each sender's segment into its reader's buffer."""
 
     def all_gather(self, send: list[torch.Tensor]) -> list[torch.Tensor]:
         cat = torch.cat([s.to(send[0].device) for s in send])
         return [cat.to(s.device) for s in send]
+
+    def all_to_all(self, items: list) -> None:
+        P = len(items)
+        s_off = [np.concatenate([[0], np.cumsum(sc)]) for _, sc, _, _ in items]
+        r_off = [np.concatenate([[0], np.cumsum(rc)]) for _, _, _, rc in items]
+        for q in range(P):                       # reader
+            for r in range(P):                   # sender
+                n = items[r][1][q]
+                assert n == items[q][3][r]
+                if n:
+                    items[q][2][r_off[q][r]: r_off[q][r] + n] = \
+                        items[r][0][s_off[r][q]: s_off[r][q] + n].to(items[q][2].device)
 
 
 class RankRun:
@@ -167,27 +200,41 @@ class RankRun:
 
     def __init__(self, lg: LocalGraph, engine, device):
         self.lg, self.eng, self.dev = lg, engine, device
-        self.exp = torch.from_numpy(lg.export_rows.view(np.int32)).to(device)
+        self.send = torch.from_numpy(lg.send_rows.view(np.int32)).to(device)
         self.halo = torch.from_numpy(lg.halo_rows.view(np.int32)).to(device)
         self.src = torch.from_numpy(lg.halo_src.view(np.int32)).to(device)
         self.gid = torch.from_numpy(lg.gid).to(device)
         B = engine.B
         self.Bpad = engine.padded_cols
         self.W = (B + 63) // 64
-        self.send_s = torch.zeros((lg.max_export, self.Bpad), dtype=torch.float32, device=device)
-        self.send_r = torch.zeros((lg.max_export, self.W), dtype=torch.int64, device=device)
+        ns, nr = len(lg.send_rows), len(lg.halo_rows)
+        self.send_s = torch.zeros((ns, self.Bpad), dtype=torch.float32, device=device)
+        self.recv_s = torch.zeros((nr, self.Bpad), dtype=torch.float32, device=device)
+        self.send_r = torch.zeros((ns, self.W), dtype=torch.int64, device=device)
+        self.recv_r = torch.zeros((nr, self.W), dtype=torch.int64, device=device)
         engine.set_owned(lg.n_owned)
+
+    @property
+    def halo_bytes_per_hop(self) -> int:
+        """Bytes this rank sends per hop (scores + reach words)."""
+        return len(self.lg.send_rows) * (self.Bpad * 4 + self.W * 8)
 
 
 def _exchange(runs: list[RankRun], comm, what: str) -> None:
-    sends = []
+    items = []
     for r in runs:
-        buf = r.send_s if what == "scores" else r.send_r
-        (r.eng.pack_scores if what == "scores" else r.eng.pack_reach)(r.exp, buf)
-        sends.append(buf)
-    recvs = comm.all_gather(sends)
-    for r, rv in zip(runs, recvs):
-        (r.eng.unpack_scores if what == "scores" else r.eng.unpack_reach)(r.halo, r.src, rv)
+        if what == "scores":
+            r.eng.pack_scores(r.send, r.send_s)
+            items.append((r.send_s, r.lg.send_counts, r.recv_s, r.lg.recv_counts))
+        else:
+            r.eng.pack_reach(r.send, r.send_r)
+            items.append((r.send_r, r.lg.send_counts, r.recv_r, r.lg.recv_counts))
+    comm.all_to_all(items)
+    for r in runs:
+        if what == "scores":
+            r.eng.unpack_scores(r.halo, r.src, r.recv_s)
+        else:
+            r.eng.unpack_reach(r.halo, r.src, r.recv_r)
 
 
 def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int):

@@ -14,10 +14,16 @@ from src.models.hypothesis import (
     HypothesisSource,
     RCAResult,
 )
-from src.models.incident import Incident, IncidentSeverity, IncidentSource, IncidentStatus
+from src.models.incident import (
+    Incident,
+    IncidentCreate,
+    IncidentSeverity,
+    IncidentSource,
+    IncidentStatus,
+)
 
 __all__ = [
     "CollectorResult", "DiagnosisRule", "Evidence", "EvidenceSource", "EvidenceType",
     "GraphEntity", "GraphRelation", "Hypothesis", "HypothesisCategory", "HypothesisSource",
-    "Incident", "IncidentSeverity", "IncidentSource", "IncidentStatus", "RCAResult",
+    "Incident", "IncidentCreate", "IncidentSeverity", "IncidentSource", "IncidentStatus", "RCAResult",
 ]

@@ -52,3 +52,19 @@ class Incident(BaseModel):
     resolved_at: datetime | None = None
     created_at: datetime = Field(default_factory=datetime.utcnow)
     updated_at: datetime = Field(default_factory=datetime.utcnow)
+
+
+class IncidentCreate(BaseModel):
+    """Schema for creating a new incident (reference src/models/incident.py:92-104); the output of
+    AlertNormalizer."""
+    fingerprint: str
+    title: str
+    description: str | None = None
+    severity: IncidentSeverity
+    source: IncidentSource
+    cluster: str
+    namespace: str
+    service: str | None = None
+    labels: dict[str, str] = Field(default_factory=dict)
+    annotations: dict[str, str] = Field(default_factory=dict)
+    started_at: datetime

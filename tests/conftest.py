@@ -38,4 +38,6 @@ def golden():
         "lut": json.loads((g / "mask_lut.json").read_text()),
         "ranker": json.loads((g / "ranker_cases.json").read_text()),
         "fingerprints": json.loads((g / "fingerprints.json").read_text()),
+        "normalizer": json.loads((g / "normalizer_cases.json").read_text()),
+        "storm": json.loads((g / "storm_cases.json").read_text()),
     }

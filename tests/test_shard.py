@@ -1,7 +1,8 @@
 """The partitioned-graph path (egraph/shard.py) on CPU.
 
 * Host maps: every owned row of every rank equals its global row with the entries remapped
-  (CSR order kept), halo rows are empty, and the halo sources point at the right exported rows.
+  (CSR order kept), halo rows are empty, and the all-to-all routing (rank r sends q the rows q reads, grouped
+  by reader) lands every halo row on the right received row.
 * The whole protocol at world size 2 under gloo (two processes, torch.distributed all_gather of
   CPU tensors): per-hop halo exchange of scores and reach words, then the top-k merge -- with
   the CPU engine (tests/shard_cpu_engine.py, the C oracle's single-hop step) in place of the
@@ -48,7 +49,7 @@ def test_local_graphs_cover_the_global_csr(P):
     rp = csr["row_ptr"].astype(np.int64)
     locs = [shard.build_local(csr, vl, owner, r, P) for r in range(P)]
     assert sum(lg.n_owned for lg in locs) == g.num_vertices
-    exports = {}
+    sent = {}
     for lg in locs:
         lrp = lg.row_ptr.astype(np.int64)
         for lv in range(lg.n_owned):
@@ -60,14 +61,20 @@ def test_local_graphs_cover_the_global_csr(P):
         assert (lrp[lg.n_owned:] == lrp[lg.n_owned]).all()          # halo rows are empty
         assert (owner[lg.gid[: lg.n_owned]] == lg.rank).all()
         assert (owner[lg.gid[lg.n_owned:]] != lg.rank).all()
-        exports[lg.rank] = lg.gid[lg.export_rows.astype(np.int64)]
-    # halo sources: the all-gathered export rows hold exactly the halo vertices
-    M = locs[0].max_export
-    flat = np.full(P * M, -1, np.int64)
-    for r in range(P):
-        flat[r * M: r * M + len(exports[r])] = exports[r]
+        assert sum(lg.send_counts) == len(lg.send_rows) and lg.send_counts[lg.rank] == 0
+        assert (lg.send_rows < lg.n_owned).all()
+        off = np.concatenate([[0], np.cumsum(lg.send_counts)])
+        for q in range(P):
+            sent[(lg.rank, q)] = lg.gid[lg.send_rows[off[q]:off[q + 1]].astype(np.int64)]
+    # routing: what q receives from r is what r sends to q; halo sources pick the right rows
     for lg in locs:
-        assert (flat[lg.halo_src.astype(np.int64)] == lg.gid[lg.n_owned:]).all()
+        assert all(lg.recv_counts[r] == len(sent[(r, lg.rank)]) for r in range(P))
+        recv = np.concatenate([sent[(r, lg.rank)] for r in range(P)])
+        assert len(recv) == len(lg.halo_rows)
+        assert (recv[lg.halo_src.astype(np.int64)] == lg.gid[lg.n_owned:]).all()
+        # every halo vertex is read by an owned row, and no boundary row is sent twice to q
+        for r in range(P):
+            assert len(np.unique(sent[(r, lg.rank)])) == len(sent[(r, lg.rank)])
 
 
 def _rank_main(rank, P, port, q):
