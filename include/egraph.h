@@ -303,6 +303,37 @@ int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_verte
                          float* out_score, uint8_t* out_depth, int64_t cap, int64_t* out_n,
                          void* stream);
 
+/* ---- Incremental snapshot update + download (csrc/update.hip) -----------------------------
+ * egr_snapshot_update   append n_new vertices (labels new_vlabel) and n_edges NEW edges
+ *                       (edge_src / edge_dst / edge_type; ids in the grown numbering) to a
+ *                       device snapshot: the result equals egr_snapshot_create on the grown
+ *                       graph (same row order, same val = w / deg with the new degrees).  All
+ *                       delta arrays are DEVICE pointers; weights as egr_snapshot_create (host).
+ *                       The edges must be absent from the snapshot and distinct -- the host
+ *                       MERGE (egr_graph_merge_edges) guarantees it; a violation or an
+ *                       out-of-range id returns EGR_EINVAL with the snapshot unchanged.
+ *                       Synchronous on `stream`.  Plans created before an update return
+ *                       EGR_ESTATE afterwards; a frontier keeps working while the snapshot
+ *                       stays within the vertex headroom it was sized with (V + V/4 + 4096).
+ *                       Replaces the per-item MERGE round trips of neo4j.py:95-167 for the
+ *                       alert storm's per-tick deltas (BASELINE config C5).
+ * egr_snapshot_download copy the CSR and labels to host buffers (NULL = skip): row_ptr [V+1],
+ *                       col / meta / val [n_entries], vlabel [V].  Synchronous.
+ * egr_snapshot_version  number of updates applied.
+ * egr_graph_export_edges  edges [first, first + n) of the host graph in creation order (the
+ *                       delta a MERGE batch appended).
+ * ---------------------------------------------------------------------------------------- */
+int egr_snapshot_update(egr_snapshot* s, const uint8_t* new_vlabel, int64_t n_new,
+                        const uint32_t* edge_src, const uint32_t* edge_dst, const uint8_t* edge_type,
+                        int64_t n_edges, const float* weights, int32_t n_types, void* stream);
+int egr_snapshot_download(const egr_snapshot* s, uint32_t* row_ptr, uint32_t* col, uint8_t* meta,
+                          float* val, uint8_t* vlabel);
+int64_t egr_snapshot_version(const egr_snapshot* s);
+/* vertex count a frontier was sized for (it runs while the snapshot stays within it) */
+int64_t egr_frontier_max_vertices(const egr_frontier* f);
+int egr_graph_export_edges(const egr_graph* g, int64_t first, int64_t n, int32_t* edge_src,
+                           int32_t* edge_dst, uint8_t* edge_type);
+
 /* ---- Alert-storm front end: fingerprints + TTL dedup table (csrc/alerts.hip) ---------------
  * egr_fingerprint   replaces AlertNormalizer._generate_fingerprint
  *                   (src/services/ingestion/normalizer.py:208-218) for a batch: key i is

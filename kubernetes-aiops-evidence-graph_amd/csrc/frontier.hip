@@ -896,6 +896,8 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
 
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
+  int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
+                                  // for incremental snapshot updates)
   int B = 0, k = 0, nbig = 0;
   int64_t max_seeds = 0;
   uint32_t gcap = 0;
@@ -940,7 +942,10 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   f->B = n_cols;
   f->k = k;
   f->max_seeds = max_seeds;
-  const uint32_t V = (uint32_t)s->V;
+  // sized with headroom so the snapshot can grow by incremental updates (egr_snapshot_update)
+  const int64_t vmax = std::min<int64_t>(s->V + s->V / 4 + 4096, (int64_t)EGR_NO_NODE - 1);
+  f->vmax = vmax;
+  const uint32_t V = (uint32_t)vmax;
   // fallback table: 2 x nextpow2(V) slots, never more than half full
   size_t gcap = 2 * LCAP;
   while (gcap < 2ull * V) gcap *= 2;
@@ -1008,12 +1013,21 @@ void egr_frontier_free(egr_frontier* f) {
   delete f;
 }
 
+
+static int frontier_outgrown(const egr_frontier* f, const char* what) {
+  return egr::fail(EGR_ESTATE, std::string(what) + ": the snapshot grew past the " +
+                   std::to_string(f->vmax) + " vertices this frontier was sized for; create a new one");
+}
+
+int64_t egr_frontier_max_vertices(const egr_frontier* f) { return f ? f->vmax : -1; }
+
 int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const uint32_t* seed_col,
                            const float* seed_val, int64_t n_seeds, void* stream) {
   if (!f || n_seeds < 0 || n_seeds > f->max_seeds ||
       (n_seeds > 0 && (!seed_vertex || !seed_col || !seed_val)))
     return egr::fail(EGR_EINVAL,
                      "egr_frontier_set_seeds: bad arguments (n_seeds above capacity?)");
+  if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_set_seeds");
   DeviceGuard guard(f->s->device);
   const uint32_t V = (uint32_t)f->s->V;
   hipStream_t st = (hipStream_t)stream;
@@ -1043,6 +1057,7 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   if (!f || !source_vertex || !out_ids || !out_scores || hops < 1 || hops > MAX_HOPS)
     return egr::fail(EGR_EINVAL, "egr_frontier_run: bad arguments (need 1 <= hops <= 60)");
   if (!f->seeds_set) return egr::fail(EGR_ESTATE, "egr_frontier_run: seeds not set");
+  if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run");
   DeviceGuard guard(f->s->device);
   hipStream_t st = (hipStream_t)stream;
   const egr_snapshot* s = f->s;

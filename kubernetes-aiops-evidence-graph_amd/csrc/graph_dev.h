@@ -20,7 +20,15 @@ struct egr_snapshot {
   float* val = nullptr;
   uint2* cv = nullptr;       // (col, val bits) per entry: one 8-B load per entry (frontier)
   uint8_t* vlabel = nullptr;
+  // incremental updates (update.hip): capacities of the live arrays, a version bumped by every
+  // update (plans built on an older version refuse to run), and the spare buffers / scratch
+  int64_t cap_v = 0, cap_e = 0;
+  uint64_t version = 0;
+  struct SnapUpdate* upd = nullptr;
 };
+
+// update.hip: frees egr_snapshot::upd (called by egr_snapshot_free)
+void snapshot_update_free(egr_snapshot* s);
 
 namespace egr {
 

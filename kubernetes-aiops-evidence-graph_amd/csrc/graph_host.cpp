@@ -184,6 +184,17 @@ int egr_graph_export(const egr_graph* g, uint8_t* vertex_label, int32_t* edge_sr
   return EGR_OK;
 }
 
+int egr_graph_export_edges(const egr_graph* g, int64_t first, int64_t n, int32_t* edge_src,
+                           int32_t* edge_dst, uint8_t* edge_type) {
+  if (!g || first < 0 || n < 0 || first + n > (int64_t)g->esrc.size())
+    return egr::fail(EGR_EINVAL, "egr_graph_export_edges: range outside the edge list");
+  if (n == 0) return EGR_OK;
+  if (edge_src) memcpy(edge_src, g->esrc.data() + first, (size_t)n * 4);
+  if (edge_dst) memcpy(edge_dst, g->edst.data() + first, (size_t)n * 4);
+  if (edge_type) memcpy(edge_type, g->etype.data() + first, (size_t)n);
+  return EGR_OK;
+}
+
 int egr_graph_csr(const egr_graph* g, const float* weights, int32_t n_types, uint32_t* row_ptr,
                   uint32_t* col, uint8_t* meta, float* val) {
   if (!g || !row_ptr || !col || !meta || !val || n_types < 0 || (n_types > 0 && !weights))

@@ -717,6 +717,7 @@ __global__ void unpack_reach_kernel(uint64_t* __restrict__ R, uint32_t RS, int W
 
 struct egr_plan {
   const egr_snapshot* s = nullptr;
+  uint64_t version = 0;      // snapshot version the V-sized buffers and chunk tables were built for
   int B = 0, TW = 0, Bpad = 0, ntiles = 0, W = 0, k = 0;
   int RG = 0, RS = 0;        // reach: RG lanes x 16 B per row, RS = 2*RG words per row
   int64_t max_seeds = 0;
@@ -894,6 +895,8 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
     return egr::fail(EGR_EDEVICE, std::string("snapshot upload: ") + hipGetErrorString(e));
   }
   s->row_ptr_host = std::move(row_ptr);
+  s->cap_v = V;
+  s->cap_e = 2 * E;
   *out = s;
   return EGR_OK;
 }
@@ -907,6 +910,7 @@ void egr_snapshot_free(egr_snapshot* s) {
   dfree(s->val);
   dfree(s->cv);
   dfree(s->vlabel);
+  snapshot_update_free(s);
   delete s;
 }
 
@@ -926,6 +930,7 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
   DeviceGuard guard(s->device);
   auto* p = new egr_plan();
   p->s = s;
+  p->version = s->version;
   p->B = n_cols;
   p->TW = choose_tile_width(n_cols);
   p->Bpad = (n_cols + p->TW - 1) / p->TW * p->TW;
@@ -997,10 +1002,17 @@ void egr_plan_free(egr_plan* p) {
 
 int egr_plan_tile_width(const egr_plan* p) { return p ? p->TW : -1; }
 
+
+static int plan_stale(const egr_plan* p, const char* what) {
+  return egr::fail(EGR_ESTATE, std::string(what) +
+                   ": the snapshot was updated after this plan was created; create a new plan");
+}
+
 int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t* seed_col,
                        const float* seed_val, int64_t n_seeds, void* stream) {
   if (!p || n_seeds < 0 || n_seeds > p->max_seeds || (n_seeds > 0 && (!seed_vertex || !seed_col || !seed_val)))
     return egr::fail(EGR_EINVAL, "egr_plan_set_seeds: bad arguments (n_seeds above plan capacity?)");
+  if (p->version != p->s->version) return plan_stale(p, "egr_plan_set_seeds");
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const uint32_t V = (uint32_t)p->s->V;
@@ -1020,6 +1032,7 @@ int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t*
 
 int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* stream) {
   if (!p || !source_vertex) return egr::fail(EGR_EINVAL, "egr_plan_set_sources: NULL argument");
+  if (p->version != p->s->version) return plan_stale(p, "egr_plan_set_sources");
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const uint32_t V = (uint32_t)p->s->V;
@@ -1034,11 +1047,15 @@ int egr_plan_set_sources(egr_plan* p, const uint32_t* source_vertex, void* strea
   return EGR_OK;
 }
 
-int egr_plan_hop(egr_plan* p, void* stream) { return plan_hop(p, stream); }
+int egr_plan_hop(egr_plan* p, void* stream) {
+  if (p && p->version != p->s->version) return plan_stale(p, "egr_plan_hop");
+  return plan_hop(p, stream);
+}
 
 int egr_plan_reach_hop(egr_plan* p, void* stream) {
   if (!p) return egr::fail(EGR_EINVAL, "egr_plan_reach_hop: NULL plan");
   if (!p->sources_set) return egr::fail(EGR_ESTATE, "egr_plan_reach_hop: sources not set");
+  if (p->version != p->s->version) return plan_stale(p, "egr_plan_reach_hop");
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   switch (p->RG) {
@@ -1221,6 +1238,8 @@ int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const ui
     return egr::fail(EGR_EDEVICE, std::string("snapshot upload: ") + hipGetErrorString(e));
   }
   s->row_ptr_host.assign(row_ptr, row_ptr + V + 1);
+  s->cap_v = V;
+  s->cap_e = NE;
   *out = s;
   return EGR_OK;
 }

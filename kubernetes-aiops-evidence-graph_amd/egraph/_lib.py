@@ -126,6 +126,11 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_phase_times": (C.c_int, [P, P, I64, P]),
     "egr_frontier_read_reach": (C.c_int, [P, P, P]),
     "egr_frontier_members": (C.c_int, [P, I32, P, P, P, I64, PI64, P]),
+    "egr_snapshot_update": (C.c_int, [P, P, I64, P, P, P, I64, P, I32, P]),
+    "egr_snapshot_download": (C.c_int, [P, P, P, P, P, P]),
+    "egr_snapshot_version": (I64, [P]),
+    "egr_frontier_max_vertices": (I64, [P]),
+    "egr_graph_export_edges": (C.c_int, [P, I64, I64, P, P, P]),
     "egr_fingerprint": (C.c_int, [P, P, I64, P, P, P]),
     "egr_dedup_create": (C.c_int, [I32, I64, C.POINTER(P)]),
     "egr_dedup_free": (None, [P]),

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from .device import require_device
+from .device import require_device, to_device
 
 # Per relationship type (forward, reverse) propagation weights -- DESIGN.md §A9.
 DEFAULT_WEIGHTS: dict[str, tuple[float, float]] = {
@@ -181,6 +181,16 @@ class EvidenceGraph:
                 "egr_graph_export")
         return vl, es, ed, et
 
+    def export_edges(self, first: int, n: int | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Edges [first, first + n) in creation order (what MERGE batches appended since)."""
+        if n is None:
+            n = self.num_edges - first
+        es, ed = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32)
+        et = np.empty(max(n, 1), np.uint8)
+        L.check(L.lib.egr_graph_export_edges(self._h, first, n, _addr(es), _addr(ed), _addr(et)),
+                "egr_graph_export_edges")
+        return es[:n], ed[:n], et[:n]
+
     def weight_array(self, weights: dict[str, tuple[float, float]] | None = None) -> np.ndarray:
         """[n_types*2] fp32 (fwd, rev) weights in this graph's type order."""
         weights = DEFAULT_WEIGHTS if weights is None else weights
@@ -220,10 +230,63 @@ class Snapshot:
         else:
             h = _handle
         self._h = h
-        nv, ne = C.c_int64(), C.c_int64()
-        L.check(L.lib.egr_snapshot_info(h, C.byref(nv), C.byref(ne)), "egr_snapshot_info")
-        self.n_vertices, self.n_entries = nv.value, ne.value
+        self.weights = weights
+        self._refresh_info()
         self.labels = graph.labels() if graph is not None else list(_labels or [])
+        # the host graph's edge count this snapshot reflects (for incremental sync)
+        self.synced_edges = graph.num_edges if graph is not None else None
+
+    def _refresh_info(self):
+        nv, ne = C.c_int64(), C.c_int64()
+        L.check(L.lib.egr_snapshot_info(self._h, C.byref(nv), C.byref(ne)), "egr_snapshot_info")
+        self.n_vertices, self.n_entries = nv.value, ne.value
+
+    @property
+    def version(self) -> int:
+        return int(L.lib.egr_snapshot_version(self._h))
+
+    def update(self, new_vlabel: torch.Tensor, edge_src: torch.Tensor, edge_dst: torch.Tensor,
+               edge_type: torch.Tensor, weight_array: np.ndarray, stream=None) -> None:
+        """egr_snapshot_update with device tensors (u8 labels, i32 ids, u8 types): append
+        vertices and NEW edges, rebuilding the affected rows and values on the device."""
+        n, m = new_vlabel.numel(), edge_src.numel()
+        if not (edge_dst.numel() == m == edge_type.numel()):
+            raise ValueError("edge arrays differ in length")
+        w = np.ascontiguousarray(weight_array, np.float32)
+        st = L.stream_handle(self.dev) if stream is None else stream
+        L.check(L.lib.egr_snapshot_update(self._h, L.ptr(new_vlabel), n, L.ptr(edge_src),
+                                          L.ptr(edge_dst), L.ptr(edge_type), m, _addr(w),
+                                          len(w) // 2, st), "egr_snapshot_update")
+        self._refresh_info()
+
+    def sync(self, graph: EvidenceGraph, stream=None) -> tuple[int, int]:
+        """Bring the snapshot up to `graph` (the one it was built from, grown by MERGE batches
+        since) with one incremental update.  Returns (new vertices, new edges)."""
+        if self.synced_edges is None:
+            raise ValueError("snapshot was not built from an EvidenceGraph")
+        V0, E0 = self.n_vertices, self.synced_edges
+        V, E = graph.num_vertices, graph.num_edges
+        if V == V0 and E == E0:
+            return 0, 0
+        vl, _, _, _ = graph.export()
+        es, ed, et = graph.export_edges(E0, E - E0)
+        with torch.cuda.device(self.dev):
+            self.update(to_device(np.ascontiguousarray(vl[V0:]), self.dev),
+                        to_device(es.view(np.uint32), self.dev), to_device(ed.view(np.uint32), self.dev),
+                        to_device(et, self.dev), graph.weight_array(self.weights), stream)
+        self.synced_edges = E
+        self.labels = graph.labels()
+        return V - V0, E - E0
+
+    def download(self) -> dict[str, np.ndarray]:
+        """Host copy of the device CSR (the layout of EvidenceGraph.csr()) and labels."""
+        V, NE = self.n_vertices, self.n_entries
+        rp = np.empty(V + 1, np.uint32)
+        col, meta = np.empty(max(NE, 1), np.uint32), np.empty(max(NE, 1), np.uint8)
+        val, vl = np.empty(max(NE, 1), np.float32), np.empty(max(V, 1), np.uint8)
+        L.check(L.lib.egr_snapshot_download(self._h, _addr(rp), _addr(col), _addr(meta), _addr(val),
+                                            _addr(vl)), "egr_snapshot_download")
+        return {"row_ptr": rp, "col": col[:NE], "meta": meta[:NE], "val": val[:NE], "vlabel": vl[:V]}
 
     @classmethod
     def from_csr(cls, row_ptr, col, meta, val, vlabel, labels=None, device=None) -> "Snapshot":
@@ -386,6 +449,7 @@ class Frontier:
         L.check(L.lib.egr_frontier_create(snap.handle, n_cols, max_seeds, k, pool_entries,
                                           C.byref(h)), "egr_frontier_create")
         self._h = h
+        self.max_vertices = int(L.lib.egr_frontier_max_vertices(h))
         self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
 

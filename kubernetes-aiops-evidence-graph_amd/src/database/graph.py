@@ -13,8 +13,10 @@ Root-cause ranking (build-defined): rank_r
 the frontier engine (egr_frontier_*) -- per incident, 3-hop typed propagation of the evidence
 rows' signal strengths over the graph, ranked over the incident's 3-hop reach set.
 
-The graph is process-wide, like the Neo4j database the reference talks to; writes invalidate
-the device snapshot, the next read rebuilds it.
+The graph is process-wide, like the Neo4j database the reference talks to.  Writes go to the host
+graph (MERGE); the next read brings the device snapshot up to date with ONE incremental update
+(egr_snapshot_update: the appended vertices and edges merged into the CSR on the device) instead
+of a rebuild and re-upload.
 """
 from __future__ import annotations
 
@@ -49,7 +51,7 @@ class GraphService:
 
     @classmethod
     def _invalidate(cls) -> None:
-        cls._snapshot, cls._plans, cls._frontiers = None, {}, {}
+        """After a write: the snapshot is synced lazily by the next read (_snap)."""
 
     @staticmethod
     async def create_entity(entity: GraphEntity) -> str:
@@ -85,22 +87,29 @@ class GraphService:
 
     @classmethod
     def _plan(cls, n_cols: int):
+        snap = cls._snap()          # syncs first: a write drops the plans
         if n_cols not in cls._plans:
-            cls._plans[n_cols] = cls._snap().plan(n_cols, max_seeds=0, k=1)
+            cls._plans[n_cols] = snap.plan(n_cols, max_seeds=0, k=1)
         return cls._plans[n_cols]
 
     @classmethod
     def _snap(cls):
+        g = cls.graph()
         if cls._snapshot is None:
-            cls._snapshot = cls.graph().snapshot(device=cls.device)
+            cls._snapshot = g.snapshot(device=cls.device)
+        elif cls._snapshot.sync(g) != (0, 0):
+            cls._plans = {}        # plans are sized for one snapshot version
+            cls._frontiers = {k: f for k, f in cls._frontiers.items()
+                              if f.max_vertices >= cls._snapshot.n_vertices}
         return cls._snapshot
 
     @classmethod
     def _frontier(cls, n_cols: int, n_seeds: int, k: int):
         """A frontier for n_cols columns, reused while its seed capacity suffices."""
+        snap = cls._snap()
         fr = cls._frontiers.get((n_cols, k))
         if fr is None or fr.max_seeds < n_seeds:
-            fr = cls._snap().frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k)
+            fr = snap.frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k)
             cls._frontiers[(n_cols, k)] = fr
         return fr
 
