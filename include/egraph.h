@@ -329,6 +329,11 @@ int egr_snapshot_update(egr_snapshot* s, const uint8_t* new_vlabel, int64_t n_ne
 int egr_snapshot_download(const egr_snapshot* s, uint32_t* row_ptr, uint32_t* col, uint8_t* meta,
                           float* val, uint8_t* vlabel);
 int64_t egr_snapshot_version(const egr_snapshot* s);
+/* multi-source BFS: out_dist[v] (device, V bytes) = undirected hops from the nearest of the n
+ * source vertices (device u32; ids >= V ignored), 0xFF beyond `hops`.  The alert storm marks
+ * the incidents an update can affect with it. */
+int egr_snapshot_within(const egr_snapshot* s, const uint32_t* sources, int64_t n, int32_t hops,
+                        uint8_t* out_dist, void* stream);
 /* vertex count a frontier was sized for (it runs while the snapshot stays within it) */
 int64_t egr_frontier_max_vertices(const egr_frontier* f);
 int egr_graph_export_edges(const egr_graph* g, int64_t first, int64_t n, int32_t* edge_src,

@@ -155,6 +155,24 @@ __global__ void __launch_bounds__(256) labels_kernel(const uint8_t* __restrict__
   out[v] = v < V ? old_l[v] : new_l[v - V];
 }
 
+// multi-source BFS over the symmetric CSR: dist[v] = hops from the nearest source, 0xFF beyond
+__global__ void __launch_bounds__(256) within_seed_kernel(const uint32_t* __restrict__ src, int64_t n,
+                                                          uint32_t V, uint8_t* __restrict__ dist) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && src[i] < V) dist[src[i]] = 0;
+}
+
+__global__ void __launch_bounds__(256) within_hop_kernel(const uint32_t* __restrict__ row_ptr,
+                                                         const uint32_t* __restrict__ col, uint32_t V,
+                                                         uint8_t h, uint8_t* __restrict__ dist) {
+  const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V || dist[v] != (uint8_t)(h - 1)) return;
+  for (uint32_t e = row_ptr[v], ee = row_ptr[v + 1]; e < ee; ++e) {
+    const uint32_t u = col[e];
+    if (dist[u] == 0xFF) dist[u] = h;   // racing writers all store h
+  }
+}
+
 inline unsigned grid(int64_t n, int bs = 256) { return (unsigned)std::max<int64_t>(1, (n + bs - 1) / bs); }
 
 int bits_for(uint64_t x) {
@@ -327,5 +345,22 @@ int egr_snapshot_download(const egr_snapshot* s, uint32_t* row_ptr, uint32_t* co
 }
 
 int64_t egr_snapshot_version(const egr_snapshot* s) { return s ? (int64_t)s->version : -1; }
+
+int egr_snapshot_within(const egr_snapshot* s, const uint32_t* sources, int64_t n, int32_t hops,
+                        uint8_t* out_dist, void* stream) {
+  if (!s || n < 0 || (n > 0 && !sources) || !out_dist || hops < 0 || hops > 254)
+    return egr::fail(EGR_EINVAL, "egr_snapshot_within: bad arguments (0 <= hops <= 254)");
+  DeviceGuard guard(s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t V = (uint32_t)s->V;
+  EGR_HIP(hipMemsetAsync(out_dist, 0xFF, V, st));
+  if (n == 0) return EGR_OK;
+  hipLaunchKernelGGL(within_seed_kernel, dim3(grid(n)), dim3(256), 0, st, sources, n, V, out_dist);
+  for (int h = 1; h <= hops; ++h)
+    hipLaunchKernelGGL(within_hop_kernel, dim3(grid(V)), dim3(256), 0, st, s->row_ptr, s->col, V,
+                       (uint8_t)h, out_dist);
+  EGR_CHECK_LAUNCH();
+  return EGR_OK;
+}
 
 }  // extern "C"

@@ -278,6 +278,15 @@ class Snapshot:
         self.labels = graph.labels()
         return V - V0, E - E0
 
+    def within(self, sources: torch.Tensor, hops: int, stream=None) -> torch.Tensor:
+        """uint8 [V] device tensor: undirected hops from the nearest source vertex (i32 device
+        tensor), 255 beyond `hops` (egr_snapshot_within)."""
+        out = torch.empty(max(self.n_vertices, 1), dtype=torch.uint8, device=self.dev)[: self.n_vertices]
+        st = L.stream_handle(self.dev) if stream is None else stream
+        L.check(L.lib.egr_snapshot_within(self._h, L.ptr(sources), sources.numel(), hops, L.ptr(out), st),
+                "egr_snapshot_within")
+        return out
+
     def download(self) -> dict[str, np.ndarray]:
         """Host copy of the device CSR (the layout of EvidenceGraph.csr()) and labels."""
         V, NE = self.n_vertices, self.n_entries

@@ -41,9 +41,12 @@ def attach_ids(ev: dict) -> list[str]:
     return []
 
 
-def seeds_for_batch(graph, evidence_lists: list[list[dict]]):
+def seeds_for_batch(graph, evidence_lists: list[list[dict]], pending: list | None = None):
     """(vertex u32, column u32, strength f32) triples for a batch: each row attaches to the
-    first of its candidate ids present in the graph; unattached rows are dropped."""
+    first of its candidate ids present in the graph; unattached rows are dropped.
+    `pending` (optional, a list) receives per column the set of candidate ids ranked before the
+    one attached (all of them for an unattached row): the vertices whose later creation would
+    re-attach a row -- the alert storm's re-rank trigger (egraph/storm.py)."""
     flat, count, col, val = [], [], [], []
     for b, evs in enumerate(evidence_lists):
         for ev in evs:
@@ -55,16 +58,23 @@ def seeds_for_batch(graph, evidence_lists: list[list[dict]]):
             count.append(len(ids))
             col.append(b)
             val.append(s)
+    if pending is not None:
+        pending[:] = [set() for _ in evidence_lists]
     if not flat:
         return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
     found = graph.lookup(flat)
     chosen = np.full(len(count), -1, np.int64)
     pos = 0
     for r, n in enumerate(count):
-        for v in found[pos:pos + n]:
+        for j, v in enumerate(found[pos:pos + n]):
             if v >= 0:
                 chosen[r] = v
+                if pending is not None and j:
+                    pending[col[r]].update(flat[pos:pos + j])
                 break
+        else:
+            if pending is not None:
+                pending[col[r]].update(flat[pos:pos + n])
         pos += n
     keep = chosen >= 0
     return (chosen[keep].astype(np.uint32), np.asarray(col, np.uint32)[keep],

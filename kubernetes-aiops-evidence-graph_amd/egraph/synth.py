@@ -201,97 +201,104 @@ def make_incidents(c: Cluster, n: int, seed: int = 7, events_per_incident: int =
     for i in range(n):
         sc = scenario or SCENARIOS[int(rng.choice(len(SCENARIOS), p=SCENARIO_P))]
         d = int(rng.integers(0, len(c.deploy_name)))
-        ns = c.ns_names[int(c.deploy_ns[d])]
-        dname = c.deploy_name[d]
         iid = f"00000000-0000-4000-8000-{seed:04x}{i:08x}"
-        inc = {"id": iid, "fingerprint": f"fp-{i}", "title": f"{sc}: {dname}",
-               "severity": "critical", "source": "synthetic", "cluster": "synthetic",
-               "namespace": ns, "service": dname, "started_at": "2026-08-21T00:00:00Z"}
-        ev, ents, rels = [], [], []
-        k = 0
-
-        def row(etype, entity, data, strength, source="kubernetes_api"):
-            nonlocal k
-            k += 1
-            ev.append({"id": f"{iid[-12:]}-{k:04d}", "incident_id": iid, "evidence_type": etype,
-                       "source": source, "entity_name": entity, "entity_namespace": ns,
-                       "data": data, "signal_strength": strength})
-
-        ents.append({"id": f"incident:{iid}", "type": "Incident",
-                     "properties": {"id": iid, "title": inc["title"], "namespace": ns}})
-        pods = c.deploy_pods[d]
-        for pname in pods:
-            restarts = int(rng.geometric(0.3)) - 1
-            wr = tr = None
-            phase = "Running"
-            if sc.startswith("crashloop"):
-                wr = "CrashLoopBackOff" if rng.random() < 0.8 else None
-                tr = "Error" if rng.random() < 0.5 else None
-            elif sc == "oom":
-                tr = "OOMKilled" if rng.random() < 0.7 else None
-            elif sc == "imagepull":
-                wr = ("ImagePullBackOff", "ErrImagePull")[int(rng.integers(0, 2))]
-                phase, restarts = "Pending", 0
-            ready = "True" if (wr is None and tr is None and rng.random() < 0.7) else "False"
-            conds = [{"type": "Ready", "status": ready,
-                      "reason": None if ready == "True" else "ContainersNotReady"}]
-            row("kubernetes_pod", pname,
-                {"name": pname, "namespace": ns, "phase": phase, "node_name": c.pod_node[pname],
-                 "restart_count": restarts, "waiting_reason": wr, "terminated_reason": tr,
-                 "conditions": conds}, _pod_strength(wr, tr, restarts, phase))
-            rels.append({"source_id": f"incident:{iid}", "target_id": f"pod:{ns}:{pname}",
-                         "relation_type": "AFFECTS"})
-        row("kubernetes_deployment", dname,
-            {"name": dname, "namespace": ns, "replicas": len(pods), "ready_replicas": 0,
-             "unavailable_replicas": len(pods)}, 0.8)
-        for j in range(events_per_incident):
-            pname = pods[j % len(pods)]
-            reason = ("BackOff", "Unhealthy", "Failed", "Pulled", "Created")[int(rng.integers(0, 5))]
-            warn = reason in ("BackOff", "Unhealthy", "Failed")
-            row("kubernetes_event", pname,
-                {"type": "Warning" if warn else "Normal", "reason": reason, "message": reason,
-                 "involved_object": {"kind": "Pod", "name": pname, "namespace": ns}, "count": 1},
-                0.9 if warn else 0.4)
-        errors = int(rng.integers(0, 40))
-        pats = ["error"] + (["network"] if rng.random() < 0.3 else []) + \
-            (["oom"] if sc == "oom" else [])
-        row("log_signal", dname, {"total_lines": 500, "error_count": errors, "warning_count": 3,
-                                  "patterns_found": pats},
-            0.9 if errors > 10 else 0.8 if errors > 5 else 0.6 if errors else 0.3, "loki")
-        cats = ["crashloop", "resource", "deployment"] + (["oom"] if sc == "oom" else ["latency", "hpa"])
-        names = [q for cat in cats for q in PROMQL[cat]]
-        for j in range(15):
-            qn = names[j % len(names)]
-            if "memory" in qn:
-                v = float(rng.uniform(0, 100))
-            elif "latency" in qn:
-                v = float(rng.uniform(0, 5))
-            elif "hpa" in qn:
-                v = float(rng.integers(0, 2))
-            else:
-                v = float(rng.uniform(0, 10))
-            st = _metric_strength(qn, v)
-            row("metric_signal", qn, {"query_name": qn, "current_value": v, "is_anomalous": st > 0.7},
-                st, "prometheus")
-        for node in sorted({c.pod_node[p] for p in pods} & c.unhealthy_nodes):
-            row("kubernetes_node", node,
-                {"name": node, "conditions": {"Ready": {"status": "False"},
-                                              "MemoryPressure": {"status": "True"}}}, 0.9)
-        recent = sc in ("crashloop_deploy", "imagepull")
-        row("deploy_change", dname, {"deployment_name": dname, "namespace": ns,
-                                     "is_recent_change": recent, "current_revision": "7"},
-            0.95 if recent else 0.3)
-        if recent:
-            cid = f"change:deployment:{ns}:{dname}:7"
-            ents.append({"id": cid, "type": "ChangeEvent",
-                         "properties": {"deployment": dname, "namespace": ns, "revision": "7"}})
-            rels.append({"source_id": f"deployment:{ns}:{dname}", "target_id": cid,
-                         "relation_type": "HAS_RECENT_CHANGE"})
-            rels.append({"source_id": f"incident:{iid}", "target_id": cid,
-                         "relation_type": "CORRELATES_WITH"})
-            row("image_change", dname, {"deployment": dname, "image_changed": True}, 0.85)
-        out.append(IncidentCase(inc, sc, ev, ents, rels))
+        out.append(incident_case(c, d, sc, iid, rng, events_per_incident, fingerprint=f"fp-{i}"))
     return out
+
+
+def incident_case(c: Cluster, d: int, sc: str, iid: str, rng: np.random.Generator,
+                  events_per_incident: int = 60, fingerprint: str | None = None) -> IncidentCase:
+    """One incident on deployment `d` with scenario `sc`: the Incident vertex, its AFFECTS /
+    CORRELATES_WITH relations and collector-shaped evidence rows."""
+    ns = c.ns_names[int(c.deploy_ns[d])]
+    dname = c.deploy_name[d]
+    inc = {"id": iid, "fingerprint": fingerprint or f"fp-{iid}", "title": f"{sc}: {dname}",
+           "severity": "critical", "source": "synthetic", "cluster": "synthetic",
+           "namespace": ns, "service": dname, "started_at": "2026-08-21T00:00:00Z"}
+    ev, ents, rels = [], [], []
+    k = 0
+
+    def row(etype, entity, data, strength, source="kubernetes_api"):
+        nonlocal k
+        k += 1
+        ev.append({"id": f"{iid[-12:]}-{k:04d}", "incident_id": iid, "evidence_type": etype,
+                   "source": source, "entity_name": entity, "entity_namespace": ns,
+                   "data": data, "signal_strength": strength})
+
+    ents.append({"id": f"incident:{iid}", "type": "Incident",
+                 "properties": {"id": iid, "title": inc["title"], "namespace": ns}})
+    pods = c.deploy_pods[d]
+    for pname in pods:
+        restarts = int(rng.geometric(0.3)) - 1
+        wr = tr = None
+        phase = "Running"
+        if sc.startswith("crashloop"):
+            wr = "CrashLoopBackOff" if rng.random() < 0.8 else None
+            tr = "Error" if rng.random() < 0.5 else None
+        elif sc == "oom":
+            tr = "OOMKilled" if rng.random() < 0.7 else None
+        elif sc == "imagepull":
+            wr = ("ImagePullBackOff", "ErrImagePull")[int(rng.integers(0, 2))]
+            phase, restarts = "Pending", 0
+        ready = "True" if (wr is None and tr is None and rng.random() < 0.7) else "False"
+        conds = [{"type": "Ready", "status": ready,
+                  "reason": None if ready == "True" else "ContainersNotReady"}]
+        row("kubernetes_pod", pname,
+            {"name": pname, "namespace": ns, "phase": phase, "node_name": c.pod_node[pname],
+             "restart_count": restarts, "waiting_reason": wr, "terminated_reason": tr,
+             "conditions": conds}, _pod_strength(wr, tr, restarts, phase))
+        rels.append({"source_id": f"incident:{iid}", "target_id": f"pod:{ns}:{pname}",
+                     "relation_type": "AFFECTS"})
+    row("kubernetes_deployment", dname,
+        {"name": dname, "namespace": ns, "replicas": len(pods), "ready_replicas": 0,
+         "unavailable_replicas": len(pods)}, 0.8)
+    for j in range(events_per_incident):
+        pname = pods[j % len(pods)]
+        reason = ("BackOff", "Unhealthy", "Failed", "Pulled", "Created")[int(rng.integers(0, 5))]
+        warn = reason in ("BackOff", "Unhealthy", "Failed")
+        row("kubernetes_event", pname,
+            {"type": "Warning" if warn else "Normal", "reason": reason, "message": reason,
+             "involved_object": {"kind": "Pod", "name": pname, "namespace": ns}, "count": 1},
+            0.9 if warn else 0.4)
+    errors = int(rng.integers(0, 40))
+    pats = ["error"] + (["network"] if rng.random() < 0.3 else []) + \
+        (["oom"] if sc == "oom" else [])
+    row("log_signal", dname, {"total_lines": 500, "error_count": errors, "warning_count": 3,
+                              "patterns_found": pats},
+        0.9 if errors > 10 else 0.8 if errors > 5 else 0.6 if errors else 0.3, "loki")
+    cats = ["crashloop", "resource", "deployment"] + (["oom"] if sc == "oom" else ["latency", "hpa"])
+    names = [q for cat in cats for q in PROMQL[cat]]
+    for j in range(15):
+        qn = names[j % len(names)]
+        if "memory" in qn:
+            v = float(rng.uniform(0, 100))
+        elif "latency" in qn:
+            v = float(rng.uniform(0, 5))
+        elif "hpa" in qn:
+            v = float(rng.integers(0, 2))
+        else:
+            v = float(rng.uniform(0, 10))
+        st = _metric_strength(qn, v)
+        row("metric_signal", qn, {"query_name": qn, "current_value": v, "is_anomalous": st > 0.7},
+            st, "prometheus")
+    for node in sorted({c.pod_node[p] for p in pods} & c.unhealthy_nodes):
+        row("kubernetes_node", node,
+            {"name": node, "conditions": {"Ready": {"status": "False"},
+                                          "MemoryPressure": {"status": "True"}}}, 0.9)
+    recent = sc in ("crashloop_deploy", "imagepull")
+    row("deploy_change", dname, {"deployment_name": dname, "namespace": ns,
+                                 "is_recent_change": recent, "current_revision": "7"},
+        0.95 if recent else 0.3)
+    if recent:
+        cid = f"change:deployment:{ns}:{dname}:7"
+        ents.append({"id": cid, "type": "ChangeEvent",
+                     "properties": {"deployment": dname, "namespace": ns, "revision": "7"}})
+        rels.append({"source_id": f"deployment:{ns}:{dname}", "target_id": cid,
+                     "relation_type": "HAS_RECENT_CHANGE"})
+        rels.append({"source_id": f"incident:{iid}", "target_id": cid,
+                     "relation_type": "CORRELATES_WITH"})
+        row("image_change", dname, {"deployment": dname, "image_changed": True}, 0.85)
+    return IncidentCase(inc, sc, ev, ents, rels)
 
 
 def add_incidents(c: Cluster, cases: list[IncidentCase]) -> None:
@@ -304,3 +311,70 @@ def add_incidents(c: Cluster, cases: list[IncidentCase]) -> None:
 
 # seeds: evidence row -> graph vertex (the product rule, DESIGN.md §5, lives in egraph.seeds)
 from .seeds import attach_ids, seeds_for_batch  # noqa: E402,F401  (re-exported for callers)
+
+
+# ---------------------------------------------------------------------------------------------
+# alert storm (BASELINE config C5): 100k alerts/min, Zipf(1.1) over 10k (alertname, namespace,
+# service) keys, incremental topology deltas every tick
+STORM_ALERTS = ("KubePodCrashLooping", "KubePodNotReady", "OOMKilled", "ImagePullBackOff")
+STORM_SCENARIO = {"KubePodCrashLooping": "crashloop", "KubePodNotReady": "crashloop_deploy",
+                  "OOMKilled": "oom", "ImagePullBackOff": "imagepull"}
+
+
+class StormWorkload:
+    """Seeded alert stream over a cluster: alert i of a tick draws key r ~ Zipf(s) over
+    `n_keys` keys; key r = (alertname, namespace, service) of deployment r % n_deployments.
+    make_case builds the incident the first alert of a fingerprint opens; topology(tick) adds
+    Event vertices to pods that had none (rows of open incidents may re-attach to them)."""
+
+    def __init__(self, c: Cluster, n_keys: int = 10_000, zipf_s: float = 1.1, seed: int = 20260825,
+                 events_per_incident: int = 20):
+        self.c = c
+        self.rng = np.random.default_rng(seed)
+        nd = len(c.deploy_name)
+        self.key_deploy = np.arange(n_keys) % nd
+        self.key_alert = (np.arange(n_keys) // nd) % len(STORM_ALERTS)
+        w = 1.0 / np.arange(1, n_keys + 1) ** zipf_s
+        self.p = w / w.sum()
+        self.n_keys = n_keys
+        self.events_per_incident = events_per_incident
+        self.keys = [f"alertmanager:{STORM_ALERTS[self.key_alert[r]]}:"
+                     f"{c.ns_names[int(c.deploy_ns[self.key_deploy[r]])]}:"
+                     f"{c.deploy_name[self.key_deploy[r]]}" for r in range(n_keys)]
+        self._tick_keys = None
+        self._events_added: set = set()
+
+    def alerts(self, n: int) -> list[str]:
+        """The next n alert keys (the normalizer.py:217 strings); remembers their key ranks."""
+        self._tick_keys = self.rng.choice(self.n_keys, size=n, p=self.p)
+        return [self.keys[r] for r in self._tick_keys]
+
+    def make_case(self, handle: int, alert_index: int):
+        from egraph.storm import StormCase
+        r = int(self._tick_keys[alert_index])
+        iid = f"00000000-0000-4000-9000-{handle:012x}"
+        case = incident_case(self.c, int(self.key_deploy[r]),
+                             STORM_SCENARIO[STORM_ALERTS[self.key_alert[r]]], iid, self.rng,
+                             self.events_per_incident)
+        return StormCase(iid, [(e["id"], e["type"]) for e in case.entities],
+                         [(x["source_id"], x["target_id"], x["relation_type"]) for x in case.relations],
+                         case.evidence)
+
+    def topology(self, n_events: int):
+        """n_events new Event vertices (+ HAS_EVENT edges) on random pods without one."""
+        ids, labels, src, dst, types = [], [], [], [], []
+        for _ in range(n_events):
+            d = int(self.rng.integers(0, len(self.c.deploy_name)))
+            pods = self.c.deploy_pods[d]
+            pname = pods[int(self.rng.integers(0, len(pods)))]
+            ns = self.c.ns_names[int(self.c.deploy_ns[d])]
+            vid = f"event:{ns}:{pname}"
+            if vid in self._events_added or any(v == vid for _, v in self.c.attachments.get(pname, ())):
+                continue
+            self._events_added.add(vid)
+            ids.append(vid)
+            labels.append("Event")
+            src.append(f"pod:{ns}:{pname}")
+            dst.append(vid)
+            types.append("HAS_EVENT")
+        return ids, labels, src, dst, types

@@ -76,3 +76,23 @@ def test_normalizer_severity_requires_string(bad):
     from src.services.ingestion.normalizer import AlertNormalizer
     with pytest.raises(AttributeError):     # labels["severity"].lower(), as in the reference
         AlertNormalizer._fields_alertmanager({"labels": {"severity": bad}}, {})
+
+
+def test_seed_pending_ids_name_the_vertices_that_would_reattach():
+    from egraph.graph import EvidenceGraph
+    from egraph.seeds import seeds_for_batch
+    g = EvidenceGraph()
+    g.merge_nodes(["pod:ns:p1", "deployment:ns:d"], ["Pod", "Deployment"])
+    ev = [[{"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "p1",
+            "data": {"involved_object": {"kind": "Pod", "name": "p1", "namespace": "ns"}},
+            "signal_strength": 0.9},
+           {"evidence_type": "log_signal", "entity_namespace": "ns", "entity_name": "d",
+            "signal_strength": 0.6},
+           {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "gone",
+            "signal_strength": 0.9},
+           {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p1",
+            "signal_strength": 0.0}]]
+    pend: list = []
+    sv, sc, ss = seeds_for_batch(g, ev, pending=pend)
+    assert sv.tolist() == [0, 1] and sc.tolist() == [0, 0]
+    assert pend == [{"event:ns:p1", "logpattern:ns:d", "service:ns:d", "pod:ns:gone"}]
