@@ -41,41 +41,55 @@ def attach_ids(ev: dict) -> list[str]:
     return []
 
 
+class SeedCandidates:
+    """The attachment candidates of a batch's evidence rows, computed once (string work) and
+    re-attached cheaply against a growing graph (`attach`): flat candidate ids, per-row
+    candidate counts, columns and strengths."""
+
+    def __init__(self, evidence_lists: list[list[dict]]):
+        flat, count, col, val = [], [], [], []
+        for b, evs in enumerate(evidence_lists):
+            for ev in evs:
+                ids = attach_ids(ev)
+                s = float(ev.get("signal_strength", 0.5))
+                if not ids or s <= 0:
+                    continue
+                flat.extend(ids)
+                count.append(len(ids))
+                col.append(b)
+                val.append(s)
+        self.n_cols = len(evidence_lists)
+        self.flat = flat
+        self.count = np.asarray(count, np.int64)
+        self.col = np.asarray(col, np.uint32)
+        self.val = np.asarray(val, np.float32)
+
+    def attach(self, graph, pending: list | None = None):
+        """(vertex u32, column u32, strength f32) triples: each row attaches to its first
+        candidate present in `graph`.  `pending` (optional list) receives per column the
+        candidate ids ranked before the attached one (all, for an unattached row)."""
+        if pending is not None:
+            pending[:] = [set() for _ in range(self.n_cols)]
+        if not self.flat:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
+        found = graph.lookup(self.flat).astype(np.int64)
+        n = len(self.flat)
+        starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])
+        pos = np.where(found >= 0, np.arange(n), n)
+        first = np.minimum.reduceat(pos, starts)            # flat index of the attached id
+        ok = first < n
+        if pending is not None:
+            row_of = np.repeat(np.arange(len(self.count)), self.count)
+            before = np.arange(n) < np.repeat(np.where(ok, first, n), self.count)
+            for i in np.flatnonzero(before):
+                pending[self.col[row_of[i]]].add(self.flat[i])
+        return (found[first[ok]].astype(np.uint32), self.col[ok], self.val[ok])
+
+
 def seeds_for_batch(graph, evidence_lists: list[list[dict]], pending: list | None = None):
     """(vertex u32, column u32, strength f32) triples for a batch: each row attaches to the
     first of its candidate ids present in the graph; unattached rows are dropped.
     `pending` (optional, a list) receives per column the set of candidate ids ranked before the
     one attached (all of them for an unattached row): the vertices whose later creation would
     re-attach a row -- the alert storm's re-rank trigger (egraph/storm.py)."""
-    flat, count, col, val = [], [], [], []
-    for b, evs in enumerate(evidence_lists):
-        for ev in evs:
-            ids = attach_ids(ev)
-            s = float(ev.get("signal_strength", 0.5))
-            if not ids or s <= 0:
-                continue
-            flat.extend(ids)
-            count.append(len(ids))
-            col.append(b)
-            val.append(s)
-    if pending is not None:
-        pending[:] = [set() for _ in evidence_lists]
-    if not flat:
-        return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
-    found = graph.lookup(flat)
-    chosen = np.full(len(count), -1, np.int64)
-    pos = 0
-    for r, n in enumerate(count):
-        for j, v in enumerate(found[pos:pos + n]):
-            if v >= 0:
-                chosen[r] = v
-                if pending is not None and j:
-                    pending[col[r]].update(flat[pos:pos + j])
-                break
-        else:
-            if pending is not None:
-                pending[col[r]].update(flat[pos:pos + n])
-        pos += n
-    keep = chosen >= 0
-    return (chosen[keep].astype(np.uint32), np.asarray(col, np.uint32)[keep],
-            np.asarray(val, np.float32)[keep])
+    return SeedCandidates(evidence_lists).attach(graph, pending)

@@ -8,14 +8,19 @@ second of the stream):
   3. the new incidents' entities / relations MERGEd       host egr_graph_merge_* (id interning)
        (+ any topology delta of the tick, e.g. new Events)
   4. the device snapshot brought up to date               GPU  egr_snapshot_update
-  5. affected incidents: BFS `hops` deep from every vertex the update touched
-                                                          GPU  egr_snapshot_within
-     An open incident is re-ranked iff a touched vertex lies within `hops` of its incident
-     vertex or of one of its seed vertices (the only places its reach set and its propagated
-     scores can change: a score at v sums walks of length <= hops from the seeds, and an entry's
-     value changes only when its column's degree does), or a vertex one of its evidence rows
-     would now attach to was created (seeds.seeds_for_batch `pending`).
+  5. affected incidents: BFS `hops - 1` deep from every vertex the update touched (a new
+     vertex or an endpoint of a new edge)                 GPU  egr_snapshot_within
+     An open incident is re-ranked iff a touched vertex lies within hops-1 of its incident
+     vertex or of one of its seed vertices, or a vertex one of its evidence rows would now
+     attach to was created (seeds.seeds_for_batch `pending`).  Why that suffices: a score is a
+     sum over walks seed = x0 -> ... -> xL = v (L <= hops) of products of entry values
+     w / deg(x_i), i < L; such a walk changes only if some x_i with i <= L-1 <= hops-1 is
+     touched (its degree changed, or a new edge leaves it).  The candidate set (vertices within
+     `hops` of the incident) grows only through a new edge with an endpoint within hops-1 of
+     the incident vertex.
   6. re-rank new + affected incidents                     GPU  egr_frontier_run
+     (seed triples are cached per incident and recomputed only for new incidents and those
+     whose pending ids appeared)
 Every cached ranking therefore equals a from-scratch ranking of the current graph
 (tests/test_storm_gpu.py checks it tick by tick).
 """
@@ -31,7 +36,7 @@ import torch
 from egraph.alerts import DedupTable, fingerprints
 from egraph.device import to_device
 from egraph.graph import EvidenceGraph
-from egraph.seeds import seeds_for_batch
+from egraph.seeds import SeedCandidates
 
 NO_NODE = 0xFFFFFFFF
 
@@ -52,8 +57,10 @@ class OpenIncident:
     incident_id: str
     evidence: list
     vertex: int = -1
-    seeds: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    sv: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))    # seed vertices
+    ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
     pending: set = field(default_factory=set)
+    cand: SeedCandidates | None = None     # its rows' attachment candidates (computed once)
     top_ids: np.ndarray | None = None      # [k] u32 vertex ids, NO_NODE padded
     top_scores: np.ndarray | None = None   # [k] f32
     ranked_at: int = -1                    # tick of the last re-rank
@@ -73,6 +80,10 @@ class StormEngine:
         self._pending: dict[str, set[int]] = {}
         self._frontiers: dict[int, object] = {}
         self.ticks = 0
+        # (vertex, incident) pairs the affected test reads: incident vertices and seed vertices
+        self._chk_v = torch.zeros(0, dtype=torch.int64, device=self.dev)
+        self._chk_o = torch.zeros(0, dtype=torch.int64, device=self.dev)
+        self._stale = 0
 
     # ---- frontier per column bucket, grown / recreated as needed ---------------------------
     def _frontier(self, n_cols: int, n_seeds: int):
@@ -86,13 +97,47 @@ class StormEngine:
             self._frontiers[b] = fr
         return fr
 
+    def _reseed(self, handles: list[int]) -> None:
+        """(Re)attach the evidence rows of these incidents to the current graph."""
+        for h in handles:
+            x = self.incidents[h]
+            if x.cand is None:
+                x.cand = SeedCandidates([x.evidence])
+            pend: list = []
+            x.sv, _, x.ss = x.cand.attach(self.g, pend)
+            for pid in x.pending:
+                hs = self._pending.get(pid)
+                if hs is not None:
+                    hs.discard(x.handle)
+            x.pending = pend[0]
+            for pid in x.pending:
+                self._pending.setdefault(pid, set()).add(x.handle)
+
+    def _check_parts(self, xs: list[OpenIncident]) -> tuple[torch.Tensor, torch.Tensor]:
+        v = np.concatenate([np.array([max(x.vertex, 0) for x in xs], np.int64)] +
+                           [x.sv.astype(np.int64) for x in xs])
+        o = np.concatenate([np.array([x.handle for x in xs], np.int64)] +
+                           [np.full(len(x.sv), x.handle, np.int64) for x in xs])
+        return to_device(v, self.dev), to_device(o, self.dev)
+
+    def _rebuild_check(self) -> None:
+        self._chk_v, self._chk_o = self._check_parts(self.incidents)
+
+    def _append_check(self, handles: list[int]) -> None:
+        if handles:
+            v, o = self._check_parts([self.incidents[h] for h in handles])
+            self._chk_v = torch.cat([self._chk_v, v])
+            self._chk_o = torch.cat([self._chk_o, o])
+
     def _rank(self, handles: list[int]) -> None:
+        """Re-rank these incidents from their cached seeds (one frontier launch per 4096)."""
         inc_label = self.g.labels().index("Incident") if "Incident" in self.g.labels() else -1
         top = self.COL_BUCKETS[-1]
         for lo in range(0, len(handles), top):
             part = [self.incidents[h] for h in handles[lo:lo + top]]
-            pend: list = []
-            sv, sc, ss = seeds_for_batch(self.g, [x.evidence for x in part], pending=pend)
+            sv = np.concatenate([x.sv for x in part]) if part else np.zeros(0, np.uint32)
+            ss = np.concatenate([x.ss for x in part]) if part else np.zeros(0, np.float32)
+            sc = np.repeat(np.arange(len(part), dtype=np.uint32), [len(x.sv) for x in part])
             fr = self._frontier(len(part), len(sv))
             src = np.full(fr.B, NO_NODE, np.uint32)
             src[: len(part)] = [x.vertex if x.vertex >= 0 else NO_NODE for x in part]
@@ -100,18 +145,8 @@ class StormEngine:
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
-            order = np.argsort(sc, kind="stable")
-            bounds = np.searchsorted(sc[order], np.arange(len(part) + 1))
             for j, x in enumerate(part):
                 x.top_ids, x.top_scores = ids[j].copy(), scores[j].copy()
-                x.seeds = np.unique(sv[order[bounds[j]:bounds[j + 1]]])
-                for pid in x.pending:
-                    s = self._pending.get(pid)
-                    if s is not None:
-                        s.discard(x.handle)
-                x.pending = pend[j]
-                for pid in x.pending:
-                    self._pending.setdefault(pid, set()).add(x.handle)
                 x.ranked_at = self.ticks
 
     def tick(self, keys: list[str], now_ms: int, make_case: Callable[[int, int], StormCase],
@@ -154,38 +189,48 @@ class StormEngine:
             ed += list(td)
             et += list(tt)
         V0, E0 = self.snap.n_vertices, self.snap.synced_edges
+        new_ids: list[str] = []
         if ids:
-            self.g.merge_nodes(ids, labels)
+            vix = self.g.merge_nodes(ids, labels)
+            new_ids = [ids[i] for i in np.flatnonzero(vix >= V0)]
         if es:
             self.g.merge_edges(es, ed, et)
-        for x in (self.incidents[h] for h in new_handles):
-            x.vertex = int(self.g.lookup([f"incident:{x.incident_id}"])[0])
+        if new_handles:
+            vs = self.g.lookup([f"incident:{self.incidents[h].incident_id}" for h in new_handles])
+            for h, v in zip(new_handles, vs):
+                self.incidents[h].vertex = int(v)
         t.append(time.perf_counter())
         n_v, n_e = self.snap.sync(self.g)                                 # GPU CSR update
         t.append(time.perf_counter())
-        # affected incidents
+        # affected incidents (before the new incidents join the check arrays)
         affected = set(new_handles)
-        old = [x for x in self.incidents[: len(self.incidents) - len(new_handles)]]
-        if (n_v or n_e) and old:
+        n_old = len(self.incidents) - len(new_handles)
+        reseed = set()
+        if n_old:
+            for vid in new_ids:                          # rows that would attach differently now
+                hs = self._pending.get(vid)
+                if hs:
+                    reseed.update(hs)
+        if (n_v or n_e) and n_old and self.hops >= 1:
             s2, d2, _ = self.g.export_edges(E0, n_e)
             touched = np.unique(np.concatenate([np.arange(V0, V0 + n_v, dtype=np.int64),
                                                 s2.astype(np.int64), d2.astype(np.int64)]))
-            dist = self.snap.within(to_device(touched.astype(np.uint32), self.dev), self.hops)
-            # incident vertices and seed vertices of every old incident, on the device
-            verts = np.concatenate([np.array([max(x.vertex, 0) for x in old], np.int64)] +
-                                   [x.seeds.astype(np.int64) for x in old])
-            owner = np.concatenate([np.arange(len(old), dtype=np.int64)] +
-                                   [np.full(len(x.seeds), j, np.int64) for j, x in enumerate(old)])
-            hit = (dist[to_device(verts, self.dev)] != 255).to(torch.int32)
-            flag = torch.zeros(len(old), dtype=torch.int32, device=self.dev)
-            flag.scatter_reduce_(0, to_device(owner, self.dev), hit, reduce="amax")
-            for j in np.flatnonzero(flag.cpu().numpy()):
-                affected.add(old[j].handle)
-            # rows that would now attach to a newly created vertex
-            for v in range(V0, V0 + n_v):
-                hs = self._pending.get(self.g.vertex_id(v))
-                if hs:
-                    affected.update(hs)
+            dist = self.snap.within(to_device(touched.astype(np.uint32), self.dev), self.hops - 1)
+            hit = (dist[self._chk_v] != 255).to(torch.int32)
+            flag = torch.zeros(n_old, dtype=torch.int32, device=self.dev)
+            flag.scatter_reduce_(0, self._chk_o, hit, reduce="amax")
+            affected.update(np.flatnonzero(flag.cpu().numpy()).tolist())
+        affected |= reseed
+        t.append(time.perf_counter())
+        # seeds: new incidents and re-attached ones
+        self._reseed(sorted(set(new_handles) | reseed))
+        # re-attached incidents: append their new seed vertices; the old entries stay (a
+        # superset only re-ranks more) until they make up half the arrays
+        self._append_check(sorted(set(new_handles) | reseed))
+        self._stale += sum(len(self.incidents[h].sv) + 1 for h in reseed)
+        if self._stale * 2 > self._chk_v.numel():
+            self._rebuild_check()
+            self._stale = 0
         t.append(time.perf_counter())
         self._rank(sorted(affected))
         torch.cuda.synchronize(self.dev)
@@ -196,7 +241,8 @@ class StormEngine:
         return {"alerts": len(keys), "duplicates": int(dup_h.sum()), "new_incidents": n_new,
                 "new_vertices": n_v, "new_edges": n_e, "affected": len(affected),
                 "open_incidents": len(self.incidents),
-                "ms": dict(zip(("fingerprint_dedup", "merge_host", "csr_update", "affected", "rerank"), ms)),
+                "ms": dict(zip(("fingerprint_dedup", "merge_host", "csr_update", "affected", "seeds_host",
+                               "rerank"), ms)),
                 "collect_ms": t_collect * 1e3}
 
     def rankings(self) -> list[tuple[np.ndarray, np.ndarray]]:
