@@ -338,6 +338,13 @@ int egr_snapshot_within(const egr_snapshot* s, const uint32_t* sources, int64_t 
 int64_t egr_frontier_max_vertices(const egr_frontier* f);
 int egr_graph_export_edges(const egr_graph* g, int64_t first, int64_t n, int32_t* edge_src,
                            int32_t* edge_dst, uint8_t* edge_type);
+/* MERGE edges given by vertex INDEX (a restore from a snapshot file, egraph/snapfile.py: the
+ * edge list in creation order reproduces the graph exactly; the label-less id MATCH of
+ * egr_graph_merge_edges would fan out over vertices sharing an id).  type_idx indexes the
+ * n_types names in type_blob/type_off.  out_new = edges created. */
+int egr_graph_add_edges_indexed(egr_graph* g, const int32_t* src, const int32_t* dst,
+                                const char* type_blob, const int64_t* type_off, int32_t n_types,
+                                const int32_t* type_idx, int64_t n, int64_t* out_new);
 
 /* ---- Alert-storm front end: fingerprints + TTL dedup table (csrc/alerts.hip) ---------------
  * egr_fingerprint   replaces AlertNormalizer._generate_fingerprint

@@ -138,6 +138,34 @@ int egr_graph_merge_edges(egr_graph* g, const char* src_blob, const int64_t* src
   return EGR_OK;
 }
 
+int egr_graph_add_edges_indexed(egr_graph* g, const int32_t* src, const int32_t* dst,
+                                const char* type_blob, const int64_t* type_off, int32_t n_types,
+                                const int32_t* type_idx, int64_t n, int64_t* out_new) {
+  if (!g || n < 0 || n_types < 0 || (n_types > 0 && (!type_blob || !type_off)) ||
+      (n > 0 && (!src || !dst || !type_idx)))
+    return egr::fail(EGR_EINVAL, "egr_graph_add_edges_indexed: bad arguments");
+  std::vector<int> tmap((size_t)n_types);
+  for (int32_t i = 0; i < n_types; ++i) {
+    tmap[i] = intern(g->rtypes, g->rtype_idx, str_at(type_blob, type_off, i), 127, "relationship types");
+    if (tmap[i] < 0) return tmap[i];
+  }
+  const int64_t V = (int64_t)g->vid.size();
+  int64_t created = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (src[i] < 0 || src[i] >= V || dst[i] < 0 || dst[i] >= V || type_idx[i] < 0 || type_idx[i] >= n_types)
+      return egr::fail(EGR_EINVAL, "egr_graph_add_edges_indexed: vertex or type index out of range");
+    egr_graph::EdgeKey k{src[i], dst[i], (uint8_t)tmap[type_idx[i]]};
+    if (g->edges.insert(k).second) {
+      g->esrc.push_back(k.s);
+      g->edst.push_back(k.d);
+      g->etype.push_back(k.t);
+      ++created;
+    }
+  }
+  if (out_new) *out_new = created;
+  return EGR_OK;
+}
+
 int64_t egr_graph_num_vertices(const egr_graph* g) { return g ? (int64_t)g->vid.size() : -1; }
 int64_t egr_graph_num_edges(const egr_graph* g) { return g ? (int64_t)g->esrc.size() : -1; }
 int32_t egr_graph_num_labels(const egr_graph* g) { return g ? (int32_t)g->labels.size() : -1; }

@@ -132,6 +132,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_snapshot_within": (C.c_int, [P, P, I64, I32, P, P]),
     "egr_frontier_max_vertices": (I64, [P]),
     "egr_graph_export_edges": (C.c_int, [P, I64, I64, P, P, P]),
+    "egr_graph_add_edges_indexed": (C.c_int, [P, P, P, C.c_char_p, P, I32, P, I64, PI64]),
     "egr_fingerprint": (C.c_int, [P, P, I64, P, P, P]),
     "egr_dedup_create": (C.c_int, [I32, I64, C.POINTER(P)]),
     "egr_dedup_free": (None, [P]),

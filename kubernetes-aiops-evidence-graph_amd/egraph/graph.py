@@ -101,6 +101,21 @@ class EvidenceGraph:
                                             len(src), C.byref(created)), "egr_graph_merge_edges")
         return created.value
 
+    def add_edges_indexed(self, src: np.ndarray, dst: np.ndarray, type_idx: np.ndarray,
+                          type_names: Sequence[str]) -> int:
+        """MERGE edges by vertex index (exact restore; egr_graph_add_edges_indexed)."""
+        src = np.ascontiguousarray(src, np.int32)
+        dst = np.ascontiguousarray(dst, np.int32)
+        ti = np.ascontiguousarray(type_idx, np.int32)
+        if not (len(src) == len(dst) == len(ti)):
+            raise ValueError("edge arrays differ in length")
+        tb, to = str_blob(type_names)
+        created = C.c_int64(0)
+        L.check(L.lib.egr_graph_add_edges_indexed(self._h, _addr(src), _addr(dst), tb, _addr(to),
+                                                  len(type_names), _addr(ti), len(src),
+                                                  C.byref(created)), "egr_graph_add_edges_indexed")
+        return created.value
+
     def create_entities_batch(self, entities: Iterable) -> int:
         """GraphService.create_entities_batch: returns the number of items attempted (:112)."""
         entities = list(entities)

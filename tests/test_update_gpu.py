@@ -215,3 +215,27 @@ def test_graph_service_reads_after_writes_use_incremental_sync():
         assert any(n["properties"]["id"] == f"incident:{ids[-1]}" for n in nodes)
     finally:
         GS.reset()
+
+
+def test_snapshot_file_roundtrip_from_the_device(tmp_path):
+    """Checkpoint an updated device snapshot (egraph/snapfile.py), upload it elsewhere without
+    the host graph: identical CSR; restore the host graph: identical again after a sync."""
+    from egraph import snapfile
+    g, _ = _base(seed=6, pods=500)
+    snap = g.snapshot()
+    rng = np.random.default_rng(2)
+    new, nl, src, dst, typ = _random_batch(rng, g, 50, 600, "ck")
+    g.merge_nodes(new, nl)
+    g.merge_edges(src, dst, typ)
+    snap.sync(g)
+    p = tmp_path / "ck.egrsnap"
+    snapfile.save(p, g, snapshot=snap)
+    loaded = snapfile.load_snapshot(p)
+    a, b = snap.download(), loaded.download()
+    for k in a:
+        assert a[k].tobytes() == b[k].tobytes()
+    g2 = snapfile.load_graph(p)
+    s2 = g2.snapshot()
+    c = s2.download()
+    for k in a:
+        assert a[k].tobytes() == c[k].tobytes()
