@@ -331,7 +331,7 @@ int egr_snapshot_download(const egr_snapshot* s, uint32_t* row_ptr, uint32_t* co
 int64_t egr_snapshot_version(const egr_snapshot* s);
 /* multi-source BFS: out_dist[v] (device, V bytes) = undirected hops from the nearest of the n
  * source vertices (device u32; ids >= V ignored), 0xFF beyond `hops`.  The alert storm marks
- * the incidents an update can affect with it (DESIGN.md §9). */
+ * the incidents an update can affect with it (DESIGN.md §7). */
 int egr_snapshot_within(const egr_snapshot* s, const uint32_t* sources, int64_t n, int32_t hops,
                         uint8_t* out_dist, void* stream);
 /* vertex count a frontier was sized for (it runs while the snapshot stays within it) */
