@@ -70,6 +70,8 @@ struct FArgs {
   const float* seed_val;       // (duplicates are max-combined in the kernel, as fmaxf)
   uint2* seed_rep;             // per seed entry: (slot, s0 bits) of a vertex's representative
   const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
+  const uint32_t* order;       // [B] launch order: workgroup i runs column order[i] (costly first)
+  uint32_t* seed_cnt;          // [2B] seed counters / costs, zeroed per column once consumed
   uint32_t* out_ids;           // [B*k]
   float* out_scores;
   // member pool: every column's (vertex, score, depth+1) after the last hop
@@ -723,7 +725,11 @@ __global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
   __shared__ uint32_t bloom[BLOOM_WORDS];
   __shared__ Shared sh;
   const uint32_t tid = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = (int)A.order[blockIdx.x];
+  if (tid == 0) {               // the seed counters are consumed: leave them zero for the next set
+    A.seed_cnt[b] = 0;
+    A.seed_cnt[A.B + b] = 0;
+  }
   for (uint32_t i = tid; i < BLOOM_WORDS; i += FT) bloom[i] = 0;
 #pragma unroll
   for (int i = 0; i < LPPT; ++i) {
@@ -846,16 +852,52 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
   return r;
 }
 
+// cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
+// the column's frontier work, for longest-first launch order).  Both are wave-aggregated: one
+// atomic per run of equal columns (a segmented sum over an inclusive wave scan).
 __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
-                                  int64_t n, uint32_t V, int B, uint32_t* cnt) {
+                                  int64_t n, uint32_t V, int B, const uint32_t* __restrict__ row_ptr,
+                                  uint32_t* cnt, uint32_t* cost) {
   const SeedRun r = seed_run(sv, sc, n, V, B);
-  if (r.ok && r.rank == 0) atomicAdd(&cnt[r.col], r.len);
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t d = 0;
+  if (r.ok) {
+    const uint32_t v = sv[i];
+    d = 1u + row_ptr[v + 1] - row_ptr[v];
+  }
+  uint32_t incl = d;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t x = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += x;
+  }
+  const int last = (int)(r.leader + r.len) - 1;
+  const uint32_t hi = __shfl(incl, r.ok ? last : lane, 64);
+  const uint32_t lo = __shfl(incl, r.ok && r.leader > 0 ? (int)r.leader - 1 : lane, 64);
+  if (r.ok && r.rank == 0) {
+    atomicAdd(&cnt[r.col], r.len);
+    atomicAdd(&cost[r.col], hi - (r.leader > 0 ? lo : 0u));
+  }
 }
 
-// ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]).  One block of
-// 1024 threads, each owning a contiguous run of columns.
-__global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr) {
+// ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]); order = the
+// columns by descending cost bucket (a log-scale counting sort: longest-processing-time-first
+// launch order, so the costly columns do not start in the last round).  One block of 1024
+// threads, each owning a contiguous run of columns.
+constexpr int COST_BUCKETS = 64;
+
+__device__ __forceinline__ int cost_bucket(uint32_t cost) {
+  const int lg = (int)(__log2f((float)cost + 1.0f) * 3.0f);
+  return COST_BUCKETS - 1 - min(COST_BUCKETS - 1, lg);
+}
+
+__global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
+                                                         const uint32_t* __restrict__ cost,
+                                                         uint32_t* order, unsigned long long* ctr,
+                                                         uint32_t* ovf) {
   __shared__ uint32_t part[1024];
+  __shared__ uint32_t hist[COST_BUCKETS];
   const int tid = threadIdx.x;
   const int per = (B + 1023) / 1024;
   const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
@@ -877,6 +919,23 @@ __global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, u
     run += x;
   }
   if (tid == 1023) ptr[B] = part[1023];
+  if (tid < 6) ctr[tid] = 0;      // the next run's pool / stats counters and overflow list
+  if (tid < 2) ovf[tid] = 0;
+  // launch order
+  if (tid < COST_BUCKETS) hist[tid] = 0;
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int i = 0; i < COST_BUCKETS; ++i) {
+      const uint32_t x = hist[i];
+      hist[i] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
@@ -903,7 +962,9 @@ struct egr_frontier {
   uint32_t gcap = 0;
   int64_t n_seeds = 0;
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
-  uint32_t* seed_cnt = nullptr;   // [B] per-column counts, then scatter cursors
+  uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; then costs
+  uint32_t* order = nullptr;      // [B] launch order of the columns
+  uint32_t* ident = nullptr;      // [B] 0..B-1 ($EGRAPH_FRONTIER_NO_ORDER: launch in column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
   uint2* seed_rep = nullptr;
@@ -925,6 +986,8 @@ struct egr_frontier {
   uint32_t* gmlist = nullptr;
   bool seeds_set = false;
   bool ran = false;
+  bool cnt_clean = true;          // seed_cnt is zero in stream order (the run's kernel zeroes it)
+  bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
 };
 
 extern "C" {
@@ -955,7 +1018,8 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
                                  : (unsigned long long)n_cols * 4096ull + 4ull * V;
   int rc = EGR_OK;
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
-  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, (size_t)n_cols)) ||
+  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
+      (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
@@ -979,9 +1043,19 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gfl, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
+      hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
       hipMemset(f->ctr, 0, 6 * 8) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
+  }
+  {
+    std::vector<uint32_t> id((size_t)n_cols);
+    for (int i = 0; i < n_cols; ++i) id[i] = (uint32_t)i;
+    if (hipMemcpy(f->ident, id.data(), (size_t)n_cols * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(f->order, id.data(), (size_t)n_cols * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      egr_frontier_free(f);
+      return egr::fail(EGR_EDEVICE, "egr_frontier_create: order init failed");
+    }
   }
   *out = f;
   return EGR_OK;
@@ -992,6 +1066,8 @@ void egr_frontier_free(egr_frontier* f) {
   DeviceGuard guard(f->s->device);
   dfree(f->seed_ptr);
   dfree(f->seed_cnt);
+  dfree(f->order);
+  dfree(f->ident);
   dfree(f->seed_v);
   dfree(f->seed_s);
   dfree(f->seed_rep);
@@ -1033,14 +1109,15 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   hipStream_t st = (hipStream_t)stream;
   // counting sort by column: count, one-block exclusive scan, scatter (order within a column
   // is arbitrary; the kernel max-combines duplicates).  Invalid triples are dropped.
-  EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 4, st));
+  if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 8, st));
   const unsigned g = (unsigned)((std::max<int64_t>(n_seeds, 1) + 255) / 256);
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_count_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
-                       n_seeds, V, f->B, f->seed_cnt);
+                       n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B);
     EGR_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(1024), 0, st, f->seed_cnt, f->B, f->seed_ptr);
+  hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(1024), 0, st, f->seed_cnt, f->B, f->seed_ptr,
+                     f->seed_cnt + f->B, f->order, f->ctr, f->ovf);
   EGR_CHECK_LAUNCH();
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_scatter_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
@@ -1049,6 +1126,8 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   }
   f->n_seeds = n_seeds;
   f->seeds_set = true;
+  f->cnt_clean = false;
+  f->ctr_clean = true;
   return EGR_OK;
 }
 
@@ -1061,8 +1140,10 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   DeviceGuard guard(f->s->device);
   hipStream_t st = (hipStream_t)stream;
   const egr_snapshot* s = f->s;
-  EGR_HIP(hipMemsetAsync(f->ctr, 0, 6 * 8, st));
-  EGR_HIP(hipMemsetAsync(f->ovf, 0, 2 * 4, st));
+  if (!f->ctr_clean) {
+    EGR_HIP(hipMemsetAsync(f->ctr, 0, 6 * 8, st));
+    EGR_HIP(hipMemsetAsync(f->ovf, 0, 2 * 4, st));
+  }
   FArgs a;
   a.row_ptr = s->row_ptr;
   a.cv = s->cv;
@@ -1077,6 +1158,8 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.seed_val = f->seed_s;
   a.seed_rep = f->seed_rep;
   a.sources = source_vertex;
+  a.order = getenv("EGRAPH_FRONTIER_NO_ORDER") ? f->ident : f->order;
+  a.seed_cnt = f->seed_cnt;
   a.out_ids = out_ids;
   a.out_scores = out_scores;
   a.pool_v = f->pool_v;
@@ -1105,6 +1188,8 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   hipLaunchKernelGGL(frontier_global_kernel, dim3(f->nbig), dim3(FT), 0, st, a);
   EGR_CHECK_LAUNCH();
   f->ran = true;
+  f->ctr_clean = false;
+  f->cnt_clean = true;
   return EGR_OK;
 }
 
