@@ -995,7 +995,7 @@ extern "C" {
 int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
                         int64_t pool_entries, egr_frontier** out) {
   if (!s || !out || n_cols <= 0 || n_cols > (1 << 20) || max_seeds < 0 || k < 1 || k > KMAXF ||
-      pool_entries < 0)
+      pool_entries < -1)
     return egr::fail(EGR_EINVAL,
                      "egr_frontier_create: bad arguments (need 0 < n_cols <= 2^20, 1 <= k <= 16)");
   *out = nullptr;
@@ -1014,7 +1014,8 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   while (gcap < 2ull * V) gcap *= 2;
   f->gcap = (uint32_t)gcap;
   f->nbig = std::min(n_cols, 32);
-  f->pool_cap = pool_entries > 0 ? (unsigned long long)pool_entries
+  f->pool_cap = pool_entries < 0 ? 0ull   // top-k only: no member pool
+              : pool_entries > 0 ? (unsigned long long)pool_entries
                                  : (unsigned long long)n_cols * 4096ull + 4ull * V;
   int rc = EGR_OK;
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
@@ -1225,6 +1226,7 @@ int egr_frontier_phase_times(const egr_frontier* f, int64_t* out, int64_t cap, v
 int egr_frontier_read_scores(const egr_frontier* f, float* out, void* stream) {
   if (!f || !out) return egr::fail(EGR_EINVAL, "egr_frontier_read_scores: NULL argument");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_read_scores: not run yet");
+  if (!f->pool_cap) return egr::fail(EGR_ESTATE, "egr_frontier_read_scores: frontier created without a member pool");
   DeviceGuard guard(f->s->device);
   hipStream_t st = (hipStream_t)stream;
   EGR_HIP(hipMemsetAsync(out, 0, (size_t)f->s->V * f->B * 4, st));
@@ -1237,6 +1239,7 @@ int egr_frontier_read_scores(const egr_frontier* f, float* out, void* stream) {
 int egr_frontier_read_reach(const egr_frontier* f, uint64_t* out, void* stream) {
   if (!f || !out) return egr::fail(EGR_EINVAL, "egr_frontier_read_reach: NULL argument");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_read_reach: not run yet");
+  if (!f->pool_cap) return egr::fail(EGR_ESTATE, "egr_frontier_read_reach: frontier created without a member pool");
   DeviceGuard guard(f->s->device);
   hipStream_t st = (hipStream_t)stream;
   EGR_HIP(hipMemsetAsync(out, 0, (size_t)((f->B + 63) / 64) * f->s->V * 8, st));
@@ -1253,6 +1256,7 @@ int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_verte
   if (!f || !out_n || col < 0 || col >= f->B || cap < 0)
     return egr::fail(EGR_EINVAL, "egr_frontier_members: bad arguments");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_members: not run yet");
+  if (!f->pool_cap) return egr::fail(EGR_ESTATE, "egr_frontier_members: frontier created without a member pool");
   DeviceGuard guard(f->s->device);
   hipStream_t st = (hipStream_t)stream;
   unsigned long long off = 0;

@@ -93,7 +93,7 @@ class StormEngine:
         fr = self._frontiers.get(b)
         if fr is None or fr.max_seeds < n_seeds or fr.max_vertices < self.snap.n_vertices:
             cap = max(n_seeds, 64 * b, fr.max_seeds * 2 if fr is not None else 0)
-            fr = self.snap.frontier(b, max_seeds=cap, k=self.k)
+            fr = self.snap.frontier(b, max_seeds=cap, k=self.k, pool_entries=-1)
             self._frontiers[b] = fr
         return fr
 

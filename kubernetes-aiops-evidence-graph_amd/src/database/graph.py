@@ -109,7 +109,7 @@ class GraphService:
         snap = cls._snap()
         fr = cls._frontiers.get((n_cols, k))
         if fr is None or fr.max_seeds < n_seeds:
-            fr = snap.frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k)
+            fr = snap.frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k, pool_entries=-1)
             cls._frontiers[(n_cols, k)] = fr
         return fr
 

@@ -164,6 +164,17 @@ def test_frontier_small_pool_still_ranks():
     assert fr.stats()["pool_used"] > 3000
 
 
+def test_frontier_without_pool_ranks_identically():
+    """pool_entries=-1 (top-k only): same top-k, and the read functions refuse."""
+    from egraph import _lib as L
+    g, sv, sc, ss, src = _world(70, seed=53, pods=1800)
+    fr = _check(g, sv, sc, ss, src, 70, pool_entries=-1, scores=False)
+    with pytest.raises(L.EgraphError, match="without a member pool"):
+        fr.read_scores()
+    with pytest.raises(L.EgraphError, match="without a member pool"):
+        fr.members(0)
+
+
 def test_frontier_bad_arguments():
     g, sv, sc, ss, src = _world(4, seed=49, pods=400)
     snap = g.snapshot()
