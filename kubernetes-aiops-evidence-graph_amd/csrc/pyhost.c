@@ -1,0 +1,582 @@
+/* _egr_pyhost: the host side of the drop-in rules boundary in native code.
+ *
+ * encode_rows  -- evidence dicts -> the row columns egr_rules_eval consumes (egraph/encode.py
+ *                 is the same encoder in Python; both follow RulesEngine._process_*_evidence,
+ *                 src/services/rca/rules_engine.py:294-376 of the reference).
+ * assemble     -- kernel outputs -> the reference's hypothesis dicts
+ *                 (rules_engine.py:235-262 / :457-478, hypothesis_ranker.py:63-71).
+ *
+ * Exactness rule for encode_rows: a row is taken here only when every value the reference
+ * would read from it is of a plain built-in type (exact dict / list / str / int / bool / float
+ * / None), where the row's Python expressions cannot run user code and cannot raise.  Any
+ * other row -- a dict subclass, an unhashable reason, a None where a number is compared, a
+ * string where a list is iterated -- is handed to the Python row encoder (`slow_row`), which
+ * evaluates the reference's expressions in the reference's order and raises what they raise.
+ * The fast path never raises on input data; it only decides "plain" or "hand over".
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+/* include/egraph.h EGR_F_* (kept in sync by tests/test_native_host.py) */
+#define F_RECENT_DEPLOY  (1u << 0)
+#define F_IMAGE_CHANGED  (1u << 1)
+#define F_MEMORY_HIGH    (1u << 2)
+#define F_HPA_AT_MAX     (1u << 3)
+#define F_LATENCY_HIGH   (1u << 4)
+#define F_NODE_ISSUE     (1u << 5)
+#define F_NOT_READY      (1u << 6)
+#define F_READINESS_FAIL (1u << 7)
+#define F_ERR_FLOAT      (1u << 8)
+#define NO_NODE 0xFFFFFFFFu
+#define INT_LIMIT 2147483648.0   /* egraph/encode.py _INT_LIMIT */
+
+enum { T_NONE, T_POD, T_DEPLOY, T_IMAGE, T_LOG, T_METRIC, T_NODE };
+
+/* interned keys and constants */
+static PyObject *k_id, *k_type, *k_data, *k_waiting, *k_terminated, *k_restart, *k_node_name,
+    *k_conditions, *k_ctype, *k_status, *k_phase, *k_reason, *k_recent, *k_image_changed,
+    *k_patterns, *k_error_count, *k_query, *k_anomalous, *k_current, *k_name, *k_ready_key;
+static PyObject *s_ready, *s_true, *s_running, *s_cnr, *s_memory, *s_hpa, *s_max, *s_latency;
+static PyObject *s_type_names[7];
+static PyObject *i_zero, *i_one, *i_ninety;
+static PyObject* type_map;   /* evidence_type name -> T_* (a dict lookup, like processors.get) */
+/* hypothesis dict keys */
+static PyObject *h_id, *h_incident, *h_category, *h_title, *h_description, *h_confidence,
+    *h_rank, *h_support_ids, *h_actions, *h_generated_by, *h_rule_id, *h_support_count,
+    *h_strength, *h_final;
+
+static int intern_all(void) {
+#define S(var, text) if (!(var = PyUnicode_InternFromString(text))) return -1
+  S(k_id, "id"); S(k_type, "evidence_type"); S(k_data, "data");
+  S(k_waiting, "waiting_reason"); S(k_terminated, "terminated_reason");
+  S(k_restart, "restart_count"); S(k_node_name, "node_name"); S(k_conditions, "conditions");
+  S(k_ctype, "type"); S(k_status, "status"); S(k_phase, "phase"); S(k_reason, "reason");
+  S(k_recent, "is_recent_change"); S(k_image_changed, "image_changed");
+  S(k_patterns, "patterns_found"); S(k_error_count, "error_count"); S(k_query, "query_name");
+  S(k_anomalous, "is_anomalous"); S(k_current, "current_value"); S(k_name, "name");
+  S(k_ready_key, "Ready");
+  S(s_ready, "Ready"); S(s_true, "True"); S(s_running, "Running");
+  S(s_cnr, "ContainersNotReady"); S(s_memory, "memory"); S(s_hpa, "hpa"); S(s_max, "max");
+  S(s_latency, "latency");
+  s_type_names[T_NONE] = NULL;
+  S(s_type_names[T_POD], "kubernetes_pod"); S(s_type_names[T_DEPLOY], "deploy_change");
+  S(s_type_names[T_IMAGE], "image_change"); S(s_type_names[T_LOG], "log_signal");
+  S(s_type_names[T_METRIC], "metric_signal"); S(s_type_names[T_NODE], "kubernetes_node");
+  S(h_id, "id"); S(h_incident, "incident_id"); S(h_category, "category"); S(h_title, "title");
+  S(h_description, "description"); S(h_confidence, "confidence"); S(h_rank, "rank");
+  S(h_support_ids, "supporting_evidence_ids"); S(h_actions, "recommended_actions");
+  S(h_generated_by, "generated_by"); S(h_rule_id, "rule_id");
+  S(h_support_count, "support_count"); S(h_strength, "signal_strength");
+  S(h_final, "final_score");
+#undef S
+  if (!(type_map = PyDict_New())) return -1;
+  for (int i = T_POD; i <= T_NODE; ++i) {
+    PyObject* v = PyLong_FromLong(i);
+    if (!v || PyDict_SetItem(type_map, s_type_names[i], v) < 0) return -1;
+    Py_DECREF(v);
+  }
+  if (!(i_zero = PyLong_FromLong(0)) || !(i_one = PyLong_FromLong(1)) ||
+      !(i_ninety = PyLong_FromLong(90)))
+    return -1;
+  return 0;
+}
+
+/* ---- plain-value helpers (no user code runs, nothing raises) ------------------------------ */
+
+/* 1: value is of a plain built-in type (NULL = key missing counts as plain) */
+static inline int plain(PyObject* o) {
+  return o == NULL || o == Py_None || PyUnicode_CheckExact(o) || PyLong_CheckExact(o) ||
+         PyBool_Check(o) || PyFloat_CheckExact(o) || PyList_CheckExact(o) ||
+         PyDict_CheckExact(o);
+}
+static inline int is_num(PyObject* o) {
+  return PyLong_CheckExact(o) || PyBool_Check(o) || PyFloat_CheckExact(o);
+}
+static inline int hashable_plain(PyObject* o) {
+  return o == Py_None || PyUnicode_CheckExact(o) || PyLong_CheckExact(o) || PyBool_Check(o) ||
+         PyFloat_CheckExact(o);
+}
+/* truthiness of a plain value (missing = None = falsy) */
+static inline int truthy(PyObject* o) {
+  if (o == NULL || o == Py_None) return 0;
+  return PyObject_IsTrue(o);   /* built-in types: no user code, cannot fail */
+}
+/* `o == <str constant>` for a plain value: only an equal str compares equal */
+static inline int eq_str(PyObject* o, PyObject* s) {
+  return o != NULL && PyUnicode_CheckExact(o) && PyUnicode_Compare(o, s) == 0;
+}
+/* dict.get on an exact dict with an interned str key: borrowed or NULL (missing).  Returns -1
+ * only if the lookup itself raised (a key whose __eq__ raises on a hash collision): hand over. */
+static inline int dget(PyObject* d, PyObject* key, PyObject** out) {
+  *out = PyDict_GetItemWithError(d, key);
+  if (*out == NULL && PyErr_Occurred()) { PyErr_Clear(); return -1; }
+  return 0;
+}
+/* number > / == constant for plain numbers (int, bool, float); cannot fail on these types */
+static inline int num_cmp(PyObject* o, PyObject* c, int op) {
+  return PyObject_RichCompareBool(o, c, op);
+}
+/* vocab lookup: bits of a hashable plain key, 0 when absent; -1 = hand over */
+static inline int64_t vocab_bits(PyObject* vocab, PyObject* key) {
+  if (!hashable_plain(key)) return -1;
+  PyObject* v = PyDict_GetItemWithError(vocab, key);
+  if (v == NULL) {
+    if (PyErr_Occurred()) { PyErr_Clear(); return -1; }
+    return 0;
+  }
+  unsigned long b = PyLong_AsUnsignedLong(v);
+  if (b == (unsigned long)-1 && PyErr_Occurred()) { PyErr_Clear(); return -1; }
+  return (int64_t)(b & 0xFFFFFFFFu);
+}
+
+typedef struct {
+  PyObject *waiting, *terminated, *patterns, *node_keys;
+} Vocab;
+
+typedef struct {
+  uint32_t flags, vocab, node;
+  double err;
+  PyObject* pending_node;   /* node_keys.setdefault(name) to apply when the row is accepted */
+} Row;
+
+/* Each returns 0 = encoded, 1 = hand the row to the Python encoder. */
+
+static int enc_pod(PyObject* d, const Vocab* V, Row* r) {
+  PyObject *wr, *tr, *rc, *nn, *conds;
+  if (dget(d, k_waiting, &wr) || dget(d, k_terminated, &tr) || dget(d, k_restart, &rc) ||
+      dget(d, k_node_name, &nn) || dget(d, k_conditions, &conds))
+    return 1;
+  if (!plain(wr) || !plain(tr) || !plain(nn)) return 1;
+  if (rc != NULL && !is_num(rc)) return 1;              /* max(int, rc) needs a number */
+  int wr_t = truthy(wr), tr_t = truthy(tr);
+  if (wr_t) {                                            /* waiting_reasons.add (:318) */
+    int64_t b = vocab_bits(V->waiting, wr);
+    if (b < 0) return 1;
+    r->vocab |= (uint32_t)b;
+  }
+  if (tr_t) {                                            /* terminated_reasons.add (:320) */
+    int64_t b = vocab_bits(V->terminated, tr);
+    if (b < 0) return 1;
+    r->vocab |= (uint32_t)b;
+  }
+  int has_issue = wr_t || tr_t || (rc != NULL && num_cmp(rc, i_zero, Py_GT) == 1);
+  if (truthy(nn) && has_issue) {                        /* pods_by_node[node_name] (:330) */
+    if (!hashable_plain(nn)) return 1;
+    r->pending_node = nn;
+  }
+  /* next(c for c in conditions if c.get("type") == "Ready") (:333-335) */
+  PyObject* ready = NULL;
+  if (conds != NULL) {
+    if (!PyList_CheckExact(conds)) return 1;
+    Py_ssize_t n = PyList_GET_SIZE(conds);
+    for (Py_ssize_t i = 0; i < n && ready == NULL; ++i) {
+      PyObject* c = PyList_GET_ITEM(conds, i);
+      if (!PyDict_CheckExact(c)) return 1;
+      PyObject* t;
+      if (dget(c, k_ctype, &t) || !plain(t)) return 1;
+      if (eq_str(t, s_ready)) ready = c;
+    }
+  }
+  if (ready != NULL && PyDict_GET_SIZE(ready) > 0) {
+    PyObject *st, *ph, *rs;
+    if (dget(ready, k_status, &st) || !plain(st)) return 1;
+    if (!eq_str(st, s_true)) {
+      if (dget(d, k_phase, &ph) || !plain(ph)) return 1;
+      if (eq_str(ph, s_running)) {
+        r->flags |= F_NOT_READY;
+        if (dget(ready, k_reason, &rs) || !plain(rs)) return 1;
+        if (eq_str(rs, s_cnr)) r->flags |= F_READINESS_FAIL;
+      }
+    }
+  }
+  return 0;
+}
+
+static int enc_flag(PyObject* d, PyObject* key, uint32_t bit, Row* r) {
+  PyObject* v;
+  if (dget(d, key, &v) || !plain(v)) return 1;
+  if (truthy(v)) r->flags |= bit;
+  return 0;
+}
+
+static int enc_log(PyObject* d, const Vocab* V, Row* r) {
+  PyObject *pf, *ec;
+  if (dget(d, k_patterns, &pf) || dget(d, k_error_count, &ec)) return 1;
+  if (pf != NULL) {                                      /* log_patterns.add (:353) */
+    if (!PyList_CheckExact(pf)) return 1;
+    Py_ssize_t n = PyList_GET_SIZE(pf);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      int64_t b = vocab_bits(V->patterns, PyList_GET_ITEM(pf, i));
+      if (b < 0) return 1;
+      r->vocab |= (uint32_t)b;
+    }
+  }
+  if (ec == NULL) return 0;                              /* error_count += 0 (:354) */
+  if (PyFloat_CheckExact(ec)) {
+    double e = PyFloat_AS_DOUBLE(ec);
+    if (!(isfinite(e) && floor(e) == e && fabs(e) < INT_LIMIT)) r->flags |= F_ERR_FLOAT;
+    r->err = e;
+  } else if (PyLong_CheckExact(ec) || PyBool_Check(ec)) {
+    int overflow = 0;
+    long long v = PyLong_AsLongLongAndOverflow(ec, &overflow);
+    if (overflow) return 1;                              /* float(huge int): let Python decide */
+    if (v >= (long long)INT_LIMIT || v <= -(long long)INT_LIMIT) r->flags |= F_ERR_FLOAT;
+    r->err = (double)v;
+  } else {
+    return 1;
+  }
+  if (r->err == 0.0) r->err = 0.0;                       /* `if e:` leaves +0 for -0.0 */
+  return 0;
+}
+
+static int contains(PyObject* q, PyObject* s) {
+  return PyUnicode_Find(q, s, 0, PY_SSIZE_T_MAX, 1) >= 0;
+}
+
+static int enc_metric(PyObject* d, Row* r) {
+  PyObject *q, *an, *cv;
+  if (dget(d, k_query, &q) || dget(d, k_anomalous, &an) || dget(d, k_current, &cv)) return 1;
+  if (q != NULL && !PyUnicode_CheckExact(q)) return 1;   /* `in` on a non-str: hand over */
+  if (!plain(an) || !plain(cv)) return 1;
+  if (q == NULL) return 0;                               /* "" contains none of the names */
+  if (contains(q, s_memory) && truthy(an)) {             /* (:359-362) */
+    if (cv != NULL && cv != Py_None) {
+      if (!is_num(cv)) {
+        if (truthy(cv)) return 1;                        /* "x" > 90 raises */
+      } else if (truthy(cv) && num_cmp(cv, i_ninety, Py_GT) == 1) {
+        r->flags |= F_MEMORY_HIGH;
+      }
+    }
+  }
+  if (contains(q, s_hpa) && contains(q, s_max)) {        /* (:364-365) */
+    if (cv != NULL && is_num(cv) && num_cmp(cv, i_one, Py_EQ) == 1) r->flags |= F_HPA_AT_MAX;
+  }
+  if (contains(q, s_latency)) {                          /* (:367-368): missing -> 0 */
+    if (cv != NULL) {
+      if (!is_num(cv)) return 1;                         /* None / str > 1 raises */
+      if (num_cmp(cv, i_one, Py_GT) == 1) r->flags |= F_LATENCY_HIGH;
+    }
+  }
+  return 0;
+}
+
+static int enc_node(PyObject* d, Row* r) {
+  PyObject *name, *conds, *ready = NULL, *st = NULL;
+  if (dget(d, k_name, &name) || dget(d, k_conditions, &conds)) return 1;
+  if (conds != NULL) {
+    if (!PyDict_CheckExact(conds)) return 1;
+    if (dget(conds, k_ready_key, &ready)) return 1;
+    if (ready != NULL) {
+      if (!PyDict_CheckExact(ready)) return 1;
+      if (dget(ready, k_status, &st) || !plain(st)) return 1;
+    }
+  }
+  if (!eq_str(st, s_true)) {                             /* node_issues[name] (:375-376) */
+    if (name != NULL && !hashable_plain(name)) return 1;
+    r->flags |= F_NODE_ISSUE;
+  }
+  return 0;
+}
+
+static int type_of(PyObject* t) {
+  if (t == NULL || t == Py_None) return T_NONE;
+  if (!PyUnicode_CheckExact(t)) return -1;
+  PyObject* v = PyDict_GetItemWithError(type_map, t);   /* str keys: cannot raise */
+  return v == NULL ? T_NONE : (int)PyLong_AS_LONG(v);
+}
+
+/* encode_rows(evidence_lists, waiting, terminated, patterns, node_keys, slow_row,
+ *             flags, vocab, node, err, seg_off) -> (first-five-ids lists, rows handed over)
+ * Output buffers are writable contiguous arrays sized by the caller (sum of len(evidence)). */
+static PyObject* encode_rows(PyObject* self, PyObject* args) {
+  PyObject *lists, *slow_row;
+  Vocab V;
+  Py_buffer bf = {0}, bv = {0}, bn = {0}, be = {0}, bs = {0};
+  if (!PyArg_ParseTuple(args, "OO!O!O!O!Ow*w*w*w*w*", &lists, &PyDict_Type, &V.waiting,
+                        &PyDict_Type, &V.terminated, &PyDict_Type, &V.patterns, &PyDict_Type,
+                        &V.node_keys, &slow_row, &bf, &bv, &bn, &be, &bs))
+    return NULL;
+  PyObject* result = NULL;
+  PyObject* seq = NULL;
+  PyObject* ids = NULL;
+  Py_ssize_t n_slow = 0;
+  uint32_t* flags = (uint32_t*)bf.buf;
+  uint32_t* vocab = (uint32_t*)bv.buf;
+  uint32_t* node = (uint32_t*)bn.buf;
+  double* err = (double*)be.buf;
+  int64_t* seg = (int64_t*)bs.buf;
+  Py_ssize_t cap = bf.len / 4;
+  if (bv.len / 4 < cap || bn.len / 4 < cap || be.len / 8 < cap) {
+    PyErr_SetString(PyExc_ValueError, "encode_rows: column buffers differ in size");
+    goto done;
+  }
+  seq = PySequence_Fast(lists, "evidence_lists must be a sequence");
+  if (!seq) goto done;
+  Py_ssize_t B = PySequence_Fast_GET_SIZE(seq);
+  if (bs.len / 8 < B + 1) {
+    PyErr_SetString(PyExc_ValueError, "encode_rows: seg_off too small");
+    goto done;
+  }
+  ids = PyList_New(B);
+  if (!ids) goto done;
+  Py_ssize_t r = 0;
+  seg[0] = 0;
+  for (Py_ssize_t i = 0; i < B; ++i) {
+    PyObject* evs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, i), "evidence is not iterable");
+    if (!evs) goto done;
+    Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
+    PyObject* first = PyList_New(0);
+    if (!first) { Py_DECREF(evs); goto done; }
+    PyList_SET_ITEM(ids, i, first);
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      if (r >= cap) {
+        PyErr_SetString(PyExc_ValueError, "encode_rows: more rows than the buffers hold");
+        Py_DECREF(evs);
+        goto done;
+      }
+      PyObject* ev = PySequence_Fast_GET_ITEM(evs, j);
+      Row row = {0, 0, NO_NODE, 0.0, NULL};
+      PyObject* ev_id = NULL;
+      int slow = 1;
+      if (PyDict_CheckExact(ev)) {
+        PyObject *t, *data;
+        if (!dget(ev, k_id, &ev_id) && !dget(ev, k_type, &t) && !dget(ev, k_data, &data)) {
+          int ty = type_of(t);
+          if (ty == T_NONE) {
+            slow = hashable_plain(t == NULL ? Py_None : t) ? 0 : 1;
+          } else if (ty > 0 && data != NULL && PyDict_CheckExact(data)) {
+            switch (ty) {
+              case T_POD: slow = enc_pod(data, &V, &row); break;
+              case T_DEPLOY: slow = enc_flag(data, k_recent, F_RECENT_DEPLOY, &row); break;
+              case T_IMAGE: slow = enc_flag(data, k_image_changed, F_IMAGE_CHANGED, &row); break;
+              case T_LOG: slow = enc_log(data, &V, &row); break;
+              case T_METRIC: slow = enc_metric(data, &row); break;
+              case T_NODE: slow = enc_node(data, &row); break;
+            }
+          } else if (ty > 0 && data == NULL) {
+            /* ev.get("data", {}) -> {}: every get misses */
+            PyObject* empty = PyDict_New();
+            if (!empty) { Py_DECREF(evs); goto done; }
+            switch (ty) {
+              case T_POD: slow = enc_pod(empty, &V, &row); break;
+              case T_DEPLOY: slow = 0; break;
+              case T_IMAGE: slow = 0; break;
+              case T_LOG: slow = enc_log(empty, &V, &row); break;
+              case T_METRIC: slow = enc_metric(empty, &row); break;
+              case T_NODE: slow = enc_node(empty, &row); break;
+            }
+            Py_DECREF(empty);
+          }
+        }
+      }
+      if (!slow && row.pending_node != NULL) {
+        PyObject* idx = PyLong_FromSsize_t(PyDict_GET_SIZE(V.node_keys));
+        if (!idx) { Py_DECREF(evs); goto done; }
+        PyObject* k = PyDict_SetDefault(V.node_keys, row.pending_node, idx);
+        Py_DECREF(idx);
+        if (!k) { Py_DECREF(evs); goto done; }
+        row.node = (uint32_t)PyLong_AsUnsignedLong(k);
+      }
+      PyObject* slow_res = NULL;
+      if (slow) {                                /* the Python encoder: same result or raise */
+        ++n_slow;
+        slow_res = PyObject_CallOneArg(slow_row, ev);
+        if (!slow_res) { Py_DECREF(evs); goto done; }
+        unsigned int f, v, k;
+        double e;
+        PyObject* sid;
+        if (!PyArg_ParseTuple(slow_res, "OIIId", &sid, &f, &v, &k, &e)) {
+          Py_DECREF(slow_res);
+          Py_DECREF(evs);
+          goto done;
+        }
+        ev_id = sid;
+        row.flags = f; row.vocab = v; row.node = k; row.err = e;
+      }
+      flags[r] = row.flags;
+      vocab[r] = row.vocab;
+      node[r] = row.node;
+      err[r] = row.err;
+      if (PyList_GET_SIZE(first) < 5 &&
+          PyList_Append(first, ev_id == NULL ? Py_None : ev_id) < 0) {
+        Py_XDECREF(slow_res);
+        Py_DECREF(evs);
+        goto done;
+      }
+      Py_XDECREF(slow_res);
+      ++r;
+    }
+    Py_DECREF(evs);
+    seg[i + 1] = r;
+  }
+  result = Py_BuildValue("(On)", ids, n_slow);
+done:
+  Py_XDECREF(ids);
+  Py_XDECREF(seq);
+  PyBuffer_Release(&bf); PyBuffer_Release(&bv); PyBuffer_Release(&bn);
+  PyBuffer_Release(&be); PyBuffer_Release(&bs);
+  return result;
+}
+
+/* ---- hypothesis dicts --------------------------------------------------------------------- */
+
+static PyObject* uuid4_str(const unsigned char* raw) {
+  /* uuid.UUID(bytes=raw, version=4): version nibble 4, RFC 4122 variant */
+  unsigned char b[16];
+  memcpy(b, raw, 16);
+  b[6] = (unsigned char)((b[6] & 0x0F) | 0x40);
+  b[8] = (unsigned char)((b[8] & 0x3F) | 0x80);
+  static const char hx[] = "0123456789abcdef";
+  char s[36];
+  int p = 0;
+  for (int i = 0; i < 16; ++i) {
+    if (i == 4 || i == 6 || i == 8 || i == 10) s[p++] = '-';
+    s[p++] = hx[b[i] >> 4];
+    s[p++] = hx[b[i] & 15];
+  }
+  return PyUnicode_FromStringAndSize(s, 36);
+}
+
+static int set_steal(PyObject* d, PyObject* k, PyObject* v) {
+  if (!v) return -1;
+  int rc = PyDict_SetItem(d, k, v);
+  Py_DECREF(v);
+  return rc;
+}
+
+/* assemble(templates, unknown, n_hyp, order, confidence, final_score, strength, incident_ids,
+ *          evidence_ids, ranked, random_bytes) -> list of hypothesis lists
+ * templates: per rule slot a tuple (category, title, description, actions list, rule_id,
+ *            support_count); unknown: (category, title, description, confidence, rank,
+ *            actions list, generated_by, rule_id, support_count, signal_strength).
+ * order is u8 [B, S], the three f64 arrays [B, S]; random_bytes holds 16 B per hypothesis. */
+static PyObject* assemble(PyObject* self, PyObject* args) {
+  PyObject *templates, *unknown, *inc_ids, *ev_ids;
+  Py_buffer bn = {0}, bo = {0}, bc = {0}, bfs = {0}, bst = {0}, brnd = {0};
+  int ranked;
+  if (!PyArg_ParseTuple(args, "O!O!y*y*y*y*y*O!O!py*", &PyTuple_Type, &templates, &PyTuple_Type,
+                        &unknown, &bn, &bo, &bc, &bfs, &bst, &PyList_Type, &inc_ids,
+                        &PyList_Type, &ev_ids, &ranked, &brnd))
+    return NULL;
+  PyObject* out = NULL;
+  PyObject* gen_by = NULL;
+  Py_ssize_t R = PyTuple_GET_SIZE(templates), S = R + 1;
+  Py_ssize_t B = PyList_GET_SIZE(inc_ids);
+  const uint8_t* n_hyp = (const uint8_t*)bn.buf;
+  const uint8_t* order = (const uint8_t*)bo.buf;
+  const double* conf = (const double*)bc.buf;
+  const double* fscore = (const double*)bfs.buf;
+  const double* strength = (const double*)bst.buf;
+  const unsigned char* rnd = (const unsigned char*)brnd.buf;
+  Py_ssize_t n_rnd = brnd.len / 16, used = 0;
+  if (PyList_GET_SIZE(ev_ids) != B || bn.len < B || bo.len < B * S ||
+      bc.len < (Py_ssize_t)(B * S * 8) || bfs.len < (Py_ssize_t)(B * S * 8) ||
+      bst.len < (Py_ssize_t)(B * S * 8) || PyTuple_GET_SIZE(unknown) != 10) {
+    PyErr_SetString(PyExc_ValueError, "assemble: inconsistent sizes");
+    goto done;
+  }
+  for (Py_ssize_t s = 0; s < R; ++s) {
+    PyObject* t = PyTuple_GET_ITEM(templates, s);
+    if (!PyTuple_Check(t) || PyTuple_GET_SIZE(t) != 6 || !PyList_Check(PyTuple_GET_ITEM(t, 3))) {
+      PyErr_SetString(PyExc_ValueError, "assemble: bad rule template");
+      goto done;
+    }
+  }
+  if (!PyList_Check(PyTuple_GET_ITEM(unknown, 5))) {
+    PyErr_SetString(PyExc_ValueError, "assemble: bad unknown template");
+    goto done;
+  }
+  gen_by = PyUnicode_InternFromString("rules_engine");
+  if (!gen_by) goto done;
+  out = PyList_New(B);
+  if (!out) goto done;
+  for (Py_ssize_t i = 0; i < B; ++i) {
+    int nh = n_hyp[i];
+    PyObject* lst = PyList_New(nh);
+    if (!lst) goto fail;
+    PyList_SET_ITEM(out, i, lst);
+    PyObject* iid = PyList_GET_ITEM(inc_ids, i);
+    PyObject* eids = PyList_GET_ITEM(ev_ids, i);
+    if (!PyList_Check(eids)) {
+      PyErr_SetString(PyExc_TypeError, "assemble: evidence ids must be lists");
+      goto fail;
+    }
+    for (int p = 0; p < nh; ++p) {
+      int slot = order[i * S + p];
+      if (slot > R || used >= n_rnd) {
+        PyErr_SetString(PyExc_ValueError, "assemble: slot out of range or random bytes short");
+        goto fail;
+      }
+      PyObject* h = PyDict_New();
+      if (!h) goto fail;
+      PyList_SET_ITEM(lst, p, h);
+      if (set_steal(h, h_id, uuid4_str(rnd + 16 * used++)) < 0) goto fail;
+      if (PyDict_SetItem(h, h_incident, iid) < 0) goto fail;
+      if (slot == R) {                          /* _create_unknown_hypothesis (:457-478) */
+        PyObject* u = unknown;
+        if (PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(u, 0)) < 0 ||
+            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(u, 1)) < 0 ||
+            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(u, 2)) < 0 ||
+            PyDict_SetItem(h, h_confidence, PyTuple_GET_ITEM(u, 3)) < 0 ||
+            PyDict_SetItem(h, h_rank, PyTuple_GET_ITEM(u, 4)) < 0 ||
+            set_steal(h, h_support_ids, PyList_GetSlice(eids, 0, PY_SSIZE_T_MAX)) < 0 ||
+            set_steal(h, h_actions, PyList_GetSlice(PyTuple_GET_ITEM(u, 5), 0, PY_SSIZE_T_MAX)) < 0 ||
+            PyDict_SetItem(h, h_generated_by, PyTuple_GET_ITEM(u, 6)) < 0 ||
+            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(u, 7)) < 0 ||
+            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(u, 8)) < 0 ||
+            PyDict_SetItem(h, h_strength, PyTuple_GET_ITEM(u, 9)) < 0)
+          goto fail;
+      } else {                                  /* _create_hypothesis (:235-262) */
+        PyObject* t = PyTuple_GET_ITEM(templates, slot);
+        if (PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(t, 0)) < 0 ||
+            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(t, 1)) < 0 ||
+            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(t, 2)) < 0 ||
+            set_steal(h, h_confidence, PyFloat_FromDouble(conf[i * S + slot])) < 0 ||
+            PyDict_SetItem(h, h_rank, i_zero) < 0 ||
+            set_steal(h, h_support_ids, PyList_GetSlice(eids, 0, PY_SSIZE_T_MAX)) < 0 ||
+            set_steal(h, h_actions, PyList_GetSlice(PyTuple_GET_ITEM(t, 3), 0, PY_SSIZE_T_MAX)) < 0 ||
+            PyDict_SetItem(h, h_generated_by, gen_by) < 0 ||
+            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(t, 4)) < 0 ||
+            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(t, 5)) < 0 ||
+            set_steal(h, h_strength, PyFloat_FromDouble(strength[i * S + slot])) < 0)
+          goto fail;
+      }
+      if (ranked) {                             /* HypothesisRanker.rank (:63-71) */
+        if (set_steal(h, h_final, PyFloat_FromDouble(fscore[i * S + slot])) < 0 ||
+            set_steal(h, h_rank, PyLong_FromLong(p + 1)) < 0)
+          goto fail;
+      }
+    }
+  }
+  goto done;
+fail:
+  Py_CLEAR(out);
+done:
+  Py_XDECREF(gen_by);
+  PyBuffer_Release(&bn); PyBuffer_Release(&bo); PyBuffer_Release(&bc);
+  PyBuffer_Release(&bfs); PyBuffer_Release(&bst); PyBuffer_Release(&brnd);
+  return out;
+}
+
+static PyObject* flag_bits(PyObject* self, PyObject* noargs) {
+  return Py_BuildValue("(IIIIIIIIII)", F_RECENT_DEPLOY, F_IMAGE_CHANGED, F_MEMORY_HIGH,
+                       F_HPA_AT_MAX, F_LATENCY_HIGH, F_NODE_ISSUE, F_NOT_READY, F_READINESS_FAIL,
+                       F_ERR_FLOAT, NO_NODE);
+}
+
+static PyMethodDef methods[] = {
+    {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},
+    {"assemble", assemble, METH_VARARGS, "kernel outputs -> hypothesis dicts"},
+    {"flag_bits", flag_bits, METH_NOARGS, "the EGR_F_* bits and EGR_NO_NODE compiled in"},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_egr_pyhost", NULL, -1, methods};
+
+PyMODINIT_FUNC PyInit__egr_pyhost(void) {
+  if (intern_all() < 0) return NULL;
+  return PyModule_Create(&module);
+}

@@ -162,6 +162,25 @@ def _load() -> C.CDLL:
 lib = _load()
 
 
+def _load_pyhost():
+    """The CPython extension with the host side of the rules boundary (csrc/pyhost.c)."""
+    import importlib.machinery
+    import importlib.util
+    import sysconfig
+    path = PKG_ROOT / "lib" / ("_egr_pyhost" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not path.is_file():
+        raise ImportError(f"{path.name} not found in {path.parent}; build it with "
+                          f"`make -C {PKG_ROOT}`")
+    loader = importlib.machinery.ExtensionFileLoader("_egr_pyhost", str(path))
+    spec = importlib.util.spec_from_file_location("_egr_pyhost", str(path), loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod
+
+
+pyhost = _load_pyhost()
+
+
 class EgraphError(RuntimeError):
     """Device-side failure reported by libegraph (retryable in the workflow's terms)."""
 

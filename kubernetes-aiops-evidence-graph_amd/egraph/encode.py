@@ -9,6 +9,11 @@ Error behaviour follows the reference row by row: the same Python expressions ar
 in the same order, so a row that makes the reference raise (restart_count=None,
 query_name=None, data=None on a known type, a latency metric whose current_value is None, ...)
 raises the same exception type here, before anything reaches the device.
+
+`encode_batch` runs the rows through the native encoder (csrc/pyhost.c, `encode_rows`): a row
+whose values are all plain built-in types is encoded there; any other row is handed to
+`_RowEncoder.row` below, the Python statement of the same predicates, which also raises what
+the reference raises.  `encode_batch_py` is the all-Python encoder the tests check it against.
 """
 from __future__ import annotations
 
@@ -88,6 +93,16 @@ class _RowEncoder:
                 flags |= L.F_READINESS_FAIL
         return flags, vocab, key, 0.0
 
+    def row(self, ev):
+        """One evidence row: (id, flags, vocab, node_key, err) (rules_engine.py:294-313)."""
+        ev_id = ev.get("id")
+        ev_type = ev.get("evidence_type")
+        data = ev.get("data", {})
+        proc = self.dispatch.get(ev_type)
+        if proc is None:
+            return ev_id, 0, 0, L.EGR_NO_NODE, 0.0
+        return (ev_id, *proc(data))
+
     @staticmethod
     def deploy(data):
         return (L.F_RECENT_DEPLOY if data.get("is_recent_change") else 0), 0, L.EGR_NO_NODE, 0.0
@@ -134,37 +149,38 @@ class _RowEncoder:
         return 0, 0, L.EGR_NO_NODE, 0.0
 
 
-def encode_batch(evidence_lists: list[list[dict]], cat: Catalog) -> EncodedBatch:
-    """Encode B evidence lists (one per incident) into batch columns."""
-    enc = _RowEncoder(cat)
-    dispatch = enc.dispatch
+def _columns(evidence_lists):
     n = sum(len(ev) for ev in evidence_lists)
-    flags = np.zeros(n, np.uint32)
-    vocab = np.zeros(n, np.uint32)
-    node = np.full(n, L.EGR_NO_NODE, np.uint32)
-    err = np.zeros(n, np.float64)
-    seg_off = np.zeros(len(evidence_lists) + 1, np.int64)
+    return (np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.full(n, L.EGR_NO_NODE, np.uint32),
+            np.zeros(n, np.float64), np.zeros(len(evidence_lists) + 1, np.int64))
+
+
+def encode_batch(evidence_lists: list[list[dict]], cat: Catalog) -> EncodedBatch:
+    """Encode B evidence lists (one per incident) into batch columns (native row encoder)."""
+    enc = _RowEncoder(cat)
+    flags, vocab, node, err, seg_off = _columns(evidence_lists)
+    ids, _ = L.pyhost.encode_rows(evidence_lists, enc.waiting, enc.terminated, enc.patterns,
+                                  enc.node_keys, enc.row, flags, vocab, node, err, seg_off)
+    return EncodedBatch(flags, vocab, node, err, seg_off, ids)
+
+
+def encode_batch_py(evidence_lists: list[list[dict]], cat: Catalog) -> EncodedBatch:
+    """The same encoding with every row in Python (checker for the native encoder)."""
+    enc = _RowEncoder(cat)
+    flags, vocab, node, err, seg_off = _columns(evidence_lists)
     ids = []
     r = 0
     for i, evidence in enumerate(evidence_lists):
         first = []
         for ev in evidence:
-            ev_id = ev.get("id")
-            ev_type = ev.get("evidence_type")
-            data = ev.get("data", {})
+            ev_id, f, v, k, e = enc.row(ev)
             if len(first) < 5:
                 first.append(ev_id)
-            proc = dispatch.get(ev_type)
-            if proc is not None:
-                f, v, k, e = proc(data)
-                if f:
-                    flags[r] = f
-                if v:
-                    vocab[r] = v
-                if k != L.EGR_NO_NODE:
-                    node[r] = k
-                if e:
-                    err[r] = e
+            flags[r] = f
+            vocab[r] = v
+            node[r] = k
+            if e:
+                err[r] = e
             r += 1
         seg_off[i + 1] = r
         ids.append(first)

@@ -6,6 +6,7 @@ turns the per-incident slot orders back into the reference's hypothesis dicts
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from uuid import uuid4
 
@@ -127,3 +128,35 @@ def hypothesis_dicts(cat: Catalog, res: RulesResult, i: int, incident_id: str,
             h["rank"] = p + 1
         out.append(h)
     return out
+
+
+def _templates(cat: Catalog) -> tuple:
+    """Per-rule (category, title, description, actions, rule_id, support_count) and the
+    unknown hypothesis's fields, in the order csrc/pyhost.c assemble() reads them."""
+    t = getattr(cat, "_hyp_templates", None)
+    if t is None:
+        rules = tuple((r["category"], r["name"], r["description"], list(r["actions"]), r["id"],
+                       len(r["conditions"])) for r in cat.rules)
+        u = cat.unknown
+        unknown = (u["category"], u["title"], u["description"], u["confidence"], u["rank"],
+                   list(u["recommended_actions"]), u["generated_by"], u["rule_id"],
+                   u["support_count"], u["signal_strength"])
+        t = (rules, unknown)
+        cat._hyp_templates = t
+    return t
+
+
+def hypothesis_lists(cat: Catalog, res: RulesResult, incident_ids: list, evidence_ids: list,
+                     ranked: bool) -> list[list[dict]]:
+    """hypothesis_dicts for every incident of a batch, assembled natively (csrc/pyhost.c).
+
+    Same dicts, keys in the same order; `id` is a fresh uuid4 string per hypothesis drawn from
+    os.urandom, as uuid.uuid4() draws it."""
+    rules, unknown = _templates(cat)
+    order = res.order_rank if ranked else res.order_conf
+    n = int(res.n_hyp.sum(dtype=np.int64))
+    return L.pyhost.assemble(
+        rules, unknown, np.ascontiguousarray(res.n_hyp), np.ascontiguousarray(order),
+        np.ascontiguousarray(res.confidence), np.ascontiguousarray(res.final_score),
+        np.ascontiguousarray(res.strength), [str(i) for i in incident_ids],
+        list(evidence_ids), bool(ranked), os.urandom(16 * n))

@@ -8,7 +8,8 @@ matches).  Additive batch entry points put many incidents into one kernel launch
 (generate + HypothesisRanker.rank fused, as the workflow runs them back to back).
 
 All signal extraction, rule matching, confidence, ranking and ordering run in
-egr_rules_eval (csrc/rules.hip); the host encodes rows and assembles dicts.  There is no CPU
+egr_rules_eval (csrc/rules.hip); the host encodes rows and assembles dicts in native code
+(csrc/pyhost.c: encode_rows, assemble).  There is no CPU
 fallback: without a ROCm GPU the call raises RuntimeError.
 """
 from __future__ import annotations
@@ -17,7 +18,7 @@ import asyncio
 
 from egraph import catalog as _catalog
 from egraph.encode import encode_batch
-from egraph.rca import RulesDeviceBatch, hypothesis_dicts
+from egraph.rca import RulesDeviceBatch, hypothesis_lists
 from src.models import HypothesisCategory
 
 # The reference's rule table, with categories as enums as in rules_engine.py:15-190.
@@ -42,8 +43,8 @@ class RulesEngine:
             raise ValueError("incidents and evidence_lists differ in length")
         enc = encode_batch(evidence_lists, self.catalog)   # raises like the reference
         res = await asyncio.to_thread(self._launch_fetch, enc)
-        return [hypothesis_dicts(self.catalog, res, i, str(inc.id), enc.evidence_ids[i], ranked)
-                for i, inc in enumerate(incidents)]
+        return hypothesis_lists(self.catalog, res, [inc.id for inc in incidents],
+                                enc.evidence_ids, ranked)
 
     def _launch_fetch(self, enc):
         batch = RulesDeviceBatch(enc, self.catalog, self.device)
