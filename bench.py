@@ -1,7 +1,7 @@
 """Benchmark: incidents RCA-ranked/s + edges/s (3-hop propagation) on the 100k-pod graph.
 
 One step = one pass of the hot path over one batch of B incidents whose inputs are already
-resident in HBM (encoded evidence rows, seed triples, incident vertices), on one stream:
+resident in HBM (encoded evidence rows, seed triples, incident vertices):
   --engine frontier (default):
     egr_rules_eval (A1-A6, fused ranker)  ->  egr_frontier_set_seeds (radix sort by (column,
     vertex) + max-combine)  ->  egr_frontier_run (per column: 3-hop reach + 3-hop propagation
@@ -10,6 +10,10 @@ resident in HBM (encoded evidence rows, seed triples, incident vertices), on one
     egr_rules_eval  ->  egr_plan_set_seeds  ->  egr_plan_set_sources
     ->  3 x (egr_plan_hop + egr_plan_reach_hop)  ->  egr_plan_candidates  ->  egr_plan_topk.
 Both engines produce bit-identical scores, reach sets and top-k (tests/test_frontier_gpu.py).
+Frontier batches are pipelined (--pipeline 2, default): two independent frontier + rules states
+on their own streams take alternate batches, so the tail of one batch's frontier launch (its
+last, unevenly long columns) overlaps the start of the next.  Every batch is computed in full;
+`value` = batches x B / wall time of the timed region.
 The default run also times a few dense steps after the timed region and reports them under
 "dense_engine" (with the dense hop kernel's HBM roofline) for comparison.
 Workload: BASELINE.json configs[2] (C3: 100k pods / 100 namespaces / 2k nodes / 10k
@@ -43,11 +47,20 @@ METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod gra
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
+
+
+def max_over_ranks(dist, x: float, dev) -> float:
+    t = torch.tensor([x], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def setup(config: str, B: int, k: int, rank: int, dev: torch.device):
+def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1):
     from egraph import catalog, synth
     from egraph.device import to_device
     from egraph.encode import encode_batch
@@ -73,13 +86,22 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device):
         plan = snap.plan(B, max_seeds=len(sv), k=k)
         fr = snap.frontier(B, max_seeds=len(sv), k=k)
         rules = RulesDeviceBatch(enc, catalog.default(), dev)
+        # --pipeline P: P independent frontier + rules states, each on its own pair of streams;
+        # consecutive batches alternate between them so one batch's tail overlaps the next
+        # batch's start (every batch is still computed in full)
+        lanes = [dict(frontier=fr, rules=rules)] + [
+            dict(frontier=snap.frontier(B, max_seeds=len(sv), k=k),
+                 rules=RulesDeviceBatch(enc, catalog.default(), dev)) for _ in range(pipeline - 1)]
+        for ln in lanes:
+            ln["main"] = torch.cuda.Stream(dev) if pipeline > 1 else None
+            ln["side"] = (None if os.environ.get("EGRAPH_BENCH_ONE_STREAM")
+                          else torch.cuda.Stream(dev))
         seeds = tuple(to_device(a, dev) for a in (sv, sc, ss))
         sources = to_device(src, dev)
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
     return dict(graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
-                side=None if os.environ.get("EGRAPH_BENCH_ONE_STREAM") else torch.cuda.Stream(dev),
-                enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
+                lanes=lanes, tick=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence)
 
 
@@ -88,14 +110,24 @@ def step_frontier(ctx, hops: int, ev=None):
     not depend on the graph stages (nor they on it), so it goes to a second stream: its waves
     (35 VGPRs, no LDS) co-reside with the frontier kernel's (101 VGPRs x 4 per SIMD) instead of
     running in front of the seed preparation.  The timed region ends with a device-wide
-    synchronize, which joins both streams."""
-    fr = ctx["frontier"]
-    side = ctx["side"]
+    synchronize, which joins every stream."""
+    lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
+    ctx["tick"] += 1
+    if lane["main"] is None:
+        _lane_step(ctx, lane, hops, ev)
+    else:
+        with torch.cuda.stream(lane["main"]):
+            _lane_step(ctx, lane, hops, ev)
+
+
+def _lane_step(ctx, lane, hops: int, ev):
+    fr = lane["frontier"]
+    side = lane["side"]
     if side is not None:
         with torch.cuda.stream(side):
-            ctx["rules"].launch()
+            lane["rules"].launch()
     else:
-        ctx["rules"].launch()
+        lane["rules"].launch()
     fr.set_seeds(*ctx["seeds"])
     if ev is not None:
         a, b = ev.pop()
@@ -231,7 +263,7 @@ def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
             "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes}
 
 
-def frontier_roofline(ctx, run_ms: float, B: int, k: int) -> tuple[dict, dict]:
+def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tuple[dict, dict]:
     """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
     (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
     (8 B), the seed entries (vertex + value, 8 B), the member pool written (vertex, score,
@@ -245,7 +277,11 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int) -> tuple[dict, dict]:
                                        "(egr_frontier_run: reach + propagation + top-k)",
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("frontier"),
-             "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes}, work)
+             "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes,
+             # with batches in flight, launches overlap: per batch the GPU delivers nbytes
+             # in one step's wall time
+             "achieved_per_step": nbytes / (step_ms * 1e-3) / 1e9,
+             "batches_in_flight": len(ctx["lanes"])}, work)
 
 
 def time_dense(ctx, hops: int, steps: int, B: int, V: int, nnz: int, dev) -> dict:
@@ -360,9 +396,7 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(dist, elapsed, dev)
     B = args.batch
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -488,6 +522,8 @@ def main():
     ap.add_argument("--hops", type=int, default=3)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="frontier batches in flight (independent states on their own streams)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the end-to-end drop-in RulesEngine measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -511,12 +547,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
-    dev = torch.device("cuda", local)
+    # EGRAPH_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device); the
+    # driver's runs use RCCL ("nccl"), one rank per GPU
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(BACKEND)
 
     if args.workload == "storm":
         storm_main(args, world, rank, dev)
@@ -528,7 +569,8 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    ctx = setup(args.config, args.batch, args.k, rank, dev)
+    ctx = setup(args.config, args.batch, args.k, rank, dev,
+                args.pipeline if args.engine == "frontier" else 1)
     run_step = step_frontier if args.engine == "frontier" else step
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
@@ -549,9 +591,7 @@ def main():
     log(f"[rank {rank}] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, "
         f"wall {elapsed / args.steps * 1e3:.4f} ms/step")
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(dist, elapsed, dev)
 
     B, V = args.batch, ctx["snap"].n_vertices
     nnz = ctx["snap"].n_entries
@@ -559,7 +599,7 @@ def main():
     timed = events.done if isinstance(events, EventPool) else events
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in timed]))
     if args.engine == "frontier":
-        roof, work = frontier_roofline(ctx, launch_ms, B, args.k)
+        roof, work = frontier_roofline(ctx, launch_ms, B, args.k, ms)
     else:
         roof, work = dense_roofline(ctx, launch_ms, B, V, nnz), None
     out = {
@@ -587,6 +627,7 @@ def main():
             "vertices": V, "csr_entries": nnz, "incidents_per_gpu": B,
             "evidence_rows_per_gpu": ctx["enc"].n_rows, "seeds_per_gpu": int(len(ctx["seed_host"][0])),
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
+            "batches_in_flight": args.pipeline if args.engine == "frontier" else 1,
         },
         "roofline": roof,
     }
