@@ -43,12 +43,21 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t NO_NODE = EGR_NO_NODE;
 constexpr int FT = 512;                     // threads per workgroup (8 waves)
 constexpr int NWAVES = FT / 64;
-constexpr uint32_t LCAP = 6144;             // LDS table slots
-constexpr uint32_t LLIMIT = 4608;           // members before a column overflows (load 0.75)
+// Table geometry (override all four together for A/B builds; scripts/ab_lib.sh).  Members per
+// column on C3 / C4 reach 3711 / 3824 at most (scripts/frontier_members.py).
+#ifndef EGR_FR_LCAP
+#define EGR_FR_LCAP 6144
+#define EGR_FR_LLIMIT 4608
+#define EGR_FR_BLOOM_LOG 16
+#define EGR_FR_WAVES_PER_EU 4
+#endif
+constexpr uint32_t LCAP = EGR_FR_LCAP;      // LDS table slots
+constexpr uint32_t LLIMIT = EGR_FR_LLIMIT;  // members before a column overflows (load 0.75)
 constexpr int LPPT = LCAP / FT;             // slots cleared per thread
 constexpr int LMAX = 16;                    // rows up to this many entries run one lane per row
 constexpr int LB = 4;                       // keys probed together per lane
-constexpr uint32_t BLOOM_WORDS = 2048;      // 64 Kbit filter: rejects absent keys in one read
+constexpr int BLOOM_LOG = EGR_FR_BLOOM_LOG;
+constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // 64 Kbit filter: rejects absent keys in one read
 constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
 constexpr int KMAXF = 16;
 constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
@@ -147,8 +156,8 @@ __device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_
   return -2;
 }
 
-__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // 16 bits
-  return (mix24(v, 0xB5297Au | 1u) >> 8) & 0xFFFFu;
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // BLOOM_LOG bits
+  return (mix24(v, 0xB5297Au | 1u) >> 8) & ((1u << BLOOM_LOG) - 1u);
 }
 
 // slot of v, inserting it if absent (-1: table full)
@@ -716,7 +725,8 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   return true;
 }
 
-__global__ __launch_bounds__(FT, 2) void frontier_lds_kernel(const FArgs A) {
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(EGR_FR_WAVES_PER_EU)))
+void frontier_lds_kernel(const FArgs A) {
   __shared__ uint32_t keys[LCAP];
   __shared__ float s[LCAP];
   __shared__ uint32_t flw[LCAP / 4];
