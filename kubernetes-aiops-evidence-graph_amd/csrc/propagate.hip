@@ -164,6 +164,10 @@ __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr
   __syncthreads();
 }
 
+#ifndef EGR_HOP_NT_STORE
+#define EGR_HOP_NT_STORE 1
+#endif
+
 template <int G, bool FROM_SEEDS>
 __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
@@ -248,7 +252,15 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
         for (int t = 0; t < NT; ++t) fma4(w[t], x[t], acc);
       }
     }
+#if EGR_HOP_NT_STORE
+    // streaming store: the output tile is not re-read in this hop, so keep it from evicting
+    // the input tile the gathers re-read from the Infinity Cache
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{acc.x, acc.y, acc.z, acc.w},
+                                reinterpret_cast<f4v*>(&Y[(size_t)v * G + gl]));
+#else
     Y[(size_t)v * G + gl] = acc;
+#endif
   };
 
   Batch<FROM_SEEDS> ba, bb;
