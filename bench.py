@@ -60,7 +60,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1):
+def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1,
+          pool_entries: int = 0):
     from egraph import catalog, synth
     from egraph.device import to_device
     from egraph.encode import encode_batch
@@ -84,13 +85,15 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     with torch.cuda.device(dev):
         snap = g.snapshot(device=dev)
         plan = snap.plan(B, max_seeds=len(sv), k=k)
-        fr = snap.frontier(B, max_seeds=len(sv), k=k)
+        # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
+        # members outside the candidate set); 0 keeps every member's score for inspection
+        fr = snap.frontier(B, max_seeds=len(sv), k=k, pool_entries=pool_entries)
         rules = RulesDeviceBatch(enc, catalog.default(), dev)
         # --pipeline P: P independent frontier + rules states, each on its own pair of streams;
         # consecutive batches alternate between them so one batch's tail overlaps the next
         # batch's start (every batch is still computed in full)
         lanes = [dict(frontier=fr, rules=rules)] + [
-            dict(frontier=snap.frontier(B, max_seeds=len(sv), k=k),
+            dict(frontier=snap.frontier(B, max_seeds=len(sv), k=k, pool_entries=pool_entries),
                  rules=RulesDeviceBatch(enc, catalog.default(), dev)) for _ in range(pipeline - 1)]
         for ln in lanes:
             ln["main"] = torch.cuda.Stream(dev) if pipeline > 1 else None
@@ -266,12 +269,12 @@ def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
 def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tuple[dict, dict]:
     """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
     (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
-    (8 B), the seed entries (vertex + value, 8 B), the member pool written (vertex, score,
-    depth: 9 B) and the top-k output (8 B per slot)."""
+    (8 B), the seed entries (vertex + value, 8 B), the member pool written when there is one
+    (vertex, score, depth: 9 B) and the top-k output (8 B per slot)."""
     work = ctx["frontier"].stats()
     n_seeds = work["seed_entries"]
     nbytes = (8 * work["pull_entries"] + 4 * work["expand_entries"] + 8 * work["rows"]
-              + 8 * n_seeds + 9 * work["members"] + 8 * B * k)
+              + 8 * n_seeds + (9 * work["members"] if ctx["frontier"].pool_entries >= 0 else 0) + 8 * B * k)
     achieved = nbytes / (run_ms * 1e-3) / 1e9
     return ({"bound": "hbm", "kernel": "frontier_lds_kernel + frontier_global_kernel "
                                        "(egr_frontier_run: reach + propagation + top-k)",
@@ -528,6 +531,8 @@ def main():
                     help="skip the end-to-end drop-in RulesEngine measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--engine", default="frontier", choices=["frontier", "dense"])
+    ap.add_argument("--pool", action="store_true",
+                    help="frontier keeps every member's score (inspection mode: no last-pull pruning)")
     ap.add_argument("--dense-steps", type=int, default=5,
                     help="dense-engine steps timed after the main run for comparison (0: skip)")
     ap.add_argument("--shard", default="incidents", choices=["incidents", "graph"],
@@ -570,7 +575,8 @@ def main():
             dist.destroy_process_group()
         return
     ctx = setup(args.config, args.batch, args.k, rank, dev,
-                args.pipeline if args.engine == "frontier" else 1)
+                args.pipeline if args.engine == "frontier" else 1,
+                pool_entries=0 if args.pool else -1)
     run_step = step_frontier if args.engine == "frontier" else step
     for _ in range(args.warmup):
         run_step(ctx, args.hops)

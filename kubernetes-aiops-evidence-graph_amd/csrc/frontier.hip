@@ -74,6 +74,7 @@ struct FArgs {
   const uint8_t* vlabel;
   uint32_t V;
   int B, hops, k, exclude;
+  int prune;                   // no member pool: the last hop pulls the candidates only
   const uint32_t* seed_ptr;    // [B+1] per column
   const uint32_t* seed_vert;   // grouped by column, any order, duplicates allowed
   const float* seed_val;       // (duplicates are max-combined in the kernel, as fmaxf)
@@ -215,6 +216,12 @@ struct Work {
   uint32_t pull = 0, expand = 0, rows = 0;
 };
 
+// a top-k candidate's depth: reached within `hops` of the incident vertex (fl = depth + 1)
+__device__ __forceinline__ bool cand_depth(uint8_t f, int hops) {
+  const uint32_t d = f & FL_DEPTH;
+  return d != 0 && d <= (uint32_t)(hops + 1);
+}
+
 // diagnostics: per-wave sums of sub-step times (profiling builds of a phase only)
 struct Ticker {
   bool on = false;
@@ -295,9 +302,9 @@ __device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q
                                            int h) {
   const int qq = q >= 0 ? q : tab_insert<GT>(t, key);
   if (qq < 0) return;
-  if (kind & K_REACH) {
+  if (kind & K_REACH) {   // walk h (SEEDS: -1) builds reach level h + 2: fl = depth + 1 = h + 3
     const uint8_t fo = t.fl[qq];
-    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 2);   // every writer writes this
+    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 3);   // every writer writes this
   }
   if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
 }
@@ -351,14 +358,17 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
 }
 
 // One pass over the members [0, n) present when it starts, a wave taking 64 at a time.
-//   SEEDS (before hop 0): the seeds insert their neighbours and mark them `need` for hop 0.
+//   SEEDS (before hop 0, h = -1): the seeds insert their neighbours and mark them `need` for
+//         hop 0; the incident vertex inserts its neighbours at depth 1.
 //   PULL (hop h): a member pulled at h (`need` bit h & 1, or a seed) recomputes its score:
 //         its sum over its row, CSR order, of val * s[neighbour] (non-members skipped: exact,
 //         see the file comment) -> snew[member index]; unless h is the last hop it also
 //         inserts its neighbours and marks them `need` for h + 1 (a superset of the expansion
 //         of the non-zero members: harmless).  Members at reach depth h + 1 insert their
-//         neighbours with depth h + 2 in the same walk.  Insertions during the pass are exact:
-//         a new member's score is +0, so a pull that sees it or not reads the same term.
+//         neighbours with depth h + 2 in the same walk (reach runs one walk ahead of the
+//         pulls, so with A.prune the last pull skips every member outside the candidate set:
+//         their final scores are never read).  Insertions during the pass are exact: a new
+//         member's score is +0, so a pull that sees it or not reads the same term.
 // Rows of <= LMAX entries run one lane per row (light_row); longer rows (hubs) run one at a
 // time across the whole wave: 64 entries loaded and probed per round, the fmaf chain over the
 // present entries in lane (= CSR) order with v_readlane operands (every lane computes the
@@ -373,6 +383,11 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   if (tk.on) tk.t0 = wall_clock64();
   const bool prop_next = h + 1 < A.hops;
   const uint32_t par = (uint32_t)h & 1u;
+  // walk h (SEEDS: h = -1) expands the members at depth h + 1 into reach level h + 2, one walk
+  // ahead of the pulls: every level <= hops exists before the last pull starts
+  const bool reach_lvl = h + 2 <= A.hops;
+  const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
+  auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
   // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
   // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves.
   // The next chunk's selection and row_ptr loads are issued before the current chunk is walked
@@ -387,11 +402,12 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       const uint32_t p = t.mlist[c.i];
       v = t.keys[p];
       const uint8_t f = t.fl[p];
+      if (reach_lvl && (f & FL_DEPTH) == (uint32_t)(h + 2)) c.kind |= K_REACH;
       if constexpr (PH == SEEDS) {
-        c.kind = (f & FL_SEED) ? K_PROP : 0u;
+        if (f & FL_SEED) c.kind |= K_PROP;
       } else {
-        if ((f & FL_DEPTH) == (uint32_t)(h + 1)) c.kind |= K_REACH;
-        if (((t.need[p] >> par) & 1u) || (f & FL_SEED)) c.kind |= K_PULL | (prop_next ? K_PROP : 0u);
+        if ((((t.need[p] >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
+          c.kind |= K_PULL | (prop_next ? K_PROP : 0u);
       }
     }
     if (c.kind) {
@@ -643,7 +659,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   stamp();
   if (sh.ovf) return false;
   for (int h = 0; h < hops; ++h) {
-    // pull hop h (+ the expansion for hop h + 1 and reach level h + 1, in the same walk)
+    // pull hop h (+ the expansion for hop h + 1 and reach level h + 2, in the same walk)
     const uint32_t n0 = sh.count;
     row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
     wstamp();
@@ -651,11 +667,14 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     stamp();
     if (sh.ovf) return false;
     // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
+    // (pruned last pull: a non-candidate was not pulled and keeps +0; nothing reads it)
     const uint32_t n = sh.count, bit = 1u << ((uint32_t)h & 1u);
+    const bool prune_now = A.prune && h == hops - 1;
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
-      const uint8_t nd = t.need[p];
-      const bool pulled = i < n0 && ((nd & bit) || (t.fl[p] & FL_SEED));
+      const uint8_t nd = t.need[p], f = t.fl[p];
+      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
+                          (!prune_now || cand_depth(f, hops));
       t.s[p] = pulled ? t.snew[i] : 0.f;
       if (nd & bit) t.need[p] = nd & ~bit;
     }
@@ -1164,6 +1183,7 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.hops = hops;
   a.k = f->k;
   a.exclude = exclude_label;
+  a.prune = (f->pool_cap == 0 && !getenv("EGRAPH_FRONTIER_NO_PRUNE")) ? 1 : 0;
   a.seed_ptr = f->seed_ptr;
   a.seed_vert = f->seed_v;
   a.seed_val = f->seed_s;

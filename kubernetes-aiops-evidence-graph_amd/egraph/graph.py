@@ -469,6 +469,7 @@ class Frontier:
         self.snap = snap
         self.dev = snap.dev
         self.B, self.k, self.max_seeds = n_cols, k, max_seeds
+        self.pool_entries = pool_entries
         h = C.c_void_p()
         L.check(L.lib.egr_frontier_create(snap.handle, n_cols, max_seeds, k, pool_entries,
                                           C.byref(h)), "egr_frontier_create")

@@ -175,6 +175,32 @@ def test_frontier_without_pool_ranks_identically():
         fr.members(0)
 
 
+@pytest.mark.parametrize("hops,k,exclude", [(1, 7, None), (2, 10, None), (3, 16, -1), (4, 5, None)])
+def test_frontier_pruned_last_pull_exact(hops, k, exclude):
+    """Without a pool the last pull skips every member outside the candidate set (reach runs
+    one walk ahead, so the set is final before it): top-k stays bit-identical to the oracle
+    and fewer CSR entries are pulled."""
+    g, sv, sc, ss, src = _world(64, seed=59, pods=2500)
+    full = _check(g, sv, sc, ss, src, 64, hops=hops, k=k, exclude=exclude)
+    pr = _check(g, sv, sc, ss, src, 64, hops=hops, k=k, exclude=exclude, pool_entries=-1,
+                scores=False)
+    fs, ps = full.stats(), pr.stats()
+    assert ps["members"] == fs["members"] and ps["rows"] <= fs["rows"]
+    assert ps["pull_entries"] < fs["pull_entries"] if hops >= 2 else ps["pull_entries"] <= fs["pull_entries"]
+
+
+def test_frontier_pruned_overflow_and_edges():
+    """The pruned last pull in the global-memory variant and on empty / invalid columns."""
+    g, sv, sc, ss, src = _hub_world()
+    fr = _check(g, sv, sc, ss, src, len(src), k=12, pool_entries=-1, scores=False)
+    assert fr.stats()["overflowed"] >= 1
+    g, sv, sc, ss, src = _world(20, seed=41, pods=1000)
+    src = src.copy()
+    src[3] = NO_NODE
+    src[7] = g.num_vertices + 5
+    _check(g, sv, sc, ss, src, 20, pool_entries=-1, scores=False)
+
+
 def test_frontier_bad_arguments():
     g, sv, sc, ss, src = _world(4, seed=49, pods=400)
     snap = g.snapshot()
