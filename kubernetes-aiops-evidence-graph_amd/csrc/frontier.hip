@@ -285,7 +285,12 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
 // Row kinds of a phase: K_REACH = reach frontier (insert neighbours, give new ones the next
 // depth), K_PULL = recompute the row's score, K_PROP = expansion for the next hop (insert
 // neighbours and mark them `need` for it).
-constexpr uint32_t K_REACH = 1u, K_PULL = 2u, K_PROP = 4u;
+// K_NOINS (pruned runs, hop hops - 2): the expansion only marks members already present --
+// every candidate exists by then, and the last pull reads nothing else.
+constexpr uint32_t K_REACH = 1u, K_PULL = 2u, K_PROP = 4u, K_NOINS = 8u;
+// Reach runs two walks ahead of the pulls: level 1 is the incident row (a pre-pass), walk h
+// (SEEDS: h = -1) expands the members at depth h + 2 into level h + 3 (fl = depth + 1).
+constexpr int REACH_AHEAD = 2;
 
 enum Phase { SEEDS, PULL };
 
@@ -300,11 +305,12 @@ __device__ __forceinline__ void set_need(const Tab<GT>& t, uint32_t q, uint32_t 
 template <bool GT>
 __device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q, uint32_t kind,
                                            int h) {
+  if (q < 0 && (kind & (K_NOINS | K_REACH)) == K_NOINS) return;
   const int qq = q >= 0 ? q : tab_insert<GT>(t, key);
   if (qq < 0) return;
-  if (kind & K_REACH) {   // walk h (SEEDS: -1) builds reach level h + 2: fl = depth + 1 = h + 3
+  if (kind & K_REACH) {   // walk h builds reach level h + 1 + REACH_AHEAD (fl = depth + 1)
     const uint8_t fo = t.fl[qq];
-    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 3);   // every writer writes this
+    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 2 + REACH_AHEAD);   // all write this
   }
   if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
 }
@@ -383,10 +389,12 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   if (tk.on) tk.t0 = wall_clock64();
   const bool prop_next = h + 1 < A.hops;
   const uint32_t par = (uint32_t)h & 1u;
-  // walk h (SEEDS: h = -1) expands the members at depth h + 1 into reach level h + 2, one walk
-  // ahead of the pulls: every level <= hops exists before the last pull starts
-  const bool reach_lvl = h + 2 <= A.hops;
+  // walk h (SEEDS: h = -1) expands the members at depth h + REACH_AHEAD into reach level
+  // h + REACH_AHEAD + 1: every level <= hops exists before the walk of hop hops - 2 starts
+  const uint32_t reach_fl = (uint32_t)(h + REACH_AHEAD + 1);   // fl of the expanded depth
+  const bool reach_lvl = h + REACH_AHEAD + 1 <= A.hops;
   const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
+  const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
   auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
   // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
   // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves.
@@ -402,12 +410,12 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       const uint32_t p = t.mlist[c.i];
       v = t.keys[p];
       const uint8_t f = t.fl[p];
-      if (reach_lvl && (f & FL_DEPTH) == (uint32_t)(h + 2)) c.kind |= K_REACH;
+      if (reach_lvl && (f & FL_DEPTH) == reach_fl) c.kind |= K_REACH;
       if constexpr (PH == SEEDS) {
-        if (f & FL_SEED) c.kind |= K_PROP;
+        if (f & FL_SEED) c.kind |= K_PROP | noins;
       } else {
         if ((((t.need[p] >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
-          c.kind |= K_PULL | (prop_next ? K_PROP : 0u);
+          c.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
       }
     }
     if (c.kind) {
@@ -648,6 +656,20 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       if (q >= 0) t.fl[q] |= 1;
     }
   }
+  __syncthreads();
+  // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
+  if (A.hops >= 1 && A.sources[b] < A.V) {
+    const uint32_t src = A.sources[b];
+    const uint32_t e0 = A.row_ptr[src], e1 = A.row_ptr[src + 1];
+    if (tid == 0) {
+      ++work.rows;
+      work.expand += e1 - e0;
+    }
+    for (uint32_t e = e0 + tid; e < e1; e += FT) {
+      const int q = tab_insert<GT>(t, A.cv[e].x);
+      if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
+    }
+  }
   wstamp();
   __syncthreads();
   stamp();
@@ -717,13 +739,23 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   }
   stamp();
   // members -> pool (coalesced by member index)
-  if (tid == 0) sh.base = atomicAdd(A.pool_ctr, (unsigned long long)n);
-  atomicAdd(&sh.w_pull, work.pull);
-  atomicAdd(&sh.w_expand, work.expand);
-  atomicAdd(&sh.w_rows, work.rows);
+  if (tid == 0) sh.base = A.pool_cap ? atomicAdd(A.pool_ctr, (unsigned long long)n) : 0ull;
+  {   // work counters: one LDS atomic per wave
+    uint32_t wp = work.pull, we = work.expand, wr = work.rows;
+    for (int o = 32; o > 0; o >>= 1) {
+      wp += __shfl_xor(wp, o);
+      we += __shfl_xor(we, o);
+      wr += __shfl_xor(wr, o);
+    }
+    if (lane == 0) {
+      atomicAdd(&sh.w_pull, wp);
+      atomicAdd(&sh.w_expand, we);
+      atomicAdd(&sh.w_rows, wr);
+    }
+  }
   __syncthreads();
   const unsigned long long base = sh.base;
-  const bool keep = base + n <= A.pool_cap;
+  const bool keep = A.pool_cap && base + n <= A.pool_cap;
   if (keep) {
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];

@@ -30,10 +30,11 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--hops", type=int, default=3)
     ap.add_argument("--out", default="")
+    ap.add_argument("--pool", action="store_true", help="keep the member pool (no last-pull pruning)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    ctx = bench.setup(args.config, args.batch, 10, 0, dev)
+    ctx = bench.setup(args.config, args.batch, 10, 0, dev, pool_entries=0 if args.pool else -1)
     for _ in range(3):
         bench.step_frontier(ctx, args.hops)
     torch.cuda.synchronize()

@@ -177,15 +177,17 @@ def test_frontier_without_pool_ranks_identically():
 
 @pytest.mark.parametrize("hops,k,exclude", [(1, 7, None), (2, 10, None), (3, 16, -1), (4, 5, None)])
 def test_frontier_pruned_last_pull_exact(hops, k, exclude):
-    """Without a pool the last pull skips every member outside the candidate set (reach runs
-    one walk ahead, so the set is final before it): top-k stays bit-identical to the oracle
-    and fewer CSR entries are pulled."""
+    """Without a pool the last pull skips every member outside the candidate set and the
+    expansion before it inserts no new member (reach runs two walks ahead, so the candidate
+    set is final by then): top-k stays bit-identical to the oracle and fewer CSR entries are
+    pulled."""
     g, sv, sc, ss, src = _world(64, seed=59, pods=2500)
     full = _check(g, sv, sc, ss, src, 64, hops=hops, k=k, exclude=exclude)
     pr = _check(g, sv, sc, ss, src, 64, hops=hops, k=k, exclude=exclude, pool_entries=-1,
                 scores=False)
     fs, ps = full.stats(), pr.stats()
-    assert ps["members"] == fs["members"] and ps["rows"] <= fs["rows"]
+    # the expansion before the last pull inserts nothing new: fewer members, fewer rows
+    assert ps["members"] <= fs["members"] and ps["rows"] <= fs["rows"]
     assert ps["pull_entries"] < fs["pull_entries"] if hops >= 2 else ps["pull_entries"] <= fs["pull_entries"]
 
 
