@@ -26,7 +26,8 @@ int fail(int code, const std::string& msg);
   do {                                                                                      \
     hipError_t e_ = hipGetLastError();                                                      \
     if (e_ != hipSuccess)                                                                   \
-      return ::egr::fail(EGR_EDEVICE, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+      return ::egr::fail(EGR_EDEVICE, std::string("kernel launch (" __FILE__ ":") +           \
+                                          std::to_string(__LINE__) + "): " + hipGetErrorString(e_)); \
   } while (0)
 
 // ---- Python-exact float rounding -----------------------------------------------------------

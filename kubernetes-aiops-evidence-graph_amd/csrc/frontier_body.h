@@ -1,0 +1,822 @@
+// Frontier engine kernels for ONE table geometry; included by csrc/frontier.hip once per
+// geometry, each time inside its own namespace (no include guard, no includes: by design).
+
+// Geometry of this instantiation (set by the includer, csrc/frontier.hip):
+//   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
+//   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU.
+constexpr int FT = FR_FT;                   // threads per workgroup
+constexpr int NWAVES = FT / 64;
+constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
+constexpr uint32_t LLIMIT = FR_LLIMIT;      // members before a column overflows (load 0.75)
+constexpr int LPPT = LCAP / FT;             // slots cleared per thread
+constexpr int LMAX = 16;                    // rows up to this many entries run one lane per row
+constexpr int LB = 4;                       // keys probed together per lane
+constexpr int BLOOM_LOG = FR_BLOOM_LOG;
+constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys in one read
+constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
+constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
+static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
+
+
+// The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
+// insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
+// index.
+template <bool GT>
+struct Tab {
+  using MT = typename std::conditional<GT, uint32_t, uint16_t>::type;
+  uint32_t* keys;
+  float* s;
+  uint8_t* fl;
+  uint8_t* need;    // touched by an expansion this hop: pulled
+  MT* mlist;
+  float* snew;
+  uint32_t cap, limit;
+  uint32_t* count;  // LDS
+  uint32_t* ovf;    // LDS
+  uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
+};
+
+// Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
+// insert CASes the lowest empty slot it sees and moves on only when that slot is taken, so a
+// bucket with an empty slot ends every probe sequence that passes through it.
+// Hashes use only full-rate 24-bit multiplies (a 32-bit v_mul_lo / v_mul_hi is quarter rate,
+// and every probed key pays for its hashes): the id is folded to 24 bits, multiplied by an odd
+// 24-bit constant, and 16 mixed bits are range-reduced to [0, nb) by a second 24-bit multiply.
+__device__ __forceinline__ uint32_t mix24(uint32_t v, uint32_t c) {
+  return (uint32_t)__umul24((v ^ (v >> 24)) & 0xFFFFFFu, c);
+}
+
+// (HIP's __umul24 returns a signed int: the product is taken as unsigned before the shift, or a
+// table of more than 2^15 buckets would get negative -- out of range -- start buckets.  Tables
+// of more than 2^16 buckets, the global-memory variant's on large graphs, reduce a full 32-bit
+// hash with __umulhi instead.)
+__device__ __forceinline__ uint32_t hbucket(uint32_t v, uint32_t nb) {
+  const uint32_t h = mix24(v, 0x9E3779u);
+  if (nb > 65536u) return __umulhi(h, nb);
+  return (uint32_t)__umul24((h >> 8) & 0xFFFFu, nb) >> 16;
+}
+
+__device__ __forceinline__ uint4 read_bucket(const uint32_t* keys, uint32_t bk) {
+  return reinterpret_cast<const uint4*>(keys)[bk];
+}
+
+// outcome of one bucket read for key v: slot (>= 0), -1 = absent, -2 = continue probing
+__device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_t bk) {
+  if (kk.x == v) return (int)(4 * bk);
+  if (kk.y == v) return (int)(4 * bk + 1);
+  if (kk.z == v) return (int)(4 * bk + 2);
+  if (kk.w == v) return (int)(4 * bk + 3);
+  if (kk.w == EMPTY) return -1;            // slots fill in order: an empty last slot ends it
+  return -2;
+}
+
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // BLOOM_LOG bits
+  return (mix24(v, 0xB5297Au | 1u) >> 8) & ((1u << BLOOM_LOG) - 1u);
+}
+
+// slot of v, inserting it if absent (-1: table full)
+template <bool GT>
+__device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk = hbucket(v, nb);
+  for (uint32_t n = 0; n < nb; ++n) {
+    uint4 kk = read_bucket(t.keys, bk);
+    uint32_t ks[4] = {kk.x, kk.y, kk.z, kk.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (ks[j] == v) return (int)(4 * bk + j);
+      if (ks[j] == EMPTY) {
+        const uint32_t p = 4 * bk + j;
+        const uint32_t old = atomicCAS(&t.keys[p], EMPTY, v);
+        if (old == EMPTY) {
+          if constexpr (!GT) {
+            const uint32_t h = bloom_hash(v);
+            atomicOr(&t.bloom[h >> 5], 1u << (h & 31u));
+          }
+          const uint32_t c = atomicAdd(t.count, 1u);
+          if (c < t.limit) t.mlist[c] = (typename Tab<GT>::MT)p;
+          else *t.ovf = 1u;
+          return (int)p;
+        }
+        if (old == v) return (int)p;
+        // taken by another key: look at the next slot
+      }
+    }
+    bk = bk + 1 == nb ? 0 : bk + 1;
+  }
+  *t.ovf = 1u;
+  return -1;
+}
+
+// slot of v or -1 (only called while no insertion is in flight)
+template <bool GT>
+__device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
+  if constexpr (!GT) {
+    const uint32_t h = bloom_hash(v);
+    if (!((t.bloom[h >> 5] >> (h & 31u)) & 1u)) return -1;
+  }
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk = hbucket(v, nb);
+  for (uint32_t n = 0; n < nb; ++n) {
+    const int r = bucket_match(read_bucket(t.keys, bk), v, bk);
+    if (r != -2) return r;
+    bk = bk + 1 == nb ? 0 : bk + 1;
+  }
+  return -1;
+}
+
+struct Work {
+  uint32_t pull = 0, expand = 0, rows = 0;
+};
+
+// a top-k candidate's depth: reached within `hops` of the incident vertex (fl = depth + 1)
+__device__ __forceinline__ bool cand_depth(uint8_t f, int hops) {
+  const uint32_t d = f & FL_DEPTH;
+  return d != 0 && d <= (uint32_t)(hops + 1);
+}
+
+// diagnostics: per-wave sums of sub-step times (profiling builds of a phase only)
+struct Ticker {
+  bool on = false;
+  uint64_t t0 = 0;
+  uint64_t sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void tick(int k) {
+    if (on) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t t1 = wall_clock64();
+      sub[k] += t1 - t0;
+      t0 = t1;
+    }
+  }
+};
+
+
+// Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
+// still unresolved, so a lane's NQ probe sequences share round trips.
+template <bool GT, int NQ>
+__device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
+                                           int (&q)[NQ]) {
+  const uint32_t nb = t.cap / 4;
+  uint32_t bk[NQ];
+  uint32_t pend = 0;
+#pragma unroll
+  for (int x = 0; x < NQ; ++x) {
+    bk[x] = hbucket(key[x], nb);
+    q[x] = -1;
+    if ((uint32_t)x < nq) pend |= 1u << x;
+  }
+  if constexpr (!GT) {
+    // the filter: a key whose bit is clear is not a member (most pulled neighbours are not)
+    uint32_t bw[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      bw[x] = (pend & (1u << x)) ? t.bloom[bloom_hash(key[x]) >> 5] : ~0u;
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      if (!((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u)) pend &= ~(1u << x);
+  }
+  for (uint32_t n = 0; n < nb && __any(pend != 0); ++n) {
+    uint4 kk[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x)
+      if (pend & (1u << x)) kk[x] = read_bucket(t.keys, bk[x]);
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) {
+      if (pend & (1u << x)) {
+        const int r = bucket_match(kk[x], key[x], bk[x]);
+        if (r != -2) {
+          q[x] = r;
+          pend &= ~(1u << x);
+        } else {
+          bk[x] = bk[x] + 1 == nb ? 0 : bk[x] + 1;
+        }
+      }
+    }
+  }
+}
+
+// Row kinds of a phase: K_REACH = reach frontier (insert neighbours, give new ones the next
+// depth), K_PULL = recompute the row's score, K_PROP = expansion for the next hop (insert
+// neighbours and mark them `need` for it).
+// K_NOINS (pruned runs, hop hops - 2): the expansion only marks members already present --
+// every candidate exists by then, and the last pull reads nothing else.
+constexpr uint32_t K_REACH = 1u, K_PULL = 2u, K_PROP = 4u, K_NOINS = 8u;
+// Reach runs two walks ahead of the pulls: level 1 is the incident row (a pre-pass), walk h
+// (SEEDS: h = -1) expands the members at depth h + 2 into level h + 3 (fl = depth + 1).
+constexpr int REACH_AHEAD = 2;
+
+enum Phase { SEEDS, PULL };
+
+// `need` bits: bit (h & 1) marks the members pulled at hop h; set with a 32-bit LDS / global
+// atomic OR because the other parity's bit of the same byte is read concurrently
+template <bool GT>
+__device__ __forceinline__ void set_need(const Tab<GT>& t, uint32_t q, uint32_t par) {
+  atomicOr(reinterpret_cast<uint32_t*>(t.need) + (q >> 2), (1u << par) << ((q & 3u) * 8u));
+}
+
+// Insertion side of a row entry (after its probe): q = the slot if present, else insert.
+template <bool GT>
+__device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q, uint32_t kind,
+                                           int h) {
+  if (q < 0 && (kind & (K_NOINS | K_REACH)) == K_NOINS) return;
+  const int qq = q >= 0 ? q : tab_insert<GT>(t, key);
+  if (qq < 0) return;
+  if (kind & K_REACH) {   // walk h builds reach level h + 1 + REACH_AHEAD (fl = depth + 1)
+    const uint8_t fo = t.fl[qq];
+    if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 2 + REACH_AHEAD);   // all write this
+  }
+  if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
+}
+
+// One row of dl <= LMAX entries, one lane per row: every entry is loaded in one round trip,
+// probed LB keys at a time (lockstep), then the in-order fmaf chain runs in registers (K_PULL)
+// and the absent neighbours are inserted (K_REACH / K_PROP).
+template <bool GT>
+__device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
+                                          uint32_t kind, int h, float& acc, Ticker& tk) {
+  uint32_t c[LMAX];
+  float w[LMAX];
+#pragma unroll
+  for (int x = 0; x < LMAX; ++x) {
+    uint2 ce = make_uint2(0u, 0u);
+    if ((uint32_t)x < dl) ce = A.cv[e0 + x];
+    c[x] = ce.x;
+    w[x] = __uint_as_float(ce.y);
+  }
+  tk.tick(4);
+#pragma unroll
+  for (int sb = 0; sb < LMAX / LB; ++sb) {
+    if (!__any(dl > (uint32_t)(sb * LB))) continue;   // (continue, not break: keeps it unrolled)
+    const uint32_t nq = dl > (uint32_t)(sb * LB) ? min(dl - sb * LB, (uint32_t)LB) : 0u;
+    uint32_t key[LB];
+#pragma unroll
+    for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
+    int q[LB];
+    find_batch<GT, LB>(t, key, nq, q);
+    tk.tick(5);
+    if (kind & K_PULL) {
+      float xs[LB];
+#pragma unroll
+      for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
+#pragma unroll
+      for (int x = 0; x < LB; ++x)
+        if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
+    }
+    tk.tick(6);
+    if (kind & (K_REACH | K_PROP)) {
+#pragma unroll
+      for (int x = 0; x < LB; ++x)
+        if ((uint32_t)x < nq) grow_entry<GT>(t, key[x], q[x], kind, h);
+    }
+    tk.tick(7);
+  }
+}
+
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// One pass over the members [0, n) present when it starts, a wave taking 64 at a time.
+//   SEEDS (before hop 0, h = -1): the seeds insert their neighbours and mark them `need` for
+//         hop 0; the incident vertex inserts its neighbours at depth 1.
+//   PULL (hop h): a member pulled at h (`need` bit h & 1, or a seed) recomputes its score:
+//         its sum over its row, CSR order, of val * s[neighbour] (non-members skipped: exact,
+//         see the file comment) -> snew[member index]; unless h is the last hop it also
+//         inserts its neighbours and marks them `need` for h + 1 (a superset of the expansion
+//         of the non-zero members: harmless).  Members at reach depth h + 1 insert their
+//         neighbours with depth h + 2 in the same walk (reach runs one walk ahead of the
+//         pulls, so with A.prune the last pull skips every member outside the candidate set:
+//         their final scores are never read).  Insertions during the pass are exact: a new
+//         member's score is +0, so a pull that sees it or not reads the same term.
+// Rows of <= LMAX entries run one lane per row (light_row); longer rows (hubs) run one at a
+// time across the whole wave: 64 entries loaded and probed per round, the fmaf chain over the
+// present entries in lane (= CSR) order with v_readlane operands (every lane computes the
+// same chain; the owner keeps it).
+template <bool GT, Phase PH>
+__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int h, Work& work,
+                                          int b = -1) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
+  Ticker tk;
+  tk.on = A.prof && b >= 0;
+  if (tk.on) tk.t0 = wall_clock64();
+  const bool prop_next = h + 1 < A.hops;
+  const uint32_t par = (uint32_t)h & 1u;
+  // walk h (SEEDS: h = -1) expands the members at depth h + REACH_AHEAD into reach level
+  // h + REACH_AHEAD + 1: every level <= hops exists before the walk of hop hops - 2 starts
+  const uint32_t reach_fl = (uint32_t)(h + REACH_AHEAD + 1);   // fl of the expanded depth
+  const bool reach_lvl = h + REACH_AHEAD + 1 <= A.hops;
+  const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
+  const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
+  auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
+  // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
+  // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves.
+  // The next chunk's selection and row_ptr loads are issued before the current chunk is walked
+  // (a member's kind cannot change during the pass: see the comment above).
+  struct Chunk {
+    uint32_t i, kind, e0, e1;
+  };
+  auto fetch = [&](uint32_t k0) {
+    Chunk c{wave + NWAVES * (lane + 64u * k0), 0u, 0u, 0u};
+    uint32_t v = 0;
+    if (c.i < n) {
+      uint32_t p = t.mlist[c.i];
+      if (p >= t.cap) {           // guard (see below)
+        atomicAdd(&A.stats[5], 1ull);
+        p = 0;
+      }
+      v = t.keys[p];
+      const uint8_t f = t.fl[p];
+      if (reach_lvl && (f & FL_DEPTH) == reach_fl) c.kind |= K_REACH;
+      if constexpr (PH == SEEDS) {
+        if (f & FL_SEED) c.kind |= K_PROP | noins;
+      } else {
+        if ((((t.need[p] >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
+          c.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
+      }
+    }
+    if (c.kind && v >= A.V) {   // a member key outside the graph: table corruption, counted
+      atomicAdd(&A.stats[5], 1ull);
+      c.kind = 0;
+    }
+    if (c.kind) {
+      c.e0 = A.row_ptr[v];
+      c.e1 = A.row_ptr[v + 1];
+    }
+    return c;
+  };
+  const uint32_t nk = (n + FT - 1) / FT;
+  Chunk nxt = nk ? fetch(0) : Chunk{0u, 0u, 0u, 0u};
+  for (uint32_t k0 = 0; k0 < nk; ++k0) {
+    const Chunk cur = nxt;
+    if (k0 + 1 < nk) nxt = fetch(k0 + 1);
+    const uint32_t i = cur.i, kind = cur.kind, e0 = cur.e0, deg = cur.e1 - cur.e0;
+    if (kind) {
+      ++work.rows;
+      if (kind & K_PULL) work.pull += deg;
+      else work.expand += deg;
+    }
+    tk.tick(0);
+    const bool light = deg <= (uint32_t)LMAX;
+    float acc = 0.f;
+    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
+    tk.tick(1);
+    uint64_t heavy = __ballot(!light);
+    while (heavy) {
+      const int m = __ffsll((long long)heavy) - 1;
+      heavy &= heavy - 1;
+      const uint32_t he0 = __builtin_amdgcn_readlane(e0, m);
+      const uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
+      const uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
+      float hacc = 0.f;
+      for (uint32_t base = 0; base < hdeg; base += 64) {
+        const uint32_t j = base + lane;
+        const bool act = j < hdeg;
+        const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
+        const uint32_t u = ce.x;
+        const int q = act ? tab_find<GT>(t, u) : -1;
+        if (hkind & K_PULL) {
+          const float w = __uint_as_float(ce.y);
+          const float x = q >= 0 ? t.s[q] : 0.f;
+          // the chain runs over the present entries only, in lane (= CSR) order
+          for (uint64_t fm = __ballot(q >= 0); fm; fm &= fm - 1) {
+            const int y = __ffsll((long long)fm) - 1;
+            hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
+          }
+        }
+        if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
+      }
+      if (lane == m) acc = hacc;
+    }
+    tk.tick(2);
+    if constexpr (PH == PULL) {
+      if (kind & K_PULL) t.snew[i] = acc;
+    }
+    tk.tick(3);
+  }
+  if (tk.on && lane == 0)
+    for (int k = 0; k < 8; ++k)
+      A.prof[((size_t)b * PROF_SLOTS + 24 + k) * PROF_W + 1 + wave] = tk.sub[k];
+}
+
+// ---- top-k keys: (score desc, vertex asc) as one u64, larger = better, 0 = none -----------
+__device__ __forceinline__ uint64_t topk_key(float s, uint32_t v) {
+  const uint32_t f = __float_as_uint(s);
+  const uint32_t o = (f & 0x80000000u) ? ~f : (f | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)~v;
+}
+
+__device__ __forceinline__ void topk_unkey(uint64_t k, float& s, uint32_t& v) {
+  if (k == 0) {
+    s = -INFINITY;
+    v = NO_NODE;
+    return;
+  }
+  const uint32_t o = (uint32_t)(k >> 32);
+  s = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+  v = ~(uint32_t)k;
+}
+
+// wave-wide max of a u32 with DPP row ops (quad perms, half / full row mirror, row broadcasts
+// 15 and 31), result from lane 63; every lane gets it
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x141, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x140, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// wave-wide max of a u64 key: the max high word, then the max low word among its holders (a
+// second reduction only when several lanes hold that high word: scores are mostly distinct)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+  const uint32_t hi = (uint32_t)(k >> 32);
+  const uint32_t mh = wave_max_u32(hi);
+  const uint64_t holders = __ballot(hi == mh);
+  const uint32_t ml = (holders & (holders - 1))
+                          ? wave_max_u32(hi == mh ? (uint32_t)k : 0u)
+                          : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, __ffsll((long long)holders) - 1);
+  return ((uint64_t)mh << 32) | ml;
+}
+
+struct Shared {
+  uint32_t count, ovf, item;
+  unsigned long long base;
+  uint64_t top[NWAVES][KMAXF];
+  uint32_t w_pull, w_expand, w_rows;
+};
+
+// candidate key of member slot p: reached within `hops`, not carrying the excluded label
+template <bool GT>
+__device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, uint32_t p,
+                                             uint8_t maxd) {
+  if (p >= t.cap) return 0;
+  const uint8_t f = t.fl[p] & FL_DEPTH;
+  if (f < 1 || f > maxd) return 0;
+  const uint32_t v = t.keys[p];
+  if (v >= A.V) return 0;
+  if (A.exclude >= 0 && A.vlabel[v] == (uint8_t)A.exclude) return 0;
+  return topk_key(t.s[p], v);
+}
+
+// This thread's best candidate key strictly below `bound` (global variant: rescans).
+template <bool GT>
+__device__ __forceinline__ uint64_t rescan_best(const FArgs& A, const Tab<GT>& t, uint32_t n,
+                                                uint8_t maxd, uint64_t bound) {
+  uint64_t b = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += FT) {
+    const uint64_t kk = cand_key<GT>(A, t, t.mlist[i], maxd);
+    if (kk < bound && kk > b) b = kk;
+  }
+  return b;
+}
+
+// Per-wave top-k into sh.top[wave][0..k) (k wave-wide max rounds, no block barrier).
+template <bool GT>
+__device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shared& sh, uint32_t n,
+                                          uint8_t maxd) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if constexpr (!GT) {
+    uint64_t kk[MPT];
+#pragma unroll
+    for (int j = 0; j < MPT; ++j) {
+      const uint32_t i = threadIdx.x + j * FT;
+      kk[j] = i < n ? cand_key<GT>(A, t, t.mlist[i], maxd) : 0ull;
+    }
+    auto best = [&]() {
+      uint64_t b = 0;
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) b = kk[j] > b ? kk[j] : b;
+      return b;
+    };
+    uint64_t lb = best();
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t wb = wave_max_u64(lb);
+      if (lane == 0) sh.top[wave][q] = wb;
+      if (wb == 0) {                         // uniform: no candidate left in this wave
+        for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+        break;
+      }
+      if (lb == wb) {
+#pragma unroll
+        for (int j = 0; j < MPT; ++j)
+          if (kk[j] == wb) kk[j] = 0;
+        lb = best();
+      }
+    }
+  } else {
+    uint64_t lb = rescan_best<GT>(A, t, n, maxd, ~0ull);
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t wb = wave_max_u64(lb);
+      if (lane == 0) sh.top[wave][q] = wb;
+      if (wb == 0) {
+        for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+        break;
+      }
+      if (lb == wb) lb = rescan_best<GT>(A, t, n, maxd, wb);
+    }
+  }
+}
+
+// Phase boundary: a barrier, then the member count and overflow flag every thread sees, then a
+// second barrier.  Reading them after a single barrier races with the next phase's inserts by
+// faster waves: a late wave could see an overflow the others missed and leave alone, and the
+// rest would walk a member list longer than the table's limit.
+__device__ __forceinline__ bool phase_sync(const Shared& sh, uint32_t& cnt) {
+  __syncthreads();
+  cnt = sh.count;
+  const bool ovf = sh.ovf != 0;
+  __syncthreads();
+  return ovf;
+}
+
+// One column end to end.  Returns false (uniformly) if the table overflowed.
+template <bool GT>
+__device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b) {
+  const uint32_t tid = threadIdx.x;
+  const int hops = A.hops;
+  Work work;
+  // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
+  // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
+  int slot = 0;
+  auto stamp = [&]() {
+    if (A.prof && tid == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
+    ++slot;
+  };
+  auto wstamp = [&]() {
+    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
+  };
+  stamp();
+  // seeds: insert (s = -inf), max-combine duplicates (fmaxf, like the dense plan's seed prep),
+  // then one entry per vertex claims it and records (slot, s0) for the per-hop seed add
+  const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_insert<GT>(t, A.seed_vert[i]);
+    if (q >= 0) {
+      t.s[q] = -INFINITY;               // every writer writes the same
+      t.fl[q] = FL_SEED;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_find<GT>(t, A.seed_vert[i]);
+    if (q < 0) continue;
+    unsigned int* sp = reinterpret_cast<unsigned int*>(&t.s[q]);
+    unsigned int old = *sp;
+    for (;;) {
+      const float m = fmaxf(__uint_as_float(old), A.seed_val[i]);
+      if (__float_as_uint(m) == old) break;
+      const unsigned int got = atomicCAS(sp, old, __float_as_uint(m));
+      if (got == old) break;
+      old = got;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = sb + tid; i < se; i += FT) {
+    const int q = tab_find<GT>(t, A.seed_vert[i]);
+    uint2 r = make_uint2(NO_NODE, 0u);
+    if (q >= 0) {
+      const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
+      const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
+                                    (uint32_t)FL_CLAIM << sh8);
+      if (!((old >> sh8) & FL_CLAIM)) r = make_uint2((uint32_t)q, __float_as_uint(t.s[q]));
+    }
+    A.seed_rep[i] = r;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t src = A.sources[b];
+    if (src < A.V) {
+      const int q = tab_insert<GT>(t, src);
+      if (q >= 0) t.fl[q] |= 1;
+    }
+  }
+  __syncthreads();
+  // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
+  if (A.hops >= 1 && A.sources[b] < A.V) {
+    const uint32_t src = A.sources[b];
+    const uint32_t e0 = A.row_ptr[src], e1 = A.row_ptr[src + 1];
+    if (tid == 0) {
+      ++work.rows;
+      work.expand += e1 - e0;
+    }
+    for (uint32_t e = e0 + tid; e < e1; e += FT) {
+      const int q = tab_insert<GT>(t, A.cv[e].x);
+      if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
+    }
+  }
+  wstamp();
+  uint32_t cnt;
+  bool ovf = phase_sync(sh, cnt);
+  stamp();
+  if (ovf) return false;
+  // the seeds' neighbours are the members pulled at hop 0
+  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1);
+  wstamp();
+  ovf = phase_sync(sh, cnt);
+  stamp();
+  if (ovf) return false;
+  for (int h = 0; h < hops; ++h) {
+    // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
+    const uint32_t n0 = cnt;
+    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
+    wstamp();
+    ovf = phase_sync(sh, cnt);
+    stamp();
+    if (ovf) return false;
+    // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
+    // (pruned last pull: a non-candidate was not pulled and keeps +0; nothing reads it)
+    const uint32_t n = cnt, bit = 1u << ((uint32_t)h & 1u);
+    const bool prune_now = A.prune && h == hops - 1;
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      if (p >= t.cap) continue;
+      const uint8_t nd = t.need[p], f = t.fl[p];
+      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
+                          (!prune_now || cand_depth(f, hops));
+      t.s[p] = pulled ? t.snew[i] : 0.f;
+      if (nd & bit) t.need[p] = nd & ~bit;
+    }
+    __syncthreads();
+    for (uint32_t i = sb + tid; i < se; i += FT) {
+      const uint2 r = A.seed_rep[i];
+      if (r.x != NO_NODE) t.s[r.x] = t.s[r.x] + __uint_as_float(r.y);
+    }
+    __syncthreads();
+    stamp();
+  }
+  const uint32_t n = cnt;
+  // top-k over the reach set: each wave its own k best, then wave 0 merges the NWAVES lists
+  const int lane = tid & 63, wave = tid >> 6;
+  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1));
+  wstamp();
+  __syncthreads();
+  if (wave == 0) {
+    uint64_t c[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int cc = lane + 64 * y, w = cc / KMAXF, r = cc % KMAXF;
+      c[y] = (w < NWAVES && r < A.k) ? sh.top[w][r] : 0ull;
+    }
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t mine = c[0] > c[1] ? c[0] : c[1];
+      const uint64_t wb = wave_max_u64(mine);
+      if (lane == 0) {
+        float sc;
+        uint32_t v;
+        topk_unkey(wb, sc, v);
+        A.out_ids[(size_t)b * A.k + q] = v;
+        A.out_scores[(size_t)b * A.k + q] = sc;
+      }
+      if (wb != 0) {
+        if (c[0] == wb) c[0] = 0;
+        if (c[1] == wb) c[1] = 0;
+      }
+    }
+  }
+  stamp();
+  // members -> pool (coalesced by member index)
+  if (tid == 0) sh.base = A.pool_cap ? atomicAdd(A.pool_ctr, (unsigned long long)n) : 0ull;
+  {   // work counters: one LDS atomic per wave
+    uint32_t wp = work.pull, we = work.expand, wr = work.rows;
+    for (int o = 32; o > 0; o >>= 1) {
+      wp += __shfl_xor(wp, o);
+      we += __shfl_xor(we, o);
+      wr += __shfl_xor(wr, o);
+    }
+    if (lane == 0) {
+      atomicAdd(&sh.w_pull, wp);
+      atomicAdd(&sh.w_expand, we);
+      atomicAdd(&sh.w_rows, wr);
+    }
+  }
+  __syncthreads();
+  const unsigned long long base = sh.base;
+  const bool keep = A.pool_cap && base + n <= A.pool_cap;
+  if (keep) {
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      A.pool_v[base + i] = t.keys[p];
+      A.pool_s[base + i] = t.s[p];
+      A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
+    }
+  }
+  if (tid == 0) {
+    A.mem_off[b] = base;
+    A.mem_cnt[b] = keep ? n : NO_NODE;
+    atomicAdd(&A.stats[0], (unsigned long long)sh.w_pull);
+    atomicAdd(&A.stats[1], (unsigned long long)sh.w_expand);
+    atomicAdd(&A.stats[2], (unsigned long long)sh.w_rows);
+    atomicAdd(&A.stats[3], (unsigned long long)n);
+  }
+  stamp();
+  return true;
+}
+
+// The LDS table of one workgroup (static shared memory of the kernel that declares it).
+struct LdsTab {
+  uint32_t keys[LCAP];
+  float s[LCAP];
+  uint32_t flw[LCAP / 4];
+  uint32_t needw[LCAP / 4];
+  uint16_t mlist[LLIMIT];
+  uint32_t bloom[BLOOM_WORDS];
+};
+
+// One column in the LDS table: clear, run, and on overflow hand the column on (A.ovf_list).
+__device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < BLOOM_WORDS; i += FT) L.bloom[i] = 0;
+#pragma unroll
+  for (int i = 0; i < LPPT; ++i) {
+    L.keys[tid + i * FT] = EMPTY;
+    L.s[tid + i * FT] = 0.f;
+  }
+  for (uint32_t i = tid; i < LCAP / 4; i += FT) L.flw[i] = 0;
+  for (uint32_t i = tid; i < LCAP / 4; i += FT) L.needw[i] = 0;
+  if (tid == 0) {
+    sh.count = 0;
+    sh.ovf = 0;
+    sh.w_pull = sh.w_expand = sh.w_rows = 0;
+  }
+  __syncthreads();
+  Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
+               L.mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom};
+  if (!run_column<false>(A, t, sh, b) && tid == 0) {
+    const uint32_t i = atomicAdd(A.ovf_n, 1u);
+    if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
+    else A.spill_list[atomicAdd(A.spill_n, 1u)] = (uint32_t)b;
+    atomicAdd(&A.stats[4], 1ull);
+  }
+}
+
+// One workgroup per column, in launch order (A.order).
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
+void frontier_lds_kernel(const FArgs A) {
+  __shared__ LdsTab L;
+  __shared__ Shared sh;
+  const int b = (int)A.order[blockIdx.x];
+  if (threadIdx.x == 0) {       // the seed counters are consumed: leave them zero for the next set
+    A.seed_cnt[b] = 0;
+    A.seed_cnt[A.B + b] = 0;
+  }
+  lds_column(A, b, L, sh);
+}
+
+// Second chance: block i takes entry i of the columns another geometry's LDS kernel handed
+// on (A.retry_list, at most gridDim.x entries kept; blocks past its end leave at once -- no
+// loop, so the code is the same as frontier_lds_kernel's); those that overflow this table too
+// go on to the global-memory variant.
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
+void frontier_lds_retry_kernel(const FArgs A) {
+  __shared__ LdsTab L;
+  __shared__ Shared sh;
+  if (blockIdx.x >= *A.retry_n) return;
+  lds_column(A, (int)A.retry_list[blockIdx.x], L, sh);
+}
+
+// Persistent fallback: each workgroup owns one global table and drains the overflow list.
+__global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
+  __shared__ Shared sh;
+  const uint32_t tid = threadIdx.x;
+  const size_t cap = A.gcap;
+  Tab<true> t{A.gkeys + blockIdx.x * cap, A.gs + blockIdx.x * cap, A.gfl + blockIdx.x * cap,
+              A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
+              A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr};
+  const uint32_t n_items = *A.ovf_n;
+  for (;;) {
+    if (tid == 0) {
+      sh.item = atomicAdd(A.ovf_next, 1u);
+      sh.count = 0;
+      sh.ovf = 0;
+      sh.w_pull = sh.w_expand = sh.w_rows = 0;
+    }
+    __syncthreads();
+    const uint32_t item = sh.item;
+    if (item >= n_items) break;
+    const int b = (int)A.ovf_list[item];
+    if (!run_column<true>(A, t, sh, b)) {   // cannot happen: members <= V
+      for (int q = tid; q < A.k; q += FT) {
+        A.out_ids[(size_t)b * A.k + q] = NO_NODE;
+        A.out_scores[(size_t)b * A.k + q] = -INFINITY;
+      }
+      if (tid == 0) A.mem_cnt[b] = NO_NODE;
+    }
+    __syncthreads();
+    // reset the slots this column used (the table starts clean: memset at creation)
+    const uint32_t n = min(sh.count, A.V);
+    for (uint32_t i = tid; i < n; i += FT) {
+      const uint32_t p = t.mlist[i];
+      if (p >= cap) continue;
+      t.keys[p] = EMPTY;
+      t.s[p] = 0.f;
+      t.fl[p] = 0;
+      t.need[p] = 0;
+    }
+    __syncthreads();
+  }
+}

@@ -503,7 +503,7 @@ class Frontier:
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",
-             "seed_entries")
+             "seed_entries", "corrupt_keys")
 
     def stats(self, stream=None) -> dict:
         """Work counters of the last run (synchronous)."""

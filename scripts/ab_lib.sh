@@ -13,6 +13,6 @@ for P in ${PIPES:-1 2}; do
   for v in base alt; do
     if [ $v = alt ]; then export EGRAPH_LIB=$PWD/$ALT; else unset EGRAPH_LIB; fi
     timeout -k 10 200 python bench.py --pipeline $P --no-cpu-baseline --no-dropin --dense-steps 0 --steps 50 ${BENCH_ARGS:-} > $OUT/$v$P.json 2> $OUT/$v$P.err
-    python -c "import json;d=json.load(open('$OUT/$v$P.json'));r=d['roofline'];print('$v P=$P', round(d['value']), round(d['ms_per_step'],4), round(r['avg_launch_ms'],4), round(r['frac'],3), r.get('traffic'))"
+    python -c "import json;d=json.load(open('$OUT/$v$P.json'));r=d['roofline'];w=d.get('frontier_work',{});print('$v P=$P', round(d['value']), round(d['ms_per_step'],4), round(r['avg_launch_ms'],4), round(r['frac'],3), r.get('traffic'), 'members', w.get('members'), 'ovf', w.get('overflowed'))"
   done
 done

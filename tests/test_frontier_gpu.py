@@ -55,6 +55,7 @@ def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, sc
     e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)
     np.testing.assert_array_equal(got_ids, e_ids)
     np.testing.assert_array_equal(got_sc, e_sc)
+    assert fr.stats()["corrupt_keys"] == 0
     if scores:
         assert fr.read_scores().cpu().numpy().tobytes() == exp.tobytes()     # bit-identical
         np.testing.assert_array_equal(fr.read_reach().cpu().numpy().view(np.uint64), er)
@@ -134,6 +135,19 @@ def test_frontier_overflow_fallback_mixed():
     st = fr.stats()
     assert st["overflowed"] >= 1             # the hub columns went through the fallback
     assert st["overflowed"] < len(src)       # the ring columns did not
+
+
+@pytest.mark.parametrize("mode", ["pool", "pruned", "narrow_unpruned"])
+def test_frontier_global_table_reuse(mode, monkeypatch):
+    """More overflowing columns than global-variant workgroups (32): each workgroup reuses its
+    table across columns and must leave it clean (wide table with a pool, narrow table pruned,
+    narrow table with pruning switched off)."""
+    if mode == "narrow_unpruned":
+        monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
+    g, sv, sc, ss, src = _hub_world(n_leaves=3000, n_cols=300)   # 150 hub columns: > 128 retries
+    fr = _check(g, sv, sc, ss, src, len(src), k=10, pool_entries=0 if mode == "pool" else -1,
+                scores=mode == "pool")
+    assert fr.stats()["overflowed"] >= 33
 
 
 def test_frontier_edge_inputs():
@@ -265,3 +279,12 @@ def test_graph_service_rank_root_causes():
         assert one == got[3]
     finally:
         GraphService.reset()
+
+
+def test_frontier_narrow_unpruned_world(monkeypatch):
+    """The narrow table with pruning switched off (an A/B knob): many columns overflow into the
+    global-memory variant, results stay exact."""
+    monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
+    g, sv, sc, ss, src = _world(300, seed=61, pods=6000, nodes=100)
+    fr = _check(g, sv, sc, ss, src, 300, pool_entries=-1, scores=False)
+    assert fr.stats()["corrupt_keys"] == 0
