@@ -518,7 +518,7 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
     ap.add_argument("--batch", type=int, default=1024, help="incidents per GPU per step")

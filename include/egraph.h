@@ -278,7 +278,7 @@ int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src
  *                         rows walked (row_ptr pairs), members, columns that overflowed the
  *                         LDS table (redone by the global-memory variant), pool entries
  *                         used, valid seed entries, member keys outside the graph (a
- *                         device-side guard: 0 unless a table is corrupt).
+ *                         device-side guard of -DEGR_FR_GUARDS builds; 0 otherwise).
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.

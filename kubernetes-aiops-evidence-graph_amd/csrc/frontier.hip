@@ -97,7 +97,7 @@ struct FArgs {
   unsigned long long* prof;     // [B][PROF_SLOTS] wall-clock stamps per phase, or nullptr
   // [0] CSR entries gathered by pulls (col + val), [1] entries read by expansions (col),
   // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed, [5] member keys
-  // outside the graph (a guard: 0 unless a table is corrupt)
+  // outside the graph (a guard compiled in with -DEGR_FR_GUARDS; 0 otherwise)
   unsigned long long* stats;
 };
 
@@ -340,7 +340,7 @@ struct egr_frontier {
   bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
 };
 
-// wide-table second chances per narrow run (pruned runs on C3 hand on none)
+// wide-table second chances per narrow run ($EGRAPH_FRONTIER_WIDE_RETRY)
 constexpr int RETRY_BLOCKS = 128;
 
 // stamps per profiling slot: the post-barrier stamp + one per wave of the kernel's workgroup
@@ -552,15 +552,17 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.prof = f->prof;
   if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
   a.stats = f->ctr + 1;
-  // narrow: its first RETRY_BLOCKS overflowing columns get a second chance in the wide LDS
-  // table (a small grid: blocks past the handed-on count leave at once), the rest and those
-  // that overflow again go to the global-memory variant
+  // narrow: its overflowing columns go to the global-memory variant.  With
+  // $EGRAPH_FRONTIER_WIDE_RETRY the first RETRY_BLOCKS of them get a second chance in the wide
+  // LDS table first (a small grid: blocks past the handed-on count leave at once).  Off by
+  // default: pruned C3 / C4 columns do not overflow, and the retry's 78-KB workgroups wait for
+  // LDS held by the other batch in flight (~30 us per run in rocprof, profiles/r01_kernel_stats_v9.csv).
   if (f->narrow) {
     FArgs an = a;
     an.ovf_n = f->ovf + 2;
     an.ovf_list = f->ovf + 4 + f->B;
-    an.ovf_cap = getenv("EGRAPH_FRONTIER_NO_RETRY") ? 0u   // (A/B and fallback tests)
-                 : (uint32_t)std::min(f->B, RETRY_BLOCKS);   // the rest straight to the fallback
+    an.ovf_cap = getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? (uint32_t)std::min(f->B, RETRY_BLOCKS)
+                                                      : 0u;
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
     hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
     EGR_CHECK_LAUNCH();

@@ -77,7 +77,7 @@ __device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // BLOOM_LOG bits
 // slot of v, inserting it if absent (-1: table full)
 template <bool GT>
 __device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
-  const uint32_t nb = t.cap / 4;
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
     uint4 kk = read_bucket(t.keys, bk);
@@ -115,7 +115,7 @@ __device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
     const uint32_t h = bloom_hash(v);
     if (!((t.bloom[h >> 5] >> (h & 31u)) & 1u)) return -1;
   }
-  const uint32_t nb = t.cap / 4;
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
     const int r = bucket_match(read_bucket(t.keys, bk), v, bk);
@@ -156,7 +156,7 @@ struct Ticker {
 template <bool GT, int NQ>
 __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
                                            int (&q)[NQ]) {
-  const uint32_t nb = t.cap / 4;
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk[NQ];
   uint32_t pend = 0;
 #pragma unroll
@@ -321,10 +321,12 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     uint32_t v = 0;
     if (c.i < n) {
       uint32_t p = t.mlist[c.i];
+#ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
       if (p >= t.cap) {           // guard (see below)
         atomicAdd(&A.stats[5], 1ull);
         p = 0;
       }
+#endif
       v = t.keys[p];
       const uint8_t f = t.fl[p];
       if (reach_lvl && (f & FL_DEPTH) == reach_fl) c.kind |= K_REACH;
@@ -335,10 +337,12 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
           c.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
       }
     }
+#ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
     if (c.kind && v >= A.V) {   // a member key outside the graph: table corruption, counted
       atomicAdd(&A.stats[5], 1ull);
       c.kind = 0;
     }
+#endif
     if (c.kind) {
       c.e0 = A.row_ptr[v];
       c.e1 = A.row_ptr[v + 1];

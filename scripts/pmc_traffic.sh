@@ -18,3 +18,4 @@ run write WRITE_SIZE
 run rdreq TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
 python3 scripts/pmc_summary.py $OUT frontier_lds_kernel "hop_kernel<32, false>" reach_kernel
 python3 scripts/pmc_traffic.py $OUT
+cp profiles/pmc_frontier.json profiles/pmc_hop.json $OUT/

@@ -137,13 +137,16 @@ def test_frontier_overflow_fallback_mixed():
     assert st["overflowed"] < len(src)       # the ring columns did not
 
 
-@pytest.mark.parametrize("mode", ["pool", "pruned", "narrow_unpruned"])
+@pytest.mark.parametrize("mode", ["pool", "pruned", "pruned_wide_retry", "narrow_unpruned"])
 def test_frontier_global_table_reuse(mode, monkeypatch):
     """More overflowing columns than global-variant workgroups (32): each workgroup reuses its
     table across columns and must leave it clean (wide table with a pool, narrow table pruned,
-    narrow table with pruning switched off)."""
+    the same with the wide-table retry (128 of the 150 hub columns; the rest go straight to the
+    fallback), narrow table with pruning switched off)."""
     if mode == "narrow_unpruned":
         monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
+    if mode == "pruned_wide_retry":
+        monkeypatch.setenv("EGRAPH_FRONTIER_WIDE_RETRY", "1")
     g, sv, sc, ss, src = _hub_world(n_leaves=3000, n_cols=300)   # 150 hub columns: > 128 retries
     fr = _check(g, sv, sc, ss, src, len(src), k=10, pool_entries=0 if mode == "pool" else -1,
                 scores=mode == "pool")

@@ -20,12 +20,10 @@ def test_fallback_large_star():
 
 
 def test_fallback_c3_columns(monkeypatch):
-    """Narrow table, pruning and the wide retry switched off: most C3 columns overflow into
-    the fallback."""
+    """Narrow table with pruning switched off: most C3 columns overflow into the fallback."""
     from egraph import synth
     from egraph.graph import EvidenceGraph
     monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
-    monkeypatch.setenv("EGRAPH_FRONTIER_NO_RETRY", "1")
     B = 48
     c = synth.build_cluster(synth.CONFIGS["C3"])
     cases = synth.make_incidents(c, B, seed=1000)
