@@ -140,6 +140,25 @@ namespace fr_narrow {
 #undef FR_WAVES_PER_EU
 }  // namespace fr_narrow
 
+// The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
+// every narrow run and nearly always finds no overflowing column; a one-wave workgroup is
+// dispatched as soon as a single SIMD has room, instead of waiting behind the other batch in
+// flight for a CU to drain (scripts/ab_global.sh).  Only frontier_global_kernel is launched
+// from this instantiation.
+namespace fr_fallback {
+#define FR_FT 64
+#define FR_LCAP 256
+#define FR_LLIMIT 192
+#define FR_BLOOM_LOG 10
+#define FR_WAVES_PER_EU 4
+#include "frontier_body.h"
+#undef FR_FT
+#undef FR_LCAP
+#undef FR_LLIMIT
+#undef FR_BLOOM_LOG
+#undef FR_WAVES_PER_EU
+}  // namespace fr_fallback
+
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
 __global__ void scatter_scores_kernel(const uint32_t* __restrict__ pool_v,
                                       const float* __restrict__ pool_s,
@@ -230,29 +249,35 @@ __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_
 
 // ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]); order = the
 // columns by descending cost bucket (a log-scale counting sort: longest-processing-time-first
-// launch order, so the costly columns do not start in the last round).  One block of 1024
-// threads, each owning a contiguous run of columns.
+// launch order, so the costly columns do not start in the last round).  One block of SCAN_T
+// threads, each owning a contiguous run of columns.  SCAN_T is 256 (one wave per SIMD), not
+// 1024: the block is launched while the other batch in flight holds the CUs, and a small block
+// is dispatched as soon as one workgroup of that batch finishes.
 constexpr int COST_BUCKETS = 64;
+#ifndef EGR_SCAN_T          // build-time knob for A/B builds
+#define EGR_SCAN_T 256
+#endif
+constexpr int SCAN_T = EGR_SCAN_T;
 
 __device__ __forceinline__ int cost_bucket(uint32_t cost) {
   const int lg = (int)(__log2f((float)cost + 1.0f) * 3.0f);
   return COST_BUCKETS - 1 - min(COST_BUCKETS - 1, lg);
 }
 
-__global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
+__global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
                                                          const uint32_t* __restrict__ cost,
                                                          uint32_t* order, unsigned long long* ctr,
                                                          uint32_t* ovf) {
-  __shared__ uint32_t part[1024];
+  __shared__ uint32_t part[SCAN_T];
   __shared__ uint32_t hist[COST_BUCKETS];
   const int tid = threadIdx.x;
-  const int per = (B + 1023) / 1024;
+  const int per = (B + SCAN_T - 1) / SCAN_T;
   const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
   uint32_t sum = 0;
   for (int c = c0; c < c1; ++c) sum += cnt[c];
   part[tid] = sum;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan of the run sums
+  for (int off = 1; off < SCAN_T; off <<= 1) {   // Hillis-Steele inclusive scan of the run sums
     const uint32_t x = tid >= off ? part[tid - off] : 0u;
     __syncthreads();
     part[tid] += x;
@@ -265,7 +290,7 @@ __global__ __launch_bounds__(1024) void seed_scan_kernel(uint32_t* cnt, int B, u
     cnt[c] = run;
     run += x;
   }
-  if (tid == 1023) ptr[B] = part[1023];
+  if (tid == SCAN_T - 1) ptr[B] = part[SCAN_T - 1];
   if (tid < 7) ctr[tid] = 0;      // the next run's pool / stats counters and overflow list
   if (tid < 4) ovf[tid] = 0;
   // launch order
@@ -478,7 +503,7 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
                        n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B);
     EGR_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(1024), 0, st, f->seed_cnt, f->B, f->seed_ptr,
+  hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, f->seed_cnt, f->B, f->seed_ptr,
                      f->seed_cnt + f->B, f->order, f->ctr, f->ovf);
   EGR_CHECK_LAUNCH();
   if (n_seeds > 0) {
@@ -573,7 +598,15 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
     hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
   }
   EGR_CHECK_LAUNCH();
-  hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
+  // the overflow fallback in its one-wave geometry; $EGRAPH_FRONTIER_AB_GLOBAL=0 / 1 launches the
+  // wide (512-thread) / narrow (256-thread) instantiation instead (scripts/ab_global.sh)
+  static const int fb_geom = getenv("EGRAPH_FRONTIER_AB_GLOBAL") ? atoi(getenv("EGRAPH_FRONTIER_AB_GLOBAL")) : 3;
+  if (fb_geom == 0)
+    hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
+  else if (fb_geom == 1)
+    hipLaunchKernelGGL(fr_narrow::frontier_global_kernel, dim3(f->nbig), dim3(fr_narrow::FT), 0, st, a);
+  else
+    hipLaunchKernelGGL(fr_fallback::frontier_global_kernel, dim3(f->nbig), dim3(fr_fallback::FT), 0, st, a);
   EGR_CHECK_LAUNCH();
   f->ran = true;
   f->ctr_clean = false;
