@@ -10,9 +10,10 @@ resident in HBM (encoded evidence rows, seed triples, incident vertices):
     egr_rules_eval  ->  egr_plan_set_seeds  ->  egr_plan_set_sources
     ->  3 x (egr_plan_hop + egr_plan_reach_hop)  ->  egr_plan_candidates  ->  egr_plan_topk.
 Both engines produce bit-identical scores, reach sets and top-k (tests/test_frontier_gpu.py).
-Frontier batches are pipelined (--pipeline 2, default): two independent frontier + rules states
-on their own streams take alternate batches, so the tail of one batch's frontier launch (its
-last, unevenly long columns) overlaps the start of the next.  Every batch is computed in full;
+Frontier batches are pipelined (--pipeline 3, default): three independent frontier + rules
+states on their own streams take batches in turn, so the tail of one batch's frontier launch
+(its last, unevenly long columns) overlaps the start of the next (P = 2 / 3 / 4: 0.103 / 0.080 /
+0.108 ms per step, profiles/r01_ab_pipe.txt).  Every batch is computed in full;
 `value` = batches x B / wall time of the timed region.
 The default run also times a few dense steps after the timed region and reports them under
 "dense_engine" (with the dense hop kernel's HBM roofline) for comparison.
@@ -525,7 +526,7 @@ def main():
     ap.add_argument("--hops", type=int, default=3)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=3,
                     help="frontier batches in flight (independent states on their own streams)")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the end-to-end drop-in RulesEngine measurement")
