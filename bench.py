@@ -109,6 +109,9 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
                 evidence=evidence)
 
 
+_GRAPH_NAME = {"C2": "10k-pod", "C3": "100k-pod", "C4": "400k-pod (1M-vertex)"}
+
+
 def step_frontier(ctx, hops: int, ev=None):
     """One pass; `ev` (EventPool) times the frontier run on its stream.  The rules launch does
     not depend on the graph stages (nor they on it), so it goes to a second stream: its waves
@@ -627,7 +630,7 @@ def main():
         # the engine actually read
         "edges_per_sec": world * args.hops * nnz * B / (ms * 1e-3),
         "config": {
-            "workload": f"{args.config}: 100k-pod multi-namespace graph, full rule set + "
+            "workload": f"{args.config}: {_GRAPH_NAME.get(args.config, args.config)} multi-namespace graph, full rule set + "
                         f"{args.hops}-hop typed propagation + reach + top-{args.k}, "
                         f"{B} incidents per GPU per step",
             "engine": args.engine,
