@@ -64,6 +64,8 @@ struct FArgs {
   uint2* seed_rep;             // per seed entry: (slot, s0 bits) of a vertex's representative
   const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
   const uint32_t* order;       // [B] launch order: workgroup i runs column order[i] (costly first)
+  uint32_t* xq;                // xcd: [0..8] region queue offsets into order, [9..16] queue heads
+  int xcd;                     // workgroups take their column from their XCD's region queue
   uint32_t* seed_cnt;          // [2B] seed counters / costs, zeroed per column once consumed
   uint32_t* out_ids;           // [B*k]
   float* out_scores;
@@ -223,7 +225,7 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 // atomic per run of equal columns (a segmented sum over an inclusive wave scan).
 __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                   int64_t n, uint32_t V, int B, const uint32_t* __restrict__ row_ptr,
-                                  uint32_t* cnt, uint32_t* cost) {
+                                  uint32_t* cnt, uint32_t* cost, uint32_t* cmax) {
   const SeedRun r = seed_run(sv, sc, n, V, B);
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -244,6 +246,7 @@ __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_
   if (r.ok && r.rank == 0) {
     atomicAdd(&cnt[r.col], r.len);
     atomicAdd(&cost[r.col], hi - (r.leader > 0 ? lo : 0u));
+    if (cmax) atomicMax(&cmax[r.col], sv[i]);   // the column's graph region (xcd launch order)
   }
 }
 
@@ -264,12 +267,33 @@ __device__ __forceinline__ int cost_bucket(uint32_t cost) {
   return COST_BUCKETS - 1 - min(COST_BUCKETS - 1, lg);
 }
 
+// XCD-aware launch (EGRAPH_FRONTIER_XCD=1): the columns are split into XCD_REGIONS queues by
+// the graph region of their largest seed vertex (vertices are laid out namespace by namespace,
+// so a region is a run of namespaces), each queue in cost order; a workgroup takes the next
+// column of its own XCD's queue (HW_REG_XCC_ID), then of the others.  The CSR rows a column
+// reads then mostly stay in one XCD's L2.  Placement changes only speed, never results.
+constexpr int XCD_REGIONS = 8;
+constexpr int NBINS = XCD_REGIONS * COST_BUCKETS;
+static_assert(NBINS % SCAN_T == 0, "seed scan bins");
+
+__device__ __forceinline__ int order_bin(uint32_t cost, const uint32_t* cmax, int c, uint32_t V,
+                                         int xcd) {
+  const int r = xcd ? (int)min((uint64_t)XCD_REGIONS - 1, (uint64_t)cmax[c] * XCD_REGIONS / V) : 0;
+  return r * COST_BUCKETS + cost_bucket(cost);
+}
+
+static bool xcd_queues() {
+  static const bool on = getenv("EGRAPH_FRONTIER_XCD") && atoi(getenv("EGRAPH_FRONTIER_XCD")) != 0;
+  return on;
+}
+
 __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
                                                          const uint32_t* __restrict__ cost,
                                                          uint32_t* order, unsigned long long* ctr,
-                                                         uint32_t* ovf) {
+                                                         uint32_t* ovf, const uint32_t* cmax,
+                                                         uint32_t V, int xcd, uint32_t* xq) {
   __shared__ uint32_t part[SCAN_T];
-  __shared__ uint32_t hist[COST_BUCKETS];
+  __shared__ uint32_t hist[NBINS];
   const int tid = threadIdx.x;
   const int per = (B + SCAN_T - 1) / SCAN_T;
   const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
@@ -293,21 +317,35 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
   if (tid == SCAN_T - 1) ptr[B] = part[SCAN_T - 1];
   if (tid < 7) ctr[tid] = 0;      // the next run's pool / stats counters and overflow list
   if (tid < 4) ovf[tid] = 0;
-  // launch order
-  if (tid < COST_BUCKETS) hist[tid] = 0;
+  // launch order: by (graph region, cost bucket); one region only unless xcd
+  for (int i = tid; i < NBINS; i += SCAN_T) hist[i] = 0;
   __syncthreads();
-  for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
+  for (int c = c0; c < c1; ++c) atomicAdd(&hist[order_bin(cost[c], cmax, c, V, xcd)], 1u);
   __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int i = 0; i < COST_BUCKETS; ++i) {
-      const uint32_t x = hist[i];
-      hist[i] = acc;
-      acc += x;
-    }
+  // exclusive scan of the NBINS bins: each thread owns BPT consecutive bins
+  constexpr int BPT = NBINS / SCAN_T;
+  uint32_t own = 0;
+  for (int j = 0; j < BPT; ++j) own += hist[tid * BPT + j];
+  __syncthreads();
+  part[tid] = own;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    const uint32_t x = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += x;
+    __syncthreads();
+  }
+  uint32_t acc = tid ? part[tid - 1] : 0u;
+  for (int j = 0; j < BPT; ++j) {
+    const uint32_t x = hist[tid * BPT + j];
+    hist[tid * BPT + j] = acc;
+    acc += x;
   }
   __syncthreads();
-  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
+  if (xcd && tid <= XCD_REGIONS) xq[tid] = tid < XCD_REGIONS ? hist[tid * COST_BUCKETS] : (uint32_t)B;
+  if (xcd && tid < XCD_REGIONS) xq[XCD_REGIONS + 1 + tid] = 0;
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[order_bin(cost[c], cmax, c, V, xcd)], 1u)] = (uint32_t)c;
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
@@ -335,7 +373,7 @@ struct egr_frontier {
   uint32_t gcap = 0;
   int64_t n_seeds = 0;
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
-  uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; then costs
+  uint32_t* seed_cnt = nullptr;   // [3B+24]: per-column counts, then scatter cursors; costs; max seed vertex; xq
   uint32_t* order = nullptr;      // [B] launch order of the columns
   uint32_t* ident = nullptr;      // [B] 0..B-1 ($EGRAPH_FRONTIER_NO_ORDER: launch in column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
@@ -405,7 +443,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
                                  : (unsigned long long)n_cols * 4096ull + 4ull * V;
   int rc = EGR_OK;
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
-  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
+  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 3 * (size_t)n_cols + 24)) ||
       (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
@@ -430,7 +468,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gfl, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
-      hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
+      hipMemset(f->seed_cnt, 0, (size_t)n_cols * 12) != hipSuccess ||
       hipMemset(f->ctr, 0, 7 * 8) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
@@ -496,15 +534,17 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   hipStream_t st = (hipStream_t)stream;
   // counting sort by column: count, one-block exclusive scan, scatter (order within a column
   // is arbitrary; the kernel max-combines duplicates).  Invalid triples are dropped.
-  if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 8, st));
+  if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 12, st));
   const unsigned g = (unsigned)((std::max<int64_t>(n_seeds, 1) + 255) / 256);
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_count_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
-                       n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B);
+                       n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B,
+                       xcd_queues() ? f->seed_cnt + 2 * f->B : nullptr);
     EGR_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, f->seed_cnt, f->B, f->seed_ptr,
-                     f->seed_cnt + f->B, f->order, f->ctr, f->ovf);
+                     f->seed_cnt + f->B, f->order, f->ctr, f->ovf, f->seed_cnt + 2 * f->B, V,
+                     xcd_queues(), f->seed_cnt + 3 * f->B);
   EGR_CHECK_LAUNCH();
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_scatter_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
@@ -547,6 +587,8 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.seed_rep = f->seed_rep;
   a.sources = source_vertex;
   a.order = getenv("EGRAPH_FRONTIER_NO_ORDER") ? f->ident : f->order;
+  a.xcd = (xcd_queues() && a.order == f->order) ? 1 : 0;
+  a.xq = f->seed_cnt + 3 * f->B;
   a.seed_cnt = f->seed_cnt;
   a.out_ids = out_ids;
   a.out_scores = out_scores;

@@ -763,10 +763,31 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER
 void frontier_lds_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
-  const int b = (int)A.order[blockIdx.x];
+  int b;
+  if (A.xcd) {                  // the next column of this XCD's region queue, else of the next
+    __shared__ int pick;
+    if (threadIdx.x == 0) {
+      const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;   // HW_REG_XCC_ID
+      int got = -1;
+      for (uint32_t j = 0; j < 8u && got < 0; ++j) {
+        const uint32_t q = (x + j) & 7u;
+        const uint32_t len = A.xq[q + 1] - A.xq[q];
+        if (len == 0) continue;
+        const uint32_t i = atomicAdd(&A.xq[9 + q], 1u);
+        if (i < len) got = (int)A.order[A.xq[q] + i];
+      }
+      pick = got;               // B workgroups, B queued columns: every workgroup gets one
+    }
+    __syncthreads();
+    b = pick;
+    if (b < 0) return;
+  } else {
+    b = (int)A.order[blockIdx.x];
+  }
   if (threadIdx.x == 0) {       // the seed counters are consumed: leave them zero for the next set
     A.seed_cnt[b] = 0;
     A.seed_cnt[A.B + b] = 0;
+    A.seed_cnt[2 * A.B + b] = 0;
   }
   lds_column(A, b, L, sh);
 }
@@ -792,6 +813,7 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
               A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
               A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr};
   const uint32_t n_items = *A.ovf_n;
+  if (A.xcd && blockIdx.x == 0 && tid < 8) A.xq[9 + tid] = 0;   // queue heads, for a rerun
   for (;;) {
     if (tid == 0) {
       sh.item = atomicAdd(A.ovf_next, 1u);
