@@ -278,7 +278,8 @@ int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src
  *                         rows walked (row_ptr pairs), members, columns that overflowed the
  *                         LDS table (redone by the global-memory variant), pool entries
  *                         used, valid seed entries, member keys outside the graph (a
- *                         device-side guard of -DEGR_FR_GUARDS builds; 0 otherwise).
+ *                         device-side guard of -DEGR_FR_GUARDS builds; -1 = not counted:
+ *                         release builds compile the guard out).
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.
@@ -315,7 +316,9 @@ int egr_frontier_members(const egr_frontier* f, int32_t col, uint32_t* out_verte
  *                       The edges must be absent from the snapshot and distinct -- the host
  *                       MERGE (egr_graph_merge_edges) guarantees it; a violation or an
  *                       out-of-range id returns EGR_EINVAL with the snapshot unchanged.
- *                       Synchronous on `stream`.  Plans created before an update return
+ *                       Synchronous on `stream`, and it first drains the whole device: the
+ *                       merge writes into the previous version's arrays, which kernels
+ *                       enqueued earlier on other streams may still read.  Plans created before an update return
  *                       EGR_ESTATE afterwards; a frontier keeps working while the snapshot
  *                       stays within the vertex headroom it was sized with (V + V/4 + 4096).
  *                       Replaces the per-item MERGE round trips of neo4j.py:95-167 for the

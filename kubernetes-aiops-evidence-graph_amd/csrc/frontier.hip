@@ -668,7 +668,11 @@ int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
   for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
   out8[5] = (int64_t)h[0];
   out8[6] = (int64_t)nu;
+#ifdef EGR_FR_GUARDS
   out8[7] = (int64_t)h[6];
+#else
+  out8[7] = -1;   // the corrupt-key guard is compiled only into debug builds: not counted
+#endif
   return EGR_OK;
 }
 

@@ -265,6 +265,10 @@ int egr_snapshot_update(egr_snapshot* s, const uint8_t* new_vlabel, int64_t n_ne
   if (n_new == 0 && n_edges == 0) return EGR_OK;
   DeviceGuard guard(s->device);
   hipStream_t st = (hipStream_t)stream;
+  // The spare set is the previous version's arrays: a plan or frontier kernel enqueued earlier
+  // on ANOTHER stream may still read them.  Drain the device before the merge (or ensure's
+  // reallocation) writes into them; updates are per alert-storm tick, not per batch.
+  EGR_HIP(hipDeviceSynchronize());
   if (!s->upd) s->upd = new SnapUpdate();
   SnapUpdate* u = s->upd;
   EGR_TRY(ensure(s, u, Vn, NEn, 2 * n_edges));

@@ -77,15 +77,45 @@ def _fp_arg(fp: torch.Tensor, dev: torch.device) -> torch.Tensor:
 
 class DedupTable:
     """The TTL table on one GPU.  Times are integer milliseconds; a key is live while
-    now_ms < expiry (Redis EX).  `capacity` = live keys it holds at <= 1/2 load."""
+    now_ms < expiry (Redis EX).  `capacity` = live keys it holds at <= 1/2 load.
 
-    def __init__(self, capacity: int = 1 << 20, device=None):
+    Expired and removed keys keep their slot (probe chains stay intact) until a compaction
+    rebuilds the table from the live keys.  With `auto_compact` (default) the table compacts
+    itself before an ingest / register could push the used slots past COMPACT_LOAD of the slot
+    count, growing when the live keys plus the batch need it -- so, like Redis expiring keys, a
+    long-running service never fills it.  Without it a full table raises MemoryError."""
+
+    COMPACT_LOAD = 0.75
+
+    def __init__(self, capacity: int = 1 << 20, device=None, auto_compact: bool = True):
         self.dev = require_device(device)
         h = C.c_void_p()
         L.check(L.lib.egr_dedup_create(self.dev.index, int(capacity), C.byref(h)), "egr_dedup_create")
         self._h = h
+        self.capacity = int(capacity)
+        self.auto_compact = auto_compact
         self.next_id = 0                 # the next incident handle ingest() hands out
+        self.compactions = 0
         self._counts = torch.zeros(2, dtype=torch.int32, device=self.dev)
+        self._slots = self.stats(0)["slots"]
+        self._used_bound = 0             # >= slots holding a key (each batch adds <= its size)
+
+    def _make_room(self, n: int, now_ms: int) -> None:
+        """Before a batch that may occupy up to n fresh slots: compact (and grow) if the used
+        slots could pass COMPACT_LOAD.  The exact count is read only when the bound says so."""
+        if not self.auto_compact or self._used_bound + n <= self.COMPACT_LOAD * self._slots:
+            return
+        st = self.stats(now_ms)
+        self._used_bound = st["used_slots"]
+        if self._used_bound + n <= self.COMPACT_LOAD * self._slots:
+            return
+        need = st["live"] + n
+        cap = self.capacity                   # the rebuilt table has >= 2 * cap slots
+        while need > self.COMPACT_LOAD * 2 * cap:
+            cap *= 2
+        self.compact(now_ms, cap)
+        self.capacity = cap
+        self.compactions += 1
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -101,6 +131,8 @@ class DedupTable:
         incident int64 [n] handles, n_new) -- device tensors, n_new an int (synchronises)."""
         fp = _fp_arg(fp, self.dev)
         n = fp.shape[0]
+        self._make_room(n, now_ms)
+        self._used_bound += n
         dup = torch.empty(max(n, 1), dtype=torch.uint8, device=self.dev)[:n]
         inc = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)[:n]
         L.check(L.lib.egr_dedup_ingest(self._h, L.ptr(fp), n, int(now_ms), int(ttl_ms),
@@ -129,6 +161,8 @@ class DedupTable:
         if incident.numel() != n:
             raise ValueError("one incident handle per fingerprint")
         inc = incident.to(device=self.dev, dtype=torch.int64).to(torch.int32).contiguous()
+        self._make_room(n, now_ms)
+        self._used_bound += n
         L.check(L.lib.egr_dedup_register(self._h, L.ptr(fp), n, int(now_ms), int(ttl_ms), L.ptr(inc),
                                          L.ptr(self._counts), self._st(stream)), "egr_dedup_register")
         if int(self._counts[0].item()):
@@ -154,4 +188,8 @@ class DedupTable:
         return {"used_slots": out[0], "live": out[1], "slots": out[2]}
 
     def compact(self, now_ms: int, capacity: int = 0) -> None:
+        """Rebuild from the live keys (expired / removed ones drop out), with room for at
+        least max(capacity, live) keys at <= 1/2 load."""
         L.check(L.lib.egr_dedup_compact(self._h, int(now_ms), int(capacity)), "egr_dedup_compact")
+        st = self.stats(now_ms)
+        self._slots, self._used_bound = st["slots"], st["used_slots"]

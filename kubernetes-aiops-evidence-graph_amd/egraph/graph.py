@@ -30,6 +30,8 @@ DEFAULT_WEIGHTS: dict[str, tuple[float, float]] = {
     "HAS_EVENT": (0.9, 0.9),
     "HAS_LOG_PATTERN": (0.9, 0.9),
     "HAS_METRIC_ANOMALY": (0.9, 0.9),
+    "OBSERVED_ON": (0.6, 0.6),
+    "AGGREGATES": (0.8, 0.8),
 }
 DEFAULT_OTHER_WEIGHT = (0.5, 0.5)
 
@@ -506,11 +508,15 @@ class Frontier:
              "seed_entries", "corrupt_keys")
 
     def stats(self, stream=None) -> dict:
-        """Work counters of the last run (synchronous)."""
+        """Work counters of the last run (synchronous).  `corrupt_keys` is present only in
+        debug builds (-DEGR_FR_GUARDS), where the kernel checks every member key it walks."""
         out = np.zeros(8, np.int64)
         L.check(L.lib.egr_frontier_stats(self._h, _addr(out), self._st(stream)),
                 "egr_frontier_stats")
-        return dict(zip(self.STATS, out.tolist()))
+        d = dict(zip(self.STATS, out.tolist()))
+        if d["corrupt_keys"] < 0:
+            del d["corrupt_keys"]
+        return d
 
     def phase_times(self, stream=None) -> np.ndarray | None:
         """[B, slots, 1 + waves] s_memrealtime stamps (100 MHz): per phase boundary the stamp

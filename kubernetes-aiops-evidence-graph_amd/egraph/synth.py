@@ -42,6 +42,11 @@ class ClusterConfig:
     attach_fraction: float = 0.2      # pods with an Event / LogPattern / MetricAnomaly vertex
     unhealthy_node_fraction: float = 0.05
     seed: int = 20260821
+    # denser telemetry links (C4's ~10M CSR entries): every Event /
+    # LogPattern / MetricAnomaly vertex is also OBSERVED_ON its pod's Node and AGGREGATED by its
+    # pod's Deployment, a Service SELECTS each pod of its deployments, and the sibling pods of a
+    # deployment share its LogPattern vertices (HAS_LOG_PATTERN)
+    dense_links: bool = False
 
 
 CONFIGS = {
@@ -49,7 +54,7 @@ CONFIGS = {
     "C3": ClusterConfig(pods=100_000, namespaces=100, nodes=2_000, deployments=10_000,
                         services=10_000, attach_fraction=0.35, seed=20260823),
     "C4": ClusterConfig(pods=400_000, namespaces=400, nodes=8_000, deployments=40_000,
-                        services=40_000, attach_fraction=0.5, seed=20260824),
+                        services=40_000, attach_fraction=0.5, seed=20260824, dense_links=True),
 }
 
 
@@ -68,6 +73,11 @@ class Cluster:
     pod_node: dict = field(default_factory=dict)       # pod name -> node name
     unhealthy_nodes: set = field(default_factory=set)
     attachments: dict = field(default_factory=dict)    # pod name -> [(label, vertex id)]
+    # dense_links: extra edges by vertex position in `ids` (EvidenceGraph.add_edges_indexed)
+    extra_src: np.ndarray | None = None
+    extra_dst: np.ndarray | None = None
+    extra_type: np.ndarray | None = None
+    EXTRA_TYPES = ("OBSERVED_ON", "AGGREGATES", "SELECTS", "HAS_LOG_PATTERN")
 
     def add_vertex(self, vid: str, label: str) -> None:
         self.ids.append(vid)
@@ -88,6 +98,9 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
     c.unhealthy_nodes = {n for n, b in zip(node_names, bad) if b}
     for n in node_names:
         c.add_vertex(f"node:{n}", "Node")
+    dense = cfg.dense_links
+    att_rows: list = []        # dense_links: (attachment, pod, node, deployment, kind) positions
+    pod_rows: list = []        # dense_links: (pod, service, deployment) positions
     c.deploy_ns = np.sort(rng.integers(0, cfg.namespaces, cfg.deployments))
     svc_ns = np.sort(rng.integers(0, cfg.namespaces, cfg.services))
     pods_per = np.full(cfg.deployments, cfg.pods // cfg.deployments)
@@ -107,6 +120,7 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
             dname = f"app-{d}"
             c.deploy_name.append(dname)
             did = f"deployment:{ns}:{dname}"
+            d_pos = len(c.ids)
             c.add_vertex(did, "Deployment")
             sv = int(svc_of_deploy[d])
             c.add_edge(f"service:{c.ns_names[svc_ns[sv]]}:svc-{sv}", did, "SELECTS")
@@ -115,8 +129,11 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
                 pname = f"{dname}-{j:02d}-{p:06x}"
                 pid = f"pod:{ns}:{pname}"
                 node = node_names[pod_nodes[p]]
+                p_pos = len(c.ids)
                 c.add_vertex(pid, "Pod")
                 c.add_edge(did, pid, "OWNS")
+                if dense:
+                    pod_rows.append((p_pos, int(svc_of_deploy[d]), d_pos))
                 c.add_edge(pid, f"node:{node}", "SCHEDULED_ON")
                 c.pod_node[pname] = node
                 att = []
@@ -125,6 +142,8 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
                                                      ("MetricAnomaly", "HAS_METRIC_ANOMALY", "metric"))):
                     if attach[p, k]:
                         vid = f"{pre}:{ns}:{pname}"
+                        if dense:
+                            att_rows.append((len(c.ids), p_pos, int(pod_nodes[p]), d_pos, k))
                         c.add_vertex(vid, lab)
                         c.add_edge(pid, vid, et)
                         att.append((lab, vid))
@@ -134,6 +153,9 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
                 p += 1
             c.deploy_pods.append(pods)
             d += 1
+    if dense:
+        _dense_links(c, np.array(att_rows, np.int64).reshape(-1, 5),
+                     np.array(pod_rows, np.int64).reshape(-1, 3), svc_ns, cfg)
     # service call graph: mostly within the namespace
     for sv in range(cfg.services):
         for _ in range(cfg.calls_per_service):
@@ -147,6 +169,49 @@ def build_cluster(cfg: ClusterConfig) -> Cluster:
                 c.add_edge(f"service:{c.ns_names[svc_ns[sv]]}:svc-{sv}",
                            f"service:{c.ns_names[svc_ns[t]]}:svc-{t}", "CALLS")
     return c
+
+
+def _dense_links(c: Cluster, att: np.ndarray, pods: np.ndarray, svc_ns: np.ndarray,
+                 cfg: ClusterConfig) -> None:
+    """The dense_links edges as position arrays (vectorised: C4 adds ~3.4M of them)."""
+    pos = {v: i for i, v in enumerate(c.ids) if v.startswith("service:")}
+    svc_pos = np.array([pos[f"service:{c.ns_names[svc_ns[s]]}:svc-{s}"] for s in range(cfg.services)],
+                       np.int64)
+    src, dst, typ = [], [], []
+    # attachment -> its pod's Node (node vertices are the first cfg.nodes positions)
+    src.append(att[:, 2]), dst.append(att[:, 0]), typ.append(np.full(len(att), 0))
+    # deployment AGGREGATES the attachment
+    src.append(att[:, 3]), dst.append(att[:, 0]), typ.append(np.full(len(att), 1))
+    # service SELECTS each pod of its deployments
+    src.append(svc_pos[pods[:, 1]]), dst.append(pods[:, 0]), typ.append(np.full(len(pods), 2))
+    # sibling pods of a deployment share its LogPattern vertices
+    lp = att[att[:, 4] == 1]
+    dep_of_pod = pods[:, 2]
+    order = np.argsort(dep_of_pod, kind="stable")
+    d_sorted = dep_of_pod[order]
+    lo = np.searchsorted(d_sorted, lp[:, 3], side="left")
+    hi = np.searchsorted(d_sorted, lp[:, 3], side="right")
+    n = hi - lo
+    rep = np.repeat(np.arange(len(lp)), n)
+    off = np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n)
+    sib = pods[order[lo[rep] + off], 0]
+    keep = sib != lp[rep, 1]                      # the owning pod already has its edge
+    src.append(sib[keep]), dst.append(lp[rep, 0][keep]), typ.append(np.full(int(keep.sum()), 3))
+    c.extra_src = np.concatenate(src).astype(np.int32)
+    c.extra_dst = np.concatenate(dst).astype(np.int32)
+    c.extra_type = np.concatenate(typ).astype(np.int32)
+
+
+def build_graph(c: Cluster):
+    """The EvidenceGraph of a cluster (+ its incidents): MERGE of every vertex and edge, the
+    dense_links edges by vertex position."""
+    from .graph import EvidenceGraph
+    g = EvidenceGraph()
+    g.merge_nodes(c.ids, c.labels)
+    g.merge_edges(c.src, c.dst, c.types)
+    if c.extra_src is not None and len(c.extra_src):
+        g.add_edges_indexed(c.extra_src, c.extra_dst, c.extra_type, list(c.EXTRA_TYPES))
+    return g
 
 
 # ---------------------------------------------------------------------------------------------

@@ -17,10 +17,17 @@ The graph is process-wide, like the Neo4j database the reference talks to.  Writ
 graph (MERGE); the next read brings the device snapshot up to date with ONE incremental update
 (egr_snapshot_update: the appended vertices and edges merged into the CSR on the device) instead
 of a rebuild and re-upload.
+
+Concurrency: Temporal runs activities concurrently, and the ranking runs in a worker thread
+(asyncio.to_thread) while writes arrive on the event loop.  Every access to the shared state --
+the host graph (whose C++ vectors a write reallocates), the snapshot sync, the cached plans and
+frontiers and their output buffers -- holds one process-wide lock, from the write or the
+set_seeds through the read-back of the results.
 """
 from __future__ import annotations
 
 import asyncio
+import threading
 
 import torch
 
@@ -37,6 +44,7 @@ class GraphService:
     _snapshot = None
     _plans: dict = {}
     _frontiers: dict = {}
+    _lock = threading.RLock()
     device = None
 
     @classmethod
@@ -47,7 +55,8 @@ class GraphService:
 
     @classmethod
     def reset(cls) -> None:
-        cls._graph, cls._snapshot, cls._plans, cls._frontiers = None, None, {}, {}
+        with cls._lock:
+            cls._graph, cls._snapshot, cls._plans, cls._frontiers = None, None, {}, {}
 
     @classmethod
     def _invalidate(cls) -> None:
@@ -64,9 +73,9 @@ class GraphService:
 
     @staticmethod
     async def create_relation(relation: GraphRelation) -> bool:
-        g = GraphService.graph()
-        known = g.lookup([relation.source_id, relation.target_id])
-        GraphService.create_relations_sync([relation])
+        with GraphService._lock:
+            known = GraphService.graph().lookup([relation.source_id, relation.target_id])
+            GraphService.create_relations_sync([relation])
         return bool((known >= 0).all())
 
     @staticmethod
@@ -75,14 +84,16 @@ class GraphService:
 
     @classmethod
     def create_entities_sync(cls, entities) -> int:
-        n = cls.graph().create_entities_batch(entities)
-        cls._invalidate()
+        with cls._lock:
+            n = cls.graph().create_entities_batch(entities)
+            cls._invalidate()
         return n
 
     @classmethod
     def create_relations_sync(cls, relations) -> int:
-        n = cls.graph().create_relations_batch(relations)
-        cls._invalidate()
+        with cls._lock:
+            n = cls.graph().create_relations_batch(relations)
+            cls._invalidate()
         return n
 
     @classmethod
@@ -131,6 +142,11 @@ class GraphService:
             raise ValueError("incident_ids and evidence_lists differ in length")
         if not incident_ids:
             return []
+        with cls._lock:
+            return cls._rank_locked(incident_ids, evidence_lists, hops, k)
+
+    @classmethod
+    def _rank_locked(cls, incident_ids, evidence_lists, hops, k):
         g = cls.graph()
         if g.num_vertices == 0:
             return [[] for _ in incident_ids]
@@ -171,6 +187,11 @@ class GraphService:
     def get_incident_graphs(cls, incident_ids: list[str], depth: int = 3,
                             resolve_bare_uuid: bool = False) -> list[dict]:
         """Batched get_incident_graph: one reach launch per hop for all incidents."""
+        with cls._lock:
+            return cls._graphs_locked(incident_ids, depth, resolve_bare_uuid)
+
+    @classmethod
+    def _graphs_locked(cls, incident_ids, depth, resolve_bare_uuid):
         g = cls.graph()
         empty = {"nodes": [], "relationships": []}
         if g.num_vertices == 0 or not incident_ids:

@@ -57,6 +57,13 @@ class AlertDeduplicator:
 
     @classmethod
     async def close(cls) -> None:
+        """The reference's close() only disconnects from Redis (:33-39); its keys survive.  The
+        table is this process's store, so close() releases nothing a later call would miss:
+        registered fingerprints stay live across close / reuse.  reset() drops them."""
+
+    @classmethod
+    def reset(cls) -> None:
+        """Drop every fingerprint and interned incident id (tests; FLUSHDB in Redis terms)."""
         cls._table = None
         cls._ids, cls._handles = [], {}
 

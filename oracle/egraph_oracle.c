@@ -15,6 +15,8 @@
  *   orc_propagate     DESIGN.md §A9 (build-defined): s^{h+1}_v = s0_v + sum_e val_e s^h_u,
  *                     fmaf in CSR order, dense; parity pinned bit-for-bit with the GPU
  *   orc_topk          per column: score desc, vertex id asc, over the reach set
+ *   orc_frontier      the three above per column over only the vertices the column touches
+ *                     (the frontier engine's algorithm on the CPU; bench.py's CPU baseline)
  *
  * Build: oracle/Makefile -> oracle/liboracle.so (gcc, -ffp-contract=off).
  */
@@ -303,5 +305,162 @@ int orc_topk(const float* scores, int64_t V, int32_t B, const uint64_t* reach,
     }
   }
   free(c);
+  return 0;
+}
+
+/* ---- orc_frontier: the same results per column, touching only what the column touches -----
+ * The CPU form of the frontier engine's algorithm (csrc/frontier.hip), used as the honest CPU
+ * baseline of bench.py (the dense orc_propagate sweeps V x B per hop although > 99 % of the
+ * values are exact zeros) and as a checker at sizes where the dense [V][B] arrays are large.
+ * Per column b, with per-thread dense scratch reset through touched lists:
+ *   T_0 = seeds, cur = s0 (max-combined as orc_propagate)
+ *   hop h: U = seeds + neighbours of every u in T_h with cur[u] != 0; for v in U the chain
+ *          acc = fmaf(val_e, cur[col_e], acc) over row v in CSR order, then acc + s0[v] --
+ *          the SAME arithmetic as orc_propagate on the same dense values (cur is exact zero
+ *          outside T_h); every other vertex is exactly 0 in the dense recurrence too.
+ *   reach: BFS from src[b] to depth `hops` (orc_reach); top-k over it as orc_topk.
+ *   prune: the last hop computes only the reach set's members (the engine's pruned last
+ *          pull): the scores top-k reads are unchanged, the others are never read.
+ * Bit-identical to orc_propagate + orc_reach + orc_topk (tests/test_oracle_frontier.py).
+ * work_out (optional, [2]): CSR entries read by the hop chains, rows walked.              */
+typedef struct { uint32_t v; float s; } seedent;
+
+static int cand_better(float s, uint32_t v, float s2, uint32_t v2) {
+  return s > s2 || (s == s2 && v < v2);
+}
+
+int orc_frontier(const uint32_t* row_ptr, const uint32_t* col, const float* val,
+                 const uint8_t* vlabel, int64_t V, const uint32_t* seed_v, const uint32_t* seed_c,
+                 const float* seed_s, int64_t n_seeds, const uint32_t* src, int32_t B,
+                 int32_t hops, int32_t exclude_label, int32_t k, int prune, uint32_t* out_ids,
+                 float* out_scores, int64_t* work_out, int threads) {
+  /* seeds grouped by column (counting sort; invalid triples dropped) */
+  int64_t* ptr = calloc((size_t)B + 1, sizeof(int64_t));
+  seedent* grp = malloc((size_t)(n_seeds > 0 ? n_seeds : 1) * sizeof(seedent));
+  if (!ptr || !grp) { free(ptr); free(grp); return -3; }
+  for (int64_t i = 0; i < n_seeds; ++i)
+    if (seed_v[i] < (uint64_t)V && seed_c[i] < (uint32_t)B) ++ptr[seed_c[i] + 1];
+  for (int32_t b = 0; b < B; ++b) ptr[b + 1] += ptr[b];
+  {
+    int64_t* cur = malloc((size_t)B * sizeof(int64_t));
+    memcpy(cur, ptr, (size_t)B * sizeof(int64_t));
+    for (int64_t i = 0; i < n_seeds; ++i)
+      if (seed_v[i] < (uint64_t)V && seed_c[i] < (uint32_t)B) {
+        grp[cur[seed_c[i]]].v = seed_v[i];
+        grp[cur[seed_c[i]]++].s = seed_s[i];
+      }
+    free(cur);
+  }
+  int64_t w_entries = 0, w_rows = 0;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel reduction(+ : w_entries, w_rows)
+#endif
+  {
+    float* cur = calloc((size_t)V, sizeof(float));
+    float* s0 = calloc((size_t)V, sizeof(float));
+    uint8_t* has = calloc((size_t)V, 1);
+    uint32_t* mark = calloc((size_t)V, sizeof(uint32_t));    /* generation stamps */
+    int* depth = malloc((size_t)V * sizeof(int));
+    uint32_t* T = malloc((size_t)V * sizeof(uint32_t));
+    uint32_t* U = malloc((size_t)V * sizeof(uint32_t));
+    float* nv = malloc((size_t)V * sizeof(float));
+    uint32_t* sd = malloc((size_t)V * sizeof(uint32_t));
+    uint32_t* queue = malloc((size_t)V * sizeof(uint32_t));
+    uint32_t gen = 0;
+    for (int64_t v = 0; v < V; ++v) depth[v] = -1;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+    for (int32_t b = 0; b < B; ++b) {
+      /* s0: max-combine the column's seeds */
+      int64_t nsd = 0;
+      for (int64_t i = ptr[b]; i < ptr[b + 1]; ++i) {
+        const uint32_t v = grp[i].v;
+        if (!has[v]) { has[v] = 1; s0[v] = grp[i].s; sd[nsd++] = v; }
+        else if (grp[i].s > s0[v]) s0[v] = grp[i].s;
+      }
+      /* the reach set of the incident vertex first (BFS to depth `hops`): with `prune` the
+       * last hop computes only its members, the only scores top-k reads */
+      int64_t qh = 0, qt = 0;
+      if (src[b] < (uint64_t)V) {
+        queue[qt++] = src[b];
+        depth[src[b]] = 0;
+      }
+      while (qh < qt) {
+        const uint32_t v = queue[qh++];
+        if (depth[v] == hops) continue;
+        for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e)
+          if (depth[col[e]] < 0) {
+            depth[col[e]] = depth[v] + 1;
+            queue[qt++] = col[e];
+          }
+      }
+      int64_t nT = 0;
+      for (int64_t i = 0; i < nsd; ++i) { cur[sd[i]] = s0[sd[i]]; T[nT++] = sd[i]; }
+      for (int32_t h = 0; h < hops; ++h) {
+        const int last_pruned = prune && h == hops - 1;
+        ++gen;
+        int64_t nU = 0;
+        for (int64_t i = 0; i < nsd; ++i)
+          if (mark[sd[i]] != gen) { mark[sd[i]] = gen; U[nU++] = sd[i]; }
+        for (int64_t i = 0; i < nT; ++i) {
+          const uint32_t u = T[i];
+          if (cur[u] == 0.0f) continue;
+          for (uint32_t e = row_ptr[u]; e < row_ptr[u + 1]; ++e)
+            if (mark[col[e]] != gen) { mark[col[e]] = gen; U[nU++] = col[e]; }
+        }
+        int64_t nW = 0;
+        for (int64_t i = 0; i < nU; ++i) {
+          const uint32_t v = U[i];
+          if (last_pruned && depth[v] < 0) continue;   /* outside the reach set: never read */
+          float acc = 0.0f;
+          for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e) acc = fmaf(val[e], cur[col[e]], acc);
+          w_entries += row_ptr[v + 1] - row_ptr[v];
+          ++w_rows;
+          nv[nW] = acc + s0[v];
+          U[nW++] = v;
+        }
+        for (int64_t i = 0; i < nT; ++i) cur[T[i]] = 0.0f;
+        for (int64_t i = 0; i < nW; ++i) { cur[U[i]] = nv[i]; T[i] = U[i]; }
+        nT = nW;
+      }
+      /* top-k over the reach set */
+      uint32_t* ids = out_ids + (size_t)b * k;
+      float* scs = out_scores + (size_t)b * k;
+      int32_t nk = 0;
+      for (int64_t i = 0; i < qt; ++i) {
+        const uint32_t v = queue[i];
+        if (exclude_label >= 0 && vlabel[v] == (uint8_t)exclude_label) continue;
+        const float s = cur[v];
+        if (nk < k || cand_better(s, v, scs[nk - 1], ids[nk - 1])) {
+          int32_t j = nk < k ? nk++ : k - 1;
+          while (j > 0 && cand_better(s, v, scs[j - 1], ids[j - 1])) {
+            scs[j] = scs[j - 1];
+            ids[j] = ids[j - 1];
+            --j;
+          }
+          scs[j] = s;
+          ids[j] = v;
+        }
+      }
+      for (int64_t i = 0; i < qt; ++i) depth[queue[i]] = -1;
+      for (int32_t q = nk; q < k; ++q) {
+        ids[q] = EGR_NO_NODE;
+        scs[q] = -INFINITY;
+      }
+      /* reset the scratch this column touched */
+      for (int64_t i = 0; i < nT; ++i) cur[T[i]] = 0.0f;
+      for (int64_t i = 0; i < nsd; ++i) { has[sd[i]] = 0; s0[sd[i]] = 0.0f; }
+    }
+    free(cur); free(s0); free(has); free(mark); free(depth); free(T); free(U); free(nv);
+    free(sd); free(queue);
+  }
+  if (work_out) {
+    work_out[0] = w_entries;
+    work_out[1] = w_rows;
+  }
+  free(ptr);
+  free(grp);
   return 0;
 }

@@ -27,7 +27,7 @@ def _load() -> C.CDLL:
     lib.orc_round.restype = C.c_double
     lib.orc_round.argtypes = [C.c_double, C.c_int]
     for name in ("orc_rules_eval", "orc_rank", "orc_reach", "orc_propagate", "orc_topk",
-                 "orc_hop_step"):
+                 "orc_hop_step", "orc_frontier"):
         getattr(lib, name).restype = C.c_int
     return lib
 
@@ -94,6 +94,25 @@ def topk(scores, reach_bits, vlabel, exclude_label, k):
                  _p(np.ascontiguousarray(reach_bits)), _p(vlabel), C.c_int32(exclude_label),
                  C.c_int32(k), _p(ids), _p(sc))
     return ids.reshape(B, k), sc.reshape(B, k)
+
+
+def frontier(row_ptr, col, val, vlabel, seed_v, seed_c, seed_s, src, hops, exclude_label, k,
+             threads=0, prune=True):
+    """orc_frontier: top-k ids / scores [B, k] equal to propagate + reach + topk, computed per
+    column over the touched vertices only; also (CSR entries read, rows walked)."""
+    V = len(row_ptr) - 1
+    B = len(src)
+    ids = np.zeros(B * k, np.uint32)
+    sc = np.zeros(B * k, np.float32)
+    work = np.zeros(2, np.int64)
+    rc = lib.orc_frontier(_p(row_ptr), _p(col), _p(val), _p(vlabel), C.c_int64(V), _p(seed_v),
+                          _p(seed_c), _p(seed_s), C.c_int64(len(seed_v)), _p(src), C.c_int32(B),
+                          C.c_int32(hops), C.c_int32(exclude_label), C.c_int32(k),
+                          C.c_int(1 if prune else 0), _p(ids),
+                          _p(sc), _p(work), C.c_int(threads))
+    if rc != 0:
+        raise MemoryError("orc_frontier")
+    return ids.reshape(B, k), sc.reshape(B, k), (int(work[0]), int(work[1]))
 
 
 # ---- pure-Python graph write semantics (neo4j.py:95-167) ---------------------------------------

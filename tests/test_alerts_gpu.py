@@ -167,7 +167,7 @@ def test_dedup_large_batches_match_oracle():
 
 def test_dedup_table_full_fails_loudly():
     from egraph import alerts
-    t = alerts.DedupTable(capacity=16)          # 64 slots
+    t = alerts.DedupTable(capacity=16, auto_compact=False)   # 64 slots
     fp, _ = alerts.fingerprints([f"k{i}" for i in range(100)])
     with pytest.raises(MemoryError):
         t.ingest(fp, 0, 1000)
@@ -177,7 +177,7 @@ def test_alert_deduplicator_reference_unit_cases(monkeypatch):
     """The reference's tests/unit/test_deduplicator.py:39-74 through the drop-in, plus the TTL
     behaviour its fake Redis does not model."""
     from src.services.ingestion.deduplicator import AlertDeduplicator as D
-    asyncio.run(D.close())
+    D.reset()
     clock = [5_000_000]
     monkeypatch.setattr(D, "now_ms", staticmethod(lambda: clock[0]))
     run = asyncio.run
@@ -212,4 +212,46 @@ def test_alert_deduplicator_reference_unit_cases(monkeypatch):
     assert dup.tolist() == [False, False, True, True, True]
     assert ids == ["n1", "n2", "n1", "b", "n2"] and created == ["n1", "n2"]
     assert alerts.NO_INCIDENT == 0xFFFFFFFF
+    # close() only disconnects, as the reference's Redis client close: keys survive
     run(D.close())
+    assert run(D.check_duplicate("fp-1")) == (True, "b")
+    D.reset()
+    assert run(D.check_duplicate("fp-1")) == (False, None)
+
+
+def test_dedup_auto_compaction_expiring_keys():
+    """More distinct fingerprints than the capacity, through expiring TTLs: the table compacts
+    itself (no MemoryError, no unbounded growth) and every decision still equals the oracle
+    webhook loop (slots were never reclaimed)."""
+    import alerts_oracle as AO
+    from egraph import alerts
+    t = alerts.DedupTable(capacity=64)           # 128 slots
+    slots0 = t.stats(0)["slots"]
+    store = AO.TTLStore()
+    nxt = 0
+    now = 1_000_000
+    for tick in range(40):                       # 40 x 60 fresh keys, 10 s TTL, 4 s per tick
+        now += 4000
+        keys = [f"alertmanager:A:ns:{tick}-{i % 50}" for i in range(60)]
+        fp, hx = alerts.fingerprints(keys, hex=True)
+        t.next_id = nxt
+        dup, inc, n_new = t.ingest(fp, now, 10_000)
+        edup, einc, en = AO.webhook_loop(store, hx, now, 10, nxt)
+        assert n_new == en
+        np.testing.assert_array_equal(dup.cpu().numpy(), np.array(edup))
+        np.testing.assert_array_equal(inc.cpu().numpy(), np.array(einc))
+        nxt += en
+    assert t.compactions > 0
+    assert t.stats(now)["slots"] <= 4 * slots0   # live keys stay ~3 ticks' worth
+
+
+def test_dedup_auto_compaction_grows_for_live_keys():
+    """Live keys beyond the requested capacity: the table grows instead of filling up."""
+    from egraph import alerts
+    t = alerts.DedupTable(capacity=16)
+    fp, _ = alerts.fingerprints([f"k{i}" for i in range(1000)])
+    dup, inc, n_new = t.ingest(fp, 0, 10**9)
+    assert n_new == 1000 and not dup.any()
+    assert t.stats(1)["live"] == 1000
+    dup, inc = t.lookup(fp, 1)
+    assert dup.all() and sorted(inc.cpu().tolist()) == list(range(1000))

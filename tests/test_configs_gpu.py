@@ -1,0 +1,207 @@
+"""Parity at the configurations the numbers come from (BASELINE.json configs C2, C3, C4).
+
+* C3, the exact bench configuration (bench.py defaults): the 100k-pod graph, B = 1024 incidents
+  per batch, top-k-only frontiers (pool_entries = -1: the pruned narrow-table kernel), three
+  frontier + rules states in flight on their own streams, rules on each lane's side stream.
+  Six batches with DIFFERENT incidents are interleaved over the three lanes exactly as
+  bench.step_frontier does; every batch's top-k ids / scores are checked against the CPU
+  frontier oracle (orc_frontier, itself pinned to the dense oracle in
+  tests/test_oracle_frontier.py) and its rule outputs against orc_rules_eval.
+* C2 (10k pods, 1k concurrent mixed incidents): the rules kernel, the drop-in dicts (against
+  the reference restatement rca_oracle, itself pinned to the reference's goldens) and the
+  frontier top-k against both oracles.
+* C4 (the 1M-vertex graph, ~10M CSR entries): the frontier engine at B = 256 against
+  orc_frontier, and the edge-cut partitioned plan at P = 2 and P = 4 (one process) against the
+  unpartitioned oracle: owned scores bit-identical, merged top-k equal.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    from egraph.device import to_device
+    return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
+
+
+def _world(config: str, batches: list[int], seed0: int = 1000):
+    """The config's cluster with len(batches) incident batches added; per batch its cases."""
+    from egraph import synth
+    cl = synth.build_cluster(synth.CONFIGS[config])
+    out = []
+    for j, B in enumerate(batches):
+        cases = synth.make_incidents(cl, B, seed=seed0 + j)
+        synth.add_incidents(cl, cases)
+        out.append(cases)
+    return synth.build_graph(cl), out
+
+
+def _batch_inputs(g, cases):
+    from egraph import synth
+    ev = [x.evidence for x in cases]
+    sv, sc, ss = synth.seeds_for_batch(g, ev)
+    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+    return ev, sv, sc, ss, src
+
+
+def _oracle_topk(g, csr, vl, sv, sc, ss, src, k=10, hops=3):
+    inc = g.labels().index("Incident")
+    ids, sco, _ = oracle.frontier(csr["row_ptr"], csr["col"], csr["val"], vl, sv, sc, ss, src,
+                                  hops, inc, k, threads=16)
+    return ids, sco
+
+
+def _check_rules(res, enc):
+    from egraph import catalog
+    exp = oracle.rules_eval(catalog.default().table, enc.flags, enc.vocab, enc.node, enc.err, enc.seg_off)
+    np.testing.assert_array_equal(res.mask, exp["mask"])
+    np.testing.assert_array_equal(res.n_hyp, exp["n_hyp"])
+    np.testing.assert_array_equal(res.order_rank, exp["order_rank"])
+    np.testing.assert_array_equal(res.order_conf, exp["order_conf"])
+    assert res.final_score.tobytes() == exp["final_score"].tobytes()
+    assert res.confidence.tobytes() == exp["confidence"].tobytes()
+
+
+def test_bench_config_c3_pipelined_lanes():
+    import bench
+    from egraph import catalog
+    from egraph.encode import encode_batch
+    from egraph.rca import RulesDeviceBatch
+    B, k, hops, P, n_batches = 1024, 10, 3, 3, 6
+    g, batches = _world("C3", [B] * n_batches)
+    dev = torch.device("cuda", 0)
+    inc = g.labels().index("Incident")
+    inputs = []
+    for cases in batches:
+        ev, sv, sc, ss, src = _batch_inputs(g, cases)
+        enc = encode_batch(ev, catalog.default())
+        inputs.append(dict(enc=enc, host=(sv, sc, ss, src),
+                           seeds=(_dev(sv), _dev(sc), _dev(ss)), sources=_dev(src),
+                           rules=RulesDeviceBatch(enc, catalog.default(), dev)))
+    max_seeds = max(len(x["host"][0]) for x in inputs)
+    snap = g.snapshot(device=dev)
+    lanes = bench.build_lanes(snap, B, max_seeds, k, P, -1, dev,
+                              [(None, x["rules"], x["seeds"], x["sources"]) for x in inputs[:P]])
+    assert all(ln["frontier"].pool_entries == -1 for ln in lanes)
+    ctx = dict(lanes=lanes, tick=0, inc_label=inc)
+    got = [(torch.empty(B * k, dtype=torch.int32, device=dev),
+            torch.empty(B * k, dtype=torch.float32, device=dev)) for _ in range(n_batches)]
+    for i, x in enumerate(inputs):                  # bench.step_frontier, one batch per step
+        lane = ctx["lanes"][ctx["tick"] % P]
+        lane.update(seeds=x["seeds"], sources=x["sources"], rules=x["rules"])
+        lane = bench.step_frontier(ctx, hops)
+        with torch.cuda.stream(lane["main"]):       # the lane's outputs before its next batch
+            got[i][0].copy_(lane["frontier"].out_ids)
+            got[i][1].copy_(lane["frontier"].out_scores)
+    torch.cuda.synchronize()
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    for i, x in enumerate(inputs):
+        sv, sc, ss, src = x["host"]
+        e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k, hops)
+        np.testing.assert_array_equal(got[i][0].cpu().numpy().view(np.uint32).reshape(B, k), e_ids,
+                                      err_msg=f"batch {i}")
+        assert got[i][1].cpu().numpy().reshape(B, k).tobytes() == e_sc.tobytes(), f"batch {i}"
+        _check_rules(x["rules"].fetch(), x["enc"])
+    st = lanes[0]["frontier"].stats()
+    assert st["overflowed"] == 0 and st["members"] > 0
+
+
+def test_c2_rules_dropin_and_frontier():
+    import asyncio
+    from types import SimpleNamespace
+
+    import rca_oracle
+    from egraph import catalog
+    from egraph.encode import encode_batch
+    from egraph.rca import RulesDeviceBatch
+    from helpers import record
+    from src.services.rca.rules_engine import RulesEngine
+    B = 1000
+    g, (cases,) = _world("C2", [B])
+    assert {x.scenario for x in cases} >= {"crashloop", "crashloop_deploy", "oom", "imagepull"}
+    ev, sv, sc, ss, src = _batch_inputs(g, cases)
+    enc = encode_batch(ev, catalog.default())
+    rb = RulesDeviceBatch(enc, catalog.default(), torch.device("cuda", 0))
+    rb.launch()
+    _check_rules(rb.fetch(), enc)
+    # the drop-in batch API against the reference restatement, every incident
+    incs = [SimpleNamespace(id=x.incident["id"]) for x in cases]
+    out = asyncio.run(RulesEngine().rank_incidents_batch(incs, ev))
+    for x, hyps in zip(cases, out):
+        assert record(hyps) == record(rca_oracle.rca(x.incident["id"], x.evidence))
+    # frontier (pruned, top-k only) against orc_frontier and the dense oracle
+    snap = g.snapshot()
+    fr = snap.frontier(B, max_seeds=len(sv), k=10, pool_entries=-1)
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    inc = g.labels().index("Incident")
+    ids, sco = fr.run(_dev(src), hops=3, exclude_label=inc)
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids)
+    assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
+    dense = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3, 16)
+    reach = oracle.reach(csr["row_ptr"], csr["col"], src, 3, 16)
+    d_ids, d_sc = oracle.topk(dense, reach, vl, inc, 10)
+    np.testing.assert_array_equal(d_ids, e_ids)
+    assert d_sc.tobytes() == e_sc.tobytes()
+
+
+@pytest.fixture(scope="module")
+def c4():
+    g, (cases,) = _world("C4", [256], seed0=2000)
+    ev, sv, sc, ss, src = _batch_inputs(g, cases)
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    assert len(csr["col"]) > 9_000_000 and g.num_vertices > 1_000_000
+    return g, csr, vl, sv, sc, ss, src
+
+
+def test_c4_frontier_b256(c4):
+    g, csr, vl, sv, sc, ss, src = c4
+    B = len(src)
+    fr = g.snapshot().frontier(B, max_seeds=len(sv), k=10, pool_entries=-1)
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    ids, sco = fr.run(_dev(src), hops=3, exclude_label=g.labels().index("Incident"))
+    e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids)
+    assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_c4_partitioned_plan(c4, P):
+    from egraph import shard
+    from egraph.graph import Snapshot
+    g, csr, vl, sv, sc, ss, src = c4
+    B, k = 64, 10
+    keep = sc < B
+    sv, sc, ss, src = sv[keep], sc[keep], ss[keep], src[:B]
+    V = g.num_vertices
+    inc = g.labels().index("Incident")
+    owner = shard.partition_vertices(csr["row_ptr"], vl, g.labels(), P)
+    runs = []
+    for r in range(P):
+        lg = shard.build_local(csr, vl, owner, r, P)
+        snap = Snapshot.from_csr(lg.row_ptr, lg.col, lg.meta, lg.val, lg.vlabel, g.labels())
+        lv, lc, ls = shard.local_seeds(lg, V, sv, sc, ss)
+        plan = snap.plan(B, max_seeds=max(len(lv), 1), k=k)
+        plan.set_seeds(_dev(lv), _dev(lc), _dev(ls))
+        plan.set_sources(_dev(shard.local_sources(lg, V, src)))
+        runs.append(shard.RankRun(lg, plan, torch.device("cuda", 0)))
+        runs[-1].snap = snap
+    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k)
+    e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k)
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3, 16)
+    for run, (ids, scores) in zip(runs, out):
+        lg = run.lg
+        own = run.eng.read_scores().cpu().numpy()[: lg.n_owned]
+        assert own.tobytes() == exp[lg.gid[: lg.n_owned]].tobytes()        # bit-identical
+        np.testing.assert_array_equal(ids.cpu().numpy(), e_ids.astype(np.int64))
+        np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
