@@ -230,6 +230,15 @@ int egr_plan_run(egr_plan* p, int32_t hops, int32_t exclude_label, uint32_t* out
  * scores out: row-major [V][n_cols]; reach out: [ceil(n_cols/64)][V].                       */
 int egr_plan_read_scores(const egr_plan* p, float* out, void* stream);
 int egr_plan_read_reach(const egr_plan* p, uint64_t* out, void* stream);
+
+/* Stand-alone top-k over explicit dense arrays (csrc/topk.hip; torch.ops.egraph.topk).
+ * scores row-major [V][n_cols] fp32, reach [ceil(n_cols/64)][V] u64 bits (the layouts of
+ * egr_plan_read_scores / egr_plan_read_reach, V = the snapshot's vertex count); per column
+ * the k best reached vertices whose label != exclude_label (-1: none excluded), score
+ * descending, vertex id ascending; out [n_cols*k], EGR_NO_NODE / -inf padded.  The engines'
+ * own top-k (egr_plan_topk, egr_frontier_run) produce the same lists from their state.      */
+int egr_topk(const egr_snapshot* s, const float* scores, const uint64_t* reach, int32_t n_cols,
+             int32_t k, int32_t exclude_label, uint32_t* out_ids, float* out_scores, void* stream);
 /* Induced subgraph of one column's reach set (get_incident_graph "relationships",
  * neo4j.py:193-200): every edge whose both endpoints are in the set, as (src, dst, type).
  * Writes min(total, cap) edges in unspecified order and the total to *out_n.  Synchronous

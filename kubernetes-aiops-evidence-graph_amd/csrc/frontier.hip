@@ -49,7 +49,7 @@ constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
 constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
 constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
 constexpr int MAX_HOPS = 60;
-constexpr int PROF_SLOTS = 32;
+constexpr int PROF_SLOTS = 40;
 
 struct FArgs {
   const uint32_t* row_ptr;
@@ -113,12 +113,14 @@ namespace fr_wide {
 #define FR_LLIMIT 4608
 #define FR_BLOOM_LOG 16
 #define FR_WAVES_PER_EU 4
+#define FR_LSNEW 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
+#undef FR_LSNEW
 }  // namespace fr_wide
 
 namespace fr_narrow {
@@ -129,17 +131,31 @@ namespace fr_narrow {
 #define EGR_FR_NARROW_BLOOM_LOG 15
 #define EGR_FR_NARROW_WAVES_PER_EU 5
 #endif
+// walk chunking (frontier_body.h row_phase): 0 = static striping over the waves, 1 = chunks
+// taken from an LDS counter, members strided over the chunks, 2 = the same, contiguous chunks
+#ifndef EGR_FR_DYN
+#define EGR_FR_DYN 0
+#endif
+// hub rows: 1 = the next 64-entry segment's loads issued before the current one is probed
+#ifndef EGR_FR_HUBPF
+#define EGR_FR_HUBPF 0
+#endif
+#ifndef EGR_FR_NARROW_LSNEW
+#define EGR_FR_NARROW_LSNEW 0
+#endif
 #define FR_FT EGR_FR_NARROW_FT
 #define FR_LCAP EGR_FR_NARROW_LCAP
 #define FR_LLIMIT EGR_FR_NARROW_LLIMIT
 #define FR_BLOOM_LOG EGR_FR_NARROW_BLOOM_LOG
 #define FR_WAVES_PER_EU EGR_FR_NARROW_WAVES_PER_EU
+#define FR_LSNEW EGR_FR_NARROW_LSNEW
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
+#undef FR_LSNEW
 }  // namespace fr_narrow
 
 // The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
@@ -153,12 +169,14 @@ namespace fr_fallback {
 #define FR_LLIMIT 192
 #define FR_BLOOM_LOG 10
 #define FR_WAVES_PER_EU 4
+#define FR_LSNEW 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
+#undef FR_LSNEW
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)

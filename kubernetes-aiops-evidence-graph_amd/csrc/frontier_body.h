@@ -3,7 +3,8 @@
 
 // Geometry of this instantiation (set by the includer, csrc/frontier.hip):
 //   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
-//   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU.
+//   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU,
+//   FR_LSNEW (1: the pull results live in LDS instead of HBM).
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -34,6 +35,7 @@ struct Tab {
   uint32_t* count;  // LDS
   uint32_t* ovf;    // LDS
   uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
+  uint32_t* chunk;  // LDS: the next chunk of a walk (dynamic chunk assignment), 0 at its start
 };
 
 // Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
@@ -139,7 +141,7 @@ __device__ __forceinline__ bool cand_depth(uint8_t f, int hops) {
 struct Ticker {
   bool on = false;
   uint64_t t0 = 0;
-  uint64_t sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t sub[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   __device__ __forceinline__ void tick(int k) {
     if (on) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -309,18 +311,32 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
   const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
   auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
-  // members are striped across the waves (i = wave + NWAVES * (lane + 64 k)): vertices inserted
-  // together (e.g. the incident's Node hubs, all reached at one level) spread over all waves.
-  // The next chunk's selection and row_ptr loads are issued before the current chunk is walked
-  // (a member's kind cannot change during the pass: see the comment above).
+  // Work split.  A walk is cut into chunks of 64 members; chunk c holds the members
+  // c + nch * lane (nch = number of chunks), so vertices inserted together (e.g. the incident's
+  // Node hubs, all reached at one level) spread over different chunks.  Waves take chunks from
+  // an LDS counter as they finish (dynamic: a wave that drew hub rows takes fewer chunks, and
+  // the walk ends within about one chunk of its fastest wave).  The next chunk's selection and
+  // row_ptr loads are issued before the current chunk is walked (a member's kind cannot change
+  // during the pass: see the comment above).
   struct Chunk {
     uint32_t i, kind, e0, e1;
   };
-  auto fetch = [&](uint32_t k0) {
-    Chunk c{wave + NWAVES * (lane + 64u * k0), 0u, 0u, 0u};
+#if EGR_FR_DYN == 0
+  // static: wave w walks chunks k = 0, 1, ... holding members w + NWAVES * (lane + 64 k)
+  const uint32_t nch = (n + FT - 1) / FT;
+  auto member_of = [&](uint32_t c) { return wave + NWAVES * (lane + 64u * c); };
+#elif EGR_FR_DYN == 1
+  const uint32_t nch = (n + 63) / 64;
+  auto member_of = [&](uint32_t c) { return c + nch * lane; };
+#else
+  const uint32_t nch = (n + 63) / 64;
+  auto member_of = [&](uint32_t c) { return 64u * c + lane; };
+#endif
+  auto fetch = [&](uint32_t c) {
+    Chunk ch{member_of(c), 0u, 0u, 0u};
     uint32_t v = 0;
-    if (c.i < n) {
-      uint32_t p = t.mlist[c.i];
+    if (c < nch && ch.i < n) {
+      uint32_t p = t.mlist[ch.i];
 #ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
       if (p >= t.cap) {           // guard (see below)
         atomicAdd(&A.stats[5], 1ull);
@@ -329,31 +345,43 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
 #endif
       v = t.keys[p];
       const uint8_t f = t.fl[p];
-      if (reach_lvl && (f & FL_DEPTH) == reach_fl) c.kind |= K_REACH;
+      if (reach_lvl && (f & FL_DEPTH) == reach_fl) ch.kind |= K_REACH;
       if constexpr (PH == SEEDS) {
-        if (f & FL_SEED) c.kind |= K_PROP | noins;
+        if (f & FL_SEED) ch.kind |= K_PROP | noins;
       } else {
         if ((((t.need[p] >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
-          c.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
+          ch.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
       }
     }
 #ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
-    if (c.kind && v >= A.V) {   // a member key outside the graph: table corruption, counted
+    if (ch.kind && v >= A.V) {   // a member key outside the graph: table corruption, counted
       atomicAdd(&A.stats[5], 1ull);
-      c.kind = 0;
+      ch.kind = 0;
     }
 #endif
-    if (c.kind) {
-      c.e0 = A.row_ptr[v];
-      c.e1 = A.row_ptr[v + 1];
+    if (ch.kind) {
+      ch.e0 = A.row_ptr[v];
+      ch.e1 = A.row_ptr[v + 1];
     }
-    return c;
+    return ch;
   };
-  const uint32_t nk = (n + FT - 1) / FT;
-  Chunk nxt = nk ? fetch(0) : Chunk{0u, 0u, 0u, 0u};
-  for (uint32_t k0 = 0; k0 < nk; ++k0) {
+#if EGR_FR_DYN == 0
+  uint32_t next_static = 0;
+  auto grab = [&]() -> uint32_t { return next_static++; };
+#else
+  auto grab = [&]() -> uint32_t {
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(t.chunk, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+  };
+#endif
+  uint32_t c_cur = grab();
+  Chunk nxt = fetch(c_cur);
+  while (c_cur < nch) {
     const Chunk cur = nxt;
-    if (k0 + 1 < nk) nxt = fetch(k0 + 1);
+    const uint32_t c_next = grab();
+    nxt = fetch(c_next);
+    c_cur = c_next;
     const uint32_t i = cur.i, kind = cur.kind, e0 = cur.e0, deg = cur.e1 - cur.e0;
     if (kind) {
       ++work.rows;
@@ -365,6 +393,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     float acc = 0.f;
     light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
     tk.tick(1);
+#if EGR_FR_HUBPF == 0
     uint64_t heavy = __ballot(!light);
     while (heavy) {
       const int m = __ffsll((long long)heavy) - 1;
@@ -378,6 +407,56 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         const bool act = j < hdeg;
         const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
         const uint32_t u = ce.x;
+        tk.tick(8);
+        const int q = act ? tab_find<GT>(t, u) : -1;
+        tk.tick(9);
+        if (hkind & K_PULL) {
+          const float w = __uint_as_float(ce.y);
+          const float x = q >= 0 ? t.s[q] : 0.f;
+          // the chain runs over the present entries only, in lane (= CSR) order
+          for (uint64_t fm = __ballot(q >= 0); fm; fm &= fm - 1) {
+            const int y = __ffsll((long long)fm) - 1;
+            hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
+          }
+        }
+        tk.tick(10);
+        if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
+        tk.tick(11);
+      }
+      if (lane == m) acc = hacc;
+    }
+#else
+    // hub rows, one at a time across the wave, 64 entries per segment; the next segment's
+    // (or the next hub's first segment's) entries are loaded before this one is probed
+    uint64_t heavy = __ballot(!light);
+    if (heavy) {
+      int m = __ffsll((long long)heavy) - 1;
+      heavy &= heavy - 1;
+      uint32_t base = 0;
+      uint32_t he0 = __builtin_amdgcn_readlane(e0, m);
+      uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
+      uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
+      uint2 ce = lane < hdeg ? A.cv[he0 + lane] : make_uint2(0u, 0u);
+      float hacc = 0.f;
+      for (;;) {
+        // the segment after this one
+        int m2 = m;
+        uint32_t base2 = base + 64, he02 = he0, hdeg2 = hdeg, hkind2 = hkind;
+        if (base2 >= hdeg) {
+          m2 = heavy ? __ffsll((long long)heavy) - 1 : -1;
+          base2 = 0;
+          if (m2 >= 0) {
+            heavy &= heavy - 1;
+            he02 = __builtin_amdgcn_readlane(e0, m2);
+            hdeg2 = __builtin_amdgcn_readlane(deg, m2);
+            hkind2 = __builtin_amdgcn_readlane(kind, m2);
+          }
+        }
+        const uint32_t j2 = base2 + lane;
+        const uint2 ce2 = (m2 >= 0 && j2 < hdeg2) ? A.cv[he02 + j2] : make_uint2(0u, 0u);
+        // this segment
+        const bool act = base + lane < hdeg;
+        const uint32_t u = ce.x;
         const int q = act ? tab_find<GT>(t, u) : -1;
         if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
@@ -389,9 +468,20 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
           }
         }
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
+        if (m2 != m) {            // the row is complete
+          if (lane == m) acc = hacc;
+          hacc = 0.f;
+        }
+        if (m2 < 0) break;
+        m = m2;
+        base = base2;
+        he0 = he02;
+        hdeg = hdeg2;
+        hkind = hkind2;
+        ce = ce2;
       }
-      if (lane == m) acc = hacc;
     }
+#endif
     tk.tick(2);
     if constexpr (PH == PULL) {
       if (kind & K_PULL) t.snew[i] = acc;
@@ -399,7 +489,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     tk.tick(3);
   }
   if (tk.on && lane == 0)
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < 12; ++k)
       A.prof[((size_t)b * PROF_SLOTS + 24 + k) * PROF_W + 1 + wave] = tk.sub[k];
 }
 
@@ -446,7 +536,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
 }
 
 struct Shared {
-  uint32_t count, ovf, item;
+  uint32_t count, ovf, item, chunk;
   unsigned long long base;
   uint64_t top[NWAVES][KMAXF];
   uint32_t w_pull, w_expand, w_rows;
@@ -528,10 +618,11 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
 // second barrier.  Reading them after a single barrier races with the next phase's inserts by
 // faster waves: a late wave could see an overflow the others missed and leave alone, and the
 // rest would walk a member list longer than the table's limit.
-__device__ __forceinline__ bool phase_sync(const Shared& sh, uint32_t& cnt) {
+__device__ __forceinline__ bool phase_sync(Shared& sh, uint32_t& cnt) {
   __syncthreads();
   cnt = sh.count;
   const bool ovf = sh.ovf != 0;
+  if (threadIdx.x == 0) sh.chunk = 0;     // the next walk's chunk counter
   __syncthreads();
   return ovf;
 }
@@ -709,6 +800,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
     }
   }
+  if (A.prof && tid == 0) A.prof[((size_t)b * PROF_SLOTS + 20) * PROF_W] = n;   // members
   if (tid == 0) {
     A.mem_off[b] = base;
     A.mem_cnt[b] = keep ? n : NO_NODE;
@@ -729,7 +821,15 @@ struct LdsTab {
   uint32_t needw[LCAP / 4];
   uint16_t mlist[LLIMIT];
   uint32_t bloom[BLOOM_WORDS];
+#if FR_LSNEW
+  float snew[LLIMIT];          // pull results by member index (FR_LSNEW: in LDS, not HBM)
+#endif
 };
+#if FR_LSNEW
+#define LSNEW_PTR L.snew
+#else
+#define LSNEW_PTR (A.lsnew + (size_t)b * LLIMIT)
+#endif
 
 // One column in the LDS table: clear, run, and on overflow hand the column on (A.ovf_list).
 __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh) {
@@ -745,11 +845,12 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   if (tid == 0) {
     sh.count = 0;
     sh.ovf = 0;
+    sh.chunk = 0;
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
   Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom};
+               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, &sh.chunk};
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
@@ -811,7 +912,8 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   const size_t cap = A.gcap;
   Tab<true> t{A.gkeys + blockIdx.x * cap, A.gs + blockIdx.x * cap, A.gfl + blockIdx.x * cap,
               A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
-              A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr};
+              A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr,
+              &sh.chunk};
   const uint32_t n_items = *A.ovf_n;
   if (A.xcd && blockIdx.x == 0 && tid < 8) A.xq[9 + tid] = 0;   // queue heads, for a rerun
   for (;;) {
@@ -819,6 +921,7 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
       sh.item = atomicAdd(A.ovf_next, 1u);
       sh.count = 0;
       sh.ovf = 0;
+      sh.chunk = 0;
       sh.w_pull = sh.w_expand = sh.w_rows = 0;
     }
     __syncthreads();
@@ -846,3 +949,4 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
     __syncthreads();
   }
 }
+#undef LSNEW_PTR

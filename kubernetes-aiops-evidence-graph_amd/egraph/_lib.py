@@ -143,6 +143,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_dedup_extend": (C.c_int, [P, P, I64, I64, I64, P, P]),
     "egr_dedup_stats": (C.c_int, [P, I64, PI64]),
     "egr_dedup_compact": (C.c_int, [P, I64, I64]),
+    "egr_topk": (C.c_int, [P, P, P, I32, I32, I32, P, P, P]),
 }
 
 

@@ -519,15 +519,16 @@ class Frontier:
         return d
 
     def phase_times(self, stream=None) -> np.ndarray | None:
-        """[B, slots, 1 + waves] s_memrealtime stamps (100 MHz): per phase boundary the stamp
-        after the barrier, then each wave's stamp before it; None when the frontier was
-        created without $EGRAPH_FRONTIER_PROFILE."""
-        cap = self.B * 32 * 64
+        """[B, 40, 1 + waves] s_memrealtime stamps (100 MHz): per phase boundary the stamp
+        after the barrier, then each wave's stamp before it (slot 20: the column's member
+        count; slots 24-35: per-wave sub-step sums of the last pull); None when the frontier
+        was created without $EGRAPH_FRONTIER_PROFILE."""
+        cap = self.B * 40 * 64
         out = np.zeros(cap, np.int64)
         slots = L.lib.egr_frontier_phase_times(self._h, _addr(out), cap, self._st(stream))
         if slots < 0:
             L.check(slots, "egr_frontier_phase_times")
-        return out[: self.B * slots].reshape(self.B, 32, -1) if slots > 0 else None
+        return out[: self.B * slots].reshape(self.B, 40, -1) if slots > 0 else None
 
     def read_scores(self, stream=None) -> torch.Tensor:
         out = torch.empty(self.snap.n_vertices * self.B, dtype=torch.float32, device=self.dev)

@@ -64,6 +64,23 @@ class RulesDeviceBatch:
             self.cat.table, L.ptr(self.flags), L.ptr(self.vocab), L.ptr(self.node),
             L.ptr(self.err), L.ptr(self.seg), self.B, self._out, st), "egr_rules_eval")
 
+    def evaluate_op(self) -> RulesResult:
+        """One evaluation through the registered custom op (torch.ops.egraph.rules_eval, the
+        same egr_rules_eval on the current stream, fresh output tensors) -> host results."""
+        from . import ops
+        outs = ops.rules_eval(self.flags, self.vocab, self.node, self.err, self.seg,
+                              self._table_tensor())
+        B = self.B
+        h = [t.cpu().numpy() for t in outs]
+        return RulesResult(h[0][:B].view(np.uint32), h[1][:B], h[2], h[3], h[4], h[5], h[6])
+
+    def _table_tensor(self) -> torch.Tensor:
+        t = getattr(self.cat, "_table_tensor", None)
+        if t is None:
+            from . import ops
+            t = self.cat._table_tensor = ops.rule_table_tensor(self.cat)
+        return t
+
     def fetch(self) -> RulesResult:
         """Copy the outputs to the host (synchronises with the current stream)."""
         S = self.cat.n_rules + 1

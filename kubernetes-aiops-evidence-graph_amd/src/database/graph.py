@@ -31,6 +31,7 @@ import threading
 
 import torch
 
+from egraph import ops
 from egraph.device import to_device
 from egraph.graph import EvidenceGraph
 from egraph.seeds import seeds_for_batch
@@ -158,11 +159,12 @@ class GraphService:
         sv, sc, ss = seeds_for_batch(g, evidence_lists)
         fr = cls._frontier(len(keys), len(sv), k)
         dev = fr.dev
-        fr.set_seeds(to_device(sv, dev), to_device(sc, dev), to_device(ss, dev))
         src = torch.tensor(keys, dtype=torch.int32, device=dev)   # -1 = EGR_NO_NODE: no column
         labels = g.labels()
         inc = labels.index("Incident") if "Incident" in labels else -1
-        ids, scores = fr.run(src, hops=hops, exclude_label=inc)
+        # torch.ops.egraph.frontier_run: the registered custom op (seeds + run of the frontier)
+        ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
+                                       to_device(ss, dev), src, hops, inc)
         ids = ids.cpu().numpy().view("uint32")
         scores = scores.cpu().numpy()
         vlabel, _, _, _ = g.export()

@@ -8,7 +8,8 @@ matches).  Additive batch entry points put many incidents into one kernel launch
 (generate + HypothesisRanker.rank fused, as the workflow runs them back to back).
 
 All signal extraction, rule matching, confidence, ranking and ordering run in
-egr_rules_eval (csrc/rules.hip); the host encodes rows and assembles dicts in native code
+egr_rules_eval (csrc/rules.hip), called as the custom op torch.ops.egraph.rules_eval
+(egraph/ops.py); the host encodes rows and assembles dicts in native code
 (csrc/pyhost.c: encode_rows, assemble).  There is no CPU
 fallback: without a ROCm GPU the call raises RuntimeError.
 """
@@ -47,9 +48,8 @@ class RulesEngine:
                                 enc.evidence_ids, ranked)
 
     def _launch_fetch(self, enc):
-        batch = RulesDeviceBatch(enc, self.catalog, self.device)
-        batch.launch()
-        return batch.fetch()
+        # torch.ops.egraph.rules_eval: the registered custom op over egr_rules_eval
+        return RulesDeviceBatch(enc, self.catalog, self.device).evaluate_op()
 
     async def generate_hypotheses(self, incident, evidence: list[dict]) -> list[dict]:
         """Generate hypotheses by matching evidence against rules (rules_engine.py:199-233)."""

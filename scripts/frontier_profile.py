@@ -38,7 +38,10 @@ def main():
     for _ in range(3):
         bench.step_frontier(ctx, args.hops)
     torch.cuda.synchronize()
-    full = ctx["frontier"].phase_times().astype(np.float64) * 10.0 / 1000.0   # -> us
+    raw = ctx["frontier"].phase_times()
+    members = raw[:, 20, 0].astype(np.int64)
+    full = raw.astype(np.float64) * 10.0 / 1000.0   # -> us
+    full[:, 20, 0] = 0
     t = full[:, :, 0]
     wv = full[:, :, 1:]
     H = args.hops
@@ -46,7 +49,7 @@ def main():
     for h in range(H):
         names += [f"pull{h}", f"copy+seed{h}"]
     names += ["topk(wave)", "merge+pool", "end"]
-    used = int((t[0, :24] > 0).sum())
+    used = int((t[0, :20] > 0).sum())
     d = np.diff(t[:, : used], axis=1)
     rep = {}
     for i in range(used - 1):
@@ -67,11 +70,16 @@ def main():
             nm = names[i - 1] if i - 1 < len(names) else f"slot{i}"
             print(f"{nm:>12}: spread mean {spread.mean():7.2f} p99 {np.percentile(spread, 99):7.2f}"
                   f"  barrier-exit mean {exitlat.mean():6.2f} us")
-    sub = wv[:, 24:32, :]
+    sub = wv[:, 24:36, :]
     if (sub > 0).any():
-        print("last pull, per-wave sums (us): member+row_ptr / light rows (rest) / hub rows / "
-              "store / light loads / light probes / light chain / light inserts:",
-              " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(8)))
+        print("last pull, per-wave sums (us): member+row_ptr / light rows (rest) / hub rows (rest)"
+              " / store / light loads / light probes / light chain / light inserts / hub loads / "
+              "hub probes / hub chain / hub inserts:",
+              " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(12)))
+    q = np.percentile(members, [50, 90, 99, 99.9, 100])
+    print("members per column: mean %.0f p50 %d p90 %d p99 %d p99.9 %d max %d; > 768: %.1f %%, "
+          "> 1024: %.1f %%" % (members.mean(), *q, 100 * (members > 768).mean(),
+                               100 * (members > 1024).mean()))
     total = t[:, used - 1] - t[:, 0]
     start = t[:, 0] - t[:, 0].min()
     end = t[:, used - 1] - t[:, 0].min()

@@ -111,3 +111,14 @@ def test_dangling_edges_dropped_and_counts_are_attempts():
     assert g.create_relations_batch(rels) == 3          # attempted, like neo4j.py:166
     assert g.num_edges == 1                              # dedup + dangling SCHEDULED_ON dropped
     assert g.node_props[("Pod", "pod:a")]["id"] == "pod:a"
+
+
+def test_custom_ops_registered():
+    """lib/_egraph_ops.so registers torch.ops.egraph.* (CPU: schemas only, no CPU kernels)."""
+    import torch
+    from egraph import ops
+    for name in ops.OPS:
+        assert hasattr(torch.ops.egraph, name), name
+    assert "Tensor rule_table" in str(torch.ops.egraph.rules_eval.default._schema)
+    with pytest.raises(NotImplementedError):       # device kernels only: no CPU fallback
+        torch.ops.egraph.reach(1, torch.zeros(4, dtype=torch.int32), 10, 3)
