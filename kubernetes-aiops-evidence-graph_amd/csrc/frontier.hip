@@ -103,6 +103,31 @@ struct FArgs {
   unsigned long long* stats;
 };
 
+// A/B switches of the frontier kernels (defaults = the shipped configuration)
+// walk chunking (frontier_body.h row_phase): 0 = static striping over the waves, 1 = chunks
+// taken from an LDS counter, members strided over the chunks, 2 = the same, contiguous chunks
+#ifndef EGR_FR_DYN
+#define EGR_FR_DYN 0
+#endif
+// hub rows: 1 = the next 64-entry segment's loads issued before the current one is probed
+#ifndef EGR_FR_HUBPF
+#define EGR_FR_HUBPF 0
+#endif
+// hub-row fmaf chains of the narrow kernel (frontier_body.h hub_chain): 0 = ballot loop over
+// the present entries, 1 = unrolled v_readlane chain over every entry, 2 = pairs through LDS,
+// one lane chains (2: +4 % at three batches in flight, profiles/r02_ab_hubchain.txt)
+#ifndef EGR_FR_HUBCHAIN
+#define EGR_FR_HUBCHAIN 2
+#endif
+// light rows probe the Bloom filter before the buckets (0: straight to the buckets)
+#ifndef EGR_FR_LBLOOM
+#define EGR_FR_LBLOOM 1
+#endif
+// narrow table slots hold (key, score) side by side: a probe returns the score (frontier_body.h)
+#ifndef EGR_FR_NARROW_KV
+#define EGR_FR_NARROW_KV 0
+#endif
+
 // Two instantiations of the kernels (frontier_body.h): the wide table keeps every member of a
 // column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
 // one serves the pruned top-k runs (~0.6k members per column on C3), whose 28 KB of LDS and
@@ -114,6 +139,8 @@ namespace fr_wide {
 #define FR_BLOOM_LOG 16
 #define FR_WAVES_PER_EU 4
 #define FR_LSNEW 0
+#define FR_KV 0
+#define FR_HUBCHAIN 1
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -121,6 +148,8 @@ namespace fr_wide {
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
 #undef FR_LSNEW
+#undef FR_KV
+#undef FR_HUBCHAIN
 }  // namespace fr_wide
 
 namespace fr_narrow {
@@ -131,15 +160,6 @@ namespace fr_narrow {
 #define EGR_FR_NARROW_BLOOM_LOG 15
 #define EGR_FR_NARROW_WAVES_PER_EU 5
 #endif
-// walk chunking (frontier_body.h row_phase): 0 = static striping over the waves, 1 = chunks
-// taken from an LDS counter, members strided over the chunks, 2 = the same, contiguous chunks
-#ifndef EGR_FR_DYN
-#define EGR_FR_DYN 0
-#endif
-// hub rows: 1 = the next 64-entry segment's loads issued before the current one is probed
-#ifndef EGR_FR_HUBPF
-#define EGR_FR_HUBPF 0
-#endif
 #ifndef EGR_FR_NARROW_LSNEW
 #define EGR_FR_NARROW_LSNEW 0
 #endif
@@ -149,6 +169,8 @@ namespace fr_narrow {
 #define FR_BLOOM_LOG EGR_FR_NARROW_BLOOM_LOG
 #define FR_WAVES_PER_EU EGR_FR_NARROW_WAVES_PER_EU
 #define FR_LSNEW EGR_FR_NARROW_LSNEW
+#define FR_KV EGR_FR_NARROW_KV
+#define FR_HUBCHAIN EGR_FR_HUBCHAIN
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -156,6 +178,8 @@ namespace fr_narrow {
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
 #undef FR_LSNEW
+#undef FR_KV
+#undef FR_HUBCHAIN
 }  // namespace fr_narrow
 
 // The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
@@ -170,6 +194,8 @@ namespace fr_fallback {
 #define FR_BLOOM_LOG 10
 #define FR_WAVES_PER_EU 4
 #define FR_LSNEW 0
+#define FR_KV 0
+#define FR_HUBCHAIN 2
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -177,6 +203,8 @@ namespace fr_fallback {
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
 #undef FR_LSNEW
+#undef FR_KV
+#undef FR_HUBCHAIN
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)

@@ -4,7 +4,8 @@
 // Geometry of this instantiation (set by the includer, csrc/frontier.hip):
 //   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
 //   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU,
-//   FR_LSNEW (1: the pull results live in LDS instead of HBM).
+//   FR_LSNEW (1: the pull results live in LDS instead of HBM), FR_KV (1: the LDS table keeps
+//   each slot's key and score side by side, so one probe returns the score), FR_HUBCHAIN.
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -22,9 +23,12 @@ static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometr
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
 // insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
 // index.
+// FR_KV: the LDS table stores slot p's key at keys[2p] and its score at keys[2p+1], so the
+// probe that finds a key (a 32-B bucket read) also returns its score; otherwise keys[p], s[p].
 template <bool GT>
 struct Tab {
   using MT = typename std::conditional<GT, uint32_t, uint16_t>::type;
+  static constexpr bool KV = !GT && FR_KV;
   uint32_t* keys;
   float* s;
   uint8_t* fl;
@@ -36,6 +40,26 @@ struct Tab {
   uint32_t* ovf;    // LDS
   uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
   uint32_t* chunk;  // LDS: the next chunk of a walk (dynamic chunk assignment), 0 at its start
+  float2* chain;    // LDS: per-wave hub-chain scratch [NWAVES][64] (EGR_FR_HUBCHAIN 2), or null
+
+  __device__ __forceinline__ uint32_t* keyp(uint32_t p) const { return KV ? keys + 2 * p : keys + p; }
+  __device__ __forceinline__ float* sp(uint32_t p) const {
+    return KV ? reinterpret_cast<float*>(keys) + 2 * p + 1 : s + p;
+  }
+  __device__ __forceinline__ uint32_t key(uint32_t p) const { return *keyp(p); }
+  __device__ __forceinline__ float& sc(uint32_t p) const { return *sp(p); }
+  // the keys of bucket bk's 4 slots (KV: and their scores, into *s4)
+  __device__ __forceinline__ uint4 bucket(uint32_t bk, uint4* s4 = nullptr) const {
+    if constexpr (KV) {
+      const uint4* q = reinterpret_cast<const uint4*>(keys) + 2 * bk;
+      const uint4 a = q[0], b = q[1];
+      if (s4) *s4 = make_uint4(a.y, a.w, b.y, b.w);
+      return make_uint4(a.x, a.z, b.x, b.z);
+    } else {
+      (void)s4;
+      return reinterpret_cast<const uint4*>(keys)[bk];
+    }
+  }
 };
 
 // Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
@@ -58,10 +82,6 @@ __device__ __forceinline__ uint32_t hbucket(uint32_t v, uint32_t nb) {
   return (uint32_t)__umul24((h >> 8) & 0xFFFFu, nb) >> 16;
 }
 
-__device__ __forceinline__ uint4 read_bucket(const uint32_t* keys, uint32_t bk) {
-  return reinterpret_cast<const uint4*>(keys)[bk];
-}
-
 // outcome of one bucket read for key v: slot (>= 0), -1 = absent, -2 = continue probing
 __device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_t bk) {
   if (kk.x == v) return (int)(4 * bk);
@@ -82,14 +102,14 @@ __device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
   const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
-    uint4 kk = read_bucket(t.keys, bk);
+    uint4 kk = t.bucket(bk);
     uint32_t ks[4] = {kk.x, kk.y, kk.z, kk.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (ks[j] == v) return (int)(4 * bk + j);
       if (ks[j] == EMPTY) {
         const uint32_t p = 4 * bk + j;
-        const uint32_t old = atomicCAS(&t.keys[p], EMPTY, v);
+        const uint32_t old = atomicCAS(t.keyp(p), EMPTY, v);
         if (old == EMPTY) {
           if constexpr (!GT) {
             const uint32_t h = bloom_hash(v);
@@ -120,7 +140,7 @@ __device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
   const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
-    const int r = bucket_match(read_bucket(t.keys, bk), v, bk);
+    const int r = bucket_match(t.bucket(bk), v, bk);
     if (r != -2) return r;
     bk = bk + 1 == nb ? 0 : bk + 1;
   }
@@ -157,7 +177,7 @@ struct Ticker {
 // still unresolved, so a lane's NQ probe sequences share round trips.
 template <bool GT, int NQ>
 __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
-                                           int (&q)[NQ]) {
+                                           int (&q)[NQ], float (&val)[NQ]) {
   const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk[NQ];
   uint32_t pend = 0;
@@ -167,8 +187,8 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
     q[x] = -1;
     if ((uint32_t)x < nq) pend |= 1u << x;
   }
-  if constexpr (!GT) {
-    // the filter: a key whose bit is clear is not a member (most pulled neighbours are not)
+  if constexpr (!GT && EGR_FR_LBLOOM) {
+    // the filter: a key whose bit is clear is not a member
     uint32_t bw[NQ];
 #pragma unroll
     for (int x = 0; x < NQ; ++x)
@@ -177,17 +197,25 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
     for (int x = 0; x < NQ; ++x)
       if (!((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u)) pend &= ~(1u << x);
   }
+#pragma unroll
+  for (int x = 0; x < NQ; ++x) val[x] = 0.f;
   for (uint32_t n = 0; n < nb && __any(pend != 0); ++n) {
-    uint4 kk[NQ];
+    uint4 kk[NQ], ss[NQ];
 #pragma unroll
     for (int x = 0; x < NQ; ++x)
-      if (pend & (1u << x)) kk[x] = read_bucket(t.keys, bk[x]);
+      if (pend & (1u << x)) kk[x] = t.bucket(bk[x], &ss[x]);
 #pragma unroll
     for (int x = 0; x < NQ; ++x) {
       if (pend & (1u << x)) {
         const int r = bucket_match(kk[x], key[x], bk[x]);
         if (r != -2) {
           q[x] = r;
+          if constexpr (Tab<GT>::KV) {
+            if (r >= 0) {
+              const uint32_t j = (uint32_t)r & 3u;
+              val[x] = __uint_as_float(j == 0 ? ss[x].x : j == 1 ? ss[x].y : j == 2 ? ss[x].z : ss[x].w);
+            }
+          }
           pend &= ~(1u << x);
         } else {
           bk[x] = bk[x] + 1 == nb ? 0 : bk[x] + 1;
@@ -254,12 +282,14 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
 #pragma unroll
     for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
     int q[LB];
-    find_batch<GT, LB>(t, key, nq, q);
+    float xs[LB];
+    find_batch<GT, LB>(t, key, nq, q, xs);
     tk.tick(5);
     if (kind & K_PULL) {
-      float xs[LB];
+      if constexpr (!Tab<GT>::KV) {
 #pragma unroll
-      for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
+        for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
+      }
 #pragma unroll
       for (int x = 0; x < LB; ++x)
         if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
@@ -276,6 +306,59 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
 
 __device__ __forceinline__ float readlane_f(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+// The in-order fmaf chain of one hub-row segment: lane j holds entry j's (w, x) (x of an
+// absent neighbour is +0: fmaf(w, +0, acc) == acc for finite w and acc != -0, so running the
+// chain over every entry equals running it over the present ones).  `rem` = entries left in
+// the row (>= 1, wave-uniform); the result is in every lane (HUBCHAIN 0/1) or in lane m (2).
+//   EGR_FR_HUBCHAIN 0: over the present entries only, v_readlane at a ballot-chosen lane
+//   EGR_FR_HUBCHAIN 1: every entry, unrolled by 8 with immediate lane indices
+//   EGR_FR_HUBCHAIN 2: the pairs go through the wave's LDS scratch and lane m runs the chain
+//                      from 16-B LDS reads (one lane, 4-cycle dependent fmas)
+__device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32_t rem, int m,
+                                          float& hacc, float2* chain) {
+  const int lane = threadIdx.x & 63;
+#if FR_HUBCHAIN == 0
+  (void)rem; (void)m; (void)chain; (void)lane;
+  for (uint64_t fm = __ballot(present); fm; fm &= fm - 1) {
+    const int y = __ffsll((long long)fm) - 1;
+    hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
+  }
+#elif FR_HUBCHAIN == 1
+  (void)present; (void)m; (void)chain; (void)lane;
+  const float xw = present ? w : 0.f;
+  const int n = (int)min(rem, 64u);
+  for (int y0 = 0; y0 < n; y0 += 8) {
+#pragma unroll
+    for (int y = 0; y < 8; ++y) hacc = fmaf(readlane_f(xw, y0 + y), readlane_f(x, y0 + y), hacc);
+  }
+#else
+  (void)present;
+  chain[lane] = make_float2(present ? w : 0.f, x);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane == m) {
+    const float4* c4 = reinterpret_cast<const float4*>(chain);
+    const int n2 = (int)((min(rem, 64u) + 1) / 2);
+    float a = hacc;
+    for (int y0 = 0; y0 < n2; y0 += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) p[y] = c4[y0 + y];     // (past n2: stale pairs of lanes >= rem,
+#pragma unroll                                           //  all (0, +0) or beyond the chain)
+      for (int y = 0; y < 4; ++y) {
+        if (y0 + y < n2) {
+          a = fmaf(p[y].x, p[y].y, a);
+          a = fmaf(p[y].z, p[y].w, a);
+        }
+      }
+    }
+    hacc = a;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#endif
 }
 
 // One pass over the members [0, n) present when it starts, a wave taking 64 at a time.
@@ -310,6 +393,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   const bool reach_lvl = h + REACH_AHEAD + 1 <= A.hops;
   const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
   const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
+  float2* const chain = t.chain ? t.chain + wave * 64 : nullptr;
   auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
   // Work split.  A walk is cut into chunks of 64 members; chunk c holds the members
   // c + nch * lane (nch = number of chunks), so vertices inserted together (e.g. the incident's
@@ -343,7 +427,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         p = 0;
       }
 #endif
-      v = t.keys[p];
+      v = t.key(p);
       const uint8_t f = t.fl[p];
       if (reach_lvl && (f & FL_DEPTH) == reach_fl) ch.kind |= K_REACH;
       if constexpr (PH == SEEDS) {
@@ -412,12 +496,8 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         tk.tick(9);
         if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
-          const float x = q >= 0 ? t.s[q] : 0.f;
-          // the chain runs over the present entries only, in lane (= CSR) order
-          for (uint64_t fm = __ballot(q >= 0); fm; fm &= fm - 1) {
-            const int y = __ffsll((long long)fm) - 1;
-            hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
-          }
+          const float x = q >= 0 ? t.sc(q) : 0.f;
+          hub_chain(w, x, q >= 0, hdeg - base, m, hacc, chain);
         }
         tk.tick(10);
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
@@ -460,12 +540,8 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         const int q = act ? tab_find<GT>(t, u) : -1;
         if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
-          const float x = q >= 0 ? t.s[q] : 0.f;
-          // the chain runs over the present entries only, in lane (= CSR) order
-          for (uint64_t fm = __ballot(q >= 0); fm; fm &= fm - 1) {
-            const int y = __ffsll((long long)fm) - 1;
-            hacc = fmaf(readlane_f(w, y), readlane_f(x, y), hacc);
-          }
+          const float x = q >= 0 ? t.sc(q) : 0.f;
+          hub_chain(w, x, q >= 0, hdeg - base, m, hacc, chain);
         }
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
         if (m2 != m) {            // the row is complete
@@ -537,6 +613,12 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
 
 struct Shared {
   uint32_t count, ovf, item, chunk;
+#if FR_HUBCHAIN == 2
+  float2 chain[NWAVES][64];     // hub-row chain pairs, one row per wave
+#define SH_CHAIN (&sh.chain[0][0])
+#else
+#define SH_CHAIN nullptr
+#endif
   unsigned long long base;
   uint64_t top[NWAVES][KMAXF];
   uint32_t w_pull, w_expand, w_rows;
@@ -549,10 +631,10 @@ __device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, u
   if (p >= t.cap) return 0;
   const uint8_t f = t.fl[p] & FL_DEPTH;
   if (f < 1 || f > maxd) return 0;
-  const uint32_t v = t.keys[p];
+  const uint32_t v = t.key(p);
   if (v >= A.V) return 0;
   if (A.exclude >= 0 && A.vlabel[v] == (uint8_t)A.exclude) return 0;
-  return topk_key(t.s[p], v);
+  return topk_key(t.sc(p), v);
 }
 
 // This thread's best candidate key strictly below `bound` (global variant: rescans).
@@ -652,7 +734,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   for (uint32_t i = sb + tid; i < se; i += FT) {
     const int q = tab_insert<GT>(t, A.seed_vert[i]);
     if (q >= 0) {
-      t.s[q] = -INFINITY;               // every writer writes the same
+      t.sc(q) = -INFINITY;              // every writer writes the same
       t.fl[q] = FL_SEED;
     }
   }
@@ -660,7 +742,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   for (uint32_t i = sb + tid; i < se; i += FT) {
     const int q = tab_find<GT>(t, A.seed_vert[i]);
     if (q < 0) continue;
-    unsigned int* sp = reinterpret_cast<unsigned int*>(&t.s[q]);
+    unsigned int* sp = reinterpret_cast<unsigned int*>(t.sp(q));
     unsigned int old = *sp;
     for (;;) {
       const float m = fmaxf(__uint_as_float(old), A.seed_val[i]);
@@ -678,7 +760,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
       const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
                                     (uint32_t)FL_CLAIM << sh8);
-      if (!((old >> sh8) & FL_CLAIM)) r = make_uint2((uint32_t)q, __float_as_uint(t.s[q]));
+      if (!((old >> sh8) & FL_CLAIM)) r = make_uint2((uint32_t)q, __float_as_uint(t.sc(q)));
     }
     A.seed_rep[i] = r;
   }
@@ -733,13 +815,13 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       const uint8_t nd = t.need[p], f = t.fl[p];
       const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
                           (!prune_now || cand_depth(f, hops));
-      t.s[p] = pulled ? t.snew[i] : 0.f;
+      t.sc(p) = pulled ? t.snew[i] : 0.f;
       if (nd & bit) t.need[p] = nd & ~bit;
     }
     __syncthreads();
     for (uint32_t i = sb + tid; i < se; i += FT) {
       const uint2 r = A.seed_rep[i];
-      if (r.x != NO_NODE) t.s[r.x] = t.s[r.x] + __uint_as_float(r.y);
+      if (r.x != NO_NODE) t.sc(r.x) = t.sc(r.x) + __uint_as_float(r.y);
     }
     __syncthreads();
     stamp();
@@ -795,8 +877,8 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   if (keep) {
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
-      A.pool_v[base + i] = t.keys[p];
-      A.pool_s[base + i] = t.s[p];
+      A.pool_v[base + i] = t.key(p);
+      A.pool_s[base + i] = t.sc(p);
       A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
     }
   }
@@ -815,8 +897,12 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
 
 // The LDS table of one workgroup (static shared memory of the kernel that declares it).
 struct LdsTab {
+#if FR_KV
+  uint32_t keys[2 * LCAP];     // (key, score bits) per slot
+#else
   uint32_t keys[LCAP];
   float s[LCAP];
+#endif
   uint32_t flw[LCAP / 4];
   uint32_t needw[LCAP / 4];
   uint16_t mlist[LLIMIT];
@@ -825,6 +911,11 @@ struct LdsTab {
   float snew[LLIMIT];          // pull results by member index (FR_LSNEW: in LDS, not HBM)
 #endif
 };
+#if FR_KV
+#define LDS_S_PTR nullptr
+#else
+#define LDS_S_PTR L.s
+#endif
 #if FR_LSNEW
 #define LSNEW_PTR L.snew
 #else
@@ -837,8 +928,12 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   for (uint32_t i = tid; i < BLOOM_WORDS; i += FT) L.bloom[i] = 0;
 #pragma unroll
   for (int i = 0; i < LPPT; ++i) {
+#if FR_KV
+    reinterpret_cast<uint2*>(L.keys)[tid + i * FT] = make_uint2(EMPTY, 0u);
+#else
     L.keys[tid + i * FT] = EMPTY;
     L.s[tid + i * FT] = 0.f;
+#endif
   }
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.flw[i] = 0;
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.needw[i] = 0;
@@ -849,8 +944,8 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
-  Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, &sh.chunk};
+  Tab<false> t{L.keys, LDS_S_PTR, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
+               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, &sh.chunk, SH_CHAIN};
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
@@ -913,7 +1008,7 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   Tab<true> t{A.gkeys + blockIdx.x * cap, A.gs + blockIdx.x * cap, A.gfl + blockIdx.x * cap,
               A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
               A.gsnew + (size_t)blockIdx.x * A.V, (uint32_t)cap, A.V, &sh.count, &sh.ovf, nullptr,
-              &sh.chunk};
+              &sh.chunk, SH_CHAIN};
   const uint32_t n_items = *A.ovf_n;
   if (A.xcd && blockIdx.x == 0 && tid < 8) A.xq[9 + tid] = 0;   // queue heads, for a rerun
   for (;;) {
@@ -941,8 +1036,8 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
       if (p >= cap) continue;
-      t.keys[p] = EMPTY;
-      t.s[p] = 0.f;
+      *t.keyp(p) = EMPTY;
+      t.sc(p) = 0.f;
       t.fl[p] = 0;
       t.need[p] = 0;
     }
@@ -950,3 +1045,5 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   }
 }
 #undef LSNEW_PTR
+#undef SH_CHAIN
+#undef LDS_S_PTR
