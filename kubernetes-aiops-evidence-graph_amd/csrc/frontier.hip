@@ -48,6 +48,7 @@ constexpr int KMAXF = 16;
 constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
 constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
 constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
+constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
 constexpr int MAX_HOPS = 60;
 constexpr int PROF_SLOTS = 40;
 
@@ -122,6 +123,10 @@ struct FArgs {
 // light rows probe the Bloom filter before the buckets (0: straight to the buckets)
 #ifndef EGR_FR_LBLOOM
 #define EGR_FR_LBLOOM 1
+#endif
+// the copy after a pull: 1 = a thread's members' loads issued together (unrolled over MPT)
+#ifndef EGR_FR_COPYU
+#define EGR_FR_COPYU 0
 #endif
 // narrow table slots hold (key, score) side by side: a probe returns the score (frontier_body.h)
 #ifndef EGR_FR_NARROW_KV

@@ -633,7 +633,7 @@ __device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, u
   if (f < 1 || f > maxd) return 0;
   const uint32_t v = t.key(p);
   if (v >= A.V) return 0;
-  if (A.exclude >= 0 && A.vlabel[v] == (uint8_t)A.exclude) return 0;
+  if (A.exclude >= 0 && (t.need[p] & NEED_EXCL)) return 0;   // marked after the last pull
   return topk_key(t.sc(p), v);
 }
 
@@ -728,61 +728,68 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   stamp();
-  // seeds: insert (s = -inf), max-combine duplicates (fmaxf, like the dense plan's seed prep),
-  // then one entry per vertex claims it and records (slot, s0) for the per-hop seed add
+  // The incident vertex and its row (reach level 1) are loaded first: their latency hides
+  // behind the seed passes.
+  const uint32_t src = A.sources[b];
+  const bool src_ok = A.hops >= 1 && src < A.V;
+  const uint32_t ie0 = src_ok ? A.row_ptr[src] : 0u, ie1 = src_ok ? A.row_ptr[src + 1] : 0u;
+  const uint32_t ic0 = ie0 + tid < ie1 ? A.cv[ie0 + tid].x : 0u;   // first stripe of the row
+  // Seeds, two passes.  Pass 1 inserts every seed vertex and max-combines duplicate entries
+  // with one atomicMax on the order-preserving u32 image of the value (ord(): the cleared
+  // slot's 0 lies below every float's image, -inf included) -- fmaxf, like the dense plan's
+  // seed prep.  Pass 2: one entry per vertex claims it, turns the slot back into the float and
+  // records (slot, s0) for the per-hop seed add; thread 0 also inserts the incident vertex.
   const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
-  for (uint32_t i = sb + tid; i < se; i += FT) {
-    const int q = tab_insert<GT>(t, A.seed_vert[i]);
+  auto ord = [](float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  };
+  auto unord = [](uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+  };
+  const uint32_t i0 = sb + tid;
+  const uint32_t v0 = i0 < se ? A.seed_vert[i0] : 0u;   // the first stripe stays in registers
+  const float x0 = i0 < se ? A.seed_val[i0] : 0.f;
+  for (uint32_t i = i0; i < se; i += FT) {
+    const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
+    const float x = i == i0 ? x0 : A.seed_val[i];
+    const int q = tab_insert<GT>(t, v);
     if (q >= 0) {
-      t.sc(q) = -INFINITY;              // every writer writes the same
-      t.fl[q] = FL_SEED;
+      atomicMax(reinterpret_cast<unsigned int*>(t.sp(q)), ord(x));
+      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
+               (uint32_t)FL_SEED << (((uint32_t)q & 3u) * 8u));
     }
   }
   __syncthreads();
-  for (uint32_t i = sb + tid; i < se; i += FT) {
-    const int q = tab_find<GT>(t, A.seed_vert[i]);
-    if (q < 0) continue;
-    unsigned int* sp = reinterpret_cast<unsigned int*>(t.sp(q));
-    unsigned int old = *sp;
-    for (;;) {
-      const float m = fmaxf(__uint_as_float(old), A.seed_val[i]);
-      if (__float_as_uint(m) == old) break;
-      const unsigned int got = atomicCAS(sp, old, __float_as_uint(m));
-      if (got == old) break;
-      old = got;
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = sb + tid; i < se; i += FT) {
-    const int q = tab_find<GT>(t, A.seed_vert[i]);
+  for (uint32_t i = i0; i < se; i += FT) {
+    const int q = tab_find<GT>(t, i == i0 ? v0 : A.seed_vert[i]);
     uint2 r = make_uint2(NO_NODE, 0u);
     if (q >= 0) {
       const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
       const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
                                     (uint32_t)FL_CLAIM << sh8);
-      if (!((old >> sh8) & FL_CLAIM)) r = make_uint2((uint32_t)q, __float_as_uint(t.sc(q)));
+      if (!((old >> sh8) & FL_CLAIM)) {        // the claimer alone touches the value now
+        const float s0 = unord(*reinterpret_cast<unsigned int*>(t.sp(q)));
+        t.sc(q) = s0;
+        r = make_uint2((uint32_t)q, __float_as_uint(s0));
+      }
     }
     A.seed_rep[i] = r;
   }
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t src = A.sources[b];
-    if (src < A.V) {
-      const int q = tab_insert<GT>(t, src);
-      if (q >= 0) t.fl[q] |= 1;
-    }
+  if (tid == 0 && src_ok) {       // (a find of a seed is unaffected by concurrent inserts)
+    const int q = tab_insert<GT>(t, src);
+    if (q >= 0)
+      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2), 1u << (((uint32_t)q & 3u) * 8u));
   }
   __syncthreads();
   // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
-  if (A.hops >= 1 && A.sources[b] < A.V) {
-    const uint32_t src = A.sources[b];
-    const uint32_t e0 = A.row_ptr[src], e1 = A.row_ptr[src + 1];
+  if (src_ok) {
     if (tid == 0) {
       ++work.rows;
-      work.expand += e1 - e0;
+      work.expand += ie1 - ie0;
     }
-    for (uint32_t e = e0 + tid; e < e1; e += FT) {
-      const int q = tab_insert<GT>(t, A.cv[e].x);
+    for (uint32_t e = ie0 + tid; e < ie1; e += FT) {
+      const int q = tab_insert<GT>(t, e == ie0 + tid ? ic0 : A.cv[e].x);
       if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
     }
   }
@@ -808,18 +815,60 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
     // (pruned last pull: a non-candidate was not pulled and keeps +0; nothing reads it)
     const uint32_t n = cnt, bit = 1u << ((uint32_t)h & 1u);
-    const bool prune_now = A.prune && h == hops - 1;
-    for (uint32_t i = tid; i < n; i += FT) {
-      const uint32_t p = t.mlist[i];
-      if (p >= t.cap) continue;
-      const uint8_t nd = t.need[p], f = t.fl[p];
+    const bool last = h == hops - 1;
+    const bool prune_now = A.prune && last;
+    // after the last pull, a candidate carrying the excluded label is marked NEED_EXCL for
+    // top-k; its label load is issued beside the member's pull-result load
+    const bool mark_excl = last && A.exclude >= 0;
+    // this thread's first seed entry: its load is issued beside the copy's loads
+    const uint32_t ir = sb + tid;
+    const uint2 r0 = ir < se ? A.seed_rep[ir] : make_uint2(NO_NODE, 0u);
+    auto copy_one = [&](uint32_t i, uint32_t p, uint8_t nd, uint8_t f, float sn, uint8_t lab) {
       const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
                           (!prune_now || cand_depth(f, hops));
-      t.sc(p) = pulled ? t.snew[i] : 0.f;
-      if (nd & bit) t.need[p] = nd & ~bit;
+      t.sc(p) = pulled ? sn : 0.f;
+      uint8_t nn = nd & ~bit;
+      if (mark_excl && cand_depth(f, hops) && lab == (uint8_t)A.exclude) nn |= NEED_EXCL;
+      if (nn != nd) t.need[p] = nn;
+    };
+    if constexpr (!GT && EGR_FR_COPYU) {
+      // every member of this thread at once (n <= LLIMIT): LDS reads, then both global loads
+      // of every member in flight together, then the stores
+      uint32_t pp[MPT];
+      uint8_t nds[MPT], fls[MPT], labs[MPT];
+      float sns[MPT];
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) {
+        const uint32_t i = tid + j * FT;
+        pp[j] = i < n ? t.mlist[i] : 0xFFFFFFFFu;
+        nds[j] = 0;
+        fls[j] = 0;
+        if (pp[j] < t.cap) {
+          nds[j] = t.need[pp[j]];
+          fls[j] = t.fl[pp[j]];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) {
+        const uint32_t i = tid + j * FT;
+        sns[j] = (pp[j] < t.cap && i < n0) ? t.snew[i] : 0.f;
+        labs[j] = (mark_excl && pp[j] < t.cap && cand_depth(fls[j], hops)) ? A.vlabel[t.key(pp[j])] : 0xFF;
+      }
+#pragma unroll
+      for (int j = 0; j < MPT; ++j)
+        if (pp[j] < t.cap) copy_one(tid + j * FT, pp[j], nds[j], fls[j], sns[j], labs[j]);
+    } else {
+      for (uint32_t i = tid; i < n; i += FT) {
+        const uint32_t p = t.mlist[i];
+        if (p >= t.cap) continue;
+        const uint8_t f = t.fl[p];
+        const uint8_t lab = (mark_excl && cand_depth(f, hops)) ? A.vlabel[t.key(p)] : 0xFF;
+        copy_one(i, p, t.need[p], f, i < n0 ? t.snew[i] : 0.f, lab);
+      }
     }
     __syncthreads();
-    for (uint32_t i = sb + tid; i < se; i += FT) {
+    if (r0.x != NO_NODE) t.sc(r0.x) = t.sc(r0.x) + __uint_as_float(r0.y);
+    for (uint32_t i = ir + FT; i < se; i += FT) {
       const uint2 r = A.seed_rep[i];
       if (r.x != NO_NODE) t.sc(r.x) = t.sc(r.x) + __uint_as_float(r.y);
     }
@@ -833,26 +882,37 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   wstamp();
   __syncthreads();
   if (wave == 0) {
+    // merge by rank: each of the NWAVES * k candidates counts the candidates above it (keys
+    // are distinct: a member is in one wave's list) and lands at its rank; the slots past the
+    // number of candidates get EGR_NO_NODE / -inf
     uint64_t c[2];
+    uint32_t nnz = 0;
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
       const int cc = lane + 64 * y, w = cc / KMAXF, r = cc % KMAXF;
       c[y] = (w < NWAVES && r < A.k) ? sh.top[w][r] : 0ull;
+      nnz += (uint32_t)__popcll(__ballot(c[y] != 0));
     }
-    for (int q = 0; q < A.k; ++q) {
-      const uint64_t mine = c[0] > c[1] ? c[0] : c[1];
-      const uint64_t wb = wave_max_u64(mine);
-      if (lane == 0) {
+    uint32_t rank[2] = {0u, 0u};
+    for (int w = 0; w < NWAVES; ++w)
+      for (int r = 0; r < A.k; ++r) {
+        const uint64_t o = sh.top[w][r];
+        rank[0] += o > c[0];
+        rank[1] += o > c[1];
+      }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      if (c[y] != 0 && rank[y] < (uint32_t)A.k) {
         float sc;
         uint32_t v;
-        topk_unkey(wb, sc, v);
-        A.out_ids[(size_t)b * A.k + q] = v;
-        A.out_scores[(size_t)b * A.k + q] = sc;
+        topk_unkey(c[y], sc, v);
+        A.out_ids[(size_t)b * A.k + rank[y]] = v;
+        A.out_scores[(size_t)b * A.k + rank[y]] = sc;
       }
-      if (wb != 0) {
-        if (c[0] == wb) c[0] = 0;
-        if (c[1] == wb) c[1] = 0;
-      }
+    }
+    for (uint32_t q = nnz + lane; q < (uint32_t)A.k; q += 64) {
+      A.out_ids[(size_t)b * A.k + q] = NO_NODE;
+      A.out_scores[(size_t)b * A.k + q] = -INFINITY;
     }
   }
   stamp();
