@@ -141,12 +141,16 @@ def step_frontier(ctx, hops: int, ev=None):
     return lane
 
 
-def lane_step(lane, hops: int, inc_label: int, ev=None):
+def lane_step(lane, hops: int, inc_label: int, ev=None, fork_join: bool = False):
     """One batch on one lane (the current stream): rules on the lane's side stream, then the
-    seed preparation and the frontier run."""
+    seed preparation and the frontier run.  fork_join (graph capture): the side stream forks
+    from the current stream and joins it again after the frontier launch."""
     fr = lane["frontier"]
     side = lane["side"]
+    cur = torch.cuda.current_stream()
     if side is not None:
+        if fork_join:
+            side.wait_stream(cur)
         with torch.cuda.stream(side):
             lane["rules"].launch()
     else:
@@ -160,6 +164,41 @@ def lane_step(lane, hops: int, inc_label: int, ev=None):
         ev.done.append((a, b))
     else:
         fr.run(lane["sources"], hops, inc_label)
+    if side is not None and fork_join:
+        cur.wait_stream(side)
+
+
+def capture_lanes(ctx, hops: int, inline_rules: bool | None = None) -> None:
+    """Capture each lane's batch (rules on the side stream, seed count / scan / scatter, the
+    frontier kernel and the overflow grid) as one HIP graph: a step then costs one graph launch
+    of host time instead of seven library calls.  The captured kernels are exactly the eager
+    ones (same arguments, same buffers); the host-side state they depend on (the frontier's
+    clean-counter flags) is constant in steady state, which one eager warm-up step settles."""
+    inc = ctx["inc_label"]
+    if inline_rules is None:
+        inline_rules = bool(os.environ.get("EGRAPH_BENCH_GRAPH_INLINE_RULES"))
+    for lane in ctx["lanes"]:
+        if inline_rules:
+            lane["side"] = None                        # rules on the lane's own stream
+        st = lane["main"] if lane["main"] is not None else torch.cuda.Stream()
+        lane["cap_stream"] = st
+        with torch.cuda.stream(st):
+            lane_step(lane, hops, inc)                 # settles the clean flags
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            lane_step(lane, hops, inc, fork_join=True)
+        torch.cuda.synchronize()
+        lane["graph"] = g
+
+
+def step_graph(ctx, hops: int, ev=None):
+    """One batch = one replay of the next lane's captured graph on that lane's stream."""
+    lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
+    ctx["tick"] += 1
+    with torch.cuda.stream(lane["cap_stream"]):
+        lane["graph"].replay()
+    return lane
 
 
 class EventPool(list):
@@ -312,6 +351,25 @@ def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
             "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes}
 
 
+def roofline_probe(ctx, hops: int, reps: int) -> float:
+    """Mean duration (ms) of `reps` isolated egr_frontier_run launches of lane 0's batch, each
+    alone on the GPU (synchronised before and after), bracketed by HIP events on its stream."""
+    lane = ctx["lanes"][0]
+    fr = lane["frontier"]
+    ms = []
+    torch.cuda.synchronize()
+    for _ in range(max(reps, 1)):
+        fr.set_seeds(*lane["seeds"])
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        fr.run(lane["sources"], hops, ctx["inc_label"])
+        b.record()
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    return float(np.mean(ms))
+
+
 def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tuple[dict, dict]:
     """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
     (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
@@ -325,7 +383,13 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
     return ({"bound": "hbm", "kernel": "frontier_lds_kernel + frontier_global_kernel "
                                        "(egr_frontier_run: reach + propagation + top-k)",
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("frontier"),
+             "frac": achieved / HBM_PEAK_GBS,
+             # not HBM-bound: the 12-MB CSR stays in the Infinity Cache and the column state in
+             # LDS; FETCH_SIZE is calibrated only for 16-B coalesced streams (MI355X_MICROARCH
+             # HBM section) and counts Infinity-Cache hits, so for these 8-B gathers it is no
+             # HBM byte count (profiles/pmc_frontier.json keeps the raw counters)
+             "traffic": None, "traffic_note": "uncalibrated for 8-B gathers; Infinity-Cache "
+                                              "resident working set (DESIGN.md §4)",
              "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes,
              # with batches in flight, launches overlap: per batch the GPU delivers nbytes
              # in one step's wall time
@@ -591,6 +655,12 @@ def main():
     ap.add_argument("--storm-rate", type=int, default=100_000, help="alerts per minute")
     ap.add_argument("--storm-keys", type=int, default=10_000)
     ap.add_argument("--storm-events", type=int, default=100, help="topology events per tick")
+    ap.add_argument("--graph", action="store_true",
+                    help="frontier: replay each lane's batch as a captured HIP graph instead of "
+                         "enqueueing it eagerly (measured slower on ROCm 7: 0.116 vs 0.077 ms "
+                         "per step, profiles/r02_graph_vs_eager.txt)")
+    ap.add_argument("--roofline-reps", type=int, default=20,
+                    help="isolated frontier launches timed after the run for the roofline")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -627,8 +697,15 @@ def main():
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
+    graphs = args.engine == "frontier" and args.graph
+    if graphs:
+        capture_lanes(ctx, args.hops)
+        run_step = step_graph
+        for _ in range(args.warmup):
+            run_step(ctx, args.hops)
+        torch.cuda.synchronize(dev)
 
-    events: list = EventPool(args.steps) if args.engine == "frontier" else []
+    events: list = EventPool(args.steps) if args.engine == "frontier" and not graphs else []
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -649,11 +726,21 @@ def main():
     nnz = ctx["snap"].n_entries
     ms = elapsed / args.steps * 1e3
     timed = events.done if isinstance(events, EventPool) else events
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in timed]))
     if args.engine == "frontier":
+        # the dominant kernel's duration: isolated launches (one at a time, HIP events on the
+        # launching stream) after the timed region -- in the timed region launches overlap
+        # across the lanes, so an event pair there also times the wait for CUs held by the
+        # other batches (reported as avg_launch_ms_in_flight when the run was eager)
+        launch_ms = roofline_probe(ctx, args.hops, args.roofline_reps)
         roof, work = frontier_roofline(ctx, launch_ms, B, args.k, ms)
+        roof["isolated_launches"] = args.roofline_reps
+        if timed:
+            roof["avg_launch_ms_in_flight"] = float(np.mean([a.elapsed_time(b) for a, b in timed]))
+        out_graph = graphs
     else:
+        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in timed]))
         roof, work = dense_roofline(ctx, launch_ms, B, V, nnz), None
+        out_graph = False
     out = {
         "metric": METRIC,
         "value": world * B / (ms * 1e-3),
@@ -682,6 +769,7 @@ def main():
             "evidence_rows_per_gpu": ctx["enc"].n_rows, "seeds_per_gpu": int(len(ctx["seed_host"][0])),
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
             "batches_in_flight": args.pipeline if args.engine == "frontier" else 1,
+            "hip_graph_replay": out_graph,
         },
         "roofline": roof,
     }

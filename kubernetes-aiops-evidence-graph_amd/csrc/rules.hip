@@ -4,9 +4,15 @@
 // One 64-lane wavefront per incident segment:
 //   * coalesced sweep of the segment's rows (20 B/row: flags, vocab, node key, error count),
 //     wave-level OR / SUM reductions = RulesEngine._extract_signals (rules_engine.py:264-376);
-//   * pods_by_node: max rows per node key by an exact in-register pairwise count (:323-330);
-//   * lane r evaluates rule r (:378-441), its confidence (:443-455) and ranker score
-//     (hypothesis_ranker.py:44-63) in float64 with Python-exact rounding;
+//     the first 128 rows are loaded in one round trip;
+//   * pods_by_node: max rows per node key (:323-330) by counting in a per-wave LDS hash table
+//     (the max of the counts the rows' atomic adds return); segments with more node rows than
+//     the table holds fall back to an exact pairwise count;
+//   * lane r evaluates rule r's conditions (:378-441).  A rule emits only when ALL its
+//     conditions hold, so its strength, confidence (:443-455) and ranker score
+//     (hypothesis_ranker.py:44-63) are constants of the rule table: the host computes them once
+//     per launch in float64 with Python-exact rounding (RuleConsts) and the kernel does no
+//     floating-point arithmetic;
 //   * both stable orders (by confidence, :228; then by final_score, hypothesis_ranker.py:67)
 //     by counting, with the unknown fallback (:230-231, :457-478).
 // The per-incident working set is a few KB, so the kernel is latency- not bandwidth-bound for
@@ -43,6 +49,15 @@ __device__ __forceinline__ double wave_sum_d(double x) {
   return x;
 }
 
+// Per-rule constants of a launch (host-computed, egr::rule_confidence / ranker_final_score).
+struct RuleConsts {
+  double conf[EGR_MAX_RULES], fin[EGR_MAX_RULES], str[EGR_MAX_RULES];
+  double unknown_fin;
+};
+
+constexpr int kNodeSlots = 256;                 // per-wave pods_by_node hash table
+constexpr uint32_t kNodeEmpty = 0xFFFFFFFFu;    // (EGR_NO_NODE rows are never inserted)
+
 struct Signals {
   uint32_t flags;    // OR of EGR_F_* over the segment
   uint32_t vocab;    // OR of vocabulary bits (waiting / terminated reasons, log patterns)
@@ -75,20 +90,44 @@ __device__ bool condition_holds(int type, uint32_t mask, double param, const Sig
 }
 
 __global__ __launch_bounds__(256) void rules_eval_kernel(
-    const egr_rule_table T, const uint32_t* __restrict__ row_flags,
+    const egr_rule_table T, const RuleConsts K, const uint32_t* __restrict__ row_flags,
     const uint32_t* __restrict__ row_vocab, const uint32_t* __restrict__ row_node,
     const double* __restrict__ row_err, const int64_t* __restrict__ seg_off, int n_incidents,
     egr_rules_out out) {
+  __shared__ uint32_t node_key[kWavesPerBlock][kNodeSlots];
+  __shared__ uint32_t node_cnt[kWavesPerBlock][kNodeSlots];
   const int lane = threadIdx.x & (kWave - 1);
-  const int inc = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int wv = threadIdx.x >> 6;
+  const int inc = blockIdx.x * kWavesPerBlock + wv;
   if (inc >= n_incidents) return;  // wave-uniform; no block barrier below
   const int64_t beg = seg_off[inc], end = seg_off[inc + 1];
+  uint32_t* hk = node_key[wv];
+  uint32_t* hc = node_cnt[wv];
+#pragma unroll
+  for (int j = 0; j < kNodeSlots / kWave; ++j) {
+    hk[lane + j * kWave] = kNodeEmpty;
+    hc[lane + j * kWave] = 0u;
+  }
 
-  // ---- signal extraction: one coalesced sweep -------------------------------------------
+  // ---- signal extraction: one coalesced sweep (the first two row blocks in one round trip) --
   uint32_t f_or = 0, v_or = 0;
   double esum = 0.0;
   int n_node = 0;
-  for (int64_t r = beg + lane; r < end; r += kWave) {
+  uint32_t k0 = EGR_NO_NODE, k1 = EGR_NO_NODE;   // this lane's node keys of rows 0..127
+  {
+    const int64_t r0 = beg + lane, r1 = beg + kWave + lane;
+    const bool a0 = r0 < end, a1 = r1 < end;
+    const uint32_t f0 = a0 ? row_flags[r0] : 0u, f1 = a1 ? row_flags[r1] : 0u;
+    const uint32_t v0 = a0 ? row_vocab[r0] : 0u, v1 = a1 ? row_vocab[r1] : 0u;
+    const double e0 = a0 ? row_err[r0] : 0.0, e1 = a1 ? row_err[r1] : 0.0;
+    k0 = a0 ? row_node[r0] : EGR_NO_NODE;
+    k1 = a1 ? row_node[r1] : EGR_NO_NODE;
+    f_or = f0 | f1;
+    v_or = v0 | v1;
+    esum = e0 + e1;
+    n_node = (k0 != EGR_NO_NODE) + (k1 != EGR_NO_NODE);
+  }
+  for (int64_t r = beg + 2 * kWave + lane; r < end; r += kWave) {
     f_or |= row_flags[r];
     v_or |= row_vocab[r];
     esum += row_err[r];
@@ -110,7 +149,29 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
 
   // ---- pods_by_node: max rows per node key ------------------------------------------------
   s.max_per_node = s.n_node_rows > 0 ? 1 : 0;
-  if (s.n_node_rows >= 2) {
+  if (s.n_node_rows >= 2 && s.n_node_rows <= kNodeSlots / 2 && end - beg <= 2 * kWave) {
+    // LDS hash count (load <= 1/2): the count a row's add returns + 1 is the number of rows
+    // of its node so far, so the max over all rows is max(pods_by_node.values())
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int best = 0;
+    const uint32_t keys[2] = {k0, k1};
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const uint32_t k = keys[x];
+      if (k == EGR_NO_NODE) continue;
+      uint32_t h = (k * 0x9E3779B1u) >> 24;        // 8 bits: kNodeSlots = 256
+      for (;;) {
+        const uint32_t old = atomicCAS(&hk[h], kNodeEmpty, k);
+        if (old == kNodeEmpty || old == k) {
+          best = max(best, (int)atomicAdd(&hc[h], 1u) + 1);
+          break;
+        }
+        h = (h + 1) & (kNodeSlots - 1);
+      }
+    }
+    s.max_per_node = wave_max_i(best);
+  } else if (s.n_node_rows >= 2) {
     int best = 0;
     for (int64_t ib = beg; ib < end; ib += kWave) {
       const int64_t i = ib + lane;
@@ -135,19 +196,14 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
     const egr_rule& rule = T.rules[lane];
     const int nc = rule.n_conds;
     int mc = 0;
-    double ssum = 0.0;
-    for (int c = 0; c < nc && c < EGR_MAX_CONDS; ++c) {
-      if (condition_holds(rule.cond_type[c], rule.cond_mask[c], rule.cond_param[c], s,
-                          T.network_vocab_bit)) {
-        ++mc;
-        ssum = ssum + rule.cond_strength[c];
-      }
-    }
+    for (int c = 0; c < nc && c < EGR_MAX_CONDS; ++c)
+      mc += condition_holds(rule.cond_type[c], rule.cond_mask[c], rule.cond_param[c], s,
+                            T.network_vocab_bit);
     matched = nc > 0 && mc == nc;
-    if (matched) {
-      stren = ssum / (double)(nc > 1 ? nc : 1);
-      conf = egr::rule_confidence(rule.confidence_base, mc, stren);
-      fin = egr::ranker_final_score(conf, rule.category_weight, (double)mc, stren);
+    if (matched) {                 // all conditions held: the rule's constants (RuleConsts)
+      conf = K.conf[lane];
+      fin = K.fin[lane];
+      stren = K.str[lane];
     }
   }
   const uint64_t mm = __ballot(matched);
@@ -196,7 +252,7 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
       const double uc = T.unknown_confidence;
       out.confidence[base + R] = uc;
       out.strength[base + R] = 0.0;
-      out.final_score[base + R] = egr::ranker_final_score(uc, T.unknown_category_weight, 0.0, 0.0);
+      out.final_score[base + R] = K.unknown_fin;
     }
   }
 }
@@ -251,8 +307,23 @@ extern "C" int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_f
       !out->final_score || !out->strength)
     return egr::fail(EGR_EINVAL, "egr_rules_eval: NULL output");
   if (n_incidents == 0) return EGR_OK;
+  // the constants of a matched rule (every condition held: strength = mean of the condition
+  // strengths), computed exactly as rules_engine.py:443-455 / hypothesis_ranker.py:44-63 do
+  RuleConsts K{};
+  for (int r = 0; r < table->n_rules; ++r) {
+    const egr_rule& rule = table->rules[r];
+    const int nc = rule.n_conds;
+    if (nc <= 0) continue;
+    double ssum = 0.0;
+    for (int c = 0; c < nc; ++c) ssum = ssum + rule.cond_strength[c];
+    K.str[r] = ssum / (double)(nc > 1 ? nc : 1);
+    K.conf[r] = egr::rule_confidence(rule.confidence_base, nc, K.str[r]);
+    K.fin[r] = egr::ranker_final_score(K.conf[r], rule.category_weight, (double)nc, K.str[r]);
+  }
+  K.unknown_fin = egr::ranker_final_score(table->unknown_confidence, table->unknown_category_weight,
+                                          0.0, 0.0);
   const dim3 grid((n_incidents + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(rules_eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, *table,
+  hipLaunchKernelGGL(rules_eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, *table, K,
                      row_flags, row_vocab, row_node, row_err, seg_off, n_incidents, *out);
   EGR_CHECK_LAUNCH();
   return EGR_OK;

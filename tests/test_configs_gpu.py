@@ -113,6 +113,45 @@ def test_bench_config_c3_pipelined_lanes():
     assert st["overflowed"] == 0 and st["members"] > 0
 
 
+def test_bench_config_c3_graph_replay():
+    """bench.py's default timed loop: each lane's batch captured as a HIP graph (rules on the
+    side stream, seed prep, frontier, overflow grid) and replayed in turn.  Three lanes with
+    different batches, two rounds of replays: every lane's outputs equal the oracle's."""
+    import bench
+    from egraph import catalog
+    from egraph.encode import encode_batch
+    from egraph.rca import RulesDeviceBatch
+    B, k, hops, P = 1024, 10, 3, 3
+    g, batches = _world("C3", [B] * P, seed0=3000)
+    dev = torch.device("cuda", 0)
+    inputs = []
+    for cases in batches:
+        ev, sv, sc, ss, src = _batch_inputs(g, cases)
+        enc = encode_batch(ev, catalog.default())
+        inputs.append(dict(enc=enc, host=(sv, sc, ss, src), seeds=(_dev(sv), _dev(sc), _dev(ss)),
+                           sources=_dev(src), rules=RulesDeviceBatch(enc, catalog.default(), dev)))
+    snap = g.snapshot(device=dev)
+    lanes = bench.build_lanes(snap, B, max(len(x["host"][0]) for x in inputs), k, P, -1, dev,
+                              [(None, x["rules"], x["seeds"], x["sources"]) for x in inputs])
+    ctx = dict(lanes=lanes, tick=0, inc_label=g.labels().index("Incident"))
+    bench.capture_lanes(ctx, hops)
+    for ln in lanes:                    # poison the outputs: the replays must rewrite them
+        ln["frontier"].out_ids.fill_(-7)
+        ln["rules"].mask.fill_(-7)
+    torch.cuda.synchronize()
+    for _ in range(2 * P):
+        bench.step_graph(ctx, hops)
+    torch.cuda.synchronize()
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    for ln, x in zip(lanes, inputs):
+        sv, sc, ss, src = x["host"]
+        e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k, hops)
+        np.testing.assert_array_equal(ln["frontier"].out_ids.cpu().numpy().view(np.uint32).reshape(B, k), e_ids)
+        assert ln["frontier"].out_scores.cpu().numpy().reshape(B, k).tobytes() == e_sc.tobytes()
+        _check_rules(x["rules"].fetch(), x["enc"])
+
+
 def test_c2_rules_dropin_and_frontier():
     import asyncio
     from types import SimpleNamespace
