@@ -231,24 +231,36 @@ def step(ctx, hops: int, ev=None):
     plan.topk(ctx["inc_label"])
 
 
-def dropin_rules(ctx, dev, reps: int = 5) -> dict:
-    """The drop-in API end to end: RulesEngine.rank_incidents_batch on the bench batch (evidence
-    dicts in, ranked hypothesis dicts out: native encode, upload, egr_rules_eval, download,
-    native dict assembly).  Host-bound; reported beside `value`, never as it."""
+def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
+    """The drop-in API end to end (host-bound; reported beside `value`, never as it):
+      * batch: RulesEngine.rank_incidents_batch on the bench batch (evidence dicts in, ranked
+        hypothesis dicts out: native encode, one packed upload, egr_rules_eval, one packed
+        download, native dict assembly);
+      * single-call latency: generate_hypotheses + HypothesisRanker.rank for one incident at a
+        time (the reference activities' pattern), p50 / p99, beside the reference's own path
+        (the pure-Python restatement) on the same incidents;
+      * concurrent: every incident of the batch as its own generate_hypotheses +
+        rank call, all in flight at once (concurrent activities): the batcher coalesces them."""
     import asyncio
     from types import SimpleNamespace
 
+    sys.path.insert(0, str(REPO / "oracle"))
+    import rca_oracle
     from egraph import catalog
+    from egraph.batcher import RulesRunner
     from egraph.encode import encode_batch
-    from egraph.rca import RulesDeviceBatch, hypothesis_lists
-    from src.services.rca.rules_engine import RulesEngine
+    from egraph.rca import hypothesis_lists
+    from src.services.rca import rules_engine as RE
+    from src.services.rca.hypothesis_ranker import HypothesisRanker
     ev = ctx["evidence"]
     incs = [SimpleNamespace(id=f"inc-{i}") for i in range(len(ev))]
-    eng = RulesEngine(device=dev)
+    eng = RE.RulesEngine(device=dev)
     cat = catalog.default()
+    ranker = HypothesisRanker()
     asyncio.run(eng.rank_incidents_batch(incs, ev))            # warm
     t = []
     parts = np.zeros(3)
+    runner = RulesRunner(cat, dev)
     for _ in range(reps):
         t0 = time.perf_counter()
         asyncio.run(eng.rank_incidents_batch(incs, ev))
@@ -256,18 +268,58 @@ def dropin_rules(ctx, dev, reps: int = 5) -> dict:
         a = time.perf_counter()
         enc = encode_batch(ev, cat)
         b = time.perf_counter()
-        batch = RulesDeviceBatch(enc, cat, dev)
-        batch.launch()
-        res = batch.fetch()
+        res = runner.run_sync(enc)
         c = time.perf_counter()
         hypothesis_lists(cat, res, [x.id for x in incs], enc.evidence_ids, True)
         parts += (b - a, c - b, time.perf_counter() - c)
     best = min(t)
+    n1 = min(n_single, len(ev))
+
+    async def single():
+        lat = []
+        for i in range(n1):
+            t0 = time.perf_counter()
+            ranker.rank(await eng.generate_hypotheses(incs[i], ev[i]))
+            lat.append(time.perf_counter() - t0)
+        return lat
+
+    asyncio.run(single())                                          # warm
+    lat = np.array(asyncio.run(single())) * 1e6
+    ref = []
+    for i in range(n1):
+        t0 = time.perf_counter()
+        rca_oracle.rca(incs[i].id, ev[i])
+        ref.append(time.perf_counter() - t0)
+    ref = np.array(ref) * 1e6
+
+    async def concurrent():
+        async def one(i):
+            return ranker.rank(await eng.generate_hypotheses(incs[i], ev[i]))
+        return await asyncio.gather(*[one(i) for i in range(len(ev))])
+
+    b0 = RE._batcher(eng.catalog, eng.device)
+    l0 = b0.launches
+    asyncio.run(concurrent())
+    t0 = time.perf_counter()
+    asyncio.run(concurrent())
+    t_conc = time.perf_counter() - t0
     return {"value": len(ev) / best, "unit": "incidents/s", "cores": 1,
             "ms_per_batch": best * 1e3, "incidents": len(ev),
             "encode_ms": parts[0] / reps * 1e3, "device_ms": parts[1] / reps * 1e3,
             "assemble_ms": parts[2] / reps * 1e3,
-            "what": "RulesEngine.rank_incidents_batch, evidence dicts -> ranked hypothesis dicts"}
+            "what": "RulesEngine.rank_incidents_batch, evidence dicts -> ranked hypothesis dicts",
+            "single_call_us": {"p50": float(np.percentile(lat, 50)), "p99": float(np.percentile(lat, 99)),
+                               "calls": n1,
+                               "what": "generate_hypotheses + HypothesisRanker.rank, one incident "
+                                       "at a time (idle engine: launched at once)"},
+            "reference_single_call_us": {"p50": float(np.percentile(ref, 50)),
+                                         "p99": float(np.percentile(ref, 99)),
+                                         "what": "the reference's Python path (oracle/rca_oracle.py "
+                                                 "restatement), same incidents, 1 core"},
+            "concurrent": {"value": len(ev) / t_conc, "unit": "incidents/s",
+                           "calls": len(ev), "launches": (b0.launches - l0) // 2,
+                           "what": "every incident its own generate_hypotheses + rank call, all "
+                                   "in flight at once; the batcher coalesces them"}}
 
 
 def cpu_baseline(ctx, hops: int, k: int, threads: int, seconds: float = 8.0) -> dict:

@@ -1,0 +1,235 @@
+"""Low-latency rules launches and the aggregator that batches concurrent RulesEngine calls.
+
+The reference runs one RulesEngine.generate_hypotheses + HypothesisRanker.rank per incident
+inside each Temporal activity (src/services/workflow/activities.py:124-170); activities run
+concurrently in one worker.  Here:
+
+  RulesRunner   one egr_rules_eval launch over persistent device / pinned host buffers: the
+                encoded columns go up in ONE host-to-device copy, the seven outputs come back in
+                ONE device-to-host copy, and the caller waits on a HIP event by polling it from
+                the event loop (no thread hop, the loop is never blocked).
+  RulesBatcher  adaptive batching: a call that finds no launch in flight starts one at once
+                (no added latency when idle); calls arriving while a launch runs are collected
+                and go out together in the next one.  Each call gets exactly the dicts a
+                single call would (the kernel is per incident), and an input that makes the
+                reference raise raises in its own call only.
+"""
+from __future__ import annotations
+
+import asyncio
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .catalog import Catalog
+from .device import require_device
+from .encode import EncodedBatch, encode_batch
+from .rca import RulesResult, hypothesis_lists
+
+
+def _align(n: int, a: int = 256) -> int:
+    return (n + a - 1) // a * a
+
+
+class RulesRunner:
+    """egr_rules_eval over persistent buffers (grown on demand) on one stream."""
+
+    def __init__(self, cat: Catalog, device=None):
+        self.cat = cat
+        self.dev = require_device(device)
+        self.S = cat.n_rules + 1
+        self.stream = torch.cuda.Stream(self.dev)
+        self.cap_rows = self.cap_inc = -1
+        self.event = torch.cuda.Event()
+
+    def _layout(self, rows: int, B: int):
+        S = self.S
+        inp = [("flags", 4 * rows), ("vocab", 4 * rows), ("node", 4 * rows), ("err", 8 * rows),
+               ("seg", 8 * (B + 1))]
+        outp = [("mask", 4 * B), ("n_hyp", B), ("oc", B * S), ("orank", B * S),
+                ("conf", 8 * B * S), ("fin", 8 * B * S), ("str", 8 * B * S)]
+        off, o = {}, 0
+        for name, nb in inp:
+            off[name] = (o, nb)
+            o = _align(o + nb)
+        in_bytes = o
+        for name, nb in outp:
+            off[name] = (o, nb)
+            o = _align(o + nb)
+        return off, in_bytes, o
+
+    def _ensure(self, rows: int, B: int) -> None:
+        if rows <= self.cap_rows and B <= self.cap_inc:
+            return
+        rows, B = max(rows, 2 * self.cap_rows, 1024), max(B, 2 * self.cap_inc, 64)
+        _, _, total = self._layout(rows, B)
+        self.dbuf = torch.empty(total, dtype=torch.uint8, device=self.dev)
+        self.hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
+        self.hnp = self.hbuf.numpy()
+        self.cap_rows, self.cap_inc = rows, B
+
+    def _h(self, name, dtype, n):
+        o, _ = self.off[name]
+        return self.hnp[o:o + n * np.dtype(dtype).itemsize].view(dtype)
+
+    def _d(self, name) -> int:
+        return self.dbuf.data_ptr() + self.off[name][0]
+
+    def launch(self, enc: EncodedBatch) -> torch.cuda.Event:
+        """Enqueue upload + kernel + download of one encoded batch; returns the event that
+        marks the results as ready in host memory (read them with results())."""
+        B, rows = enc.n_incidents, enc.n_rows
+        self._ensure(rows, B)
+        # this launch's layout inside the buffers: only its own bytes cross the bus
+        self.off, self.in_bytes, self.total = self._layout(rows, B)
+        for name, arr, dt in (("flags", enc.flags, np.uint32), ("vocab", enc.vocab, np.uint32),
+                              ("node", enc.node, np.uint32), ("err", enc.err, np.float64),
+                              ("seg", enc.seg_off, np.int64)):
+            if len(arr):
+                self._h(name, dt, len(arr))[:] = arr
+        self._B, self._rows = B, rows
+        out_lo = self.off["mask"][0]
+        st = self.stream
+        with torch.cuda.stream(st):
+            self.dbuf[:self.in_bytes].copy_(self.hbuf[:self.in_bytes], non_blocking=True)
+            o = L.EgrRulesOut(self._d("mask"), self._d("n_hyp"), self._d("oc"), self._d("orank"),
+                              self._d("conf"), self._d("fin"), self._d("str"))
+            L.check(L.lib.egr_rules_eval(self.cat.table, self._d("flags"), self._d("vocab"),
+                                         self._d("node"), self._d("err"), self._d("seg"), B, o,
+                                         st.cuda_stream), "egr_rules_eval")
+            self.hbuf[out_lo:self.total].copy_(self.dbuf[out_lo:self.total], non_blocking=True)
+            self.event.record(st)
+        return self.event
+
+    def results(self) -> RulesResult:
+        """Host copies of the last launch's outputs (after its event completed)."""
+        B, S = self._B, self.S
+        g = self._h
+        return RulesResult(g("mask", np.uint32, B).copy(), g("n_hyp", np.uint8, B).copy(),
+                           g("oc", np.uint8, B * S).reshape(B, S).copy(),
+                           g("orank", np.uint8, B * S).reshape(B, S).copy(),
+                           g("conf", np.float64, B * S).reshape(B, S).copy(),
+                           g("fin", np.float64, B * S).reshape(B, S).copy(),
+                           g("str", np.float64, B * S).reshape(B, S).copy())
+
+    def run_sync(self, enc: EncodedBatch) -> RulesResult:
+        self.launch(enc).synchronize()
+        return self.results()
+
+    async def run(self, enc: EncodedBatch) -> RulesResult:
+        ev = self.launch(enc)
+        while not ev.query():                       # poll from the loop: never blocks it
+            await asyncio.sleep(0)
+        return self.results()
+
+
+def concat(encs: list[EncodedBatch]) -> EncodedBatch:
+    """One batch of several encoded batches (segments re-based; node keys only ever meet
+    inside one incident's segment, so per-batch key numberings do not collide)."""
+    if len(encs) == 1:
+        return encs[0]
+    seg = [np.zeros(1, np.int64)]
+    base = 0
+    for e in encs:
+        seg.append(e.seg_off[1:] + base)
+        base += e.n_rows
+    return EncodedBatch(np.concatenate([e.flags for e in encs]), np.concatenate([e.vocab for e in encs]),
+                        np.concatenate([e.node for e in encs]), np.concatenate([e.err for e in encs]),
+                        np.concatenate(seg), [i for e in encs for i in e.evidence_ids])
+
+
+@dataclass
+class _Call:
+    incident_ids: list
+    evidence_lists: list
+    ranked: bool
+    fut: asyncio.Future
+
+
+class RulesBatcher:
+    """Coalesces concurrent rules calls into launches of up to max_batch incidents."""
+
+    def __init__(self, cat: Catalog, device=None, max_batch: int = 16384):
+        self.cat = cat
+        self.runner = RulesRunner(cat, device)
+        self.max_batch = max_batch
+        self.queue: list[_Call] = []
+        self.busy = False
+        self.launches = 0                             # diagnostics: launches / calls
+        self.calls = 0
+
+    async def submit(self, incident_id, evidence: list[dict], ranked: bool) -> list[dict]:
+        """One incident's hypothesis list (generate_hypotheses, ranked or not)."""
+        return (await self.submit_many([incident_id], [evidence], ranked))[0]
+
+    async def submit_many(self, incident_ids: list, evidence_lists: list, ranked: bool
+                          ) -> list[list[dict]]:
+        """Several incidents as ONE call (it raises as a whole if any row makes the
+        reference raise, as the reference's loop over them would)."""
+        fut = asyncio.get_running_loop().create_future()
+        self.queue.append(_Call([str(i) for i in incident_ids], list(evidence_lists), ranked, fut))
+        self.calls += 1
+        if not self.busy:
+            self.busy = True
+            asyncio.get_running_loop().create_task(self._drain())
+        return await fut
+
+    async def _drain(self) -> None:
+        try:
+            while self.queue:
+                take, n = 0, 0
+                while take < len(self.queue) and (take == 0 or n + len(self.queue[take].incident_ids)
+                                                  <= self.max_batch):
+                    n += len(self.queue[take].incident_ids)
+                    take += 1
+                calls, self.queue = self.queue[:take], self.queue[take:]
+                await self._run(calls)
+        finally:
+            self.busy = False
+
+    async def _run(self, calls: list[_Call]) -> None:
+        # encode: the whole batch at once; if a row raises, call by call, so that only the
+        # calls whose evidence makes the reference raise get the exception
+        try:
+            encs = [encode_batch([ev for c in calls for ev in c.evidence_lists], self.cat)]
+            ok = calls
+        except Exception:
+            encs, ok = [], []
+            for c in calls:
+                try:
+                    encs.append(encode_batch(c.evidence_lists, self.cat))
+                    ok.append(c)
+                except Exception as e:                      # noqa: BLE001 (re-raised per call)
+                    if not c.fut.done():
+                        c.fut.set_exception(e)
+        if not ok:
+            return
+        enc = concat(encs)
+        try:
+            self.launches += 1
+            res = await self.runner.run(enc)
+        except Exception as e:                              # noqa: BLE001 (device failure)
+            for c in ok:
+                if not c.fut.done():
+                    c.fut.set_exception(e)
+            return
+        # incident rows of every call, then one native assembly per ranking mode
+        starts = np.cumsum([0] + [len(c.incident_ids) for c in ok])
+        for ranked in (False, True):
+            cs = [j for j, c in enumerate(ok) if c.ranked == ranked]
+            if not cs:
+                continue
+            idx = np.concatenate([np.arange(starts[j], starts[j + 1]) for j in cs])
+            sub = res if len(idx) == enc.n_incidents else RulesResult(*(a[idx] for a in (
+                res.mask, res.n_hyp, res.order_conf, res.order_rank, res.confidence,
+                res.final_score, res.strength)))
+            ids = [i for j in cs for i in ok[j].incident_ids]
+            lists = hypothesis_lists(self.cat, sub, ids, [enc.evidence_ids[i] for i in idx], ranked)
+            pos = 0
+            for j in cs:
+                n = len(ok[j].incident_ids)
+                if not ok[j].fut.done():
+                    ok[j].fut.set_result(lists[pos:pos + n])
+                pos += n

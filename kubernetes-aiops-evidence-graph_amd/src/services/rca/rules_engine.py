@@ -8,18 +8,16 @@ matches).  Additive batch entry points put many incidents into one kernel launch
 (generate + HypothesisRanker.rank fused, as the workflow runs them back to back).
 
 All signal extraction, rule matching, confidence, ranking and ordering run in
-egr_rules_eval (csrc/rules.hip), called as the custom op torch.ops.egraph.rules_eval
-(egraph/ops.py); the host encodes rows and assembles dicts in native code
+egr_rules_eval (csrc/rules.hip), launched by egraph/batcher.py's RulesRunner (the same
+entry point is registered as torch.ops.egraph.rules_eval, egraph/ops.py); the host encodes
+rows and assembles dicts in native code
 (csrc/pyhost.c: encode_rows, assemble).  There is no CPU
 fallback: without a ROCm GPU the call raises RuntimeError.
 """
 from __future__ import annotations
 
-import asyncio
-
 from egraph import catalog as _catalog
-from egraph.encode import encode_batch
-from egraph.rca import RulesDeviceBatch, hypothesis_lists
+from egraph.batcher import RulesBatcher
 from src.models import HypothesisCategory
 
 # The reference's rule table, with categories as enums as in rules_engine.py:15-190.
@@ -30,8 +28,26 @@ DIAGNOSIS_RULES = [
 ]
 
 
+_BATCHERS: dict = {}
+
+
+def _batcher(catalog: _catalog.Catalog, device) -> RulesBatcher:
+    """The process-wide batcher of a (catalog, device): concurrent activities share it, so
+    calls that overlap in time go out in one launch."""
+    key = (id(catalog), str(device))
+    b = _BATCHERS.get(key)
+    if b is None:
+        b = _BATCHERS[key] = RulesBatcher(catalog, device)
+    return b
+
+
 class RulesEngine:
-    """Deterministic rules engine; evaluation is batched on the GPU."""
+    """Deterministic rules engine; evaluation is batched on the GPU.
+
+    Every call goes through a process-wide RulesBatcher (egraph/batcher.py): an idle engine
+    launches a single call at once (one packed upload, one kernel, one packed download, the
+    completion polled from the event loop); calls that arrive while a launch is in flight --
+    concurrent Temporal activities -- are coalesced into the next launch."""
 
     def __init__(self, catalog: _catalog.Catalog | None = None, device=None):
         self.catalog = catalog or _catalog.default()
@@ -42,18 +58,12 @@ class RulesEngine:
     async def _run(self, incidents, evidence_lists, ranked: bool) -> list[list[dict]]:
         if len(incidents) != len(evidence_lists):
             raise ValueError("incidents and evidence_lists differ in length")
-        enc = encode_batch(evidence_lists, self.catalog)   # raises like the reference
-        res = await asyncio.to_thread(self._launch_fetch, enc)
-        return hypothesis_lists(self.catalog, res, [inc.id for inc in incidents],
-                                enc.evidence_ids, ranked)
-
-    def _launch_fetch(self, enc):
-        # torch.ops.egraph.rules_eval: the registered custom op over egr_rules_eval
-        return RulesDeviceBatch(enc, self.catalog, self.device).evaluate_op()
+        return await _batcher(self.catalog, self.device).submit_many(
+            [inc.id for inc in incidents], evidence_lists, ranked)
 
     async def generate_hypotheses(self, incident, evidence: list[dict]) -> list[dict]:
         """Generate hypotheses by matching evidence against rules (rules_engine.py:199-233)."""
-        return (await self._run([incident], [evidence], ranked=False))[0]
+        return await _batcher(self.catalog, self.device).submit(incident.id, evidence, False)
 
     async def generate_hypotheses_batch(self, incidents: list, evidence_lists: list[list[dict]]
                                         ) -> list[list[dict]]:
