@@ -28,6 +28,7 @@ PROMQL = {  # query names of src/config/promql_queries.yaml used by the metric r
     "hpa": ["hpa_at_max", "hpa_current_replicas", "hpa_max_replicas"],
     "resource": ["cpu_usage_percentage", "cpu_throttling", "disk_usage"],
     "deployment": ["deployment_replicas_unavailable", "deployment_generation_mismatch"],
+    "error_rate": ["http_5xx_rate", "grpc_error_rate", "error_rate_increase"],
 }
 
 
@@ -218,6 +219,91 @@ def build_graph(c: Cluster):
 # incidents
 SCENARIOS = ("crashloop_deploy", "crashloop", "oom", "imagepull")
 SCENARIO_P = (0.2, 0.2, 0.3, 0.3)   # BASELINE C2 mix: 40 % CrashLoop (half with deploy), 30/30
+# the reference simulator's four scenarios (src/simulator/incident_simulator.py:13-160, :164-169)
+SIMULATOR_SCENARIOS = ("crashloop", "oom", "imagepull", "slowapp")
+
+# ---- log lines and the logs collector's analysis (logs_collector.py:166-244) ----------------
+# The (regex, category) table and the stack-trace regexes are the collector's own, exported from
+# the reference by oracle/gen_golden_simulator.py (data, like rules_catalog.json).
+_LOG_PATTERNS = None
+
+
+def _log_patterns():
+    global _LOG_PATTERNS
+    if _LOG_PATTERNS is None:
+        import json
+        import re
+        from pathlib import Path
+        d = json.loads((Path(__file__).with_name("log_patterns.json")).read_text())
+        _LOG_PATTERNS = ([(re.compile(p), c) for p, c in d["error_patterns"]],
+                         [re.compile(p) for p in d["stack_trace_patterns"]])
+    return _LOG_PATTERNS
+
+
+def log_analysis(lines: list[str]) -> dict:
+    """_extract_log_patterns + _calculate_log_signal_strength over log lines: per line the FIRST
+    matching error pattern decides (:193-208): its category joins patterns_found, and the line
+    counts as an error if the category names "error" or "critical", else as a warning."""
+    errs, stacks = _log_patterns()
+    error_count = warning_count = 0
+    found: set = set()
+    sample_errors: list = []
+    stack_traces: list = []
+    for line in lines:
+        for rx, cat in errs:
+            if rx.search(line):
+                found.add(cat)
+                if "error" in cat or "critical" in cat:
+                    if len(sample_errors) < 10:
+                        sample_errors.append(line[:500])
+                    error_count += 1
+                else:
+                    warning_count += 1
+                break
+        if len(stack_traces) < 5:
+            for rx in stacks:
+                if rx.search(line):
+                    stack_traces.append(line[:1000])
+                    break
+    strength = 0.3
+    if error_count > 10:
+        strength = 0.9
+    elif error_count > 5:
+        strength = 0.8
+    elif error_count > 0:
+        strength = 0.6
+    elif warning_count > 10:
+        strength = 0.5
+    if "oom" in found or "critical" in found:
+        strength = max(strength, 0.95)
+    return {"error_count": error_count, "warning_count": warning_count,
+            "patterns_found": sorted(found), "sample_errors": sample_errors,
+            "stack_traces": stack_traces, "signal_strength": strength}
+
+
+# log lines a pod of each scenario writes (what Loki would return for the incident window)
+_LOG_LINES = {
+    "crashloop": ["Starting", "exit status 1", "Error: container exited with code 1",
+                  "Back-off restarting failed container", "panic: runtime error: invalid memory address",
+                  "goroutine 1 [running]:", "failed to load config: no such file or directory"],
+    "oom": ["Killed process 4242 (python) total-vm:2097152kB", "MemoryError: out of memory",
+            "container terminated: OOMKilled", "java.lang.OutOfMemoryError: Java heap space",
+            "allocating 10000000 bytes", "GC overhead limit exceeded"],
+    "imagepull": [],          # the container never starts: no application log lines
+    "slowapp": ["GET / HTTP/1.1 200 OK", "GET / HTTP/1.1 500 Internal Server Error",
+                "upstream request timed out after 5.0s", "connection reset by peer",
+                "GET /health HTTP/1.1 200 OK", "slow request: 4.2s",
+                '  File "/app/server.py", line 12, in do_GET'],
+}
+
+
+def scenario_log_lines(sc: str, rng: np.random.Generator, n: int | None = None) -> list[str]:
+    base = "crashloop" if sc.startswith("crashloop") else sc
+    pool = _LOG_LINES.get(base, [])
+    if not pool:
+        return []
+    n = int(rng.integers(0, 60)) if n is None else n
+    return [pool[int(i)] for i in rng.integers(0, len(pool), n)]
 
 
 @dataclass
@@ -305,6 +391,8 @@ def incident_case(c: Cluster, d: int, sc: str, iid: str, rng: np.random.Generato
         elif sc == "imagepull":
             wr = ("ImagePullBackOff", "ErrImagePull")[int(rng.integers(0, 2))]
             phase, restarts = "Pending", 0
+        elif sc == "slowapp":
+            restarts = 0               # serves, slowly: 500s on 30 % of requests, 1-5 s latency
         ready = "True" if (wr is None and tr is None and rng.random() < 0.7) else "False"
         conds = [{"type": "Ready", "status": ready,
                   "reason": None if ready == "True" else "ContainersNotReady"}]
@@ -325,20 +413,27 @@ def incident_case(c: Cluster, d: int, sc: str, iid: str, rng: np.random.Generato
             {"type": "Warning" if warn else "Normal", "reason": reason, "message": reason,
              "involved_object": {"kind": "Pod", "name": pname, "namespace": ns}, "count": 1},
             0.9 if warn else 0.4)
-    errors = int(rng.integers(0, 40))
-    pats = ["error"] + (["network"] if rng.random() < 0.3 else []) + \
-        (["oom"] if sc == "oom" else [])
-    row("log_signal", dname, {"total_lines": 500, "error_count": errors, "warning_count": 3,
-                              "patterns_found": pats},
-        0.9 if errors > 10 else 0.8 if errors > 5 else 0.6 if errors else 0.3, "loki")
-    cats = ["crashloop", "resource", "deployment"] + (["oom"] if sc == "oom" else ["latency", "hpa"])
+    lines = scenario_log_lines(sc, rng)
+    la = log_analysis(lines)
+    row("log_signal", dname, {"total_lines": len(lines), "error_count": la["error_count"],
+                              "warning_count": la["warning_count"],
+                              "patterns_found": la["patterns_found"],
+                              "sample_errors": la["sample_errors"],
+                              "stack_traces": la["stack_traces"]},
+        la["signal_strength"], "loki")
+    if sc == "slowapp":
+        cats = ["deployment", "resource", "latency", "error_rate"]
+    else:
+        cats = ["crashloop", "resource", "deployment"] + (["oom"] if sc == "oom" else ["latency", "hpa"])
     names = [q for cat in cats for q in PROMQL[cat]]
     for j in range(15):
         qn = names[j % len(names)]
         if "memory" in qn:
             v = float(rng.uniform(0, 100))
         elif "latency" in qn:
-            v = float(rng.uniform(0, 5))
+            v = float(rng.uniform(1, 5) if sc == "slowapp" else rng.uniform(0, 5))
+        elif "5xx" in qn or "error" in qn:
+            v = float(rng.uniform(0.2, 0.4) if sc == "slowapp" else rng.uniform(0, 0.05))
         elif "hpa" in qn:
             v = float(rng.integers(0, 2))
         else:
@@ -364,6 +459,33 @@ def incident_case(c: Cluster, d: int, sc: str, iid: str, rng: np.random.Generato
                      "relation_type": "CORRELATES_WITH"})
         row("image_change", dname, {"deployment": dname, "image_changed": True}, 0.85)
     return IncidentCase(inc, sc, ev, ents, rels)
+
+
+def c1_world(seed: int = 20260820) -> tuple[Cluster, IncidentCase]:
+    """BASELINE config C1: ONE CrashLoopBackOff incident after a recent deploy
+    on a small cluster -- 1 Deployment with 10 Pods on 3 Nodes (one NotReady), its Service, the
+    recent ChangeEvent, 60 Kubernetes Event rows (each its own Event vertex), 1 log row and 15
+    metric rows: ~100 evidence rows and ~100 graph vertices.  Returns the cluster with the
+    incident added and the incident case."""
+    cfg = ClusterConfig(pods=10, namespaces=1, nodes=3, deployments=1, services=1,
+                        calls_per_service=0, attach_fraction=1.0, unhealthy_node_fraction=0.0,
+                        seed=seed)
+    c = build_cluster(cfg)
+    c.unhealthy_nodes = {"node-00001"}            # one of the three Nodes is NotReady
+    rng = np.random.default_rng(seed + 1)
+    case = incident_case(c, 0, "crashloop_deploy", f"00000000-0000-4000-8000-{seed:012x}", rng,
+                         events_per_incident=60, fingerprint="c1")
+    # each event row is its own Event vertex (event:<ns>:<event name>) attached to its pod
+    ns = c.ns_names[0]
+    for j, ev in enumerate(x for x in case.evidence if x["evidence_type"] == "kubernetes_event"):
+        pod = ev["entity_name"]
+        ev["entity_name"] = f"{pod}.{j:04x}"
+        case.entities.append({"id": f"event:{ns}:{ev['entity_name']}", "type": "Event",
+                              "properties": {"reason": ev["data"]["reason"]}})
+        case.relations.append({"source_id": f"pod:{ns}:{pod}", "target_id": f"event:{ns}:{ev['entity_name']}",
+                               "relation_type": "HAS_EVENT"})
+    add_incidents(c, [case])
+    return c, case
 
 
 def add_incidents(c: Cluster, cases: list[IncidentCase]) -> None:

@@ -45,7 +45,7 @@ def test_concurrent_calls_coalesce_and_match_golden(golden):
     """All golden cases as concurrent single calls (half generate -> rank, half the fused
     batch API with one incident): fewer launches than calls, every result as recorded from
     the reference."""
-    from src.services.hypothesis_ranker import HypothesisRanker
+    from src.services.rca.hypothesis_ranker import HypothesisRanker
     from src.services.rca import rules_engine as RE
     eng = RE.RulesEngine()
     cases = golden["rules"]["cases"]

@@ -244,3 +244,52 @@ def test_c4_partitioned_plan(c4, P):
         assert own.tobytes() == exp[lg.gid[: lg.n_owned]].tobytes()        # bit-identical
         np.testing.assert_array_equal(ids.cpu().numpy(), e_ids.astype(np.int64))
         np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
+
+
+def test_simulator_scenarios_and_c1_through_the_dropin():
+    """The four reference-simulator scenarios and C1 (tests/golden/simulator_cases.json, judged
+    by the reference) through the drop-in RulesEngine; C1's graph through GraphService (the
+    activities' build_evidence_graph + rank_root_causes) against the oracle."""
+    import asyncio
+    import json
+    from types import SimpleNamespace
+
+    from conftest import REPO
+    from egraph import synth
+    from helpers import golden_record, record
+    from src.database import GraphService
+    from src.models import GraphEntity, GraphRelation
+    from src.services.rca.hypothesis_ranker import HypothesisRanker
+    from src.services.rca.rules_engine import RulesEngine
+    sim = json.loads((REPO / "tests" / "golden" / "simulator_cases.json").read_text())
+    eng = RulesEngine()
+    out = asyncio.run(eng.rank_incidents_batch([SimpleNamespace(id=c["incident_id"]) for c in sim["cases"]],
+                                               [c["evidence"] for c in sim["cases"]]))
+    for c, hyps in zip(sim["cases"], out):
+        assert record(hyps) == golden_record(c["expected"]), c["name"]
+    c1 = next(c for c in sim["cases"] if c["name"] == "C1")
+    one = HypothesisRanker().rank(asyncio.run(eng.generate_hypotheses(SimpleNamespace(id=c1["incident_id"]),
+                                                                      c1["evidence"])))
+    assert record(one) == golden_record(c1["expected"])
+    assert one[0]["rule_id"] == "crashloop_recent_deploy"
+    # C1's evidence graph through the drop-in GraphService
+    cl, case = synth.c1_world()
+    GraphService.reset()
+    try:
+        asyncio.run(GraphService.create_entities_batch([GraphEntity(id=i, type=lab)
+                                                        for i, lab in zip(cl.ids, cl.labels)]))
+        asyncio.run(GraphService.create_relations_batch([GraphRelation(source_id=s, target_id=d, relation_type=t)
+                                                         for s, d, t in zip(cl.src, cl.dst, cl.types)]))
+        got = asyncio.run(GraphService.rank_root_causes([case.incident["id"]], [case.evidence], hops=3, k=10))[0]
+        g = GraphService.graph()
+        sv, sc, ss = synth.seeds_for_batch(g, [case.evidence])
+        src = g.lookup([f"incident:{case.incident['id']}"]).astype(np.uint32)
+        csr = g.csr()
+        vl, _, _, _ = g.export()
+        e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src)
+        want = [(g.vertex_id(int(v)), float(s)) for v, s in zip(e_ids[0], e_sc[0]) if v != 0xFFFFFFFF]
+        assert [(r["id"], r["score"]) for r in got] == want and len(want) == 10
+        sub = asyncio.run(GraphService.get_incident_graph(f"incident:{case.incident['id']}"))
+        assert 90 <= len(sub["nodes"]) <= g.num_vertices
+    finally:
+        GraphService.reset()
