@@ -105,7 +105,8 @@ typedef struct egr_rule_table {
  *   mask[i]                  bit r = rule r matched
  *   order_conf[i*(R+1)+p]    slot index at position p in generate_hypotheses order (:228)
  *   order_rank[i*(R+1)+p]    slot index at position p after HypothesisRanker.rank (:67)
- *   confidence / final_score / strength [i*(R+1)+slot]  (float64, bit-exact with Python)   */
+ *   confidence / final_score / strength [i*(R+1)+slot]  (float64, bit-exact with Python;
+ *                            every slot is written: 0 for rules that did not match)       */
 typedef struct egr_rules_out {
   uint32_t* mask;
   uint8_t* n_hyp;

@@ -240,20 +240,17 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
     out.order_conf[base + lane] = (uint8_t)at_c;
     out.order_rank[base + lane] = (uint8_t)at_r;
   }
-  if (matched) {
-    out.confidence[base + lane] = conf;
-    out.final_score[base + lane] = fin;
+  // every slot is written (0 for a rule that did not match; slot R = unknown, set only when
+  // nothing matched), so the outputs need no clearing before a launch
+  if (lane < S) {
+    const bool unk = lane == R && nh == 0;
+    out.confidence[base + lane] = unk ? T.unknown_confidence : conf;
+    out.final_score[base + lane] = unk ? K.unknown_fin : fin;
     out.strength[base + lane] = stren;
   }
   if (lane == 0) {
     out.mask[inc] = (uint32_t)mm;
     out.n_hyp[inc] = (uint8_t)(nh > 0 ? nh : 1);
-    if (nh == 0) {
-      const double uc = T.unknown_confidence;
-      out.confidence[base + R] = uc;
-      out.strength[base + R] = 0.0;
-      out.final_score[base + R] = K.unknown_fin;
-    }
   }
 }
 

@@ -94,8 +94,6 @@ class RulesRunner:
         st = self.stream
         with torch.cuda.stream(st):
             self.dbuf[:self.in_bytes].copy_(self.hbuf[:self.in_bytes], non_blocking=True)
-            # slots of rules that did not match are never written: zero, like RulesDeviceBatch
-            self.dbuf[out_lo:self.total].zero_()
             o = L.EgrRulesOut(self._d("mask"), self._d("n_hyp"), self._d("oc"), self._d("orank"),
                               self._d("conf"), self._d("fin"), self._d("str"))
             L.check(L.lib.egr_rules_eval(self.cat.table, self._d("flags"), self._d("vocab"),
