@@ -176,7 +176,9 @@ def capture_lanes(ctx, hops: int, inline_rules: bool | None = None) -> None:
     clean-counter flags) is constant in steady state, which one eager warm-up step settles."""
     inc = ctx["inc_label"]
     if inline_rules is None:
-        inline_rules = bool(os.environ.get("EGRAPH_BENCH_GRAPH_INLINE_RULES"))
+        # rules inline on the lane's stream (default): a captured fork / join to a side stream
+        # made replays slower on ROCm 7 (0.113 vs 0.0745 ms per step, profiles/r02_graph_ab.txt)
+        inline_rules = os.environ.get("EGRAPH_BENCH_GRAPH_FORK_RULES") is None
     for lane in ctx["lanes"]:
         if inline_rules:
             lane["side"] = None                        # rules on the lane's own stream
@@ -707,10 +709,9 @@ def main():
     ap.add_argument("--storm-rate", type=int, default=100_000, help="alerts per minute")
     ap.add_argument("--storm-keys", type=int, default=10_000)
     ap.add_argument("--storm-events", type=int, default=100, help="topology events per tick")
-    ap.add_argument("--graph", action="store_true",
-                    help="frontier: replay each lane's batch as a captured HIP graph instead of "
-                         "enqueueing it eagerly (measured slower on ROCm 7: 0.116 vs 0.077 ms "
-                         "per step, profiles/r02_graph_vs_eager.txt)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="frontier: enqueue each batch eagerly instead of replaying the lane's "
+                         "captured HIP graph")
     ap.add_argument("--roofline-reps", type=int, default=20,
                     help="isolated frontier launches timed after the run for the roofline")
     args = ap.parse_args()
@@ -749,7 +750,7 @@ def main():
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
-    graphs = args.engine == "frontier" and args.graph
+    graphs = args.engine == "frontier" and not args.no_graph
     if graphs:
         capture_lanes(ctx, args.hops)
         run_step = step_graph

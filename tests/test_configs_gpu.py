@@ -113,10 +113,12 @@ def test_bench_config_c3_pipelined_lanes():
     assert st["overflowed"] == 0 and st["members"] > 0
 
 
-def test_bench_config_c3_graph_replay():
-    """bench.py's default timed loop: each lane's batch captured as a HIP graph (rules on the
-    side stream, seed prep, frontier, overflow grid) and replayed in turn.  Three lanes with
-    different batches, two rounds of replays: every lane's outputs equal the oracle's."""
+@pytest.mark.parametrize("inline", [True, False])
+def test_bench_config_c3_graph_replay(inline):
+    """bench.py's default timed loop: each lane's batch captured as a HIP graph (rules inline on
+    the lane's stream -- the default -- or forked to its side stream, seed prep, frontier,
+    overflow grid) and replayed in turn.  Three lanes with different batches, two rounds of
+    replays: every lane's outputs equal the oracle's."""
     import bench
     from egraph import catalog
     from egraph.encode import encode_batch
@@ -134,7 +136,7 @@ def test_bench_config_c3_graph_replay():
     lanes = bench.build_lanes(snap, B, max(len(x["host"][0]) for x in inputs), k, P, -1, dev,
                               [(None, x["rules"], x["seeds"], x["sources"]) for x in inputs])
     ctx = dict(lanes=lanes, tick=0, inc_label=g.labels().index("Incident"))
-    bench.capture_lanes(ctx, hops)
+    bench.capture_lanes(ctx, hops, inline_rules=inline)
     for ln in lanes:                    # poison the outputs: the replays must rewrite them
         ln["frontier"].out_ids.fill_(-7)
         ln["rules"].mask.fill_(-7)
