@@ -66,7 +66,6 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     from egraph import catalog, synth
     from egraph.device import to_device
     from egraph.encode import encode_batch
-    from egraph.graph import EvidenceGraph
     from egraph.rca import RulesDeviceBatch
     t0 = time.time()
     cl = synth.build_cluster(synth.CONFIGS[config])
@@ -74,9 +73,7 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     # ranks the slice of columns it owns; one incident set per rank keeps per-GPU work fixed
     cases = synth.make_incidents(cl, B, seed=1000 + rank)
     synth.add_incidents(cl, cases)
-    g = EvidenceGraph()
-    g.merge_nodes(cl.ids, cl.labels)
-    g.merge_edges(cl.src, cl.dst, cl.types)
+    g = synth.build_graph(cl)                 # C4: with its dense telemetry links (~10M entries)
     evidence = [x.evidence for x in cases]
     enc = encode_batch(evidence, catalog.default())
     sv, sc, ss = synth.seeds_for_batch(g, evidence)
@@ -491,16 +488,14 @@ def shard_setup(args, world: int, rank: int, dev: torch.device):
     from egraph import catalog, shard, synth
     from egraph.device import to_device
     from egraph.encode import encode_batch
-    from egraph.graph import EvidenceGraph, Snapshot
+    from egraph.graph import Snapshot
     from egraph.rca import RulesDeviceBatch
     t0 = time.time()
     B = args.batch
     cl = synth.build_cluster(synth.CONFIGS[args.config])
     cases = synth.make_incidents(cl, B, seed=1000)       # one global batch, same on every rank
     synth.add_incidents(cl, cases)
-    g = EvidenceGraph()
-    g.merge_nodes(cl.ids, cl.labels)
-    g.merge_edges(cl.src, cl.dst, cl.types)
+    g = synth.build_graph(cl)
     csr = g.csr()
     vl, _, _, _ = g.export()
     V = g.num_vertices
@@ -543,15 +538,19 @@ def shard_step(ctx, hops: int, k: int, ev=None):
         plan.set_seeds(*seeds)
         plan.set_sources(sources)
         run.eng = _TimedPlan(plan, ev)
-    return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k)
+    return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k,
+                                 sparse=not ctx.get("dense_halo", False))
 
 
 def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     ctx = shard_setup(args, world, rank, dev)
+    ctx["dense_halo"] = args.dense_halo
     for _ in range(args.warmup):
         shard_step(ctx, args.hops, args.k)
     torch.cuda.synchronize(dev)
     events: list = []
+    for r in ctx["runs"]:
+        r.sent_bytes, r.exchanges = 0, 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -574,6 +573,8 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
     nnz = len(ctx["csr"]["col"])
     halo = max(r.halo_bytes_per_hop for r in ctx["runs"])
+    per_hop = max(1, args.steps * max(args.hops - 1, 1))
+    sent = max(r.sent_bytes for r in ctx["runs"]) / per_hop
     out = {
         "metric": METRIC, "value": B / (ms * 1e-3), "unit": "incidents/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
@@ -588,6 +589,9 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "parallelism": f"edge-cut x{ctx['P']}" + (" (one process)" if world == 1 else ""),
             "local_vertices": [len(r.lg.gid) for r in ctx["runs"]],
             "halo_bytes_per_hop_max_rank": halo,
+            "halo_exchange": "dense" if args.dense_halo else "sparse (non-zero entries only)",
+            "halo_bytes_sent_per_hop_max_rank": sent,
+            "halo_reduction_vs_dense": halo / sent if sent else None,
         },
         "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -621,36 +625,49 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
     stream: fingerprints + TTL dedup, MERGE of the new incidents and topology delta, incremental
     CSR update, affected-incident BFS and re-rank (egraph/storm.py)."""
     from egraph import synth
-    from egraph.graph import EvidenceGraph
     from egraph.storm import StormEngine
-    if world > 1:
-        raise SystemExit("--workload storm runs on one GPU (DESIGN.md §9: fingerprint-range "
-                         "sharding across GPUs is the next step)")
     t0 = time.time()
     cl = synth.build_cluster(synth.CONFIGS[args.config])
-    g = EvidenceGraph()
-    g.merge_nodes(cl.ids, cl.labels)
-    g.merge_edges(cl.src, cl.dst, cl.types)
+    g = synth.build_graph(cl)
+    # every rank replays the same global stream (same seed): the alerts of a tick arrive spread
+    # over the ranks (alert i at rank i % world) and each rank's webhook share stays at
+    # storm_rate / 60 per tick (weak scaling); the table is fingerprint-sharded, the graph
+    # replicated, incident h ranked on rank h % world (egraph/storm.py)
     wl = synth.StormWorkload(cl, n_keys=args.storm_keys, seed=20260826)
-    eng = StormEngine(g, device=dev, hops=args.hops, k=args.k, dedup_capacity=1 << 17)
+    comm = None
+    if world > 1:
+        from egraph.shard import TorchComm
+        comm = TorchComm()
+    eng = StormEngine(g, device=dev, hops=args.hops, k=args.k, dedup_capacity=1 << 17,
+                      comm=comm, rank=rank)
     per_tick = args.storm_rate // 60
-    log(f"built {args.config} + storm: V={g.num_vertices} keys={args.storm_keys} "
-        f"alerts/tick={per_tick} in {time.time() - t0:.1f}s")
+    n_tick = per_tick * world
+    log(f"[rank {rank}] built {args.config} + storm: V={g.num_vertices} keys={args.storm_keys} "
+        f"alerts/tick={n_tick} ({per_tick} per rank) in {time.time() - t0:.1f}s")
     now = 1_790_000_000_000
     stats = []
+    mine = np.arange(rank, n_tick, world, dtype=np.int64)
     for i in range(args.warmup + args.steps):
         now += 1000
-        keys = wl.alerts(per_tick)
+        keys = wl.alerts(n_tick)
         topo = wl.topology(args.storm_events)
+        local = [keys[j] for j in mine]
         torch.cuda.synchronize(dev)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
         a = time.perf_counter()
-        st = eng.tick(keys, now, wl.make_case, topology=topo)
+        st = eng.tick(local, now, wl.make_case, topology=topo, seq=mine if world > 1 else None)
         torch.cuda.synchronize(dev)
         st["wall_ms"] = (time.perf_counter() - a) * 1e3 - st["collect_ms"]
+        if world > 1:
+            import torch.distributed as dist
+            st["wall_ms"] = max_over_ranks(dist, st["wall_ms"], dev)
         if i >= args.warmup:
             stats.append(st)
-        log(f"tick {i}: {st['new_incidents']} new, {st['affected']} affected / "
-            f"{st['open_incidents']} open, {st['new_edges']} edges, {st['wall_ms']:.2f} ms")
+        if rank == 0:
+            log(f"tick {i}: {st['new_incidents']} new, {st['affected']} affected (rank 0) / "
+                f"{st['open_incidents']} open, {st['new_edges']} edges, {st['wall_ms']:.2f} ms")
     wall = np.array([s_["wall_ms"] for s_ in stats])
     total_alerts = sum(s_["alerts"] for s_ in stats)
     stage = {k_: float(np.mean([s_["ms"][k_] for s_ in stats])) for k_ in stats[0]["ms"]}
@@ -660,8 +677,8 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": float(wall.mean()),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8/u32/fp32",
         "data": "synthetic",
-        "config": {"workload": f"C5: {args.storm_rate} alerts/min (one tick = 1 s of stream = "
-                               f"{per_tick} alerts), Zipf(1.1) over {args.storm_keys} keys, "
+        "config": {"workload": f"C5: {args.storm_rate} alerts/min per GPU (one tick = 1 s of stream = "
+                               f"{n_tick} alerts over {world} GPU(s)), Zipf(1.1) over {args.storm_keys} keys, "
                                f"{args.config} graph, {args.storm_events} topology events/tick, "
                                f"{args.hops}-hop re-rank top-{args.k}",
                    "tick_ms_p50": float(np.percentile(wall, 50)),
@@ -670,6 +687,8 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
                    "new_incidents_per_tick": float(np.mean([s_["new_incidents"] for s_ in stats])),
                    "affected_per_tick": float(np.mean([s_["affected"] for s_ in stats])),
                    "open_incidents_end": stats[-1]["open_incidents"],
+                   "parallelism": (f"fingerprint-sharded dedup x{world}, replicated graph, "
+                                   f"incidents re-ranked by owner rank") if world > 1 else "one GPU",
                    "realtime_headroom": 1000.0 / float(wall.mean())},
         "note": "value = alerts of the timed ticks / pipeline time (collector-side evidence "
                 "generation excluded); a tick covers 1 s of stream, so realtime_headroom = "
@@ -702,6 +721,8 @@ def main():
     ap.add_argument("--shard", default="incidents", choices=["incidents", "graph"],
                     help="incidents: replicated snapshot, incident-sharded (default); graph: "
                          "edge-cut partitioned graph with halo exchange (C4)")
+    ap.add_argument("--dense-halo", action="store_true",
+                    help="--shard graph: exchange whole boundary rows instead of their non-zero entries")
     ap.add_argument("--partitions", type=int, default=1,
                     help="--shard graph on one process: partitions run on this GPU")
     ap.add_argument("--workload", default="rank", choices=["rank", "storm"],

@@ -45,6 +45,13 @@ extern "C" {
 
 const char* egr_last_error(void);
 int egr_version(void);
+
+/* Pinned host memory mapped into the GPU address space (hipHostMalloc mapped + coherent):
+ * *host is the CPU address, *dev the address kernels use.  The drop-in's small launches read
+ * their inputs from and write their results to it directly (no DMA copies; egraph/batcher.py,
+ * egraph/ranker.py).  Free with egr_host_free.                                              */
+int egr_host_alloc(int64_t bytes, void** host, void** dev);
+int egr_host_free(void* host);
 /* Number of HIP devices visible (0 on a GPU-less host; never fails). */
 int egr_device_count(void);
 
@@ -120,6 +127,16 @@ typedef struct egr_rules_out {
 int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_flags, const uint32_t* row_vocab,
                    const uint32_t* row_node, const double* row_err, const int64_t* seg_off,
                    int32_t n_incidents, const egr_rules_out* out, void* stream);
+
+/* egr_rules_eval with its staging in the same call (the drop-in's low-latency launches,
+ * egraph/batcher.py): [0, in_bytes) of the pinned host_in buffer is copied to dev_buf, the
+ * kernel runs on the device copy -- off[12] = byte offsets, identical in both buffers, of
+ * row_flags, row_vocab, row_node, row_err, seg_off, mask, n_hyp, order_conf, order_rank,
+ * confidence, final_score, strength -- and [out_lo, out_hi) is copied back into host_out.
+ * Asynchronous on `stream` (record an event to wait).                                      */
+int egr_rules_eval_staged(const egr_rule_table* table, const void* host_in, void* dev_buf,
+                          void* host_out, const int64_t* off, int64_t in_bytes, int64_t out_lo,
+                          int64_t out_hi, int32_t n_incidents, void* stream);
 
 /* Ranker (A6) over arbitrary hypothesis lists.  List j owns entries [list_off[j], list_off[j+1]).
  *   score = confidence * cat_weight; if support > 0: *= 1 + min(support,5)*0.05;

@@ -326,6 +326,36 @@ extern "C" int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_f
   return EGR_OK;
 }
 
+// One call for the drop-in's single / coalesced launches: inputs staged in ONE host buffer
+// (pinned) go up in one copy, the kernel runs on the device copy, the outputs come back in one
+// copy -- three stream operations, one host call.  off[12] = byte offsets (in both buffers) of
+// flags, vocab, node, err, seg_off, mask, n_hyp, order_conf, order_rank, confidence,
+// final_score, strength; [0, in_bytes) is copied up and [out_lo, out_hi) copied back.
+extern "C" int egr_rules_eval_staged(const egr_rule_table* table, const void* host_in,
+                                     void* dev_buf, void* host_out, const int64_t* off,
+                                     int64_t in_bytes, int64_t out_lo, int64_t out_hi,
+                                     int32_t n_incidents, void* stream) {
+  if (!table || !host_in || !dev_buf || !host_out || !off || in_bytes < 0 || out_lo < in_bytes ||
+      out_hi < out_lo || n_incidents < 0)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval_staged: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* d = static_cast<uint8_t*>(dev_buf);
+  if (in_bytes) EGR_HIP(hipMemcpyAsync(d, host_in, (size_t)in_bytes, hipMemcpyHostToDevice, st));
+  const egr_rules_out out{reinterpret_cast<uint32_t*>(d + off[5]), d + off[6], d + off[7], d + off[8],
+                          reinterpret_cast<double*>(d + off[9]), reinterpret_cast<double*>(d + off[10]),
+                          reinterpret_cast<double*>(d + off[11])};
+  const int rc = egr_rules_eval(table, reinterpret_cast<const uint32_t*>(d + off[0]),
+                                reinterpret_cast<const uint32_t*>(d + off[1]),
+                                reinterpret_cast<const uint32_t*>(d + off[2]),
+                                reinterpret_cast<const double*>(d + off[3]),
+                                reinterpret_cast<const int64_t*>(d + off[4]), n_incidents, &out, stream);
+  if (rc != EGR_OK) return rc;
+  if (out_hi > out_lo)
+    EGR_HIP(hipMemcpyAsync(static_cast<uint8_t*>(host_out) + out_lo, d + out_lo,
+                           (size_t)(out_hi - out_lo), hipMemcpyDeviceToHost, st));
+  return EGR_OK;
+}
+
 extern "C" int egr_rank(const double* confidence, const double* cat_weight, const double* support,
                         const double* strength, const int64_t* list_off, int32_t n_lists,
                         double* out_final, int32_t* out_order, void* stream) {

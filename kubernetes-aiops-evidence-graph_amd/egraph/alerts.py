@@ -193,3 +193,118 @@ class DedupTable:
         L.check(L.lib.egr_dedup_compact(self._h, int(now_ms), int(capacity)), "egr_dedup_compact")
         st = self.stats(now_ms)
         self._slots, self._used_bound = st["slots"], st["used_slots"]
+
+
+class ShardedDedup:
+    """The TTL table sharded by fingerprint range over the ranks of a process group (BASELINE
+    C5 across GPUs).  The reference keeps one Redis (deduplicator.py:41-104) that every webhook
+    replica shares; here rank r owns the fingerprints whose first digest byte b has
+    b * world >> 8 == r, in its own DedupTable on its own GPU.
+
+    ingest() runs the webhook loop (main.py:141-170) over a GLOBAL batch whose alerts arrive
+    spread over the ranks, each alert carrying its global arrival number `seq`:
+      1. every rank routes its alerts' (fingerprint, seq) to the owner ranks (all-to-all; RCCL
+         over xGMI between GPUs);
+      2. each owner runs its table's ingest over the alerts it owns IN ARRIVAL ORDER -- the loop
+         is per key (get / set of one fingerprint), so the owners' loops together make exactly
+         the single table's decisions;
+      3. the owners' (seq, duplicate, owner-local handle) are all-gathered, and every rank
+         numbers the new incidents globally in arrival order (the single table's numbering)
+         and maps each owner-local handle to its global one.
+    Every rank ends with the whole batch's decisions; the host state (the handle maps) is
+    identical on all ranks.  `table` is a DedupTable (or any object with its ingest / remove /
+    extend methods; the CPU tests use the oracle's TTL store), `comm` an egraph.shard.TorchComm."""
+
+    def __init__(self, table, comm, rank: int):
+        self.table, self.comm, self.rank, self.world = table, comm, rank, comm.P
+        self.dev = table.dev
+        self.next_id = 0                                  # the next global incident handle
+        self._g_of = [np.zeros(0, np.int64) for _ in range(self.world)]   # owner-local -> global
+
+    def owner(self, fp: torch.Tensor) -> torch.Tensor:
+        """Owning rank of each [n, 16] fingerprint (range partition of the first byte)."""
+        return (fp[:, 0].to(torch.int64) * self.world) >> 8
+
+    def owns(self, fp: torch.Tensor) -> torch.Tensor:
+        return self.owner(fp) == self.rank
+
+    def _all_gather_v(self, x: torch.Tensor) -> list[torch.Tensor]:
+        """Variable-length all-gather of a 1-D int64 tensor -> one tensor per rank."""
+        n = torch.tensor([x.numel()], dtype=torch.int64, device=x.device)
+        (counts,) = self.comm.all_gather([n])
+        counts = counts.cpu().tolist()
+        m = max(max(counts), 1)
+        pad = torch.zeros(m, dtype=torch.int64, device=x.device)
+        pad[: x.numel()] = x
+        (allx,) = self.comm.all_gather([pad])
+        return [allx[r * m: r * m + counts[r]] for r in range(self.world)]
+
+    def ingest(self, fp: torch.Tensor, seq: torch.Tensor, now_ms: int, ttl_ms: int):
+        """This rank's alerts ([n, 16] uint8 fingerprints, int64 global arrival numbers) ->
+        (dup bool [N], incident int64 [N], n_new) for ALL N alerts of the global batch, in
+        arrival order (numpy arrays; seq must number the global batch 0..N-1)."""
+        fp = _fp_arg(fp, self.dev)
+        seq = seq.to(device=self.dev, dtype=torch.int64)
+        own = self.owner(fp)
+        order = torch.argsort(own, stable=True)
+        words = fp.reshape(-1).view(torch.int64).reshape(-1, 2)[order]             # 16 B = 2 int64
+        payload = torch.cat([words, seq[order, None]], dim=1).reshape(-1)
+        counts = torch.bincount(own, minlength=self.world).cpu().tolist()
+        ((recv, rc),) = self.comm.all_to_all_v([(payload.contiguous(), [3 * c for c in counts])])
+        recv = recv.reshape(-1, 3)
+        rseq = recv[:, 2]
+        o = torch.argsort(rseq)                                         # arrival order
+        mine_fp = recv[o, :2].contiguous().reshape(-1).view(torch.uint8).reshape(-1, 16)
+        mine_seq = rseq[o]
+        dup, local, _ = self.table.ingest(mine_fp, now_ms, ttl_ms)
+        rec = torch.stack([mine_seq, dup.to(torch.int64), local.to(torch.int64)], dim=1).reshape(-1)
+        parts = [p.cpu().numpy().reshape(-1, 3) for p in self._all_gather_v(rec)]
+        N = sum(len(p) for p in parts)
+        dup_all = np.zeros(N, bool)
+        inc_all = np.zeros(N, np.int64)
+        owner_all = np.zeros(N, np.int64)
+        local_all = np.zeros(N, np.int64)
+        for r, p in enumerate(parts):
+            s = p[:, 0]
+            if len(s) and (s.min() < 0 or s.max() >= N):
+                raise ValueError("seq must number the global batch 0..N-1")
+            dup_all[s], owner_all[s], local_all[s] = p[:, 1] != 0, r, p[:, 2]
+        new = np.flatnonzero(~dup_all)
+        g = self.next_id + np.arange(len(new), dtype=np.int64)
+        for r in range(self.world):                     # owner-local handles of the new ones
+            sel = owner_all[new] == r
+            if sel.any():
+                loc = local_all[new][sel]
+                need = int(loc.max()) + 1
+                if need > len(self._g_of[r]):
+                    grown = np.full(max(need, 2 * len(self._g_of[r])), -1, np.int64)
+                    grown[: len(self._g_of[r])] = self._g_of[r]
+                    self._g_of[r] = grown
+                self._g_of[r][loc] = g[sel]
+        inc_all[new] = g
+        d = np.flatnonzero(dup_all)
+        for r in range(self.world):
+            sel = d[owner_all[d] == r]
+            if len(sel):
+                inc_all[sel] = self._g_of[r][local_all[sel]]
+        self.next_id += len(new)
+        return dup_all, inc_all, len(new)
+
+    def remove(self, fp: torch.Tensor) -> None:
+        """DEL of every fingerprint in fp (each rank passes the same list; owners apply)."""
+        fp = _fp_arg(fp, self.dev)
+        m = self.owns(fp)
+        if bool(m.any()):
+            self.table.remove(fp[m].contiguous())
+
+    def extend(self, fp: torch.Tensor, now_ms: int, ttl_ms: int) -> np.ndarray:
+        """EXPIRE of every fingerprint in fp (same list on every rank): bool [n], the key was
+        live, gathered from the owners."""
+        fp = _fp_arg(fp, self.dev)
+        n = fp.shape[0]
+        m = self.owns(fp)
+        ok = torch.zeros(n, dtype=torch.int64, device=self.dev)
+        if bool(m.any()):
+            ok[m] = self.table.extend(fp[m].contiguous(), now_ms, ttl_ms).to(torch.int64)
+        parts = self._all_gather_v(ok)
+        return (torch.stack([p.cpu() for p in parts]).sum(0) != 0).numpy()

@@ -4,10 +4,15 @@ The reference runs one RulesEngine.generate_hypotheses + HypothesisRanker.rank p
 inside each Temporal activity (src/services/workflow/activities.py:124-170); activities run
 concurrently in one worker.  Here:
 
-  RulesRunner   one egr_rules_eval launch over persistent device / pinned host buffers: the
-                encoded columns go up in ONE host-to-device copy, the seven outputs come back in
-                ONE device-to-host copy, and the caller waits on a HIP event by polling it from
-                the event loop (no thread hop, the loop is never blocked).
+  RulesRunner   one egr_rules_eval launch per call.  Small batches (the single-incident
+                calls of the activities) are ZERO-COPY: the kernel reads the encoded rows from,
+                and writes its outputs to, pinned host memory mapped into the GPU address space
+                (egr_host_alloc), so a call is one kernel launch with no DMA copies.  Large
+                batches go through a device buffer: the columns go up in ONE host-to-device copy
+                and the seven outputs come back in ONE device-to-host copy, issued with the
+                kernel in one library call (egr_rules_eval_staged).  Either way the caller waits
+                on a HIP event by polling it from the event loop (no thread hop, the loop is
+                never blocked).
   RulesBatcher  adaptive batching: a call that finds no launch in flight starts one at once
                 (no added latency when idle); calls arriving while a launch runs are collected
                 and go out together in the next one.  Each call gets exactly the dicts a
@@ -24,8 +29,9 @@ import torch
 
 from . import _lib as L
 from .catalog import Catalog
-from .device import require_device
+from .device import MappedBuffer, require_device
 from .encode import EncodedBatch, encode_batch
+from .ranker import FUSED
 from .rca import RulesResult, hypothesis_lists
 
 
@@ -34,7 +40,12 @@ def _align(n: int, a: int = 256) -> int:
 
 
 class RulesRunner:
-    """egr_rules_eval over persistent buffers (grown on demand) on one stream."""
+    """egr_rules_eval over persistent buffers (grown on demand) on one stream.  One launch at
+    a time: the next launch reuses the buffers, so read results() before launching again."""
+
+    # batches up to this many rows are zero-copy (mapped host memory; about 0.4 MB read over
+    # PCIe at the limit); above it the staged device buffer and its two DMA copies win
+    ZERO_COPY_ROWS = 16384
 
     def __init__(self, cat: Catalog, device=None):
         self.cat = cat
@@ -43,6 +54,9 @@ class RulesRunner:
         self.stream = torch.cuda.Stream(self.dev)
         self.cap_rows = self.cap_inc = -1
         self.event = torch.cuda.Event()
+        self._offs = np.zeros(12, np.int64)
+        self.mapped: MappedBuffer | None = None
+        self.zero_copy = False                        # mode of the last launch
 
     def _layout(self, rows: int, B: int):
         S = self.S
@@ -67,7 +81,6 @@ class RulesRunner:
         _, _, total = self._layout(rows, B)
         self.dbuf = torch.empty(total, dtype=torch.uint8, device=self.dev)
         self.hbuf = torch.empty(total, dtype=torch.uint8).pin_memory()
-        self.hnp = self.hbuf.numpy()
         self.cap_rows, self.cap_inc = rows, B
 
     def _h(self, name, dtype, n):
@@ -77,30 +90,45 @@ class RulesRunner:
     def _d(self, name) -> int:
         return self.dbuf.data_ptr() + self.off[name][0]
 
-    def launch(self, enc: EncodedBatch) -> torch.cuda.Event:
-        """Enqueue upload + kernel + download of one encoded batch; returns the event that
-        marks the results as ready in host memory (read them with results())."""
-        B, rows = enc.n_incidents, enc.n_rows
-        self._ensure(rows, B)
-        # this launch's layout inside the buffers: only its own bytes cross the bus
-        self.off, self.in_bytes, self.total = self._layout(rows, B)
+    def _stage_inputs(self, enc: EncodedBatch) -> None:
         for name, arr, dt in (("flags", enc.flags, np.uint32), ("vocab", enc.vocab, np.uint32),
                               ("node", enc.node, np.uint32), ("err", enc.err, np.float64),
                               ("seg", enc.seg_off, np.int64)):
             if len(arr):
                 self._h(name, dt, len(arr))[:] = arr
+
+    def launch(self, enc: EncodedBatch) -> torch.cuda.Event:
+        """Enqueue one encoded batch; returns the event that marks the results as ready in host
+        memory (read them with results())."""
+        B, rows = enc.n_incidents, enc.n_rows
         self._B, self._rows = B, rows
-        out_lo = self.off["mask"][0]
+        # this launch's layout inside the buffers: only its own bytes are touched
+        self.off, self.in_bytes, self.total = self._layout(rows, B)
         st = self.stream
-        with torch.cuda.stream(st):
-            self.dbuf[:self.in_bytes].copy_(self.hbuf[:self.in_bytes], non_blocking=True)
-            o = L.EgrRulesOut(self._d("mask"), self._d("n_hyp"), self._d("oc"), self._d("orank"),
-                              self._d("conf"), self._d("fin"), self._d("str"))
-            L.check(L.lib.egr_rules_eval(self.cat.table, self._d("flags"), self._d("vocab"),
-                                         self._d("node"), self._d("err"), self._d("seg"), B, o,
-                                         st.cuda_stream), "egr_rules_eval")
-            self.hbuf[out_lo:self.total].copy_(self.dbuf[out_lo:self.total], non_blocking=True)
+        if rows <= self.ZERO_COPY_ROWS:
+            if self.mapped is None or self.mapped.nbytes < self.total:
+                self.mapped = MappedBuffer(max(self.total, 1 << 20))
+            self.hnp, self.zero_copy = self.mapped.np, True
+            self._stage_inputs(enc)
+            base = self.mapped.dev
+            d = {k: base + o for k, (o, _) in self.off.items()}
+            o = L.EgrRulesOut(d["mask"], d["n_hyp"], d["oc"], d["orank"], d["conf"], d["fin"], d["str"])
+            L.check(L.lib.egr_rules_eval(self.cat.table, d["flags"], d["vocab"], d["node"], d["err"],
+                                         d["seg"], B, o, st.cuda_stream), "egr_rules_eval")
             self.event.record(st)
+            return self.event
+        self._ensure(rows, B)
+        self.hnp, self.zero_copy = self.hbuf.numpy(), False
+        self._stage_inputs(enc)
+        out_lo = self.off["mask"][0]
+        self._offs[:] = [self.off[k][0] for k in ("flags", "vocab", "node", "err", "seg", "mask",
+                                                   "n_hyp", "oc", "orank", "conf", "fin", "str")]
+        # upload, kernel and download in ONE library call (egr_rules_eval_staged)
+        hp = self.hbuf.data_ptr()
+        L.check(L.lib.egr_rules_eval_staged(self.cat.table, hp, self.dbuf.data_ptr(), hp,
+                                            self._offs.ctypes.data, self.in_bytes, out_lo,
+                                            self.total, B, st.cuda_stream), "egr_rules_eval_staged")
+        self.event.record(st)
         return self.event
 
     def results(self) -> RulesResult:
@@ -227,6 +255,8 @@ class RulesBatcher:
                 res.final_score, res.strength)))
             ids = [i for j in cs for i in ok[j].incident_ids]
             lists = hypothesis_lists(self.cat, sub, ids, [enc.evidence_ids[i] for i in idx], ranked)
+            if not ranked:             # the kernel ranked them too: HypothesisRanker.rank reuses it
+                FUSED.register(self.cat, sub, lists, range(len(lists)))
             pos = 0
             for j in cs:
                 n = len(ok[j].incident_ids)

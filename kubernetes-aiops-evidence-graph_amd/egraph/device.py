@@ -37,3 +37,25 @@ def to_device(a, dev: torch.device) -> torch.Tensor:
     if t.numel() == 0:
         return torch.empty(t.shape, dtype=t.dtype, device=dev)
     return t.pin_memory().to(dev, non_blocking=True)
+
+
+class MappedBuffer:
+    """Pinned host memory mapped into the GPU address space (egr_host_alloc): `np` is the host
+    view, `dev` the address kernels read and write.  The drop-in's small launches use it so
+    that a call is one kernel launch with no DMA copies (egraph/batcher.py, egraph/ranker.py)."""
+
+    def __init__(self, nbytes: int):
+        import ctypes as C
+
+        from . import _lib as L
+        h, d = C.c_void_p(), C.c_void_p()
+        L.check(L.lib.egr_host_alloc(int(nbytes), C.byref(h), C.byref(d)), "egr_host_alloc")
+        self._free = L.lib.egr_host_free
+        self.host, self.dev, self.nbytes = h.value, d.value, int(nbytes)
+        self.np = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.host))
+
+    def __del__(self):
+        h, self.host = getattr(self, "host", None), None
+        if h:
+            self.np = None
+            self._free(h)

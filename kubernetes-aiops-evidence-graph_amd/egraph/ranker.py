@@ -3,19 +3,30 @@
 The host gathers the four numbers the reference reads from each dict (with its defaults and
 its TypeErrors); egr_rank computes final_score with Python-exact float64 rounding and the
 stable descending order of every list in one launch, over persistent pinned / device buffers
-(one packed copy each way), so a single small list costs one kernel round trip.
+(one packed copy each way; zero-copy mapped host memory for small lists), so a single small
+list costs one kernel round trip.
+
+Fused ranks.  egr_rules_eval already ranks every hypothesis list it generates (the ranker's
+score and order are fused into the rules kernel, csrc/rules.hip).  The workflow ranks exactly
+those lists in its next activity (activities.py:124-170), so the rules path registers each
+generated list here (keyed by its hypothesis ids; bounded, least recently used first out) and
+rank() reuses the kernel's final scores and order when the list it gets has the same ids, in the
+same order, with the four inputs the ranker reads unchanged -- verified field by field, so the
+result is exactly what egr_rank would compute.  Any other list (edited, reordered, foreign)
+goes to egr_rank.
 """
 from __future__ import annotations
 
 import math
 import threading
+from collections import OrderedDict
 
 import numpy as np
 import torch
 
 from . import _lib as L
 from .catalog import CATEGORY_WEIGHTS
-from .device import require_device
+from .device import MappedBuffer, require_device
 
 
 def _num(x, what: str) -> float:
@@ -47,32 +58,54 @@ class _RankRunner:
     """egr_rank over persistent device / pinned host buffers on its own stream: one packed
     host-to-device copy, the kernel, one packed device-to-host copy, one event wait."""
 
+    ZERO_COPY_ENTRIES = 4096     # lists with up to this many hypotheses in total: mapped memory
+
     def __init__(self, dev: torch.device):
         self.dev = dev
         self.stream = torch.cuda.Stream(dev)
         self.event = torch.cuda.Event()
         self.cap = 0
         self.lock = threading.Lock()
+        self.mapped = None
+
+    def _layout(self, n: int, nl: int):
+        ino = 32 * n
+        in_bytes = ino + 8 * (nl + 1)
+        fo = (in_bytes + 7) // 8 * 8                      # final f64 [n], then order i32 [n]
+        oo = fo + 8 * n
+        return ino, in_bytes, fo, oo, oo + 4 * n
+
+    def _fill(self, h, cols, off, n, nl, ino) -> None:
+        f64 = h[: 8 * (4 * n + nl + 1)].view(np.float64)
+        for j, col in enumerate(cols):
+            f64[j * n:(j + 1) * n] = col
+        h[ino: ino + 8 * (nl + 1)].view(np.int64)[:] = off
 
     def run(self, cols, off):
         n, nl = len(cols[0]), len(off) - 1
         need = 8 * (5 * n + nl + 1) + 4 * n + 64
         with self.lock:
+            if n <= self.ZERO_COPY_ENTRIES:
+                # zero-copy: the kernel reads the columns from and writes the results to mapped
+                # host memory -- one launch, no DMA copies
+                if self.mapped is None:
+                    self.mapped = MappedBuffer(1 << 20)
+                h, base = self.mapped.np, self.mapped.dev
+                ino, _, fo, oo, end = self._layout(n, nl)
+                self._fill(h, cols, off, n, nl, ino)
+                L.check(L.lib.egr_rank(base, base + 8 * n, base + 16 * n, base + 24 * n, base + ino,
+                                       nl, base + fo, base + oo, self.stream.cuda_stream), "egr_rank")
+                self.event.record(self.stream)
+                self.event.synchronize()
+                return h[fo:oo].view(np.float64).copy(), h[oo:end].view(np.int32).copy()
             if need > self.cap:
                 self.cap = max(need, 2 * self.cap, 1 << 16)
                 self.dbuf = torch.empty(self.cap, dtype=torch.uint8, device=self.dev)
                 self.hbuf = torch.empty(self.cap, dtype=torch.uint8).pin_memory()
                 self.hnp = self.hbuf.numpy()
             h = self.hnp
-            f64 = h[: 8 * (4 * n + nl + 1)].view(np.float64)
-            for j, col in enumerate(cols):
-                f64[j * n:(j + 1) * n] = col
-            ino = 32 * n
-            h[ino: ino + 8 * (nl + 1)].view(np.int64)[:] = off
-            in_bytes = ino + 8 * (nl + 1)
-            fo = (in_bytes + 7) // 8 * 8                      # final f64 [n], then order i32 [n]
-            oo = fo + 8 * n
-            end = oo + 4 * n
+            ino, in_bytes, fo, oo, end = self._layout(n, nl)
+            self._fill(h, cols, off, n, nl, ino)
             base = self.dbuf.data_ptr()
             with torch.cuda.stream(self.stream):
                 self.dbuf[:in_bytes].copy_(self.hbuf[:in_bytes], non_blocking=True)
@@ -87,29 +120,106 @@ class _RankRunner:
 _RUNNERS: dict = {}
 
 
+class FusedRanks:
+    """The rules kernel's ranking of the lists it generated, for rank() to reuse (module doc).
+    A record is (hypothesis ids, per-position (confidence, category, support_count,
+    signal_strength) as the kernel emitted them, final scores, ranked positions)."""
+
+    def __init__(self, capacity: int = 1 << 16):
+        self.capacity = capacity
+        self.recs: OrderedDict = OrderedDict()
+        self.lock = threading.Lock()
+        self.hits = self.misses = 0
+
+    def register(self, cat, res, lists: list[list[dict]], rows) -> None:
+        """lists[j] = the unranked dicts of result row rows[j] (confidence order)."""
+        rules, R = cat.rules, cat.n_rules
+        unknown = (cat.unknown["confidence"], cat.unknown["category"],
+                   cat.unknown["support_count"], cat.unknown["signal_strength"])
+        recs = []
+        for hyps, i in zip(lists, rows):
+            n = len(hyps)
+            oc, orank = res.order_conf[i], res.order_rank[i]
+            pos = {int(oc[p]): p for p in range(n)}
+            fields, fin = [], []
+            for p in range(n):
+                slot = int(oc[p])
+                if slot == R:
+                    fields.append(unknown)
+                else:
+                    r = rules[slot]
+                    fields.append((float(res.confidence[i, slot]), r["category"],
+                                   len(r["conditions"]), float(res.strength[i, slot])))
+                fin.append(float(res.final_score[i, slot]))
+            ranked = tuple(pos[int(orank[q])] for q in range(n))
+            recs.append((hyps[0]["id"], (tuple(h["id"] for h in hyps), tuple(fields), fin, ranked)))
+        with self.lock:
+            for key, rec in recs:
+                self.recs[key] = rec
+            while len(self.recs) > self.capacity:
+                self.recs.popitem(last=False)
+
+    def apply(self, hyps: list) -> list | None:
+        """Rank `hyps` from its record if it is exactly a registered list; else None."""
+        if not hyps or not isinstance(hyps[0], dict):
+            return None
+        with self.lock:
+            rec = self.recs.get(hyps[0].get("id"))
+        if rec is None:
+            self.misses += 1
+            return None
+        ids, fields, fin, ranked = rec
+        if len(hyps) != len(ids):
+            self.misses += 1
+            return None
+        for h, hid, (c, cat, sup, st) in zip(hyps, ids, fields):
+            if not isinstance(h, dict) or h.get("id") != hid or \
+                    h.get("confidence", 0.5) != c or h.get("category", "unknown") != cat or \
+                    h.get("support_count", 0) != sup or h.get("signal_strength", 0) != st:
+                self.misses += 1
+                return None
+        self.hits += 1
+        for h, f in zip(hyps, fin):
+            h["final_score"] = f
+        out = [hyps[p] for p in ranked]
+        for q, h in enumerate(out):
+            h["rank"] = q + 1
+        return out
+
+
+FUSED = FusedRanks()
+
+
 def rank_lists(lists: list[list[dict]], device=None) -> list[list[dict]]:
-    """Rank every list in one launch; mutates and returns the dicts like the reference."""
+    """Rank every list in one launch; mutates and returns the dicts like the reference.  Lists
+    the rules kernel generated and already ranked are served from FUSED."""
     dev = require_device(device)
+    out: list = [FUSED.apply(hyps) for hyps in lists]
+    todo = [j for j, r in enumerate(out) if r is None]
+    if not todo:
+        return out
     cols = ([], [], [], [])
     off = [0]
-    for hyps in lists:
+    for j in todo:
+        hyps = lists[j]
         for acc, vals in zip(cols, gather(hyps)):
             acc.extend(vals)
         off.append(off[-1] + len(hyps))
     n = off[-1]
     if n == 0:
-        return [[] for _ in lists]
+        for j in todo:
+            out[j] = []
+        return out
     r = _RUNNERS.get(dev)
     if r is None:
         r = _RUNNERS[dev] = _RankRunner(dev)
     final_h, order_h = r.run(cols, off)
-    out = []
-    for j, hyps in enumerate(lists):
-        b = off[j]
+    for t, j in enumerate(todo):
+        hyps, b = lists[j], off[t]
         for i, h in enumerate(hyps):
             h["final_score"] = float(final_h[b + i])
         ranked = [hyps[int(order_h[b + p])] for p in range(len(hyps))]
         for p, h in enumerate(ranked):
             h["rank"] = p + 1
-        out.append(ranked)
+        out[j] = ranked
     return out

@@ -13,9 +13,12 @@ one); then the halo (non-owned neighbours of owned vertices), in global order, w
 Rank r sends q the r-owned rows that q's rows read.
 
 Per hop (run_partitioned): the engine computes its rows; the fresh rows other ranks read are
-packed (one contiguous segment per reader), exchanged point-to-point (RCCL over xGMI:
-torch.distributed all_to_all_single with per-peer row counts; [rows][Bpad] fp32 for scores and
-[rows][ceil(B/64)] u64 for reach) and unpacked into the halo rows.  After the last hop each rank ranks its owned candidates; the (score, global id)
+packed (one contiguous segment per reader) and exchanged point-to-point (RCCL over xGMI:
+torch.distributed all_to_all_single with per-peer counts), then unpacked into the halo rows.
+The default exchange is SPARSE: only the non-zero entries of the packed rows cross the link
+(a boundary row is non-zero only in the columns whose 3-hop frontier reached it), as
+(index, value) int64 words after a per-peer count exchange; the dense exchange ([rows][Bpad]
+fp32 for scores, [rows][ceil(B/64)] u64 for reach) remains as run_partitioned(sparse=False).  After the last hop each rank ranks its owned candidates; the (score, global id)
 lists are all-gathered and merged (score desc, global id asc) -- the unpartitioned top-k.
 Scores, reach sets and top-k are bit-identical to the single-GPU plan (tests/test_shard*.py).
 """
@@ -172,6 +175,31 @@ class TorchComm:
         self.dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
                                     group=self.group)
 
+    def all_to_all_v(self, items: list) -> list:
+        """items = [(send 1-D int64, send_counts)] for this process's one rank -> [recv, with
+        the per-sender counts]: sizes are exchanged first (one int64 per peer), then the data."""
+        ((send, sc),) = items
+        dev = send.device
+        cnt = torch.tensor(sc, dtype=torch.int64)
+        rcnt = torch.empty(self.P, dtype=torch.int64)
+        if self.gloo:
+            self.dist.all_to_all_single(rcnt, cnt, group=self.group)
+        else:
+            rc_d = torch.empty(self.P, dtype=torch.int64, device=dev)
+            self.dist.all_to_all_single(rc_d, cnt.to(dev), group=self.group)
+            rcnt = rc_d.cpu()
+        rc = rcnt.tolist()
+        recv = torch.empty(sum(rc), dtype=send.dtype, device=dev)
+        if self.gloo:
+            hr = torch.empty(sum(rc), dtype=send.dtype)
+            self.dist.all_to_all_single(hr, send.cpu(), output_split_sizes=rc, input_split_sizes=sc,
+                                        group=self.group)
+            recv.copy_(hr)
+        else:
+            self.dist.all_to_all_single(recv, send, output_split_sizes=rc, input_split_sizes=sc,
+                                        group=self.group)
+        return [(recv, rc)]
+
 
 class LocalComm:
     """All ranks in one process (tests, and a multi-partition single-GPU run): gathers are
@@ -194,6 +222,17 @@ class LocalComm:
                         items[r][0][s_off[r][q]: s_off[r][q] + n].to(items[q][2].device)
 
 
+    def all_to_all_v(self, items: list) -> list:
+        P = len(items)
+        s_off = [np.concatenate([[0], np.cumsum(sc)]) for _, sc in items]
+        out = []
+        for q in range(P):
+            parts = [items[r][0][s_off[r][q]: s_off[r][q] + items[r][1][q]].to(items[q][0].device)
+                     for r in range(P)]
+            out.append((torch.cat(parts), [items[r][1][q] for r in range(P)]))
+        return out
+
+
 class RankRun:
     """One rank's part of a partitioned pass.  `engine` is the HIP Plan of the local snapshot
     (egraph.graph.Plan); any object with the same methods works (the CPU tests use the oracle)."""
@@ -212,12 +251,73 @@ class RankRun:
         self.recv_s = torch.zeros((nr, self.Bpad), dtype=torch.float32, device=device)
         self.send_r = torch.zeros((ns, self.W), dtype=torch.int64, device=device)
         self.recv_r = torch.zeros((nr, self.W), dtype=torch.int64, device=device)
+        self.sent_bytes = 0        # bytes this rank put on the wire (every exchange so far)
+        self.exchanges = 0
         engine.set_owned(lg.n_owned)
 
     @property
     def halo_bytes_per_hop(self) -> int:
-        """Bytes this rank sends per hop (scores + reach words)."""
+        """Bytes this rank sends per hop with the dense exchange (scores + reach words)."""
         return len(self.lg.send_rows) * (self.Bpad * 4 + self.W * 8)
+
+
+
+
+def _seg_starts(counts) -> np.ndarray:
+    return np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+
+
+def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
+    """The halo exchange with only the NON-ZERO entries on the wire: a boundary row's scores
+    are non-zero only in the columns whose frontier reached it, and its reach words only where
+    a column reached it.  Each rank packs its send rows (device-local), keeps the non-zero
+    (row-in-segment, column) entries as one int64 each -- index << 32 | value bits (scores) or
+    index + word (reach, two int64) -- exchanges the per-peer counts, then the entries, and
+    scatters them into its zeroed halo rows.  Bit-identical to the dense exchange."""
+    items, meta = [], []
+    for r in runs:
+        if what == "scores":
+            r.eng.pack_scores(r.send, r.send_s)
+            buf, width = r.send_s, r.Bpad
+        else:
+            r.eng.pack_reach(r.send, r.send_r)
+            buf, width = r.send_r, r.W
+        flat = buf.view(-1)
+        nz = torch.nonzero(flat, as_tuple=True)[0]               # row-major: grouped by peer
+        row = nz // width
+        seg = _seg_starts(r.lg.send_counts)
+        seg_t = torch.from_numpy(seg).to(nz.device)
+        peer = torch.searchsorted(seg_t[1:], row, right=True)
+        local = (row - seg_t[peer]) * width + (nz % width)       # index inside the peer's segment
+        counts = torch.bincount(peer, minlength=len(r.lg.send_counts)).cpu().tolist()
+        if what == "scores":
+            vbits = flat[nz].view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+            payload = (local << 32) | vbits
+            n_per = [c for c in counts]
+        else:
+            payload = torch.stack([local, flat[nz]], dim=1).reshape(-1)
+            n_per = [2 * c for c in counts]
+        r.sent_bytes += int(payload.numel()) * 8 + 8 * len(counts)
+        r.exchanges += 1
+        items.append((payload.contiguous(), n_per))
+        meta.append(width)
+    out = comm.all_to_all_v(items)
+    for r, (recv, rc), width in zip(runs, out, meta):
+        dst = r.recv_s if what == "scores" else r.recv_r
+        dst.zero_()
+        roff = _seg_starts(r.lg.recv_counts)
+        base = torch.from_numpy(np.repeat(roff[:-1] * width,
+                                          [c // (1 if what == "scores" else 2) for c in rc])).to(dst.device)
+        if what == "scores":
+            idx = (recv >> 32) + base
+            dst.view(-1)[idx] = (recv & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
+        else:
+            pairs = recv.view(-1, 2)
+            dst.view(-1)[pairs[:, 0] + base] = pairs[:, 1]
+        if what == "scores":
+            r.eng.unpack_scores(r.halo, r.src, r.recv_s)
+        else:
+            r.eng.unpack_reach(r.halo, r.src, r.recv_r)
 
 
 def _exchange(runs: list[RankRun], comm, what: str) -> None:
@@ -231,25 +331,29 @@ def _exchange(runs: list[RankRun], comm, what: str) -> None:
             items.append((r.send_r, r.lg.send_counts, r.recv_r, r.lg.recv_counts))
     comm.all_to_all(items)
     for r in runs:
+        r.sent_bytes += len(r.lg.send_rows) * (r.Bpad * 4 if what == "scores" else r.W * 8)
+        r.exchanges += 1
         if what == "scores":
             r.eng.unpack_scores(r.halo, r.src, r.recv_s)
         else:
             r.eng.unpack_reach(r.halo, r.src, r.recv_r)
 
 
-def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int):
+def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int,
+                    sparse: bool = True):
     """`hops` hops of propagation and reach on every local rank in `runs` (seeds and sources
     already set on their engines), halo exchanges between hops, then the merged global top-k.
     Returns (ids int64 [B, k] global vertex ids (NO_NODE = none), scores f32 [B, k])."""
     for h in range(hops):
         for r in runs:
             r.eng.hop()
+        xch = _exchange_sparse if sparse else _exchange
         if h + 1 < hops:
-            _exchange(runs, comm, "scores")
+            xch(runs, comm, "scores")
         for r in runs:
             r.eng.reach_hop()
         if h + 1 < hops:
-            _exchange(runs, comm, "reach")
+            xch(runs, comm, "reach")
     cands = []
     for r in runs:
         r.eng.candidates(exclude_label)

@@ -23,6 +23,17 @@ second of the stream):
      whose pending ids appeared)
 Every cached ranking therefore equals a from-scratch ranking of the current graph
 (tests/test_storm_gpu.py checks it tick by tick).
+
+Across GPUs (`comm` given: one process per GPU, BASELINE C5 "across 8xMI355X"):
+  * the dedup table is sharded by fingerprint range (egraph.alerts.ShardedDedup): each rank
+    fingerprints the alerts that arrived at it, routes them to their owners (all-to-all) and
+    every rank receives the whole tick's decisions, numbered as one table would;
+  * the graph is replicated: every rank MERGEs every new incident and the topology delta in
+    the same order and updates its own device CSR (the delta is small; the host MERGE is the
+    part that does not shrink with more ranks);
+  * incident h is owned by rank h % world: only the owner keeps its seeds and ranking, checks
+    whether it is affected and re-ranks it.
+The union of the owners' rankings equals the single-GPU engine's (tests/test_storm_gpu.py).
 """
 from __future__ import annotations
 
@@ -33,7 +44,7 @@ from typing import Callable
 import numpy as np
 import torch
 
-from egraph.alerts import DedupTable, fingerprints
+from egraph.alerts import DedupTable, ShardedDedup, fingerprints
 from egraph.device import to_device
 from egraph.graph import EvidenceGraph
 from egraph.seeds import SeedCandidates
@@ -70,12 +81,16 @@ class StormEngine:
     COL_BUCKETS = (64, 256, 1024, 4096)
 
     def __init__(self, graph: EvidenceGraph, *, device=None, hops: int = 3, k: int = 10,
-                 ttl_ms: int = 4 * 3600 * 1000, dedup_capacity: int = 1 << 16, weights=None):
+                 ttl_ms: int = 4 * 3600 * 1000, dedup_capacity: int = 1 << 16, weights=None,
+                 comm=None, rank: int = 0):
         self.g = graph
         self.snap = graph.snapshot(weights, device)
         self.dev = self.snap.dev
         self.hops, self.k, self.ttl_ms = hops, k, ttl_ms
         self.table = DedupTable(dedup_capacity, self.dev)
+        # comm (egraph.shard.TorchComm): fingerprint-sharded table, incidents owned round-robin
+        self.rank, self.world = (rank, comm.P) if comm is not None else (0, 1)
+        self.dedup = ShardedDedup(self.table, comm, rank) if comm is not None else None
         self.incidents: list[OpenIncident] = []
         self._pending: dict[str, set[int]] = {}
         self._frontiers: dict[int, object] = {}
@@ -120,8 +135,12 @@ class StormEngine:
                            [np.full(len(x.sv), x.handle, np.int64) for x in xs])
         return to_device(v, self.dev), to_device(o, self.dev)
 
+    def owns(self, handle: int) -> bool:
+        return handle % self.world == self.rank
+
     def _rebuild_check(self) -> None:
-        self._chk_v, self._chk_o = self._check_parts(self.incidents)
+        self._chk_v, self._chk_o = self._check_parts(
+            [x for x in self.incidents if self.owns(x.handle)])
 
     def _append_check(self, handles: list[int]) -> None:
         if handles:
@@ -150,16 +169,25 @@ class StormEngine:
                 x.ranked_at = self.ticks
 
     def tick(self, keys: list[str], now_ms: int, make_case: Callable[[int, int], StormCase],
-             topology: tuple | None = None) -> dict:
+             topology: tuple | None = None, seq=None) -> dict:
         """One batch of alerts.  `keys`: the alerts' fingerprint keys, in arrival order
         (normalizer.py:217 strings).  `make_case(handle, alert_index)` builds the incident an
         alert opens.  `topology`: optional (vertex ids, labels, edge src, dst, types) MERGEd in
-        the same tick.  Returns counts and per-stage wall times (ms)."""
+        the same tick.  Across GPUs `keys` are the alerts that arrived at this rank and `seq`
+        their numbers in the tick's global arrival order (alert_index refers to that order;
+        make_case and topology must be the same on every rank).  Returns counts and per-stage
+        wall times (ms)."""
         t = [time.perf_counter()]
         fp, _ = fingerprints(keys, self.dev)
-        dup, inc, n_new = self.table.ingest(fp, now_ms, self.ttl_ms)     # synchronises
-        dup_h = dup.cpu().numpy()
-        inc_h = inc.cpu().numpy()
+        if self.dedup is None:
+            dup, inc, n_new = self.table.ingest(fp, now_ms, self.ttl_ms)     # synchronises
+            dup_h = dup.cpu().numpy()
+            inc_h = inc.cpu().numpy()
+        else:
+            if seq is None:
+                raise ValueError("a sharded tick needs the alerts' global arrival numbers (seq)")
+            dup_h, inc_h, n_new = self.dedup.ingest(
+                fp, torch.as_tensor(np.asarray(seq, np.int64)), now_ms, self.ttl_ms)
         t.append(time.perf_counter())
         # host MERGE of the new incidents and the tick's topology
         openers = np.flatnonzero(~dup_h)
@@ -202,9 +230,11 @@ class StormEngine:
         t.append(time.perf_counter())
         n_v, n_e = self.snap.sync(self.g)                                 # GPU CSR update
         t.append(time.perf_counter())
-        # affected incidents (before the new incidents join the check arrays)
-        affected = set(new_handles)
+        # affected incidents (before the new incidents join the check arrays); only this
+        # rank's own incidents are checked and re-ranked
         n_old = len(self.incidents) - len(new_handles)
+        new_handles = [h for h in new_handles if self.owns(h)]
+        affected = set(new_handles)
         reseed = set()
         if n_old:
             for vid in new_ids:                          # rows that would attach differently now
@@ -238,7 +268,7 @@ class StormEngine:
         self.ticks += 1
         ms = [(b - a) * 1e3 for a, b in zip(t, t[1:])]
         ms[1] -= t_collect * 1e3          # the incidents' evidence comes from the collectors
-        return {"alerts": len(keys), "duplicates": int(dup_h.sum()), "new_incidents": n_new,
+        return {"alerts": len(dup_h), "duplicates": int(dup_h.sum()), "new_incidents": n_new,
                 "new_vertices": n_v, "new_edges": n_e, "affected": len(affected),
                 "open_incidents": len(self.incidents),
                 "ms": dict(zip(("fingerprint_dedup", "merge_host", "csr_update", "affected", "seeds_host",
@@ -246,4 +276,5 @@ class StormEngine:
                 "collect_ms": t_collect * 1e3}
 
     def rankings(self) -> list[tuple[np.ndarray, np.ndarray]]:
+        """(top ids, top scores) of every incident (None for those another rank owns)."""
         return [(x.top_ids, x.top_scores) for x in self.incidents]

@@ -29,9 +29,12 @@ def test_runner_matches_oracle():
     rng = random.Random(17)
     cat = catalog.default()
     runner = RulesRunner(cat)
-    for n in (1, 3, 700, 40):                # grows, then reuses the buffers with a smaller batch
+    # zero-copy (mapped host memory) for small batches, the staged device buffer above
+    # ZERO_COPY_ROWS; grows, then reuses the buffers with a smaller batch
+    for n in (1, 3, 700, 40, 2000, 0, 5):
         enc = encode_batch([evidence_fuzz.random_evidence(rng) for _ in range(n)], cat)
         res = runner.run_sync(enc)
+        assert runner.zero_copy == (enc.n_rows <= runner.ZERO_COPY_ROWS)
         exp = oracle.rules_eval(cat.table, enc.flags, enc.vocab, enc.node, enc.err, enc.seg_off)
         np.testing.assert_array_equal(res.mask, exp["mask"])
         np.testing.assert_array_equal(res.order_rank, exp["order_rank"])
@@ -60,11 +63,13 @@ def test_concurrent_calls_coalesce_and_match_golden(golden):
     async def go():
         return await asyncio.gather(*[one(i, c) for i, c in enumerate(cases)])
 
+    from egraph.ranker import FUSED
     b = RE._batcher(eng.catalog, eng.device)
-    l0, c0 = b.launches, b.calls
+    l0, c0, h0 = b.launches, b.calls, FUSED.hits
     out = asyncio.run(go())
     assert b.calls - c0 == len(cases)
     assert b.launches - l0 < len(cases) // 4            # coalesced
+    assert FUSED.hits - h0 == len(cases) // 2           # rank() reused the kernel's ranking
     for case, hyps in zip(cases, out):
         assert record(hyps) == golden_record(case["expected"]), case["name"]
 

@@ -77,7 +77,7 @@ def test_local_graphs_cover_the_global_csr(P):
             assert len(np.unique(sent[(r, lg.rank)])) == len(sent[(r, lg.rank)])
 
 
-def _rank_main(rank, P, port, q):
+def _rank_main(rank, P, port, q, sparse=True):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=P)
@@ -95,8 +95,9 @@ def _rank_main(rank, P, port, q):
         eng.set_sources(shard.local_sources(lg, V, src))
         run = shard.RankRun(lg, eng, torch.device("cpu"))
         inc = g.labels().index("Incident")
-        (ids, scores), = shard.run_partitioned([run], shard.TorchComm(), 3, inc, 6)
-        q.put((rank, lg.gid[: lg.n_owned], eng.scores_owned(), ids.numpy(), scores.numpy()))
+        (ids, scores), = shard.run_partitioned([run], shard.TorchComm(), 3, inc, 6, sparse=sparse)
+        q.put((rank, lg.gid[: lg.n_owned], eng.scores_owned(), ids.numpy(), scores.numpy(),
+               run.sent_bytes, 2 * run.halo_bytes_per_hop))
     finally:
         dist.destroy_process_group()
 
@@ -107,13 +108,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("P", [2])
-def test_partitioned_protocol_gloo_world_size_2(P):
+@pytest.mark.parametrize("P,sparse", [(2, True), (2, False)])
+def test_partitioned_protocol_gloo_world_size_2(P, sparse):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, P, port, q)) for r in range(P)]
+    procs = [ctx.Process(target=_rank_main, args=(r, P, port, q, sparse)) for r in range(P)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(P)]
@@ -128,7 +129,9 @@ def test_partitioned_protocol_gloo_world_size_2(P):
     vl, _, _, _ = g.export()
     e_ids, e_sc = oracle.topk(exp, er, vl, g.labels().index("Incident"), 6)
     covered = 0
-    for rank, gids, owned_scores, ids, scores in res:
+    for rank, gids, owned_scores, ids, scores, sent, dense in res:
+        # 2 exchanges (scores + reach) x 2 hops; the sparse one sends only non-zero entries
+        assert sent == dense if not sparse else 0 < sent < dense
         assert owned_scores.tobytes() == exp[gids].tobytes()          # bit-identical rows
         covered += len(gids)
         got = ids.astype(np.int64)

@@ -36,8 +36,9 @@ def _dev(a):
     return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
 
 
-@pytest.mark.parametrize("P,B", [(2, 40), (3, 130), (4, 70)])
-def test_partitioned_plan_equals_unpartitioned(P, B):
+@pytest.mark.parametrize("P,B,sparse", [(2, 40, True), (3, 130, True), (4, 70, True),
+                                        (2, 40, False), (4, 70, False)])
+def test_partitioned_plan_equals_unpartitioned(P, B, sparse):
     from egraph import shard
     from egraph.graph import Snapshot
     g, sv, sc, ss, src = _graph(B, seed=80 + P, pods=2500)
@@ -56,7 +57,10 @@ def test_partitioned_plan_equals_unpartitioned(P, B):
         plan.set_sources(_dev(shard.local_sources(lg, V, src)))
         runs.append(shard.RankRun(lg, plan, torch.device("cuda", 0)))
         runs[-1].snap = snap
-    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k)
+    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k, sparse=sparse)
+    for run in runs:                 # 2 hops x (scores + reach) exchanged
+        dense = 2 * run.halo_bytes_per_hop
+        assert run.sent_bytes == dense if not sparse else run.sent_bytes < dense
     exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
     er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
     e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)

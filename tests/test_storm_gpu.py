@@ -72,3 +72,91 @@ def test_storm_ticks_match_full_recompute_and_oracle():
     e_ids, e_sc = oracle.topk(exp, er, vl, g.labels().index("Incident"), 8)
     np.testing.assert_array_equal(ids, e_ids)
     assert scores.tobytes() == e_sc.tobytes()
+
+
+def _storm_setup():
+    from egraph import synth
+    cfg = synth.ClusterConfig(pods=3000, namespaces=10, nodes=600, deployments=600, services=300,
+                              attach_fraction=0.2, seed=77)
+    c = synth.build_cluster(cfg)
+    g = synth.build_graph(c)
+    wl = synth.StormWorkload(c, n_keys=900, seed=5, events_per_incident=10)
+    return g, wl
+
+
+def _storm_ticks():
+    """(clock step, alerts) per tick: bursts, quiet ticks and jumps past the 20 s TTL."""
+    return [([1000, 1000, 7000, 25_000][t % 4], 60 if t < 2 else 12) for t in range(10)]
+
+
+def _storm_rank_main(rank, world, port, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from egraph.shard import TorchComm
+        from egraph.storm import StormEngine
+        g, wl = _storm_setup()
+        eng = StormEngine(g, hops=3, k=8, ttl_ms=20_000, dedup_capacity=4096, comm=TorchComm(),
+                          rank=rank)
+        now, decisions = 1_000_000, []
+        for step, n in _storm_ticks():
+            now += step
+            keys = wl.alerts(n)
+            topo = wl.topology(4)
+            mine = np.arange(rank, n, world)
+            before = len(eng.incidents)
+            st = eng.tick([keys[i] for i in mine], now, wl.make_case, topology=topo, seq=mine)
+            decisions.append((st["new_incidents"], st["duplicates"], len(eng.incidents) - before))
+        owned = {x.handle: (x.top_ids, x.top_scores) for x in eng.incidents if eng.owns(x.handle)}
+        q.put((rank, decisions, owned, eng.table.stats(now)["live"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_storm_sharded_two_ranks_equals_one_gpu():
+    """BASELINE C5 across GPUs: two processes (gloo, sharing the one GPU) with the fingerprint-
+    sharded table, the replicated graph and incidents ranked by their owner rank make the same
+    dedup decisions and, incident by incident, the same rankings as the one-GPU engine."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from egraph.storm import StormEngine
+    g, wl = _storm_setup()
+    one = StormEngine(g, hops=3, k=8, ttl_ms=20_000, dedup_capacity=4096)
+    now, want = 1_000_000, []
+    for step, n in _storm_ticks():
+        now += step
+        keys = wl.alerts(n)
+        before = len(one.incidents)
+        st = one.tick(keys, now, wl.make_case, topology=wl.topology(4))
+        want.append((st["new_incidents"], st["duplicates"], len(one.incidents) - before))
+    live = one.table.stats(now)["live"]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_storm_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=200) for _ in range(2)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owned = {}
+    for rank, decisions, mine, n_live in res:
+        assert decisions == want
+        assert all(h % 2 == rank for h in mine)
+        owned.update(mine)
+    assert sum(r[3] for r in res) == live                 # the shards hold the table's keys
+    assert sorted(owned) == [x.handle for x in one.incidents]
+    for x in one.incidents:
+        ids, scores = owned[x.handle]
+        np.testing.assert_array_equal(ids, x.top_ids, err_msg=f"incident {x.handle}")
+        assert scores.tobytes() == x.top_scores.tobytes()
