@@ -421,6 +421,34 @@ def roofline_probe(ctx, hops: int, reps: int) -> float:
     return float(np.mean(ms))
 
 
+def rules_probe(ctx, reps: int = 50) -> dict:
+    """egr_rules_eval alone on the GPU: the bench batch's launch timed `reps` times with HIP
+    events on its stream, one at a time (in the timed region it shares the CUs with the
+    frontier launches of the other batches in flight)."""
+    rules = ctx["rules"]
+    st = torch.cuda.Stream()
+    ms = []
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        rules.launch(st.cuda_stream)
+        b.record(st)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    rows = ctx["enc"].n_rows
+    B = rules.B
+    # algorithmic bytes: the rows once (20 B: flags, vocab, node, err), the segment offsets,
+    # and the outputs (mask, n_hyp, 2 x S order bytes, 3 x S doubles per incident)
+    S = 11
+    nbytes = 20 * rows + 8 * (B + 1) + B * (5 + 2 * S + 24 * S)
+    us = float(np.median(ms)) * 1e3
+    return {"kernel": "rules_eval_kernel", "isolated_us_median": us,
+            "isolated_us_min": float(np.min(ms)) * 1e3, "launches": reps,
+            "incidents": B, "rows": rows, "algorithmic_bytes": nbytes,
+            "achieved_GBps": nbytes / (us * 1e-6) / 1e9}
+
+
 def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tuple[dict, dict]:
     """Algorithmic bytes of one egr_frontier_run: every CSR entry a pull reads
     (col + val, 8 B), every entry an expansion reads (col, 4 B), a row_ptr pair per row walk
@@ -808,6 +836,7 @@ def main():
         launch_ms = roofline_probe(ctx, args.hops, args.roofline_reps)
         roof, work = frontier_roofline(ctx, launch_ms, B, args.k, ms)
         roof["isolated_launches"] = args.roofline_reps
+        rules_iso = rules_probe(ctx)
         if timed:
             roof["avg_launch_ms_in_flight"] = float(np.mean([a.elapsed_time(b) for a, b in timed]))
         out_graph = graphs
@@ -847,6 +876,8 @@ def main():
         },
         "roofline": roof,
     }
+    if args.engine == "frontier":
+        out["rules_kernel"] = rules_iso
     if work is not None:
         out["edges_per_sec"] = world * (work["pull_entries"] + work["expand_entries"]) / (ms * 1e-3)
         out["frontier_work"] = work

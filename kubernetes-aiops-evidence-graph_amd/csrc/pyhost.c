@@ -344,7 +344,10 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
       int slow = 1;
       if (PyDict_CheckExact(ev)) {
         PyObject *t, *data;
-        if (!dget(ev, k_id, &ev_id) && !dget(ev, k_type, &t) && !dget(ev, k_data, &data)) {
+        /* evidence_ids[:5] reads only the first five rows' ids (an exact dict's get of a str
+         * key cannot raise or run user code, so skipping the rest changes nothing) */
+        const int want_id = PyList_GET_SIZE(first) < 5;
+        if (!(want_id && dget(ev, k_id, &ev_id)) && !dget(ev, k_type, &t) && !dget(ev, k_data, &data)) {
           int ty = type_of(t);
           if (ty == T_NONE) {
             slow = hashable_plain(t == NULL ? Py_None : t) ? 0 : 1;

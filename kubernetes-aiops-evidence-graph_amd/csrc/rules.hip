@@ -10,13 +10,17 @@
 //     the table holds fall back to an exact pairwise count;
 //   * lane r evaluates rule r's conditions (:378-441).  A rule emits only when ALL its
 //     conditions hold, so its strength, confidence (:443-455) and ranker score
-//     (hypothesis_ranker.py:44-63) are constants of the rule table: the host computes them once
-//     per launch in float64 with Python-exact rounding (RuleConsts) and the kernel does no
-//     floating-point arithmetic;
+//     (hypothesis_ranker.py:44-63) are constants of the rule table: the host computes them in
+//     float64 with Python-exact rounding into the compiled table (RulesDev), uploaded once per
+//     distinct table, and the kernel does no floating-point arithmetic;
 //   * both stable orders (by confidence, :228; then by final_score, hypothesis_ranker.py:67)
 //     by counting, with the unknown fallback (:230-231, :457-478).
 // The per-incident working set is a few KB, so the kernel is latency- not bandwidth-bound for
 // realistic batches; its HBM cost is one read of the rows.
+#include <mutex>
+#include <tuple>
+#include <vector>
+
 #include "egr_internal.h"
 
 namespace {
@@ -49,10 +53,24 @@ __device__ __forceinline__ double wave_sum_d(double x) {
   return x;
 }
 
-// Per-rule constants of a launch (host-computed, egr::rule_confidence / ranker_final_score).
-struct RuleConsts {
-  double conf[EGR_MAX_RULES], fin[EGR_MAX_RULES], str[EGR_MAX_RULES];
-  double unknown_fin;
+// The rule table as the kernel reads it: compiled on the host from egr_rule_table (conditions
+// plus the constants of a matched rule: its strength, confidence (:443-455) and ranker score
+// (hypothesis_ranker.py:44-63), computed in float64 with Python-exact rounding) and uploaded
+// ONCE per distinct table into device memory (rules_table_dev below).  The kernel then gets one
+// pointer instead of a 4.6-KB by-value argument block, and lane r reads rule r with a few
+// 16-B loads of L2-resident data.
+struct RuleDev {
+  int32_t n_conds;
+  int32_t cond_type[EGR_MAX_CONDS];
+  uint32_t cond_mask[EGR_MAX_CONDS];
+  double cond_param[EGR_MAX_CONDS];
+  double conf, fin, str;
+};
+struct RulesDev {
+  int32_t n_rules;
+  uint32_t network_vocab_bit;
+  double unknown_confidence, unknown_fin;
+  RuleDev rules[EGR_MAX_RULES];
 };
 
 constexpr int kNodeSlots = 256;                 // per-wave pods_by_node hash table
@@ -90,7 +108,7 @@ __device__ bool condition_holds(int type, uint32_t mask, double param, const Sig
 }
 
 __global__ __launch_bounds__(256) void rules_eval_kernel(
-    const egr_rule_table T, const RuleConsts K, const uint32_t* __restrict__ row_flags,
+    const RulesDev* __restrict__ D, const uint32_t* __restrict__ row_flags,
     const uint32_t* __restrict__ row_vocab, const uint32_t* __restrict__ row_node,
     const double* __restrict__ row_err, const int64_t* __restrict__ seg_off, int n_incidents,
     egr_rules_out out) {
@@ -103,11 +121,11 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
   const int64_t beg = seg_off[inc], end = seg_off[inc + 1];
   uint32_t* hk = node_key[wv];
   uint32_t* hc = node_cnt[wv];
-#pragma unroll
-  for (int j = 0; j < kNodeSlots / kWave; ++j) {
-    hk[lane + j * kWave] = kNodeEmpty;
-    hc[lane + j * kWave] = 0u;
-  }
+  // lane r's rule, loaded up front (independent of the rows: its latency overlaps theirs)
+  const int R = D->n_rules;
+  const uint32_t network_bit = D->network_vocab_bit;
+  const RuleDev* rule = &D->rules[lane < EGR_MAX_RULES ? lane : 0];
+  const int nc = lane < R ? rule->n_conds : 0;
 
   // ---- signal extraction: one coalesced sweep (the first two row blocks in one round trip) --
   uint32_t f_or = 0, v_or = 0;
@@ -152,6 +170,11 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
   if (s.n_node_rows >= 2 && s.n_node_rows <= kNodeSlots / 2 && end - beg <= 2 * kWave) {
     // LDS hash count (load <= 1/2): the count a row's add returns + 1 is the number of rows
     // of its node so far, so the max over all rows is max(pods_by_node.values())
+#pragma unroll
+    for (int j = 0; j < kNodeSlots / kWave; ++j) {
+      hk[lane + j * kWave] = kNodeEmpty;
+      hc[lane + j * kWave] = 0u;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     int best = 0;
@@ -189,21 +212,18 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
   }
 
   // ---- rule r on lane r -----------------------------------------------------------------
-  const int R = T.n_rules;
   bool matched = false;
   double conf = 0.0, fin = 0.0, stren = 0.0;
   if (lane < R) {
-    const egr_rule& rule = T.rules[lane];
-    const int nc = rule.n_conds;
     int mc = 0;
     for (int c = 0; c < nc && c < EGR_MAX_CONDS; ++c)
-      mc += condition_holds(rule.cond_type[c], rule.cond_mask[c], rule.cond_param[c], s,
-                            T.network_vocab_bit);
+      mc += condition_holds(rule->cond_type[c], rule->cond_mask[c], rule->cond_param[c], s,
+                            network_bit);
     matched = nc > 0 && mc == nc;
-    if (matched) {                 // all conditions held: the rule's constants (RuleConsts)
-      conf = K.conf[lane];
-      fin = K.fin[lane];
-      stren = K.str[lane];
+    if (matched) {                 // all conditions held: the rule's constants
+      conf = rule->conf;
+      fin = rule->fin;
+      stren = rule->str;
     }
   }
   const uint64_t mm = __ballot(matched);
@@ -244,8 +264,8 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
   // nothing matched), so the outputs need no clearing before a launch
   if (lane < S) {
     const bool unk = lane == R && nh == 0;
-    out.confidence[base + lane] = unk ? T.unknown_confidence : conf;
-    out.final_score[base + lane] = unk ? K.unknown_fin : fin;
+    out.confidence[base + lane] = unk ? D->unknown_confidence : conf;
+    out.final_score[base + lane] = unk ? D->unknown_fin : fin;
     out.strength[base + lane] = stren;
   }
   if (lane == 0) {
@@ -289,6 +309,63 @@ __global__ __launch_bounds__(256) void rank_kernel(
 
 }  // namespace
 
+// The compiled table of `table` in device memory: compiled on the host (cheap) and looked up
+// by content; a table seen for the first time on this device is uploaded once (synchronous
+// copy into a new buffer -- never overwritten, so launches in flight keep their table valid).
+// A first upload inside a HIP-graph capture is refused: run the table once uncaptured.
+static int rules_table_dev(const egr_rule_table& table, hipStream_t stream, const RulesDev** out) {
+  RulesDev h;
+  std::memset(&h, 0, sizeof h);
+  h.n_rules = table.n_rules;
+  h.network_vocab_bit = table.network_vocab_bit;
+  h.unknown_confidence = table.unknown_confidence;
+  h.unknown_fin = egr::ranker_final_score(table.unknown_confidence, table.unknown_category_weight,
+                                          0.0, 0.0);
+  for (int r = 0; r < table.n_rules; ++r) {
+    const egr_rule& rule = table.rules[r];
+    RuleDev& d = h.rules[r];
+    const int nc = rule.n_conds;
+    d.n_conds = nc;
+    for (int c = 0; c < EGR_MAX_CONDS; ++c) {
+      d.cond_type[c] = rule.cond_type[c];
+      d.cond_mask[c] = rule.cond_mask[c];
+      d.cond_param[c] = rule.cond_param[c];
+    }
+    if (nc <= 0) continue;
+    // a rule emits only when ALL its conditions hold: strength = the mean of the condition
+    // strengths, then the confidence and the ranker's score of that strength
+    double ssum = 0.0;
+    for (int c = 0; c < nc; ++c) ssum = ssum + rule.cond_strength[c];
+    d.str = ssum / (double)(nc > 1 ? nc : 1);
+    d.conf = egr::rule_confidence(rule.confidence_base, nc, d.str);
+    d.fin = egr::ranker_final_score(d.conf, rule.category_weight, (double)nc, d.str);
+  }
+  hipDevice_t dev = 0;                           // the stream's device (null stream: current)
+  EGR_HIP(hipStreamGetDevice(stream, &dev));
+  static std::mutex mu;
+  static std::vector<std::tuple<hipDevice_t, std::vector<uint8_t>, RulesDev*>> cache;
+  const uint8_t* hb = reinterpret_cast<const uint8_t*>(&h);
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& [d, bytes, ptr] : cache)
+    if (d == dev && std::memcmp(bytes.data(), hb, sizeof h) == 0) {
+      *out = ptr;
+      return EGR_OK;
+    }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  EGR_HIP(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval: a rule table's first launch on a device "
+                                 "cannot be captured (launch it once uncaptured)");
+  if (cache.size() >= 256)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval: more than 256 distinct rule tables");
+  RulesDev* ptr = nullptr;
+  EGR_HIP(hipMalloc(&ptr, sizeof h));
+  EGR_HIP(hipMemcpy(ptr, &h, sizeof h, hipMemcpyHostToDevice));
+  cache.emplace_back(dev, std::vector<uint8_t>(hb, hb + sizeof h), ptr);
+  *out = ptr;
+  return EGR_OK;
+}
+
 extern "C" int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_flags,
                               const uint32_t* row_vocab, const uint32_t* row_node,
                               const double* row_err, const int64_t* seg_off, int32_t n_incidents,
@@ -304,24 +381,12 @@ extern "C" int egr_rules_eval(const egr_rule_table* table, const uint32_t* row_f
       !out->final_score || !out->strength)
     return egr::fail(EGR_EINVAL, "egr_rules_eval: NULL output");
   if (n_incidents == 0) return EGR_OK;
-  // the constants of a matched rule (every condition held: strength = mean of the condition
-  // strengths), computed exactly as rules_engine.py:443-455 / hypothesis_ranker.py:44-63 do
-  RuleConsts K{};
-  for (int r = 0; r < table->n_rules; ++r) {
-    const egr_rule& rule = table->rules[r];
-    const int nc = rule.n_conds;
-    if (nc <= 0) continue;
-    double ssum = 0.0;
-    for (int c = 0; c < nc; ++c) ssum = ssum + rule.cond_strength[c];
-    K.str[r] = ssum / (double)(nc > 1 ? nc : 1);
-    K.conf[r] = egr::rule_confidence(rule.confidence_base, nc, K.str[r]);
-    K.fin[r] = egr::ranker_final_score(K.conf[r], rule.category_weight, (double)nc, K.str[r]);
-  }
-  K.unknown_fin = egr::ranker_final_score(table->unknown_confidence, table->unknown_category_weight,
-                                          0.0, 0.0);
+  const RulesDev* D = nullptr;
+  const int rc = rules_table_dev(*table, (hipStream_t)stream, &D);
+  if (rc != EGR_OK) return rc;
   const dim3 grid((n_incidents + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(rules_eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, *table, K,
-                     row_flags, row_vocab, row_node, row_err, seg_off, n_incidents, *out);
+  hipLaunchKernelGGL(rules_eval_kernel, grid, dim3(256), 0, (hipStream_t)stream, D, row_flags,
+                     row_vocab, row_node, row_err, seg_off, n_incidents, *out);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
