@@ -799,6 +799,15 @@ def main():
     for _ in range(args.warmup):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
+    if args.engine == "frontier":
+        # graphs with large 3-hop neighbourhoods (the dense C4): columns that overflow the
+        # narrow table get the wide-table retry from here on (egraph.graph.Frontier.adapt)
+        for lane in ctx["lanes"]:
+            if lane["frontier"].adapt():
+                log(f"[rank {rank}] wide-table retry on ({lane['frontier'].retry_blocks} blocks)")
+        for _ in range(args.warmup):
+            run_step(ctx, args.hops)
+        torch.cuda.synchronize(dev)
     graphs = args.engine == "frontier" and not args.no_graph
     if graphs:
         capture_lanes(ctx, args.hops)

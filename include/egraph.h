@@ -287,6 +287,25 @@ int egr_plan_pack_reach(const egr_plan* p, const uint32_t* rows, int64_t n, uint
 int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src, int64_t n,
                           const uint64_t* in, void* stream);
 
+/* Sparse halo exchange (the production form of the pack / unpack above): only the NON-ZERO
+ * entries of the boundary rows cross the link.  what: 0 = scores (after a hop), 1 = reach
+ * words.  pack: rows[0, n) grouped by destination rank, seg[P + 1] (host) their segment
+ * starts; writes each peer's entries contiguously into `out` (device, int64 words: scores one
+ * word per entry = (row-in-segment * width + column) << 32 | value bits, reach two words =
+ * index, word; width = padded columns resp. reach words per row) and the entry count per
+ * peer into counts[P] (host; the call synchronises its stream to learn them).  unpack: zeroes
+ * the received halo rows (recv_vertex[n_rows]: the local vertex of each received row, rows
+ * grouped by sender) and scatters n_entries entries (device; sender s owns entries
+ * [eseg[s], eseg[s+1]) and its rows start at recv row rbase[s], both device arrays).
+ * Bit-identical to the dense exchange.  At most EGR_SX_MAX_PEERS ranks.                     */
+#define EGR_SX_MAX_PEERS 64
+int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_t n,
+                         const int64_t* seg, int32_t P, int64_t* out, int64_t cap,
+                         int64_t* counts, void* stream);
+int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
+                           const int64_t* in, int64_t n_entries, const int64_t* eseg,
+                           const int64_t* rbase, int32_t P, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Frontier engine: the same A8 + A9 + top-k results as a plan's egr_plan_run, computed per
  * incident column over only the vertices the column touches (one workgroup per column, the
@@ -300,13 +319,13 @@ int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src
  *                         still ranked.
  *   egr_frontier_run    : one pass; sources [n_cols] device; outputs [n_cols*k] as
  *                         egr_plan_topk (EGR_NO_NODE / -inf in unused slots).
- *   egr_frontier_stats  : synchronous; out[8] of the last run = CSR entries gathered by
+ *   egr_frontier_stats  : synchronous; out[9] of the last run = CSR entries gathered by
  *                         pulls (col + val read), CSR entries read by expansions (col only),
- *                         rows walked (row_ptr pairs), members, columns that overflowed the
- *                         LDS table (redone by the global-memory variant), pool entries
- *                         used, valid seed entries, member keys outside the graph (a
- *                         device-side guard of -DEGR_FR_GUARDS builds; -1 = not counted:
- *                         release builds compile the guard out).
+ *                         rows walked (row_ptr pairs), members, LDS-table overflows (narrow
+ *                         and, with the retry on, wide), pool entries used, valid seed
+ *                         entries, member keys outside the graph (a device-side guard of
+ *                         -DEGR_FR_GUARDS builds; -1 = not counted: release builds compile
+ *                         the guard out), columns ranked by the global-memory variant.
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.
@@ -315,6 +334,13 @@ int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src
  * ---------------------------------------------------------------------------------------- */
 typedef struct egr_frontier egr_frontier;
 
+/* Narrow (top-k-only) frontiers: give the columns that overflow the narrow LDS table (more than
+ * 1536 members) a second chance in the wide LDS table (4608 members) before the global-memory
+ * variant, on a persistent grid of `blocks` workgroups (0 = off, the default; graphs whose
+ * 3-hop neighbourhoods are small never overflow and skip the launch).  Takes effect from the
+ * next egr_frontier_run (capture it into a graph after setting it).                       */
+int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
+
 int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
                         int64_t pool_entries, egr_frontier** out);
 void egr_frontier_free(egr_frontier* f);
@@ -322,7 +348,7 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
                            const float* seed_val, int64_t n_seeds, void* stream);
 int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hops,
                      int32_t exclude_label, uint32_t* out_ids, float* out_scores, void* stream);
-int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream);
+int egr_frontier_stats(const egr_frontier* f, int64_t* out9, void* stream);
 int egr_frontier_read_scores(const egr_frontier* f, float* out, void* stream);
 /* Diagnostics: with $EGRAPH_FRONTIER_PROFILE set when the frontier was created, each column's
  * workgroup stamps s_memrealtime (100 MHz) at its phase boundaries: per column and slot, the

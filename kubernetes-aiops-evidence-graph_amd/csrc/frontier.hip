@@ -416,6 +416,9 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
 
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
+  bool big_geom = false;          // global variant in 256-thread workgroups (egr_frontier_set_retry)
+  int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
+                                  // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
   int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
                                   // for incremental snapshot updates)
   int B = 0, k = 0, nbig = 0;
@@ -454,8 +457,11 @@ struct egr_frontier {
   bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
 };
 
-// wide-table second chances per narrow run ($EGRAPH_FRONTIER_WIDE_RETRY)
-constexpr int RETRY_BLOCKS = 128;
+// default persistent grid of the wide-table second chance ($EGRAPH_FRONTIER_WIDE_RETRY, or
+// egr_frontier_set_retry): two 78-KB workgroups per CU on 256 CUs
+constexpr int RETRY_BLOCKS = 512;
+// global-memory variant workgroups once the retry is on (one 2V-slot HBM table each)
+constexpr int GLOBAL_BLOCKS_BIG = 128;
 
 // stamps per profiling slot: the post-barrier stamp + one per wave of the kernel's workgroup
 static int prof_w(const egr_frontier* f) { return f->narrow ? fr_narrow::PROF_W : fr_wide::PROF_W; }
@@ -670,30 +676,34 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.prof = f->prof;
   if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
   a.stats = f->ctr + 1;
-  // narrow: its overflowing columns go to the global-memory variant.  With
-  // $EGRAPH_FRONTIER_WIDE_RETRY the first RETRY_BLOCKS of them get a second chance in the wide
-  // LDS table first (a small grid: blocks past the handed-on count leave at once).  Off by
-  // default: pruned C3 / C4 columns do not overflow, and the retry's 78-KB workgroups wait for
-  // LDS held by the other batch in flight (~30 us per run in rocprof, profiles/r01_kernel_stats_v9.csv).
+  // narrow: its overflowing columns go to the global-memory variant -- or, with the wide retry
+  // on (egr_frontier_set_retry / $EGRAPH_FRONTIER_WIDE_RETRY), to a persistent grid of the wide
+  // LDS table first, which hands on only what overflows 4608 members.  Off by default: pruned
+  // C2 / C3 columns never overflow, and the retry's 78-KB workgroups would wait for LDS held by
+  // the other batches in flight (~30 us per run in rocprof, profiles/r01_kernel_stats_v9.csv).
+  // Graphs whose 3-hop neighbourhoods are larger (the dense C4) turn it on after a run reports
+  // overflowing columns (egraph.graph.Frontier.adapt).
   if (f->narrow) {
     FArgs an = a;
     an.ovf_n = f->ovf + 2;
     an.ovf_list = f->ovf + 4 + f->B;
-    an.ovf_cap = getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? (uint32_t)std::min(f->B, RETRY_BLOCKS)
-                                                      : 0u;
+    const int32_t rb = f->retry_blocks >= 0 ? f->retry_blocks
+                       : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
+    an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
     hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
     EGR_CHECK_LAUNCH();
-    if (an.ovf_cap)
-      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(an.ovf_cap), dim3(fr_wide::FT),
-                         0, st, a);
+    if (rb > 0)
+      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
+                         dim3(fr_wide::FT), 0, st, a);
   } else {
     hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
   }
   EGR_CHECK_LAUNCH();
   // the overflow fallback in its one-wave geometry; $EGRAPH_FRONTIER_AB_GLOBAL=0 / 1 launches the
   // wide (512-thread) / narrow (256-thread) instantiation instead (scripts/ab_global.sh)
-  static const int fb_geom = getenv("EGRAPH_FRONTIER_AB_GLOBAL") ? atoi(getenv("EGRAPH_FRONTIER_AB_GLOBAL")) : 3;
+  static const int fb_env = getenv("EGRAPH_FRONTIER_AB_GLOBAL") ? atoi(getenv("EGRAPH_FRONTIER_AB_GLOBAL")) : 3;
+  const int fb_geom = f->big_geom ? 1 : fb_env;
   if (fb_geom == 0)
     hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
   else if (fb_geom == 1)
@@ -707,15 +717,53 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   return EGR_OK;
 }
 
+int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
+  if (!f || blocks < 0) return egr::fail(EGR_EINVAL, "egr_frontier_set_retry: bad arguments");
+  f->retry_blocks = blocks;
+  // graphs that need the retry also send more columns past the wide table: the global-memory
+  // variant then gets up to GLOBAL_BLOCKS_BIG workgroups (one HBM table each) in 256-thread
+  // workgroups instead of 32 one-wave ones
+  const int want = blocks > 0 ? std::min(f->B, GLOBAL_BLOCKS_BIG) : f->nbig;
+  if (want > f->nbig) {
+    DeviceGuard guard(f->s->device);
+    EGR_HIP(hipDeviceSynchronize());            // runs in flight still use the old tables
+    const size_t gcap = f->gcap, V = (size_t)f->vmax;
+    dfree(f->gkeys);
+    dfree(f->gs);
+    dfree(f->gfl);
+    dfree(f->gneed);
+    dfree(f->gsnew);
+    dfree(f->gmlist);
+    f->nbig = want;
+    int rc;
+    if ((rc = dalloc(&f->gkeys, gcap * want)) || (rc = dalloc(&f->gs, gcap * want)) ||
+        (rc = dalloc(&f->gfl, gcap * want)) || (rc = dalloc(&f->gneed, gcap * want)) ||
+        (rc = dalloc(&f->gsnew, V * want)) || (rc = dalloc(&f->gmlist, V * want))) {
+      f->nbig = 0;
+      return rc;
+    }
+    if (hipMemset(f->gkeys, 0xFF, gcap * want * 4) != hipSuccess ||
+        hipMemset(f->gs, 0, gcap * want * 4) != hipSuccess ||
+        hipMemset(f->gfl, 0, gcap * want) != hipSuccess ||
+        hipMemset(f->gneed, 0, gcap * want) != hipSuccess)
+      return egr::fail(EGR_EDEVICE, "egr_frontier_set_retry: table init failed");
+    f->big_geom = true;
+  }
+  return EGR_OK;
+}
+
 int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
+  // out8 holds 9 values (egraph.h: out9)
   if (!f || !out8) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_stats: not run yet");
   DeviceGuard guard(f->s->device);
   unsigned long long h[7];
-  uint32_t nu = 0;
+  uint32_t nu = 0, ng = 0;
   EGR_HIP(hipMemcpyAsync(h, f->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
   EGR_HIP(hipMemcpyAsync(&nu, f->seed_ptr + f->B, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  EGR_HIP(hipMemcpyAsync(&ng, f->ovf, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  out8[8] = (int64_t)ng;     // columns the global-memory variant ranked
   for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
   out8[5] = (int64_t)h[0];
   out8[6] = (int64_t)nu;

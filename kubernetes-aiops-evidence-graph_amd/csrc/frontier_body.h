@@ -1048,16 +1048,19 @@ void frontier_lds_kernel(const FArgs A) {
   lds_column(A, b, L, sh);
 }
 
-// Second chance: block i takes entry i of the columns another geometry's LDS kernel handed
-// on (A.retry_list, at most gridDim.x entries kept; blocks past its end leave at once -- no
-// loop, so the code is the same as frontier_lds_kernel's); those that overflow this table too
-// go on to the global-memory variant.
+// Second chance: a persistent grid over the columns another geometry's LDS kernel handed on
+// (A.retry_list, *A.retry_n entries): block i takes entries i, i + gridDim.x, ...; those that
+// overflow this table too go on to the global-memory variant.  Every block leaves once the
+// list is drained (an empty list: at once).
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
 void frontier_lds_retry_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
-  if (blockIdx.x >= *A.retry_n) return;
-  lds_column(A, (int)A.retry_list[blockIdx.x], L, sh);
+  const uint32_t n = *A.retry_n;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    lds_column(A, (int)A.retry_list[i], L, sh);
+    __syncthreads();              // the next column clears the table this one used
+  }
 }
 
 // Persistent fallback: each workgroup owns one global table and drains the overflow list.

@@ -725,6 +725,115 @@ __global__ void unpack_reach_kernel(uint64_t* __restrict__ R, uint32_t RS, int W
   for (int w = threadIdx.x; w < W; w += blockDim.x) R[(size_t)v * RS + w] = in[o + w];
 }
 
+// ---- sparse halo exchange: only the non-zero entries of the boundary rows cross the link ----
+// Row r of the send list (rows grouped by destination rank: seg[q] .. seg[q+1]) contributes its
+// non-zero columns b as entries ((r - seg[q]) * width + b) << 32 | bits (scores, one int64) or
+// ((r - seg[q]) * W + w, word) (reach, two int64), written at the row's offset of an exclusive
+// scan over the per-row counts (so each peer's entries are contiguous, in (row, column) order).
+// One 256-thread block per row.
+__device__ __forceinline__ uint32_t sx_value(const float* X, const uint64_t* R, uint32_t V, int TW,
+                                             uint32_t RS, uint32_t v, int b, bool reach,
+                                             uint64_t* word) {
+  if (reach) {
+    *word = R[(size_t)v * RS + b];
+    return *word != 0ull;
+  }
+  const uint32_t bits = __float_as_uint(X[((size_t)(b / TW) * V + v) * TW + (b % TW)]);
+  *word = bits;
+  return bits != 0u;     // -0.0 is not +0: sent (bit-exact)
+}
+
+__global__ __launch_bounds__(256) void sx_count_kernel(const float* __restrict__ X,
+    const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
+    const uint32_t* __restrict__ rows, int64_t* __restrict__ cnt) {
+  __shared__ int wsum[4];
+  const uint32_t v = rows[blockIdx.x];
+  int c = 0;
+  for (int b = threadIdx.x; b < width; b += 256) {
+    uint64_t w;
+    c += sx_value(X, R, V, TW, RS, v, b, reach, &w);
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ X,
+    const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
+    const uint32_t* __restrict__ rows, const int64_t* __restrict__ seg, int P,
+    const int64_t* __restrict__ off, int64_t* __restrict__ out) {
+  __shared__ int wcnt[4];
+  const int64_t r = blockIdx.x;
+  const uint32_t v = rows[r];
+  int q = 0;
+  while (q + 1 < P && seg[q + 1] <= r) ++q;
+  const int64_t rl = r - seg[q];
+  int64_t pos = off[r];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int b0 = 0; b0 < width; b0 += 256) {
+    const int b = b0 + (int)threadIdx.x;
+    uint64_t w = 0;
+    const bool nz = b < width && sx_value(X, R, V, TW, RS, v, b, reach, &w);
+    const uint64_t m = __ballot(nz);
+    if (lane == 0) wcnt[wv] = __popcll(m);
+    __syncthreads();
+    int before = __popcll(m & ((1ull << lane) - 1ull));
+    for (int j = 0; j < wv; ++j) before += wcnt[j];
+    const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (nz) {
+      const int64_t idx = rl * width + b;
+      if (reach) {
+        out[2 * (pos + before)] = idx;
+        out[2 * (pos + before) + 1] = (int64_t)w;
+      } else {
+        out[pos + before] = (idx << 32) | (int64_t)w;
+      }
+    }
+    pos += total;
+    __syncthreads();                      // wcnt is reused by the next round
+  }
+}
+
+// Receiver: zero the received halo rows, then scatter the entries (one thread per entry; the
+// sender s of entry e: eseg[s] <= e < eseg[s+1]; its recv rows start at rbase[s]).
+__global__ void sx_zero_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V, int TW,
+                               uint32_t RS, int width, bool reach,
+                               const uint32_t* __restrict__ recv_vertex) {
+  const uint32_t v = recv_vertex[blockIdx.x];
+  for (int b = threadIdx.x; b < width; b += blockDim.x) {
+    if (reach) R[(size_t)v * RS + b] = 0ull;
+    else X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = 0.f;
+  }
+}
+
+__global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V,
+                                  int TW, uint32_t RS, int width, bool reach,
+                                  const uint32_t* __restrict__ recv_vertex,
+                                  const int64_t* __restrict__ in, int64_t n,
+                                  const int64_t* __restrict__ eseg,
+                                  const int64_t* __restrict__ rbase, int P) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  int s = 0;
+  while (s + 1 < P && eseg[s + 1] <= e) ++s;
+  int64_t idx;
+  uint64_t w;
+  if (reach) {
+    idx = in[2 * e];
+    w = (uint64_t)in[2 * e + 1];
+  } else {
+    const uint64_t x = (uint64_t)in[e];
+    idx = (int64_t)(x >> 32);
+    w = x & 0xFFFFFFFFull;
+  }
+  const int64_t row = rbase[s] + idx / width;
+  const int b = (int)(idx % width);
+  const uint32_t v = recv_vertex[row];
+  if (reach) R[(size_t)v * RS + b] = w;
+  else X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = __uint_as_float((uint32_t)w);
+}
+
 }  // namespace
 
 struct egr_plan {
@@ -760,6 +869,12 @@ struct egr_plan {
   int cand_exclude = -1;
   uint32_t owned = 0;               // rows [0, owned) are top-k candidates (partition: no halo)
   unsigned long long* counter = nullptr;
+  // sparse halo exchange scratch: per-row non-zero counts / offsets, scan temp, peer totals
+  int64_t* sx_off = nullptr;
+  size_t sx_cap = 0;
+  void* sx_tmp = nullptr;
+  size_t sx_tmp_bytes = 0;
+  int64_t* sx_tot = nullptr;        // [EGR_SX_MAX_PEERS + 1]
 };
 
 namespace {
@@ -1009,6 +1124,9 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->counter);
   dfree(p->chunk_start);
   dfree(p->rchunk_start);
+  dfree(p->sx_off);
+  dfree(p->sx_tot);
+  if (p->sx_tmp) (void)hipFree(p->sx_tmp);
   delete p;
 }
 
@@ -1312,6 +1430,97 @@ int egr_plan_unpack_reach(egr_plan* p, const uint32_t* rows, const uint32_t* src
   hipLaunchKernelGGL(unpack_reach_kernel, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream,
                      p->reach[p->rcur], (uint32_t)p->RS, p->W, rows, src, in);
   EGR_CHECK_LAUNCH();
+  p->cand_valid = false;
+  return EGR_OK;
+}
+
+int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_t n,
+                         const int64_t* seg, int32_t P, int64_t* out, int64_t cap,
+                         int64_t* counts, void* stream) {
+  if (!p || (what != 0 && what != 1) || n < 0 || P < 1 || P > EGR_SX_MAX_PEERS || !seg ||
+      !counts || (n > 0 && (!rows || !out)) || cap < 0 || seg[0] != 0 || seg[P] != n)
+    return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse: bad arguments");
+  for (int q = 0; q < P; ++q)
+    if (seg[q + 1] < seg[q]) return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse: bad segments");
+  const bool reach = what == 1;
+  if (reach ? !p->sources_set : p->hops_done < 1)
+    return egr::fail(EGR_ESTATE, "egr_plan_pack_sparse: nothing computed yet");
+  for (int q = 0; q < P; ++q) counts[q] = 0;
+  if (n == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int width = reach ? p->W : p->Bpad;
+  if ((size_t)n + 1 > p->sx_cap) {
+    dfree(p->sx_off);
+    p->sx_cap = 0;
+    int rc = dalloc(&p->sx_off, (size_t)n + 1);
+    if (rc != EGR_OK) return rc;
+    p->sx_cap = (size_t)n + 1;
+    if (p->sx_tmp) (void)hipFree(p->sx_tmp);
+    p->sx_tmp = nullptr;
+    size_t tb = 0;
+    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
+    EGR_HIP(hipMalloc(&p->sx_tmp, tb));
+    p->sx_tmp_bytes = tb;
+  }
+  if (!p->sx_tot) {
+    const int rc = dalloc(&p->sx_tot, (size_t)EGR_SX_MAX_PEERS + 1 + EGR_SX_MAX_PEERS + 1);
+    if (rc != EGR_OK) return rc;
+  }
+  int64_t* dseg = p->sx_tot + EGR_SX_MAX_PEERS + 1;
+  EGR_HIP(hipMemcpyAsync(dseg, seg, sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, st));
+  const float* X = reach ? nullptr : p->x[p->xcur];
+  const uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
+  const uint32_t V = (uint32_t)p->s->V;
+  EGR_HIP(hipMemsetAsync(p->sx_off + n, 0, sizeof(int64_t), st));
+  hipLaunchKernelGGL(sx_count_kernel, dim3((unsigned)n), dim3(256), 0, st, X, R, V, p->TW,
+                     (uint32_t)p->RS, width, reach, rows, p->sx_off);
+  EGR_CHECK_LAUNCH();
+  size_t tb = p->sx_tmp_bytes;
+  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sx_tmp, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
+  // the entry offsets at the peer boundaries (P + 1 values) decide the all-to-all split sizes
+  std::vector<int64_t> bound((size_t)P + 1);
+  for (int q = 0; q <= P; ++q)
+    EGR_HIP(hipMemcpyAsync(&bound[q], p->sx_off + seg[q], sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  EGR_HIP(hipStreamSynchronize(st));
+  const int64_t total = bound[P];
+  const int64_t words = reach ? 2 * total : total;
+  if (words > cap) return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse: output too small (" +
+                                                    std::to_string(words) + " words)");
+  for (int q = 0; q < P; ++q) counts[q] = bound[q + 1] - bound[q];
+  if (total > 0) {
+    hipLaunchKernelGGL(sx_emit_kernel, dim3((unsigned)n), dim3(256), 0, st, X, R, V, p->TW,
+                       (uint32_t)p->RS, width, reach, rows, dseg, P, p->sx_off, out);
+    EGR_CHECK_LAUNCH();
+  }
+  return EGR_OK;
+}
+
+int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
+                           const int64_t* in, int64_t n_entries, const int64_t* eseg,
+                           const int64_t* rbase, int32_t P, void* stream) {
+  if (!p || (what != 0 && what != 1) || n_rows < 0 || n_entries < 0 || P < 1 ||
+      (n_rows > 0 && !recv_vertex) || (n_entries > 0 && (!in || !eseg || !rbase)))
+    return egr::fail(EGR_EINVAL, "egr_plan_unpack_sparse: bad arguments");
+  const bool reach = what == 1;
+  if (reach ? !p->sources_set : p->hops_done < 1)
+    return egr::fail(EGR_ESTATE, "egr_plan_unpack_sparse: nothing computed yet");
+  if (n_rows == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int width = reach ? p->W : p->Bpad;
+  float* X = reach ? nullptr : p->x[p->xcur];
+  uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
+  const uint32_t V = (uint32_t)p->s->V;
+  hipLaunchKernelGGL(sx_zero_kernel, dim3((unsigned)n_rows), dim3(256), 0, st, X, R, V, p->TW,
+                     (uint32_t)p->RS, width, reach, recv_vertex);
+  EGR_CHECK_LAUNCH();
+  if (n_entries > 0) {
+    hipLaunchKernelGGL(sx_scatter_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0,
+                       st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, in,
+                       n_entries, eseg, rbase, P);
+    EGR_CHECK_LAUNCH();
+  }
   p->cand_valid = false;
   return EGR_OK;
 }

@@ -571,7 +571,234 @@ static PyObject* flag_bits(PyObject* self, PyObject* noargs) {
                        F_ERR_FLOAT, NO_NODE);
 }
 
+/* ---- propagation seeds: attachment candidates of evidence rows (egraph/seeds.py) ----------- */
+
+static PyObject *a_ns, *a_name, *a_strength, *a_involved, *a_kind, *a_namespace, *a_half,
+    *t_pod, *t_deploy, *t_dchange, *t_ichange, *t_node, *t_hpa, *t_config, *t_event, *t_log,
+    *t_metric, *s_empty, *s_node_lc, *s_colon, *p_pod, *p_deploy, *p_node, *p_hpa, *p_config,
+    *p_logpattern, *p_service, *p_metric, *p_event, *kind_cache;
+
+static int intern_seeds(void) {
+#define S(var, text) if (!(var = PyUnicode_InternFromString(text))) return -1
+  S(a_ns, "entity_namespace"); S(a_name, "entity_name"); S(a_strength, "signal_strength");
+  S(a_involved, "involved_object"); S(a_kind, "kind"); S(a_namespace, "namespace");
+  S(t_pod, "kubernetes_pod"); S(t_deploy, "kubernetes_deployment"); S(t_dchange, "deploy_change");
+  S(t_ichange, "image_change"); S(t_node, "kubernetes_node"); S(t_hpa, "kubernetes_hpa");
+  S(t_config, "config_change"); S(t_event, "kubernetes_event"); S(t_log, "log_signal");
+  S(t_metric, "metric_signal"); S(s_empty, ""); S(s_node_lc, "node"); S(s_colon, ":");
+  S(p_pod, "pod:"); S(p_deploy, "deployment:"); S(p_node, "node:"); S(p_hpa, "hpa:");
+  S(p_config, "configmap:"); S(p_logpattern, "logpattern:"); S(p_service, "service:");
+  S(p_metric, "metric:"); S(p_event, "event:");
+#undef S
+  if (!(kind_cache = PyDict_New())) return -1;
+  if (!(a_half = PyFloat_FromDouble(0.5))) return -1;
+  return 0;
+}
+
+/* values an f-string / str() formats without running user code: format(x, '') == str(x) */
+static inline int fmt_plain(PyObject* o) {
+  return o == Py_None || PyUnicode_CheckExact(o) || PyLong_CheckExact(o) || PyBool_Check(o) ||
+         PyFloat_CheckExact(o);
+}
+
+/* str(x) of a plain value (new reference) */
+static inline PyObject* as_str(PyObject* o) {
+  if (PyUnicode_CheckExact(o)) {
+    Py_INCREF(o);
+    return o;
+  }
+  return PyObject_Str(o);
+}
+
+/* append the id prefix + str(a) [+ ":" + str(b)] (f"{prefix}{a}:{b}"), built in one allocation;
+ * -1 on error */
+static int push_id(PyObject* ids, PyObject* prefix, PyObject* a, PyObject* b) {
+  PyObject* part[4] = {prefix, as_str(a), b ? s_colon : NULL, b ? as_str(b) : NULL};
+  const int np = b ? 4 : 2;
+  int rc = -1;
+  PyObject* out = NULL;
+  Py_ssize_t len = 0;
+  Py_UCS4 maxc = 127;
+  for (int i = 0; i < np; ++i) {
+    if (!part[i]) goto done;
+    len += PyUnicode_GET_LENGTH(part[i]);
+    const Py_UCS4 m = PyUnicode_MAX_CHAR_VALUE(part[i]);
+    if (m > maxc) maxc = m;
+  }
+  out = PyUnicode_New(len, maxc);
+  if (!out) goto done;
+  {
+    Py_ssize_t at = 0;
+    for (int i = 0; i < np; ++i) {
+      const Py_ssize_t n = PyUnicode_GET_LENGTH(part[i]);
+      if (PyUnicode_CopyCharacters(out, at, part[i], 0, n) < 0) goto done;
+      at += n;
+    }
+  }
+  rc = PyList_Append(ids, out);
+done:
+  Py_XDECREF(out);
+  Py_XDECREF(part[1]);
+  Py_XDECREF(part[3]);
+  return rc;
+}
+
+/* attach_ids(ev) of egraph/seeds.py for an exact dict: 1 = done (ids filled), 0 = hand over to
+ * the Python statement, -1 = error */
+static int cand_ids(PyObject* ev, PyObject* ids) {
+  PyObject *t, *ns, *name, *data;
+  if (dget(ev, k_type, &t) || dget(ev, a_ns, &ns) || dget(ev, a_name, &name) || dget(ev, k_data, &data))
+    return 0;
+  if (t != NULL && t != Py_None && !PyUnicode_CheckExact(t)) return 0;   /* == may run user code */
+  if (!ns) ns = Py_None;
+  if (!name) name = Py_None;
+  if (!fmt_plain(ns) || !fmt_plain(name)) return 0;
+  if (data != NULL && data != Py_None && !PyDict_CheckExact(data)) return 0;   /* `or {}` */
+  if (t == NULL || t == Py_None) return 1;
+  if (eq_str(t, t_pod)) return push_id(ids, p_pod, ns, name) < 0 ? -1 : 1;
+  if (eq_str(t, t_deploy) || eq_str(t, t_dchange) || eq_str(t, t_ichange))
+    return push_id(ids, p_deploy, ns, name) < 0 ? -1 : 1;
+  if (eq_str(t, t_node)) return push_id(ids, p_node, name, NULL) < 0 ? -1 : 1;
+  if (eq_str(t, t_hpa)) return push_id(ids, p_hpa, ns, name) < 0 ? -1 : 1;
+  if (eq_str(t, t_config)) return push_id(ids, p_config, ns, name) < 0 ? -1 : 1;
+  if (eq_str(t, t_log)) {
+    if (push_id(ids, p_logpattern, ns, name) < 0 || push_id(ids, p_service, ns, name) < 0 ||
+        push_id(ids, p_deploy, ns, name) < 0)
+      return -1;
+    return 1;
+  }
+  if (eq_str(t, t_metric)) return push_id(ids, p_metric, ns, name) < 0 ? -1 : 1;
+  if (eq_str(t, t_event)) {
+    PyObject *obj = NULL, *kind = NULL, *oname = NULL, *ons = NULL;
+    if (data != NULL && data != Py_None && PyDict_GET_SIZE(data) > 0) {
+      if (dget(data, a_involved, &obj)) return 0;
+    }
+    if (obj != NULL && obj != Py_None && !PyDict_CheckExact(obj)) return 0;
+    if (obj != NULL && (obj == Py_None || PyDict_GET_SIZE(obj) == 0)) obj = NULL;
+    if (obj != NULL) {
+      if (dget(obj, a_kind, &kind) || dget(obj, k_name, &oname) || dget(obj, a_namespace, &ons))
+        return 0;
+      if ((kind && !fmt_plain(kind)) || (oname && !fmt_plain(oname)) || (ons && !fmt_plain(ons)))
+        return 0;
+    }
+    if (push_id(ids, p_event, ns, name) < 0) return -1;
+    /* kind = str(obj.get("kind", "")).lower(); the id prefix "<kind>:" is cached per str(kind)
+     * (kind_cache: str(kind) -> kind.lower() + ":") */
+    PyObject* ks = kind ? as_str(kind) : (Py_INCREF(s_empty), s_empty);
+    if (!ks) return -1;
+    PyObject* kc = PyDict_GetItemWithError(kind_cache, ks);   /* borrowed; exact str keys */
+    if (!kc) {
+      if (PyErr_Occurred()) { Py_DECREF(ks); return -1; }
+      PyObject* kl = PyObject_CallMethod(ks, "lower", NULL);
+      if (!kl) { Py_DECREF(ks); return -1; }
+      kc = PyUnicode_Concat(kl, s_colon);
+      Py_DECREF(kl);
+      if (PyDict_GET_SIZE(kind_cache) >= 4096) PyDict_Clear(kind_cache);   /* bounded */
+      if (!kc || PyDict_SetItem(kind_cache, ks, kc) < 0) { Py_XDECREF(kc); Py_DECREF(ks); return -1; }
+      Py_DECREF(kc);                                   /* the cache holds it */
+    }
+    Py_DECREF(ks);
+    if (PyUnicode_Compare(kc, p_node) == 0)            /* kind == "node" */
+      return push_id(ids, p_node, oname ? oname : Py_None, NULL) < 0 ? -1 : 1;
+    if (PyUnicode_GET_LENGTH(kc) > 1)                  /* kind != "": f"{kind}:{ns}:{name}" */
+      return push_id(ids, kc, ons ? ons : ns, oname ? oname : Py_None) < 0 ? -1 : 1;
+    return 1;
+  }
+  return 1;   /* any other type: no candidate */
+}
+
+/* seed_candidates(evidence_lists, slow) -> (flat ids, per-row counts (int64 bytes), columns
+ * (uint32 bytes), strengths (float64 bytes)):
+ * SeedCandidates.__init__ of egraph/seeds.py.  `slow(ev)` is the Python statement of one row
+ * (attach_ids + the strength), used for rows whose values are not plain. */
+static PyObject* seed_candidates(PyObject* self, PyObject* args) {
+  PyObject *lists, *slow;
+  if (!PyArg_ParseTuple(args, "OO", &lists, &slow)) return NULL;
+  PyObject* seq = PySequence_Fast(lists, "evidence_lists must be a sequence");
+  if (!seq) return NULL;
+  PyObject* flat = PyList_New(0);
+  PyObject* result = NULL;
+  int64_t* cnt = NULL;      /* per seeding row: candidate count, column, strength */
+  uint32_t* col = NULL;
+  double* val = NULL;
+  Py_ssize_t nrow = 0, cap = 0;
+  if (!flat) goto done;
+  const Py_ssize_t B = PySequence_Fast_GET_SIZE(seq);
+  for (Py_ssize_t b = 0; b < B; ++b) {
+    PyObject* evs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, b), "evidence is not iterable");
+    if (!evs) goto done;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      PyObject* ev = PySequence_Fast_GET_ITEM(evs, j);
+      PyObject* ids = PyList_New(0);
+      if (!ids) { Py_DECREF(evs); goto done; }
+      double sv = 0.0;
+      int fast = 0;
+      if (PyDict_CheckExact(ev)) {
+        PyObject* st;
+        fast = cand_ids(ev, ids);
+        if (fast == 1) {
+          if (dget(ev, a_strength, &st)) fast = 0;
+          else if (st == NULL) sv = 0.5;
+          else if (PyFloat_CheckExact(st)) sv = PyFloat_AS_DOUBLE(st);
+          else if (PyLong_CheckExact(st) || PyBool_Check(st)) {
+            sv = PyLong_AsDouble(st);
+            if (sv == -1.0 && PyErr_Occurred()) { PyErr_Clear(); fast = 0; }
+          } else fast = 0;
+        }
+      }
+      if (fast < 0) { Py_DECREF(ids); Py_DECREF(evs); goto done; }
+      if (!fast) {                                   /* the Python statement decides (or raises) */
+        Py_DECREF(ids);
+        PyObject* r = PyObject_CallOneArg(slow, ev);
+        if (!r) { Py_DECREF(evs); goto done; }
+        if (!PyArg_ParseTuple(r, "Od", &ids, &sv) || !PyList_Check(ids)) {
+          if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "seed_candidates: bad slow row");
+          Py_DECREF(r);
+          Py_DECREF(evs);
+          goto done;
+        }
+        Py_INCREF(ids);
+        Py_DECREF(r);
+      }
+      const Py_ssize_t k = PyList_GET_SIZE(ids);
+      if (k > 0 && !(sv <= 0.0)) {                   /* `if not ids or s <= 0: continue` (NaN kept) */
+        int bad = 0;
+        for (Py_ssize_t i = 0; i < k && !bad; ++i) bad = PyList_Append(flat, PyList_GET_ITEM(ids, i)) < 0;
+        if (!bad && nrow == cap) {
+          cap = cap ? 2 * cap : 256;
+          int64_t* c2 = PyMem_Realloc(cnt, cap * sizeof(int64_t));
+          if (c2) cnt = c2;
+          uint32_t* o2 = PyMem_Realloc(col, cap * sizeof(uint32_t));
+          if (o2) col = o2;
+          double* v2 = PyMem_Realloc(val, cap * sizeof(double));
+          if (v2) val = v2;
+          if (!c2 || !o2 || !v2) { PyErr_NoMemory(); bad = 1; }
+        }
+        if (bad) { Py_DECREF(ids); Py_DECREF(evs); goto done; }
+        cnt[nrow] = k;
+        col[nrow] = (uint32_t)b;
+        val[nrow] = sv;
+        ++nrow;
+      }
+      Py_DECREF(ids);
+    }
+    Py_DECREF(evs);
+  }
+  result = Py_BuildValue("(Oy#y#y#)", flat, (const char*)cnt, nrow * (Py_ssize_t)sizeof(int64_t),
+                         (const char*)col, nrow * (Py_ssize_t)sizeof(uint32_t), (const char*)val,
+                         nrow * (Py_ssize_t)sizeof(double));
+done:
+  Py_XDECREF(flat);
+  PyMem_Free(cnt);
+  PyMem_Free(col);
+  PyMem_Free(val);
+  Py_DECREF(seq);
+  return result;
+}
+
 static PyMethodDef methods[] = {
+    {"seed_candidates", seed_candidates, METH_VARARGS, "evidence rows -> seed attachment candidates"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},
     {"assemble", assemble, METH_VARARGS, "kernel outputs -> hypothesis dicts"},
     {"flag_bits", flag_bits, METH_NOARGS, "the EGR_F_* bits and EGR_NO_NODE compiled in"},
@@ -580,6 +807,6 @@ static PyMethodDef methods[] = {
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_egr_pyhost", NULL, -1, methods};
 
 PyMODINIT_FUNC PyInit__egr_pyhost(void) {
-  if (intern_all() < 0) return NULL;
+  if (intern_all() < 0 || intern_seeds() < 0) return NULL;
   return PyModule_Create(&module);
 }

@@ -117,11 +117,14 @@ SIGNATURES: dict[str, tuple] = {
     "egr_plan_unpack_scores": (C.c_int, [P, P, P, I64, P, P]),
     "egr_plan_pack_reach": (C.c_int, [P, P, I64, P, P]),
     "egr_plan_unpack_reach": (C.c_int, [P, P, P, I64, P, P]),
+    "egr_plan_pack_sparse": (C.c_int, [P, I32, P, I64, P, I32, P, I64, P, P]),
+    "egr_plan_unpack_sparse": (C.c_int, [P, I32, P, I64, P, I64, P, P, I32, P]),
     "egr_frontier_create": (C.c_int, [P, I32, I64, I32, I64, C.POINTER(P)]),
     "egr_frontier_free": (None, [P]),
     "egr_frontier_set_seeds": (C.c_int, [P, P, P, P, I64, P]),
     "egr_frontier_run": (C.c_int, [P, P, I32, I32, P, P, P]),
     "egr_frontier_stats": (C.c_int, [P, P, P]),
+    "egr_frontier_set_retry": (C.c_int, [P, I32]),
     "egr_frontier_read_scores": (C.c_int, [P, P, P]),
     "egr_frontier_phase_times": (C.c_int, [P, P, I64, P]),
     "egr_frontier_read_reach": (C.c_int, [P, P, P]),

@@ -14,14 +14,15 @@ concurrently in one worker.  Here:
                 on a HIP event by polling it from the event loop (no thread hop, the loop is
                 never blocked).
   RulesBatcher  adaptive batching: a call that finds no launch in flight starts one at once
-                (no added latency when idle); calls arriving while a launch runs are collected
-                and go out together in the next one.  Each call gets exactly the dicts a
+                from its own task (no added latency when idle); calls arriving while a launch
+                runs are collected and go out together in the next one.  Each call gets exactly the dicts a
                 single call would (the kernel is per incident), and an input that makes the
                 reference raise raises in its own call only.
 """
 from __future__ import annotations
 
 import asyncio
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -146,10 +147,21 @@ class RulesRunner:
         self.launch(enc).synchronize()
         return self.results()
 
+    # the first SPIN_S of a launch's wait spin on its event without yielding (a single
+    # incident's round trip is ~25-30 us, and every event-loop hop adds several us); past it
+    # the wait yields to the loop between polls.  The reference runs its rules inline in the
+    # coroutine (~65 us per incident), so a bounded spin blocks the loop no longer than it did.
+    SPIN_S = 100e-6
+
     async def run(self, enc: EncodedBatch) -> RulesResult:
         ev = self.launch(enc)
-        while not ev.query():                       # poll from the loop: never blocks it
-            await asyncio.sleep(0)
+        # one loop turn while the kernel runs: calls made in this turn (e.g. the rest of an
+        # asyncio.gather) queue up for the next launch instead of waiting behind a spin
+        await asyncio.sleep(0)
+        t0 = time.perf_counter()
+        while not ev.query():
+            if time.perf_counter() - t0 > self.SPIN_S:
+                await asyncio.sleep(0)              # long launch: poll from the loop
         return self.results()
 
 
@@ -196,24 +208,38 @@ class RulesBatcher:
                           ) -> list[list[dict]]:
         """Several incidents as ONE call (it raises as a whole if any row makes the
         reference raise, as the reference's loop over them would)."""
-        fut = asyncio.get_running_loop().create_future()
-        self.queue.append(_Call([str(i) for i in incident_ids], list(evidence_lists), ranked, fut))
+        loop = asyncio.get_running_loop()
+        call = _Call([str(i) for i in incident_ids], list(evidence_lists), ranked, loop.create_future())
         self.calls += 1
-        if not self.busy:
-            self.busy = True
-            asyncio.get_running_loop().create_task(self._drain())
-        return await fut
+        self.queue.append(call)
+        if self.busy:
+            return await call.fut
+        # idle: this call launches at once from its own task; calls arriving while it runs
+        # (its wait yields one loop turn) go out together from a drain task afterwards
+        self.busy = True
+        try:
+            await self._run(self._take())
+        finally:
+            if self.queue:
+                loop.create_task(self._drain())          # stays busy until the queue is empty
+            else:
+                self.busy = False
+        return await call.fut
+
+    def _take(self) -> list[_Call]:
+        """The next launch's calls: queue order, up to max_batch incidents (at least one call)."""
+        take, n = 0, 0
+        while take < len(self.queue) and (take == 0 or n + len(self.queue[take].incident_ids)
+                                          <= self.max_batch):
+            n += len(self.queue[take].incident_ids)
+            take += 1
+        calls, self.queue = self.queue[:take], self.queue[take:]
+        return calls
 
     async def _drain(self) -> None:
         try:
             while self.queue:
-                take, n = 0, 0
-                while take < len(self.queue) and (take == 0 or n + len(self.queue[take].incident_ids)
-                                                  <= self.max_batch):
-                    n += len(self.queue[take].incident_ids)
-                    take += 1
-                calls, self.queue = self.queue[:take], self.queue[take:]
-                await self._run(calls)
+                await self._run(self._take())
         finally:
             self.busy = False
 

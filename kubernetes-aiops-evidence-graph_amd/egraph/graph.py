@@ -38,6 +38,12 @@ DEFAULT_OTHER_WEIGHT = (0.5, 0.5)
 
 def str_blob(strs: Sequence[str]) -> tuple[bytes, np.ndarray]:
     """UTF-8 blob + int64 offsets [n+1] for the C-ABI string arrays."""
+    if isinstance(strs, list) and strs and all(type(s) is str for s in strs):
+        joined = "".join(strs)
+        if joined.isascii():                  # one encode; byte lengths = character lengths
+            off = np.zeros(len(strs) + 1, np.int64)
+            np.cumsum(np.fromiter(map(len, strs), np.int64, len(strs)), out=off[1:])
+            return joined.encode("ascii"), off
     enc = [s.encode() for s in strs]
     off = np.zeros(len(enc) + 1, np.int64)
     if enc:
@@ -392,6 +398,26 @@ class Plan:
         L.check(L.lib.egr_plan_unpack_reach(self._h, L.ptr(rows), L.ptr(src), rows.numel(),
                                             L.ptr(inp), self._st(stream)), "egr_plan_unpack_reach")
 
+    def pack_sparse(self, what: str, rows: torch.Tensor, seg: np.ndarray, out: torch.Tensor,
+                    stream=None) -> list[int]:
+        """Non-zero entries of the send rows (egr_plan_pack_sparse) into `out` (int64, device);
+        returns the entry count per peer (synchronises the stream)."""
+        P = len(seg) - 1
+        seg = np.ascontiguousarray(seg, dtype=np.int64)
+        counts = np.zeros(P, np.int64)
+        L.check(L.lib.egr_plan_pack_sparse(self._h, 1 if what == "reach" else 0, L.ptr(rows),
+                                           rows.numel(), _addr(seg), P, L.ptr(out), out.numel(),
+                                           _addr(counts), self._st(stream)), "egr_plan_pack_sparse")
+        return counts.tolist()
+
+    def unpack_sparse(self, what: str, recv_vertex: torch.Tensor, entries: torch.Tensor,
+                      eseg: torch.Tensor, rbase: torch.Tensor, stream=None) -> None:
+        n = entries.numel() // (2 if what == "reach" else 1)
+        L.check(L.lib.egr_plan_unpack_sparse(self._h, 1 if what == "reach" else 0,
+                                             L.ptr(recv_vertex), recv_vertex.numel(), L.ptr(entries),
+                                             n, L.ptr(eseg), L.ptr(rbase), rbase.numel(),
+                                             self._st(stream)), "egr_plan_unpack_sparse")
+
     def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
         n = vertex.numel()
         if not (col.numel() == n == val.numel()):
@@ -479,6 +505,8 @@ class Frontier:
         self.max_vertices = int(L.lib.egr_frontier_max_vertices(h))
         self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
+        self.retry_blocks = 0
+        self._adapt_calls = 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -505,12 +533,34 @@ class Frontier:
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",
-             "seed_entries", "corrupt_keys")
+             "seed_entries", "corrupt_keys", "global_columns")
+
+    RETRY_BLOCKS = 512          # two wide workgroups per CU
+
+    def set_retry(self, blocks: int) -> None:
+        """Wide-table second chance for the columns that overflow the narrow table (see
+        egr_frontier_set_retry); 0 turns it off."""
+        L.check(L.lib.egr_frontier_set_retry(self._h, int(blocks)), "egr_frontier_set_retry")
+        self.retry_blocks = int(blocks)
+
+    def adapt(self, stats: dict | None = None) -> bool:
+        """After a run: turn the wide retry on if that run had overflowing columns (graphs with
+        large 3-hop neighbourhoods, e.g. the dense C4).  Returns True if it changed."""
+        if self.retry_blocks != 0 or self.pool_entries >= 0:
+            return False
+        self._adapt_calls += 1
+        if stats is None and self._adapt_calls % 16 != 1:      # a stats read synchronises
+            return False
+        st = self.stats() if stats is None else stats
+        if st["overflowed"] > 0:
+            self.set_retry(min(self.RETRY_BLOCKS, self.B))
+            return True
+        return False
 
     def stats(self, stream=None) -> dict:
         """Work counters of the last run (synchronous).  `corrupt_keys` is present only in
         debug builds (-DEGR_FR_GUARDS), where the kernel checks every member key it walks."""
-        out = np.zeros(8, np.int64)
+        out = np.zeros(9, np.int64)
         L.check(L.lib.egr_frontier_stats(self._h, _addr(out), self._st(stream)),
                 "egr_frontier_stats")
         d = dict(zip(self.STATS, out.tolist()))

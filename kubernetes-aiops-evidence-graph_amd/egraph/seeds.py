@@ -41,28 +41,41 @@ def attach_ids(ev: dict) -> list[str]:
     return []
 
 
+def _row(ev) -> tuple[list, float]:
+    """One row's candidates and strength, in the order the statement below evaluates them."""
+    return attach_ids(ev), float(ev.get("signal_strength", 0.5))
+
+
+def candidates_py(evidence_lists: list[list[dict]]) -> tuple[list, list, list, list]:
+    """(flat candidate ids, per-row counts, columns, strengths) of every row that seeds:
+    the Python statement of the native pyhost.seed_candidates (tests compare the two)."""
+    flat, count, col, val = [], [], [], []
+    for b, evs in enumerate(evidence_lists):
+        for ev in evs:
+            ids, s = _row(ev)
+            if not ids or s <= 0:
+                continue
+            flat.extend(ids)
+            count.append(len(ids))
+            col.append(b)
+            val.append(s)
+    return flat, count, col, val
+
+
 class SeedCandidates:
-    """The attachment candidates of a batch's evidence rows, computed once (string work) and
-    re-attached cheaply against a growing graph (`attach`): flat candidate ids, per-row
-    candidate counts, columns and strengths."""
+    """The attachment candidates of a batch's evidence rows, computed once (string work, in
+    native code: csrc/pyhost.c seed_candidates, with _row as its hand-over for rows whose values
+    are not plain built-ins) and re-attached cheaply against a growing graph (`attach`): flat
+    candidate ids, per-row candidate counts, columns and strengths."""
 
     def __init__(self, evidence_lists: list[list[dict]]):
-        flat, count, col, val = [], [], [], []
-        for b, evs in enumerate(evidence_lists):
-            for ev in evs:
-                ids = attach_ids(ev)
-                s = float(ev.get("signal_strength", 0.5))
-                if not ids or s <= 0:
-                    continue
-                flat.extend(ids)
-                count.append(len(ids))
-                col.append(b)
-                val.append(s)
+        from . import _lib
+        flat, count, col, val = _lib.pyhost.seed_candidates(evidence_lists, _row)
         self.n_cols = len(evidence_lists)
         self.flat = flat
-        self.count = np.asarray(count, np.int64)
-        self.col = np.asarray(col, np.uint32)
-        self.val = np.asarray(val, np.float32)
+        self.count = np.frombuffer(count, np.int64)
+        self.col = np.frombuffer(col, np.uint32)
+        self.val = np.frombuffer(val, np.float64).astype(np.float32)
 
     def attach(self, graph, pending: list | None = None):
         """(vertex u32, column u32, strength f32) triples: each row attaches to its first
@@ -72,7 +85,15 @@ class SeedCandidates:
             pending[:] = [set() for _ in range(self.n_cols)]
         if not self.flat:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
-        found = graph.lookup(self.flat).astype(np.int64)
+        return self.attach_found(graph.lookup(self.flat), pending)
+
+    def attach_found(self, found: np.ndarray, pending: list | None = None):
+        """attach() with the graph lookup of self.flat already done (callers batch it)."""
+        if pending is not None:
+            pending[:] = [set() for _ in range(self.n_cols)]
+        if not self.flat:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
+        found = np.asarray(found).astype(np.int64)
         n = len(self.flat)
         starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])
         pos = np.where(found >= 0, np.arange(n), n)

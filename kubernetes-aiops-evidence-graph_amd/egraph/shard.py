@@ -247,13 +247,32 @@ class RankRun:
         self.Bpad = engine.padded_cols
         self.W = (B + 63) // 64
         ns, nr = len(lg.send_rows), len(lg.halo_rows)
-        self.send_s = torch.zeros((ns, self.Bpad), dtype=torch.float32, device=device)
-        self.recv_s = torch.zeros((nr, self.Bpad), dtype=torch.float32, device=device)
-        self.send_r = torch.zeros((ns, self.W), dtype=torch.int64, device=device)
-        self.recv_r = torch.zeros((nr, self.W), dtype=torch.int64, device=device)
+        self._dense = None         # dense exchange buffers, allocated on first use
         self.sent_bytes = 0        # bytes this rank put on the wire (every exchange so far)
         self.exchanges = 0
+        # sparse exchange: the local vertex of each received row (rows grouped by sender) and
+        # each sender's first received row
+        rv = np.zeros(nr, np.uint32)
+        rv[lg.halo_src.astype(np.int64)] = lg.halo_rows
+        self.recv_vertex = torch.from_numpy(rv.view(np.int32)).to(device)
+        self.recv_base = torch.from_numpy(_seg_starts(lg.recv_counts)[:-1]).to(device)
+        self.send_seg = _seg_starts(lg.send_counts)
+        self._sx = {}              # sparse send buffers (int64 words), grown on demand
         engine.set_owned(lg.n_owned)
+
+    def _dense_bufs(self):
+        if self._dense is None:
+            ns, nr, dev = len(self.lg.send_rows), len(self.lg.halo_rows), self.send.device
+            self._dense = (torch.zeros((ns, self.Bpad), dtype=torch.float32, device=dev),
+                           torch.zeros((nr, self.Bpad), dtype=torch.float32, device=dev),
+                           torch.zeros((ns, self.W), dtype=torch.int64, device=dev),
+                           torch.zeros((nr, self.W), dtype=torch.int64, device=dev))
+        return self._dense
+
+    send_s = property(lambda self: self._dense_bufs()[0])   # [rows][Bpad] fp32 scores
+    recv_s = property(lambda self: self._dense_bufs()[1])
+    send_r = property(lambda self: self._dense_bufs()[2])   # [rows][W] reach words
+    recv_r = property(lambda self: self._dense_bufs()[3])
 
     @property
     def halo_bytes_per_hop(self) -> int:
@@ -268,6 +287,34 @@ def _seg_starts(counts) -> np.ndarray:
 
 
 def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
+    """The halo exchange with only the NON-ZERO entries on the wire (module doc).  Engines
+    with native sparse packing (the HIP plan: egr_plan_pack_sparse / unpack_sparse) pack and
+    scatter on the device; other engines (the CPU test engine) go through _exchange_sparse_py,
+    the same entries built with tensor ops."""
+    if not all(hasattr(r.eng, "pack_sparse") for r in runs):
+        return _exchange_sparse_py(runs, comm, what)
+    items = []
+    for r in runs:
+        ns = len(r.lg.send_rows)
+        width = r.W if what == "reach" else r.Bpad
+        per = 2 if what == "reach" else 1
+        buf = r._sx.get(what)
+        cap = ns * width * per
+        if buf is None or buf.numel() < max(cap, 1):
+            buf = r._sx[what] = torch.empty(max(cap, 1), dtype=torch.int64, device=r.send.device)
+        counts = r.eng.pack_sparse(what, r.send, r.send_seg, buf)
+        n_words = [per * c for c in counts]
+        r.sent_bytes += 8 * sum(n_words) + 8 * len(counts)
+        r.exchanges += 1
+        items.append((buf[: sum(n_words)], n_words))
+    out = comm.all_to_all_v(items)
+    for r, (recv, rc) in zip(runs, out):
+        per = 2 if what == "reach" else 1
+        eseg = torch.from_numpy(_seg_starts([c // per for c in rc])).to(recv.device)
+        r.eng.unpack_sparse(what, r.recv_vertex, recv, eseg, r.recv_base)
+
+
+def _exchange_sparse_py(runs: list[RankRun], comm, what: str) -> None:
     """The halo exchange with only the NON-ZERO entries on the wire: a boundary row's scores
     are non-zero only in the columns whose frontier reached it, and its reach words only where
     a column reached it.  Each rank packs its send rows (device-local), keeps the non-zero

@@ -113,13 +113,21 @@ class StormEngine:
         return fr
 
     def _reseed(self, handles: list[int]) -> None:
-        """(Re)attach the evidence rows of these incidents to the current graph."""
-        for h in handles:
-            x = self.incidents[h]
+        """(Re)attach the evidence rows of these incidents to the current graph: their
+        candidate ids are extracted once per incident (native, egraph/seeds.py) and looked up
+        in ONE graph call for all of them."""
+        xs = [self.incidents[h] for h in handles]
+        for x in xs:
             if x.cand is None:
                 x.cand = SeedCandidates([x.evidence])
+        flat = [i for x in xs for i in x.cand.flat]
+        found = self.g.lookup(flat) if flat else np.zeros(0, np.int64)
+        off = 0
+        for x in xs:
+            n = len(x.cand.flat)
             pend: list = []
-            x.sv, _, x.ss = x.cand.attach(self.g, pend)
+            x.sv, _, x.ss = x.cand.attach_found(found[off:off + n], pend)
+            off += n
             for pid in x.pending:
                 hs = self._pending.get(pid)
                 if hs is not None:

@@ -167,6 +167,7 @@ class GraphService:
                                        to_device(ss, dev), src, hops, inc)
         ids = ids.cpu().numpy().view("uint32")
         scores = scores.cpu().numpy()
+        fr.adapt()              # overflowing columns: the wide-table retry from the next call on
         vlabel, _, _, _ = g.export()
         out = []
         for b in range(len(keys)):

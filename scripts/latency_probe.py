@@ -62,6 +62,18 @@ def empty(i):
 
 
 stat("empty kernel + event sync", empty)
+
+
+def empty_spin(i):
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(0)
+    ev0.record(st)
+    while not ev0.query():
+        pass
+
+
+stat("empty kernel + event query spin", empty_spin)
+stat("runner launch only (host enqueue)", lambda i: r.launch(encs[i]) and torch.cuda.synchronize())
 stat("runner zero-copy launch+query spin", lambda i: [None for _ in iter(r.launch(encs[i]).query, True)])
 
 

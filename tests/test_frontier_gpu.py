@@ -137,17 +137,31 @@ def test_frontier_overflow_fallback_mixed():
     assert st["overflowed"] < len(src)       # the ring columns did not
 
 
-@pytest.mark.parametrize("mode", ["pool", "pruned", "pruned_wide_retry", "narrow_unpruned"])
+@pytest.mark.parametrize("mode", ["pool", "pruned", "pruned_wide_retry", "narrow_unpruned",
+                                  "retry_grid_7", "retry_grid_7_big_hubs"])
 def test_frontier_global_table_reuse(mode, monkeypatch):
     """More overflowing columns than global-variant workgroups (32): each workgroup reuses its
     table across columns and must leave it clean (wide table with a pool, narrow table pruned,
-    the same with the wide-table retry (128 of the 150 hub columns; the rest go straight to the
-    fallback), narrow table with pruning switched off)."""
+    the same with the wide-table retry on its default 512-block grid, narrow table with pruning
+    switched off).  retry_grid_7: the wide retry on a 7-block persistent grid, so each block
+    takes ~21 of the 150 hub columns in turn (its LDS table reused); _big_hubs: hubs past the
+    wide table's 4608 members, so the retry hands every one of them on to the global variant."""
     if mode == "narrow_unpruned":
         monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
     if mode == "pruned_wide_retry":
         monkeypatch.setenv("EGRAPH_FRONTIER_WIDE_RETRY", "1")
-    g, sv, sc, ss, src = _hub_world(n_leaves=3000, n_cols=300)   # 150 hub columns: > 128 retries
+    # retry_grid_7: ~2000 members per hub column (over the narrow table's 1536, within the
+    # wide 4608); otherwise ~6000 (past both LDS tables)
+    leaves = 1000 if mode == "retry_grid_7" else 3000
+    g, sv, sc, ss, src = _hub_world(n_leaves=leaves, n_cols=300)   # 150 hub columns
+    if mode.startswith("retry_grid"):
+        from egraph.graph import Frontier
+        real_run = Frontier.run
+
+        def run(self, *a, **kw):                    # the retry switched on before the run
+            self.set_retry(7)
+            return real_run(self, *a, **kw)
+        monkeypatch.setattr(Frontier, "run", run)
     fr = _check(g, sv, sc, ss, src, len(src), k=10, pool_entries=0 if mode == "pool" else -1,
                 scores=mode == "pool")
     assert fr.stats()["overflowed"] >= 33

@@ -1,0 +1,137 @@
+"""The native seed-candidate extraction (csrc/pyhost.c seed_candidates behind
+egraph.seeds.SeedCandidates) against its Python statement (egraph.seeds.candidates_py): the same
+candidate ids, counts, columns and strengths on collector-shaped evidence and on edge rows, and
+the same exception where the statement raises."""
+from __future__ import annotations
+
+import math
+import random
+
+import numpy as np
+import pytest
+
+
+def _both(lists):
+    from egraph import _lib
+    from egraph.seeds import _row, candidates_py
+    f, c, o, v = _lib.pyhost.seed_candidates(lists, _row)
+    a = (f, np.frombuffer(c, np.int64).tolist(), np.frombuffer(o, np.uint32).tolist(),
+         np.frombuffer(v, np.float64).tolist())
+    b = candidates_py(lists)
+    return a, b
+
+
+def _same(a, b):
+    fa, ca, cola, va = a
+    fb, cb, colb, vb = b
+    assert fa == fb and ca == cb and cola == colb
+    assert len(va) == len(vb)
+    for x, y in zip(va, vb):
+        assert (math.isnan(x) and math.isnan(y)) or x == y
+
+
+class _D(dict):
+    pass
+
+
+EDGE = [
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": {"kind": "Node", "name": "n1"}}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": {"kind": "Pod", "name": "p", "namespace": "other"}}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": {"kind": None}}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": {}}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e", "data": {}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e", "data": None},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": {"kind": 7, "name": 3, "namespace": None}}},
+    {"evidence_type": "kubernetes_event", "entity_name": "e", "data": {"involved_object": None}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": _D(kind="Deployment", name="d")}},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e", "data": ""},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": None, "entity_name": 5},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": 0},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": -0.5},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": float("nan")},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": "0.7"},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": True},
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": 2},
+    {"evidence_type": "log_signal", "entity_namespace": "ns", "entity_name": "svc"},
+    {"evidence_type": "metric_signal", "entity_namespace": 1.5, "entity_name": False},
+    {"evidence_type": "kubernetes_node", "entity_name": "n"},
+    {"evidence_type": "kubernetes_hpa", "entity_namespace": "ns", "entity_name": "h"},
+    {"evidence_type": "config_change", "entity_namespace": "ns", "entity_name": "c"},
+    {"evidence_type": "image_change", "entity_namespace": "ns", "entity_name": "d"},
+    {"evidence_type": "deploy_change", "entity_namespace": "ns", "entity_name": "d"},
+    {"evidence_type": "kubernetes_deployment", "entity_namespace": "ns", "entity_name": "d"},
+    {"evidence_type": "unknown_kind", "entity_namespace": "ns", "entity_name": "x"},
+    {"entity_namespace": "ns", "entity_name": "x"},
+    _D(evidence_type="kubernetes_pod", entity_namespace="ns", entity_name="sub"),
+    {"evidence_type": "kubernetes_pod", "entity_namespace": ["l"], "entity_name": "p"},
+]
+
+
+def test_native_matches_python_on_collector_evidence():
+    from egraph import synth
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    lists = [x.evidence for x in synth.make_incidents(c, 120, seed=10)]
+    a, b = _both(lists)
+    _same(a, b)
+    assert len(a[0]) > 5000
+
+
+def test_native_matches_python_on_edge_rows():
+    rng = random.Random(3)
+    lists = [EDGE, [], EDGE[::-1]] + [rng.sample(EDGE, 8) for _ in range(20)]
+    a, b = _both(lists)
+    _same(a, b)
+
+
+@pytest.mark.parametrize("bad", [
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": "x"},                                      # float("x"): ValueError
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": None},                                     # float(None): TypeError
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": ["x"]}},                          # list.get: AttributeError
+    ["not", "a", "dict"],                                          # list.get: AttributeError
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": 10 ** 400},                                # float(huge): OverflowError
+])
+def test_native_raises_like_python(bad):
+    from egraph import _lib
+    from egraph.seeds import _row, candidates_py
+    with pytest.raises(Exception) as e1:
+        candidates_py([[bad]])
+    with pytest.raises(Exception) as e2:
+        _lib.pyhost.seed_candidates([[bad]], _row)
+    assert type(e1.value) is type(e2.value)
+
+
+def test_seed_candidates_attach_unchanged():
+    from egraph import synth
+    from egraph.seeds import SeedCandidates, candidates_py
+    c = synth.build_cluster(synth.ClusterConfig(pods=800, namespaces=4, nodes=20,
+                                                deployments=80, services=60, seed=5))
+    cases = synth.make_incidents(c, 30, seed=6)
+    synth.add_incidents(c, cases)
+    g = synth.build_graph(c)
+    lists = [x.evidence for x in cases]
+    sc = SeedCandidates(lists)
+    flat, count, col, val = candidates_py(lists)
+    assert sc.flat == flat and sc.count.tolist() == count
+    p1, p2 = [], []
+    a = sc.attach(g, p1)
+    b = sc.attach_found(g.lookup(sc.flat), p2)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert p1 == p2
