@@ -57,6 +57,28 @@ def max_over_ranks(dist, x: float, dev) -> float:
     return float(t.item())
 
 
+def timed_steps(one_step, steps: int, dist, rank: int, sync, dev) -> float:
+    """The timed region of the contract: barrier + device sync, exactly `steps` steps, device
+    sync + barrier; returns the MAX over ranks of the elapsed seconds (every rank returns it).
+    `sync` waits for this rank's device work (torch.cuda.synchronize on the GPU)."""
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one_step()
+    t_enq = time.perf_counter() - t0
+    sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    log(f"[rank {rank}] host enqueue {t_enq / steps * 1e3:.4f} ms/step, "
+        f"wall {elapsed / steps * 1e3:.4f} ms/step")
+    if dist:
+        elapsed = max_over_ranks(dist, elapsed, dev)
+    return elapsed
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -817,21 +839,8 @@ def main():
         torch.cuda.synchronize(dev)
 
     events: list = EventPool(args.steps) if args.engine == "frontier" and not graphs else []
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run_step(ctx, args.hops, events)
-    t_enq = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    log(f"[rank {rank}] host enqueue {t_enq / args.steps * 1e3:.4f} ms/step, "
-        f"wall {elapsed / args.steps * 1e3:.4f} ms/step")
-    if dist:
-        elapsed = max_over_ranks(dist, elapsed, dev)
+    elapsed = timed_steps(lambda: run_step(ctx, args.hops, events), args.steps, dist, rank,
+                          lambda: torch.cuda.synchronize(dev), dev)
 
     B, V = args.batch, ctx["snap"].n_vertices
     nnz = ctx["snap"].n_entries

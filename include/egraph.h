@@ -138,6 +138,14 @@ int egr_rules_eval_staged(const egr_rule_table* table, const void* host_in, void
                           void* host_out, const int64_t* off, int64_t in_bytes, int64_t out_lo,
                           int64_t out_hi, int32_t n_incidents, void* stream);
 
+/* egr_rules_eval for ONE incident of at most 128 rows whose row columns are HOST arrays: the
+ * rows are copied into the kernel's argument block (no DMA copy, no PCIe reads by the kernel);
+ * the outputs (one incident: mask[1], n_hyp[1], S-slot arrays) go to `out`, typically mapped
+ * host memory (egr_host_alloc).  The drop-in's single generate_hypotheses calls.          */
+int egr_rules_eval_small(const egr_rule_table* table, const uint32_t* row_flags,
+                         const uint32_t* row_vocab, const uint32_t* row_node, const double* row_err,
+                         int32_t n_rows, const egr_rules_out* out, void* stream);
+
 /* Ranker (A6) over arbitrary hypothesis lists.  List j owns entries [list_off[j], list_off[j+1]).
  *   score = confidence * cat_weight; if support > 0: *= 1 + min(support,5)*0.05;
  *   *= 1 + strength*0.2; final = round(score, 4); stable sort descending.

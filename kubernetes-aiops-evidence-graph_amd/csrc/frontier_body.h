@@ -96,12 +96,20 @@ __device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // BLOOM_LOG bits
   return (mix24(v, 0xB5297Au | 1u) >> 8) & ((1u << BLOOM_LOG) - 1u);
 }
 
-// slot of v, inserting it if absent (-1: table full)
+// slot of v, inserting it if absent (-1: table full, or an LDS table that has overflowed)
 template <bool GT>
 __device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
   const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
+    // An LDS table past its member limit hands its column on (the result is discarded), so an
+    // insert that has to probe past its first bucket stops there -- a table filled to the last
+    // slot would make every insert of a new key scan all its buckets (the dense C4 spent ~4 ms
+    // per launch there before this exit).  Checked only past the first bucket: the common
+    // insert pays nothing.
+    if constexpr (!GT) {
+      if (n > 0 && *t.ovf) return -1;
+    }
     uint4 kk = t.bucket(bk);
     uint32_t ks[4] = {kk.x, kk.y, kk.z, kk.w};
 #pragma unroll
@@ -462,6 +470,9 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   uint32_t c_cur = grab();
   Chunk nxt = fetch(c_cur);
   while (c_cur < nch) {
+    if constexpr (!GT) {
+      if (*t.ovf) break;        // overflowed LDS table: the column is redone elsewhere
+    }
     const Chunk cur = nxt;
     const uint32_t c_next = grab();
     nxt = fetch(c_next);

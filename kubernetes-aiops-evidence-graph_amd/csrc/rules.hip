@@ -107,20 +107,13 @@ __device__ bool condition_holds(int type, uint32_t mask, double param, const Sig
   }
 }
 
-__global__ __launch_bounds__(256) void rules_eval_kernel(
+// One incident (rows [beg, end) of the row arrays) on one wave; hk / hc = the wave's LDS hash.
+__device__ __forceinline__ void rules_incident(
     const RulesDev* __restrict__ D, const uint32_t* __restrict__ row_flags,
     const uint32_t* __restrict__ row_vocab, const uint32_t* __restrict__ row_node,
-    const double* __restrict__ row_err, const int64_t* __restrict__ seg_off, int n_incidents,
-    egr_rules_out out) {
-  __shared__ uint32_t node_key[kWavesPerBlock][kNodeSlots];
-  __shared__ uint32_t node_cnt[kWavesPerBlock][kNodeSlots];
+    const double* __restrict__ row_err, int64_t beg, int64_t end, int inc,
+    const egr_rules_out& out, uint32_t* hk, uint32_t* hc) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int wv = threadIdx.x >> 6;
-  const int inc = blockIdx.x * kWavesPerBlock + wv;
-  if (inc >= n_incidents) return;  // wave-uniform; no block barrier below
-  const int64_t beg = seg_off[inc], end = seg_off[inc + 1];
-  uint32_t* hk = node_key[wv];
-  uint32_t* hc = node_cnt[wv];
   // lane r's rule, loaded up front (independent of the rows: its latency overlaps theirs)
   const int R = D->n_rules;
   const uint32_t network_bit = D->network_vocab_bit;
@@ -274,6 +267,38 @@ __global__ __launch_bounds__(256) void rules_eval_kernel(
   }
 }
 
+__global__ __launch_bounds__(256) void rules_eval_kernel(
+    const RulesDev* __restrict__ D, const uint32_t* __restrict__ row_flags,
+    const uint32_t* __restrict__ row_vocab, const uint32_t* __restrict__ row_node,
+    const double* __restrict__ row_err, const int64_t* __restrict__ seg_off, int n_incidents,
+    egr_rules_out out) {
+  __shared__ uint32_t node_key[kWavesPerBlock][kNodeSlots];
+  __shared__ uint32_t node_cnt[kWavesPerBlock][kNodeSlots];
+  const int wv = threadIdx.x >> 6;
+  const int inc = blockIdx.x * kWavesPerBlock + wv;
+  if (inc >= n_incidents) return;  // wave-uniform; no block barrier below
+  rules_incident(D, row_flags, row_vocab, row_node, row_err, seg_off[inc], seg_off[inc + 1], inc,
+                 out, node_key[wv], node_cnt[wv]);
+}
+
+// One small incident whose rows travel IN THE KERNEL ARGUMENTS (the drop-in's single calls:
+// no host-to-device copy, and no row read over PCIe from mapped host memory -- the argument
+// block is in device memory when the kernel starts).  One wave.
+constexpr int kSmallRows = 128;
+struct SmallRows {
+  const RulesDev* D;
+  egr_rules_out out;
+  int32_t n_rows;
+  uint32_t flags[kSmallRows], vocab[kSmallRows], node[kSmallRows];
+  double err[kSmallRows];
+};
+
+__global__ __launch_bounds__(64) void rules_small_kernel(const SmallRows a) {
+  __shared__ uint32_t node_key[kNodeSlots];
+  __shared__ uint32_t node_cnt[kNodeSlots];
+  rules_incident(a.D, a.flags, a.vocab, a.node, a.err, 0, a.n_rows, 0, a.out, node_key, node_cnt);
+}
+
 // Stand-alone ranker: one wave per hypothesis list, stable descending order by counting.
 __global__ __launch_bounds__(256) void rank_kernel(
     const double* __restrict__ conf, const double* __restrict__ catw,
@@ -418,6 +443,36 @@ extern "C" int egr_rules_eval_staged(const egr_rule_table* table, const void* ho
   if (out_hi > out_lo)
     EGR_HIP(hipMemcpyAsync(static_cast<uint8_t*>(host_out) + out_lo, d + out_lo,
                            (size_t)(out_hi - out_lo), hipMemcpyDeviceToHost, st));
+  return EGR_OK;
+}
+
+extern "C" int egr_rules_eval_small(const egr_rule_table* table, const uint32_t* row_flags,
+                                    const uint32_t* row_vocab, const uint32_t* row_node,
+                                    const double* row_err, int32_t n_rows,
+                                    const egr_rules_out* out, void* stream) {
+  if (!table || !out || n_rows < 0 || n_rows > kSmallRows ||
+      (n_rows > 0 && (!row_flags || !row_vocab || !row_node || !row_err)))
+    return egr::fail(EGR_EINVAL, "egr_rules_eval_small: bad arguments (at most 128 rows)");
+  if (!out->mask || !out->n_hyp || !out->order_conf || !out->order_rank || !out->confidence ||
+      !out->final_score || !out->strength)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval_small: NULL output");
+  if (table->n_rules < 0 || table->n_rules > EGR_MAX_RULES)
+    return egr::fail(EGR_EINVAL, "egr_rules_eval_small: n_rules out of range");
+  const RulesDev* D = nullptr;
+  const int rc = rules_table_dev(*table, (hipStream_t)stream, &D);
+  if (rc != EGR_OK) return rc;
+  SmallRows a;
+  a.D = D;
+  a.out = *out;
+  a.n_rows = n_rows;
+  if (n_rows > 0) {
+    std::memcpy(a.flags, row_flags, sizeof(uint32_t) * n_rows);
+    std::memcpy(a.vocab, row_vocab, sizeof(uint32_t) * n_rows);
+    std::memcpy(a.node, row_node, sizeof(uint32_t) * n_rows);
+    std::memcpy(a.err, row_err, sizeof(double) * n_rows);
+  }
+  hipLaunchKernelGGL(rules_small_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
 

@@ -149,6 +149,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_topk": (C.c_int, [P, P, P, I32, I32, I32, P, P, P]),
     "egr_host_alloc": (C.c_int, [I64, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "egr_host_free": (C.c_int, [P]),
+    "egr_rules_eval_small": (C.c_int, [C.POINTER(EgrRuleTable), P, P, P, P, I32, C.POINTER(EgrRulesOut), P]),
     "egr_rules_eval_staged": (C.c_int, [C.POINTER(EgrRuleTable), P, P, P, P, I64, I64, I64, I32, P]),
 }
 

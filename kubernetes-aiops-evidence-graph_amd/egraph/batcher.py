@@ -57,9 +57,25 @@ class RulesRunner:
         self.event = torch.cuda.Event()
         self._offs = np.zeros(12, np.int64)
         self.mapped: MappedBuffer | None = None
-        self.zero_copy = False                        # mode of the last launch
+        self.zero_copy = False                        # the last launch's outputs in mapped memory
+        self.mode = ""                                # "small" / "zero_copy" / "staged"
+        self._layouts: dict = {}
+        self._small_out = None                        # EgrRulesOut of the single-incident layout
+
+    # a single incident of at most this many rows travels in the kernel's arguments
+    # (egr_rules_eval_small): one launch, no copies, no PCIe reads by the kernel
+    SMALL_ROWS = 128
 
     def _layout(self, rows: int, B: int):
+        key = (rows, B)
+        hit = self._layouts.get(key)
+        if hit is None:
+            if len(self._layouts) > 4096:
+                self._layouts.clear()
+            hit = self._layouts[key] = self._layout_new(rows, B)
+        return hit
+
+    def _layout_new(self, rows: int, B: int):
         S = self.S
         inp = [("flags", 4 * rows), ("vocab", 4 * rows), ("node", 4 * rows), ("err", 8 * rows),
                ("seg", 8 * (B + 1))]
@@ -106,10 +122,27 @@ class RulesRunner:
         # this launch's layout inside the buffers: only its own bytes are touched
         self.off, self.in_bytes, self.total = self._layout(rows, B)
         st = self.stream
-        if rows <= self.ZERO_COPY_ROWS:
-            if self.mapped is None or self.mapped.nbytes < self.total:
-                self.mapped = MappedBuffer(max(self.total, 1 << 20))
+        if rows <= self.ZERO_COPY_ROWS and (self.mapped is None or self.mapped.nbytes < self.total):
+            self.mapped = MappedBuffer(max(self.total, 1 << 20))
+            self._small_out = None
+        if B == 1 and rows <= self.SMALL_ROWS:
+            # the rows in the kernel arguments, the outputs into mapped host memory
             self.hnp, self.zero_copy = self.mapped.np, True
+            if self._small_out is None:
+                base = self.mapped.dev
+                so = self._layout(0, 1)[0]                # output offsets do not depend on rows
+                self._small_out = (so, L.EgrRulesOut(*(base + so[k][0] for k in (
+                    "mask", "n_hyp", "oc", "orank", "conf", "fin", "str"))))
+            self.off, self.mode = self._small_out[0], "small"
+            f = enc.flags.ctypes.data if rows else None
+            L.check(L.lib.egr_rules_eval_small(
+                self.cat.table, f, enc.vocab.ctypes.data if rows else None,
+                enc.node.ctypes.data if rows else None, enc.err.ctypes.data if rows else None,
+                rows, self._small_out[1], st.cuda_stream), "egr_rules_eval_small")
+            self.event.record(st)
+            return self.event
+        if rows <= self.ZERO_COPY_ROWS:
+            self.hnp, self.zero_copy, self.mode = self.mapped.np, True, "zero_copy"
             self._stage_inputs(enc)
             base = self.mapped.dev
             d = {k: base + o for k, (o, _) in self.off.items()}
@@ -119,7 +152,7 @@ class RulesRunner:
             self.event.record(st)
             return self.event
         self._ensure(rows, B)
-        self.hnp, self.zero_copy = self.hbuf.numpy(), False
+        self.hnp, self.zero_copy, self.mode = self.hbuf.numpy(), False, "staged"
         self._stage_inputs(enc)
         out_lo = self.off["mask"][0]
         self._offs[:] = [self.off[k][0] for k in ("flags", "vocab", "node", "err", "seg", "mask",

@@ -122,8 +122,9 @@ _RUNNERS: dict = {}
 
 class FusedRanks:
     """The rules kernel's ranking of the lists it generated, for rank() to reuse (module doc).
-    A record is (hypothesis ids, per-position (confidence, category, support_count,
-    signal_strength) as the kernel emitted them, final scores, ranked positions)."""
+    A record keeps the list's hypothesis ids and a reference to its launch's results (row i);
+    the fields to verify and the final scores / order are read from those results only when
+    rank() asks, so registering a list costs one tuple."""
 
     def __init__(self, capacity: int = 1 << 16):
         self.capacity = capacity
@@ -133,31 +134,23 @@ class FusedRanks:
 
     def register(self, cat, res, lists: list[list[dict]], rows) -> None:
         """lists[j] = the unranked dicts of result row rows[j] (confidence order)."""
-        rules, R = cat.rules, cat.n_rules
-        unknown = (cat.unknown["confidence"], cat.unknown["category"],
-                   cat.unknown["support_count"], cat.unknown["signal_strength"])
-        recs = []
-        for hyps, i in zip(lists, rows):
-            n = len(hyps)
-            oc, orank = res.order_conf[i], res.order_rank[i]
-            pos = {int(oc[p]): p for p in range(n)}
-            fields, fin = [], []
-            for p in range(n):
-                slot = int(oc[p])
-                if slot == R:
-                    fields.append(unknown)
-                else:
-                    r = rules[slot]
-                    fields.append((float(res.confidence[i, slot]), r["category"],
-                                   len(r["conditions"]), float(res.strength[i, slot])))
-                fin.append(float(res.final_score[i, slot]))
-            ranked = tuple(pos[int(orank[q])] for q in range(n))
-            recs.append((hyps[0]["id"], (tuple(h["id"] for h in hyps), tuple(fields), fin, ranked)))
+        recs = [(hyps[0]["id"], (tuple(h["id"] for h in hyps), cat, res, int(i)))
+                for hyps, i in zip(lists, rows) if hyps]
         with self.lock:
             for key, rec in recs:
                 self.recs[key] = rec
             while len(self.recs) > self.capacity:
                 self.recs.popitem(last=False)
+
+    @staticmethod
+    def _fields(cat, res, i: int, slot: int) -> tuple:
+        """(confidence, category, support_count, signal_strength) the kernel emitted for a slot."""
+        if slot == cat.n_rules:
+            u = cat.unknown
+            return (u["confidence"], u["category"], u["support_count"], u["signal_strength"])
+        r = cat.rules[slot]
+        return (float(res.confidence[i, slot]), r["category"], len(r["conditions"]),
+                float(res.strength[i, slot]))
 
     def apply(self, hyps: list) -> list | None:
         """Rank `hyps` from its record if it is exactly a registered list; else None."""
@@ -165,23 +158,27 @@ class FusedRanks:
             return None
         with self.lock:
             rec = self.recs.get(hyps[0].get("id"))
-        if rec is None:
+        if rec is None or len(hyps) != len(rec[0]):
             self.misses += 1
             return None
-        ids, fields, fin, ranked = rec
-        if len(hyps) != len(ids):
-            self.misses += 1
-            return None
-        for h, hid, (c, cat, sup, st) in zip(hyps, ids, fields):
-            if not isinstance(h, dict) or h.get("id") != hid or \
-                    h.get("confidence", 0.5) != c or h.get("category", "unknown") != cat or \
+        ids, cat, res, i = rec
+        oc = res.order_conf[i]
+        slots = [int(oc[p]) for p in range(len(ids))]
+        for h, hid, slot in zip(hyps, ids, slots):
+            if not isinstance(h, dict) or h.get("id") != hid:
+                self.misses += 1
+                return None
+            c, catg, sup, st = self._fields(cat, res, i, slot)
+            if h.get("confidence", 0.5) != c or h.get("category", "unknown") != catg or \
                     h.get("support_count", 0) != sup or h.get("signal_strength", 0) != st:
                 self.misses += 1
                 return None
         self.hits += 1
-        for h, f in zip(hyps, fin):
-            h["final_score"] = f
-        out = [hyps[p] for p in ranked]
+        pos = {slot: p for p, slot in enumerate(slots)}
+        for h, slot in zip(hyps, slots):
+            h["final_score"] = float(res.final_score[i, slot])
+        orank = res.order_rank[i]
+        out = [hyps[pos[int(orank[q])]] for q in range(len(ids))]
         for q, h in enumerate(out):
             h["rank"] = q + 1
         return out

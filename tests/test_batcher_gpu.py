@@ -31,10 +31,19 @@ def test_runner_matches_oracle():
     runner = RulesRunner(cat)
     # zero-copy (mapped host memory) for small batches, the staged device buffer above
     # ZERO_COPY_ROWS; grows, then reuses the buffers with a smaller batch
-    for n in (1, 3, 700, 40, 2000, 0, 5):
-        enc = encode_batch([evidence_fuzz.random_evidence(rng) for _ in range(n)], cat)
+    # and a single incident of <= 128 rows in the kernel arguments (egr_rules_eval_small)
+    seen = set()
+    for n, big in ((1, False), (3, False), (700, False), (40, False), (2000, False), (0, False),
+                   (5, False), (1, True), (1, False)):
+        lists = [evidence_fuzz.random_evidence(rng) for _ in range(n)]
+        if big:
+            lists = [(lists[0] or [{"id": "x"}]) * 200]   # one incident of > 128 rows
+        enc = encode_batch(lists, cat)
         res = runner.run_sync(enc)
-        assert runner.zero_copy == (enc.n_rows <= runner.ZERO_COPY_ROWS)
+        want = ("small" if n == 1 and enc.n_rows <= runner.SMALL_ROWS else
+                "zero_copy" if enc.n_rows <= runner.ZERO_COPY_ROWS else "staged")
+        assert runner.mode == want
+        seen.add(want)
         exp = oracle.rules_eval(cat.table, enc.flags, enc.vocab, enc.node, enc.err, enc.seg_off)
         np.testing.assert_array_equal(res.mask, exp["mask"])
         np.testing.assert_array_equal(res.order_rank, exp["order_rank"])
@@ -42,6 +51,7 @@ def test_runner_matches_oracle():
         assert res.final_score.tobytes() == exp["final_score"].tobytes()
         assert res.confidence.tobytes() == exp["confidence"].tobytes()
         assert res.strength.tobytes() == exp["strength"].tobytes()
+    assert seen == {"small", "zero_copy", "staged"}
 
 
 def test_concurrent_calls_coalesce_and_match_golden(golden):
