@@ -818,7 +818,8 @@ def main():
                 args.pipeline if args.engine == "frontier" else 1,
                 pool_entries=0 if args.pool else -1)
     run_step = step_frontier if args.engine == "frontier" else step
-    for _ in range(args.warmup):
+    # (at least one step per lane: every lane's frontier has run before adapt() reads its stats)
+    for _ in range(max(args.warmup, len(ctx.get("lanes", ())))):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
     if args.engine == "frontier":

@@ -25,8 +25,8 @@
 //
 // Capacity: two instantiations of the kernels (frontier_body.h).  The wide one (member-pool
 // runs, every member's score exact) holds 6144 slots in ~78 KB of LDS, 8-wave workgroups, two
-// per CU; the narrow one (pruned top-k runs: ~0.6k members per column on C3) holds 2048 slots
-// in 28 KB, 4-wave workgroups, five per CU.  A column with more members than the table's limit
+// per CU; the narrow one (pruned top-k runs: ~0.6k members per column on C3) holds 1536 slots
+// and two score buffers in 30 KB, 4-wave workgroups, five per CU.  A column with more members than the table's limit
 // is flagged and redone by the global-memory variant of the same code (a table of >= 2V slots
 // per resident workgroup, never overflows), launched unconditionally right after (it drains an
 // empty work list at once).
@@ -135,7 +135,7 @@ struct FArgs {
 
 // Two instantiations of the kernels (frontier_body.h): the wide table keeps every member of a
 // column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
-// one serves the pruned top-k runs (~0.6k members per column on C3), whose 28 KB of LDS and
+// one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
 // 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
 namespace fr_wide {
 #define FR_FT 512
@@ -146,6 +146,7 @@ namespace fr_wide {
 #define FR_LSNEW 0
 #define FR_KV 0
 #define FR_HUBCHAIN 1
+#define FR_DBUF 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -155,18 +156,22 @@ namespace fr_wide {
 #undef FR_LSNEW
 #undef FR_KV
 #undef FR_HUBCHAIN
+#undef FR_DBUF
 }  // namespace fr_wide
 
 namespace fr_narrow {
 #ifndef EGR_FR_NARROW_FT   // build-time knobs for A/B builds (scripts/ab_lib.sh)
 #define EGR_FR_NARROW_FT 256
-#define EGR_FR_NARROW_LCAP 2048
-#define EGR_FR_NARROW_LLIMIT 1536
+#define EGR_FR_NARROW_LCAP 1536
+#define EGR_FR_NARROW_LLIMIT 1152
 #define EGR_FR_NARROW_BLOOM_LOG 15
 #define EGR_FR_NARROW_WAVES_PER_EU 5
 #endif
 #ifndef EGR_FR_NARROW_LSNEW
 #define EGR_FR_NARROW_LSNEW 0
+#endif
+#ifndef EGR_FR_NARROW_DBUF   // two slot-indexed score buffers, no copy phase (+2.5 %, abdb)
+#define EGR_FR_NARROW_DBUF 1
 #endif
 #define FR_FT EGR_FR_NARROW_FT
 #define FR_LCAP EGR_FR_NARROW_LCAP
@@ -176,6 +181,7 @@ namespace fr_narrow {
 #define FR_LSNEW EGR_FR_NARROW_LSNEW
 #define FR_KV EGR_FR_NARROW_KV
 #define FR_HUBCHAIN EGR_FR_HUBCHAIN
+#define FR_DBUF EGR_FR_NARROW_DBUF
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -185,6 +191,7 @@ namespace fr_narrow {
 #undef FR_LSNEW
 #undef FR_KV
 #undef FR_HUBCHAIN
+#undef FR_DBUF
 }  // namespace fr_narrow
 
 // The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
@@ -201,6 +208,7 @@ namespace fr_fallback {
 #define FR_LSNEW 0
 #define FR_KV 0
 #define FR_HUBCHAIN 2
+#define FR_DBUF 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -210,6 +218,7 @@ namespace fr_fallback {
 #undef FR_LSNEW
 #undef FR_KV
 #undef FR_HUBCHAIN
+#undef FR_DBUF
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
@@ -491,6 +500,8 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const uint32_t lcap = f->narrow ? fr_narrow::LCAP : fr_wide::LCAP;
   // pull results by member index: the narrow kernel and the wide retry index the same buffer
   const uint32_t llimit = std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT);
+  static_assert(fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
+                "FR_DBUF: the narrow kernel keeps its seed values by slot in lsnew's column stride");
   size_t gcap = 2 * lcap;
   while (gcap < 2ull * V) gcap *= 2;
   f->gcap = (uint32_t)gcap;

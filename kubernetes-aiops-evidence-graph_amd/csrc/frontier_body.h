@@ -5,7 +5,9 @@
 //   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
 //   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU,
 //   FR_LSNEW (1: the pull results live in LDS instead of HBM), FR_KV (1: the LDS table keeps
-//   each slot's key and score side by side, so one probe returns the score), FR_HUBCHAIN.
+//   each slot's key and score side by side, so one probe returns the score), FR_HUBCHAIN,
+//   FR_DBUF (1: two slot-indexed score buffers; a pull reads hop h's and writes hop h + 1's
+//   directly, seed add and need-bit clearing included, so no copy phase follows the walk).
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -18,6 +20,8 @@ constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys
 constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
+constexpr bool DBUF = FR_DBUF;
+static_assert(!(FR_DBUF && (FR_KV || FR_LSNEW)), "FR_DBUF replaces the member-indexed pull results");
 
 
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
@@ -41,6 +45,9 @@ struct Tab {
   uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
   uint32_t* chunk;  // LDS: the next chunk of a walk (dynamic chunk assignment), 0 at its start
   float2* chain;    // LDS: per-wave hub-chain scratch [NWAVES][64] (EGR_FR_HUBCHAIN 2), or null
+  // FR_DBUF (LDS tables): snew is the slot-indexed buffer the walk writes (hop h + 1's scores)
+  // and s0g the column's seed values by slot, in global memory (read by the seeds' pullers)
+  const float* s0g = nullptr;
 
   __device__ __forceinline__ uint32_t* keyp(uint32_t p) const { return KV ? keys + 2 * p : keys + p; }
   __device__ __forceinline__ float* sp(uint32_t p) const {
@@ -410,8 +417,17 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   // the walk ends within about one chunk of its fastest wave).  The next chunk's selection and
   // row_ptr loads are issued before the current chunk is walked (a member's kind cannot change
   // during the pass: see the comment above).
+  // FR_DBUF pulls (DW): every member of the walk writes its hop h + 1 score into the other
+  // buffer (0 when not pulled, + s0 for a seed), clears its hop-h need bit and, after the last
+  // pull, gets NEED_EXCL when it is a candidate carrying the excluded label.
+  constexpr bool DW = DBUF && !GT && PH == PULL;
+  const bool last_pull = h == A.hops - 1;
+  const bool mark_excl = DW && last_pull && A.exclude >= 0;
+  constexpr uint32_t NOP = 0xFFFFFFFFu;
   struct Chunk {
     uint32_t i, kind, e0, e1;
+    uint32_t p;      // DW: the member's slot | (0x100 | label) << 16 for a candidate (NOP: none)
+    float s0;        // DW: the member's seed value (0 unless a seed)
   };
 #if EGR_FR_DYN == 0
   // static: wave w walks chunks k = 0, 1, ... holding members w + NWAVES * (lane + 64 k)
@@ -425,7 +441,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   auto member_of = [&](uint32_t c) { return 64u * c + lane; };
 #endif
   auto fetch = [&](uint32_t c) {
-    Chunk ch{member_of(c), 0u, 0u, 0u};
+    Chunk ch{member_of(c), 0u, 0u, 0u, NOP, 0.f};
     uint32_t v = 0;
     if (c < nch && ch.i < n) {
       uint32_t p = t.mlist[ch.i];
@@ -441,8 +457,18 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       if constexpr (PH == SEEDS) {
         if (f & FL_SEED) ch.kind |= K_PROP | noins;
       } else {
-        if ((((t.need[p] >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
+        const uint32_t nd = t.need[p];
+        if ((((nd >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
           ch.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
+        if constexpr (DW) {
+          // the hop-h bit is consumed here (the copy phase of the single-buffer scheme cleared
+          // it); expansions of this walk set the other parity's bit of the same word
+          if (((nd >> par) & 1u) && !last_pull)
+            atomicAnd(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), ~((1u << par) << ((p & 3u) * 8u)));
+          ch.p = p;
+          if (f & FL_SEED) ch.s0 = t.s0g[p];
+          if (mark_excl && is_cand(f)) ch.p |= (0x100u | A.vlabel[v]) << 16;   // candidate | label
+        }
       }
     }
 #ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
@@ -570,7 +596,16 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     }
 #endif
     tk.tick(2);
-    if constexpr (PH == PULL) {
+    if constexpr (DW) {
+      if (cur.p != NOP) {
+        const uint32_t p = cur.p & 0xFFFFu;
+        // = the copy (pulled ? acc : +0) then the seed add (+ s0): the same fadd, bit for bit
+        // (s0 is +0 for a non-seed, and r + +0 == r: r is never -0)
+        t.snew[p] = ((kind & K_PULL) ? acc : 0.f) + cur.s0;
+        if (mark_excl && (cur.p >> 16) == (0x100u | (uint8_t)A.exclude))
+          atomicOr(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), (uint32_t)NEED_EXCL << ((p & 3u) * 8u));
+      }
+    } else if constexpr (PH == PULL) {
       if (kind & K_PULL) t.snew[i] = acc;
     }
     tk.tick(3);
@@ -720,15 +755,13 @@ __device__ __forceinline__ bool phase_sync(Shared& sh, uint32_t& cnt) {
   return ovf;
 }
 
-// One column end to end.  Returns false (uniformly) if the table overflowed.
+// The end of a column after its last pull: top-k over the reach set, the member pool, the
+// work counters.  `slot` continues run_column's profiling stamps.
 template <bool GT>
-__device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b) {
+__device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b,
+                                              uint32_t cnt, const Work& work, int slot) {
   const uint32_t tid = threadIdx.x;
   const int hops = A.hops;
-  Work work;
-  // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
-  // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
-  int slot = 0;
   auto stamp = [&]() {
     if (A.prof && tid == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
@@ -738,154 +771,6 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
-  stamp();
-  // The incident vertex and its row (reach level 1) are loaded first: their latency hides
-  // behind the seed passes.
-  const uint32_t src = A.sources[b];
-  const bool src_ok = A.hops >= 1 && src < A.V;
-  const uint32_t ie0 = src_ok ? A.row_ptr[src] : 0u, ie1 = src_ok ? A.row_ptr[src + 1] : 0u;
-  const uint32_t ic0 = ie0 + tid < ie1 ? A.cv[ie0 + tid].x : 0u;   // first stripe of the row
-  // Seeds, two passes.  Pass 1 inserts every seed vertex and max-combines duplicate entries
-  // with one atomicMax on the order-preserving u32 image of the value (ord(): the cleared
-  // slot's 0 lies below every float's image, -inf included) -- fmaxf, like the dense plan's
-  // seed prep.  Pass 2: one entry per vertex claims it, turns the slot back into the float and
-  // records (slot, s0) for the per-hop seed add; thread 0 also inserts the incident vertex.
-  const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
-  auto ord = [](float f) {
-    const uint32_t u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  };
-  auto unord = [](uint32_t o) {
-    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
-  };
-  const uint32_t i0 = sb + tid;
-  const uint32_t v0 = i0 < se ? A.seed_vert[i0] : 0u;   // the first stripe stays in registers
-  const float x0 = i0 < se ? A.seed_val[i0] : 0.f;
-  for (uint32_t i = i0; i < se; i += FT) {
-    const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
-    const float x = i == i0 ? x0 : A.seed_val[i];
-    const int q = tab_insert<GT>(t, v);
-    if (q >= 0) {
-      atomicMax(reinterpret_cast<unsigned int*>(t.sp(q)), ord(x));
-      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
-               (uint32_t)FL_SEED << (((uint32_t)q & 3u) * 8u));
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = i0; i < se; i += FT) {
-    const int q = tab_find<GT>(t, i == i0 ? v0 : A.seed_vert[i]);
-    uint2 r = make_uint2(NO_NODE, 0u);
-    if (q >= 0) {
-      const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
-      const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
-                                    (uint32_t)FL_CLAIM << sh8);
-      if (!((old >> sh8) & FL_CLAIM)) {        // the claimer alone touches the value now
-        const float s0 = unord(*reinterpret_cast<unsigned int*>(t.sp(q)));
-        t.sc(q) = s0;
-        r = make_uint2((uint32_t)q, __float_as_uint(s0));
-      }
-    }
-    A.seed_rep[i] = r;
-  }
-  if (tid == 0 && src_ok) {       // (a find of a seed is unaffected by concurrent inserts)
-    const int q = tab_insert<GT>(t, src);
-    if (q >= 0)
-      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2), 1u << (((uint32_t)q & 3u) * 8u));
-  }
-  __syncthreads();
-  // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
-  if (src_ok) {
-    if (tid == 0) {
-      ++work.rows;
-      work.expand += ie1 - ie0;
-    }
-    for (uint32_t e = ie0 + tid; e < ie1; e += FT) {
-      const int q = tab_insert<GT>(t, e == ie0 + tid ? ic0 : A.cv[e].x);
-      if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
-    }
-  }
-  wstamp();
-  uint32_t cnt;
-  bool ovf = phase_sync(sh, cnt);
-  stamp();
-  if (ovf) return false;
-  // the seeds' neighbours are the members pulled at hop 0
-  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1);
-  wstamp();
-  ovf = phase_sync(sh, cnt);
-  stamp();
-  if (ovf) return false;
-  for (int h = 0; h < hops; ++h) {
-    // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
-    const uint32_t n0 = cnt;
-    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
-    wstamp();
-    ovf = phase_sync(sh, cnt);
-    stamp();
-    if (ovf) return false;
-    // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
-    // (pruned last pull: a non-candidate was not pulled and keeps +0; nothing reads it)
-    const uint32_t n = cnt, bit = 1u << ((uint32_t)h & 1u);
-    const bool last = h == hops - 1;
-    const bool prune_now = A.prune && last;
-    // after the last pull, a candidate carrying the excluded label is marked NEED_EXCL for
-    // top-k; its label load is issued beside the member's pull-result load
-    const bool mark_excl = last && A.exclude >= 0;
-    // this thread's first seed entry: its load is issued beside the copy's loads
-    const uint32_t ir = sb + tid;
-    const uint2 r0 = ir < se ? A.seed_rep[ir] : make_uint2(NO_NODE, 0u);
-    auto copy_one = [&](uint32_t i, uint32_t p, uint8_t nd, uint8_t f, float sn, uint8_t lab) {
-      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
-                          (!prune_now || cand_depth(f, hops));
-      t.sc(p) = pulled ? sn : 0.f;
-      uint8_t nn = nd & ~bit;
-      if (mark_excl && cand_depth(f, hops) && lab == (uint8_t)A.exclude) nn |= NEED_EXCL;
-      if (nn != nd) t.need[p] = nn;
-    };
-    if constexpr (!GT && EGR_FR_COPYU) {
-      // every member of this thread at once (n <= LLIMIT): LDS reads, then both global loads
-      // of every member in flight together, then the stores
-      uint32_t pp[MPT];
-      uint8_t nds[MPT], fls[MPT], labs[MPT];
-      float sns[MPT];
-#pragma unroll
-      for (int j = 0; j < MPT; ++j) {
-        const uint32_t i = tid + j * FT;
-        pp[j] = i < n ? t.mlist[i] : 0xFFFFFFFFu;
-        nds[j] = 0;
-        fls[j] = 0;
-        if (pp[j] < t.cap) {
-          nds[j] = t.need[pp[j]];
-          fls[j] = t.fl[pp[j]];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < MPT; ++j) {
-        const uint32_t i = tid + j * FT;
-        sns[j] = (pp[j] < t.cap && i < n0) ? t.snew[i] : 0.f;
-        labs[j] = (mark_excl && pp[j] < t.cap && cand_depth(fls[j], hops)) ? A.vlabel[t.key(pp[j])] : 0xFF;
-      }
-#pragma unroll
-      for (int j = 0; j < MPT; ++j)
-        if (pp[j] < t.cap) copy_one(tid + j * FT, pp[j], nds[j], fls[j], sns[j], labs[j]);
-    } else {
-      for (uint32_t i = tid; i < n; i += FT) {
-        const uint32_t p = t.mlist[i];
-        if (p >= t.cap) continue;
-        const uint8_t f = t.fl[p];
-        const uint8_t lab = (mark_excl && cand_depth(f, hops)) ? A.vlabel[t.key(p)] : 0xFF;
-        copy_one(i, p, t.need[p], f, i < n0 ? t.snew[i] : 0.f, lab);
-      }
-    }
-    __syncthreads();
-    if (r0.x != NO_NODE) t.sc(r0.x) = t.sc(r0.x) + __uint_as_float(r0.y);
-    for (uint32_t i = ir + FT; i < se; i += FT) {
-      const uint2 r = A.seed_rep[i];
-      if (r.x != NO_NODE) t.sc(r.x) = t.sc(r.x) + __uint_as_float(r.y);
-    }
-    __syncthreads();
-    stamp();
-  }
   const uint32_t n = cnt;
   // top-k over the reach set: each wave its own k best, then wave 0 merges the NWAVES lists
   const int lane = tid & 63, wave = tid >> 6;
@@ -966,6 +851,196 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   return true;
 }
 
+// One column end to end.  Returns false (uniformly) if the table overflowed.
+template <bool GT>
+__device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b) {
+  const uint32_t tid = threadIdx.x;
+  const int hops = A.hops;
+  Work work;
+  // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
+  // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
+  int slot = 0;
+  auto stamp = [&]() {
+    if (A.prof && tid == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
+    ++slot;
+  };
+  auto wstamp = [&]() {
+    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
+  };
+  stamp();
+  // The incident vertex and its row (reach level 1) are loaded first: their latency hides
+  // behind the seed passes.
+  const uint32_t src = A.sources[b];
+  const bool src_ok = A.hops >= 1 && src < A.V;
+  const uint32_t ie0 = src_ok ? A.row_ptr[src] : 0u, ie1 = src_ok ? A.row_ptr[src + 1] : 0u;
+  const uint32_t ic0 = ie0 + tid < ie1 ? A.cv[ie0 + tid].x : 0u;   // first stripe of the row
+  // Seeds, two passes.  Pass 1 inserts every seed vertex and max-combines duplicate entries
+  // with one atomicMax on the order-preserving u32 image of the value (ord(): the cleared
+  // slot's 0 lies below every float's image, -inf included) -- fmaxf, like the dense plan's
+  // seed prep.  Pass 2: one entry per vertex claims it, turns the slot back into the float and
+  // records (slot, s0) for the per-hop seed add; thread 0 also inserts the incident vertex.
+  const uint32_t sb = A.seed_ptr[b], se = A.seed_ptr[b + 1];
+  auto ord = [](float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  };
+  auto unord = [](uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+  };
+  const uint32_t i0 = sb + tid;
+  const uint32_t v0 = i0 < se ? A.seed_vert[i0] : 0u;   // the first stripe stays in registers
+  const float x0 = i0 < se ? A.seed_val[i0] : 0.f;
+  for (uint32_t i = i0; i < se; i += FT) {
+    const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
+    const float x = i == i0 ? x0 : A.seed_val[i];
+    const int q = tab_insert<GT>(t, v);
+    if (q >= 0) {
+      atomicMax(reinterpret_cast<unsigned int*>(t.sp(q)), ord(x));
+      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
+               (uint32_t)FL_SEED << (((uint32_t)q & 3u) * 8u));
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = i0; i < se; i += FT) {
+    const int q = tab_find<GT>(t, i == i0 ? v0 : A.seed_vert[i]);
+    uint2 r = make_uint2(NO_NODE, 0u);
+    if (q >= 0) {
+      const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
+      const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
+                                    (uint32_t)FL_CLAIM << sh8);
+      if (!((old >> sh8) & FL_CLAIM)) {        // the claimer alone touches the value now
+        const float s0 = unord(*reinterpret_cast<unsigned int*>(t.sp(q)));
+        t.sc(q) = s0;
+        r = make_uint2((uint32_t)q, __float_as_uint(s0));
+        if constexpr (DBUF && !GT) const_cast<float*>(t.s0g)[q] = s0;   // read by its pullers
+      }
+    }
+    if constexpr (!(DBUF && !GT)) A.seed_rep[i] = r;
+    else (void)r;
+  }
+  if (tid == 0 && src_ok) {       // (a find of a seed is unaffected by concurrent inserts)
+    const int q = tab_insert<GT>(t, src);
+    if (q >= 0)
+      atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2), 1u << (((uint32_t)q & 3u) * 8u));
+  }
+  __syncthreads();
+  // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
+  if (src_ok) {
+    if (tid == 0) {
+      ++work.rows;
+      work.expand += ie1 - ie0;
+    }
+    for (uint32_t e = ie0 + tid; e < ie1; e += FT) {
+      const int q = tab_insert<GT>(t, e == ie0 + tid ? ic0 : A.cv[e].x);
+      if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
+    }
+  }
+  wstamp();
+  uint32_t cnt;
+  bool ovf = phase_sync(sh, cnt);
+  stamp();
+  if (ovf) return false;
+  // the seeds' neighbours are the members pulled at hop 0
+  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1);
+  wstamp();
+  ovf = phase_sync(sh, cnt);
+  stamp();
+  if (ovf) return false;
+  if constexpr (DBUF && !GT) {
+    // two slot-indexed score buffers: pull h reads t.s / t.snew alternately and writes the
+    // other one (the copy, the seed add and the excluded-label marks happen in the walk)
+    float* const sbuf[2] = {t.s, t.snew};
+    for (int h = 0; h < hops; ++h) {
+      Tab<GT> th = t;
+      th.s = sbuf[h & 1];
+      th.snew = sbuf[(h + 1) & 1];
+      row_phase<GT, PULL>(A, th, cnt, h, work, h == hops - 1 ? b : -1);
+      wstamp();
+      ovf = phase_sync(sh, cnt);
+      stamp();
+      if (ovf) return false;
+      stamp();                      // (an empty copy phase: the profile's slots keep their meaning)
+    }
+    Tab<GT> tf = t;
+    tf.s = sbuf[hops & 1];
+    return finish_column<GT>(A, tf, sh, b, cnt, work, slot);
+  }
+  for (int h = 0; h < hops; ++h) {
+    // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
+    const uint32_t n0 = cnt;
+    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
+    wstamp();
+    ovf = phase_sync(sh, cnt);
+    stamp();
+    if (ovf) return false;
+    // members not pulled at h have no non-zero neighbour and are no seed: exactly +0
+    // (pruned last pull: a non-candidate was not pulled and keeps +0; nothing reads it)
+    const uint32_t n = cnt, bit = 1u << ((uint32_t)h & 1u);
+    const bool last = h == hops - 1;
+    const bool prune_now = A.prune && last;
+    // after the last pull, a candidate carrying the excluded label is marked NEED_EXCL for
+    // top-k; its label load is issued beside the member's pull-result load
+    const bool mark_excl = last && A.exclude >= 0;
+    // this thread's first seed entry: its load is issued beside the copy's loads
+    const uint32_t ir = sb + tid;
+    const uint2 r0 = ir < se ? A.seed_rep[ir] : make_uint2(NO_NODE, 0u);
+    auto copy_one = [&](uint32_t i, uint32_t p, uint8_t nd, uint8_t f, float sn, uint8_t lab) {
+      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
+                          (!prune_now || cand_depth(f, hops));
+      t.sc(p) = pulled ? sn : 0.f;
+      uint8_t nn = nd & ~bit;
+      if (mark_excl && cand_depth(f, hops) && lab == (uint8_t)A.exclude) nn |= NEED_EXCL;
+      if (nn != nd) t.need[p] = nn;
+    };
+    if constexpr (!GT && EGR_FR_COPYU) {
+      // every member of this thread at once (n <= LLIMIT): LDS reads, then both global loads
+      // of every member in flight together, then the stores
+      uint32_t pp[MPT];
+      uint8_t nds[MPT], fls[MPT], labs[MPT];
+      float sns[MPT];
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) {
+        const uint32_t i = tid + j * FT;
+        pp[j] = i < n ? t.mlist[i] : 0xFFFFFFFFu;
+        nds[j] = 0;
+        fls[j] = 0;
+        if (pp[j] < t.cap) {
+          nds[j] = t.need[pp[j]];
+          fls[j] = t.fl[pp[j]];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MPT; ++j) {
+        const uint32_t i = tid + j * FT;
+        sns[j] = (pp[j] < t.cap && i < n0) ? t.snew[i] : 0.f;
+        labs[j] = (mark_excl && pp[j] < t.cap && cand_depth(fls[j], hops)) ? A.vlabel[t.key(pp[j])] : 0xFF;
+      }
+#pragma unroll
+      for (int j = 0; j < MPT; ++j)
+        if (pp[j] < t.cap) copy_one(tid + j * FT, pp[j], nds[j], fls[j], sns[j], labs[j]);
+    } else {
+      for (uint32_t i = tid; i < n; i += FT) {
+        const uint32_t p = t.mlist[i];
+        if (p >= t.cap) continue;
+        const uint8_t f = t.fl[p];
+        const uint8_t lab = (mark_excl && cand_depth(f, hops)) ? A.vlabel[t.key(p)] : 0xFF;
+        copy_one(i, p, t.need[p], f, i < n0 ? t.snew[i] : 0.f, lab);
+      }
+    }
+    __syncthreads();
+    if (r0.x != NO_NODE) t.sc(r0.x) = t.sc(r0.x) + __uint_as_float(r0.y);
+    for (uint32_t i = ir + FT; i < se; i += FT) {
+      const uint2 r = A.seed_rep[i];
+      if (r.x != NO_NODE) t.sc(r.x) = t.sc(r.x) + __uint_as_float(r.y);
+    }
+    __syncthreads();
+    stamp();
+  }
+  return finish_column<GT>(A, t, sh, b, cnt, work, slot);
+}
+
 // The LDS table of one workgroup (static shared memory of the kernel that declares it).
 struct LdsTab {
 #if FR_KV
@@ -981,6 +1056,9 @@ struct LdsTab {
 #if FR_LSNEW
   float snew[LLIMIT];          // pull results by member index (FR_LSNEW: in LDS, not HBM)
 #endif
+#if FR_DBUF
+  float s2[LCAP];              // the second slot-indexed score buffer (FR_DBUF)
+#endif
 };
 #if FR_KV
 #define LDS_S_PTR nullptr
@@ -989,6 +1067,8 @@ struct LdsTab {
 #endif
 #if FR_LSNEW
 #define LSNEW_PTR L.snew
+#elif FR_DBUF
+#define LSNEW_PTR L.s2
 #else
 #define LSNEW_PTR (A.lsnew + (size_t)b * LLIMIT)
 #endif
@@ -1005,6 +1085,9 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
     L.keys[tid + i * FT] = EMPTY;
     L.s[tid + i * FT] = 0.f;
 #endif
+#if FR_DBUF
+    L.s2[tid + i * FT] = 0.f;
+#endif
   }
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.flw[i] = 0;
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.needw[i] = 0;
@@ -1016,7 +1099,8 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   }
   __syncthreads();
   Tab<false> t{L.keys, LDS_S_PTR, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, &sh.chunk, SH_CHAIN};
+               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, &sh.chunk, SH_CHAIN,
+               A.lsnew + (size_t)b * LCAP};   // (FR_DBUF: seed values by slot; LCAP <= lsnew's stride)
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;

@@ -150,7 +150,7 @@ def test_frontier_global_table_reuse(mode, monkeypatch):
         monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
     if mode == "pruned_wide_retry":
         monkeypatch.setenv("EGRAPH_FRONTIER_WIDE_RETRY", "1")
-    # retry_grid_7: ~2000 members per hub column (over the narrow table's 1536, within the
+    # retry_grid_7: ~2000 members per hub column (over the narrow table's 1152, within the
     # wide 4608); otherwise ~6000 (past both LDS tables)
     leaves = 1000 if mode == "retry_grid_7" else 3000
     g, sv, sc, ss, src = _hub_world(n_leaves=leaves, n_cols=300)   # 150 hub columns
