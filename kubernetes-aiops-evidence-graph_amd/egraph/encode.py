@@ -58,14 +58,22 @@ class _RowEncoder:
         self.terminated = cat.terminated_vocab
         self.patterns = cat.pattern_vocab
         self.node_keys: dict = {}
-        self.dispatch = {
-            "kubernetes_pod": self.pod,
-            "deploy_change": self.deploy,
-            "image_change": self.image,
-            "log_signal": self.log,
-            "metric_signal": self.metric,
-            "kubernetes_node": self.node,
-        }
+        self._dispatch = None
+
+    @property
+    def dispatch(self) -> dict:
+        """evidence_type -> processor (built on first use: the native encoder needs it only
+        for the rows it hands over)"""
+        if self._dispatch is None:
+            self._dispatch = {
+                "kubernetes_pod": self.pod,
+                "deploy_change": self.deploy,
+                "image_change": self.image,
+                "log_signal": self.log,
+                "metric_signal": self.metric,
+                "kubernetes_node": self.node,
+            }
+        return self._dispatch
 
     # each returns (flags, vocab, node_key, err)
     def pod(self, data):
@@ -155,10 +163,24 @@ def _columns(evidence_lists):
             np.zeros(n, np.float64), np.zeros(len(evidence_lists) + 1, np.int64))
 
 
+def _columns_native(evidence_lists):
+    """The five columns as views of ONE uninitialised buffer: encode_rows writes every row's
+    flags / vocab / node / err and every seg_off entry (a single-incident call pays one
+    allocation instead of five)."""
+    n = sum(len(ev) for ev in evidence_lists)
+    nb = len(evidence_lists) + 1
+    buf = np.empty(8 * (n + nb) + 12 * n, np.uint8)
+    err = buf[:8 * n].view(np.float64)
+    seg = buf[8 * n:8 * (n + nb)].view(np.int64)
+    o = 8 * (n + nb)
+    return (buf[o:o + 4 * n].view(np.uint32), buf[o + 4 * n:o + 8 * n].view(np.uint32),
+            buf[o + 8 * n:o + 12 * n].view(np.uint32), err, seg)
+
+
 def encode_batch(evidence_lists: list[list[dict]], cat: Catalog) -> EncodedBatch:
     """Encode B evidence lists (one per incident) into batch columns (native row encoder)."""
     enc = _RowEncoder(cat)
-    flags, vocab, node, err, seg_off = _columns(evidence_lists)
+    flags, vocab, node, err, seg_off = _columns_native(evidence_lists)
     ids, _ = L.pyhost.encode_rows(evidence_lists, enc.waiting, enc.terminated, enc.patterns,
                                   enc.node_keys, enc.row, flags, vocab, node, err, seg_off)
     return EncodedBatch(flags, vocab, node, err, seg_off, ids)

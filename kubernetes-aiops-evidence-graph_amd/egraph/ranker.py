@@ -142,16 +142,6 @@ class FusedRanks:
             while len(self.recs) > self.capacity:
                 self.recs.popitem(last=False)
 
-    @staticmethod
-    def _fields(cat, res, i: int, slot: int) -> tuple:
-        """(confidence, category, support_count, signal_strength) the kernel emitted for a slot."""
-        if slot == cat.n_rules:
-            u = cat.unknown
-            return (u["confidence"], u["category"], u["support_count"], u["signal_strength"])
-        r = cat.rules[slot]
-        return (float(res.confidence[i, slot]), r["category"], len(r["conditions"]),
-                float(res.strength[i, slot]))
-
     def apply(self, hyps: list) -> list | None:
         """Rank `hyps` from its record if it is exactly a registered list; else None."""
         if not hyps or not isinstance(hyps[0], dict):
@@ -162,23 +152,31 @@ class FusedRanks:
             self.misses += 1
             return None
         ids, cat, res, i = rec
-        oc = res.order_conf[i]
-        slots = [int(oc[p]) for p in range(len(ids))]
+        n = len(ids)
+        # the result row as Python numbers, one conversion per array (not per element)
+        slots = res.order_conf[i, :n].tolist()
+        conf, strength = res.confidence[i].tolist(), res.strength[i].tolist()
+        R, rules, u = cat.n_rules, cat.rules, cat.unknown
         for h, hid, slot in zip(hyps, ids, slots):
             if not isinstance(h, dict) or h.get("id") != hid:
                 self.misses += 1
                 return None
-            c, catg, sup, st = self._fields(cat, res, i, slot)
+            # the (confidence, category, support_count, signal_strength) the kernel emitted
+            if slot == R:
+                c, catg, sup, st = u["confidence"], u["category"], u["support_count"], u["signal_strength"]
+            else:
+                r = rules[slot]
+                c, catg, sup, st = conf[slot], r["category"], len(r["conditions"]), strength[slot]
             if h.get("confidence", 0.5) != c or h.get("category", "unknown") != catg or \
                     h.get("support_count", 0) != sup or h.get("signal_strength", 0) != st:
                 self.misses += 1
                 return None
         self.hits += 1
+        final = res.final_score[i].tolist()
         pos = {slot: p for p, slot in enumerate(slots)}
         for h, slot in zip(hyps, slots):
-            h["final_score"] = float(res.final_score[i, slot])
-        orank = res.order_rank[i]
-        out = [hyps[pos[int(orank[q])]] for q in range(len(ids))]
+            h["final_score"] = final[slot]
+        out = [hyps[pos[s]] for s in res.order_rank[i, :n].tolist()]
         for q, h in enumerate(out):
             h["rank"] = q + 1
         return out

@@ -107,8 +107,28 @@ for name, fn in (("generate_hypotheses (one loop)", gen), ("generate + rank (one
     print(f"{name:42s} p50 {np.percentile(t, 50):8.1f}  p99 {np.percentile(t, 99):8.1f}", flush=True)
 hyps = [asyncio.run(gen(i)) for i in range(N)]
 import copy
-stat("rank via fused record", lambda i: rk.rank(copy.deepcopy(hyps[i])))
 from egraph import ranker
+
+
+def stat_pre(name, f, prep):
+    """like stat(), with an untimed per-call input built by prep(i)"""
+    t = []
+    for i in range(N):
+        x = prep(i)
+        a = time.perf_counter()
+        f(x)
+        t.append(time.perf_counter() - a)
+    t = np.array(t) * 1e6
+    print(f"{name:42s} p50 {np.percentile(t, 50):8.1f}  p99 {np.percentile(t, 99):8.1f}", flush=True)
+
+
+stat("runner small launch+spin+results", lambda i: (lambda e: ([None for _ in iter(e.query, True)], r.results()))(r.launch(encs[i])))
+r.launch(encs[0]).synchronize()
+stat("runner results() copy", lambda i: r.results())
+stat("FUSED.register (1 list)", lambda i: ranker.FUSED.register(cat, res, [hyps[i]], [0]))
+for i in range(N):                                  # re-register the generated lists
+    asyncio.run(gen(i))
+hyps = [asyncio.run(gen(i)) for i in range(N)]
+stat_pre("rank via fused record", rk.rank, lambda i: copy.deepcopy(hyps[i]))
 ranker.FUSED.recs.clear()
-stat("rank via egr_rank (zero-copy)", lambda i: rk.rank(copy.deepcopy(hyps[i])))
-stat("deepcopy only", lambda i: copy.deepcopy(hyps[i]))
+stat_pre("rank via egr_rank (zero-copy)", rk.rank, lambda i: copy.deepcopy(hyps[i]))
