@@ -289,20 +289,560 @@ static int type_of(PyObject* t) {
   return v == NULL ? T_NONE : (int)PyLong_AS_LONG(v);
 }
 
+/* One row on the calling thread (GIL held): the fast path, or the Python row encoder for a row
+ * it hands over.  `want_id`: also read the row's id (the first five rows of an incident).
+ * Leaves row->pending_node for the caller (node_keys numbering follows row order).
+ * Returns 0, or -1 with an exception set; *slow_res is a new reference to keep while *ev_id is used. */
+static int encode_row_serial(PyObject* ev, const Vocab* V, PyObject* slow_row, int want_id, Row* row,
+                             PyObject** ev_id, PyObject** slow_res, Py_ssize_t* n_slow) {
+  Row r0 = {0, 0, NO_NODE, 0.0, NULL};
+  *row = r0;
+  *ev_id = NULL;
+  *slow_res = NULL;
+  int slow = 1;
+  if (PyDict_CheckExact(ev)) {
+    PyObject *t, *data;
+    /* evidence_ids[:5] reads only the first five rows' ids (an exact dict's get of a str key
+     * cannot raise or run user code, so skipping the rest changes nothing) */
+    if (!(want_id && dget(ev, k_id, ev_id)) && !dget(ev, k_type, &t) && !dget(ev, k_data, &data)) {
+      int ty = type_of(t);
+      if (ty == T_NONE) {
+        slow = hashable_plain(t == NULL ? Py_None : t) ? 0 : 1;
+      } else if (ty > 0 && data != NULL && PyDict_CheckExact(data)) {
+        switch (ty) {
+          case T_POD: slow = enc_pod(data, V, row); break;
+          case T_DEPLOY: slow = enc_flag(data, k_recent, F_RECENT_DEPLOY, row); break;
+          case T_IMAGE: slow = enc_flag(data, k_image_changed, F_IMAGE_CHANGED, row); break;
+          case T_LOG: slow = enc_log(data, V, row); break;
+          case T_METRIC: slow = enc_metric(data, row); break;
+          case T_NODE: slow = enc_node(data, row); break;
+        }
+      } else if (ty > 0 && data == NULL) {
+        /* ev.get("data", {}) -> {}: every get misses */
+        PyObject* empty = PyDict_New();
+        if (!empty) return -1;
+        switch (ty) {
+          case T_POD: slow = enc_pod(empty, V, row); break;
+          case T_DEPLOY: slow = 0; break;
+          case T_IMAGE: slow = 0; break;
+          case T_LOG: slow = enc_log(empty, V, row); break;
+          case T_METRIC: slow = enc_metric(empty, row); break;
+          case T_NODE: slow = enc_node(empty, row); break;
+        }
+        Py_DECREF(empty);
+      }
+    }
+  }
+  if (slow) {                                /* the Python encoder: same result or raise */
+    ++*n_slow;
+    row->pending_node = NULL;
+    *slow_res = PyObject_CallOneArg(slow_row, ev);
+    if (!*slow_res) return -1;
+    unsigned int f, v, k;
+    double e;
+    PyObject* sid;
+    if (!PyArg_ParseTuple(*slow_res, "OIIId", &sid, &f, &v, &k, &e)) {
+      Py_CLEAR(*slow_res);
+      return -1;
+    }
+    *ev_id = sid;
+    row->flags = f; row->vocab = v; row->node = k; row->err = e;
+  }
+  return 0;
+}
+
+/* node_keys.setdefault(name, len(node_keys)) -> the row's node key (a name seen before is a
+ * plain lookup: no index object is built for it) */
+static int resolve_node(const Vocab* V, Row* row) {
+  if (row->pending_node == NULL) return 0;
+  PyObject* seen = PyDict_GetItemWithError(V->node_keys, row->pending_node);
+  if (seen != NULL) {
+    row->node = (uint32_t)PyLong_AsUnsignedLong(seen);
+    return 0;
+  }
+  if (PyErr_Occurred()) return -1;
+  PyObject* idx = PyLong_FromSsize_t(PyDict_GET_SIZE(V->node_keys));
+  if (!idx) return -1;
+  PyObject* k = PyDict_SetDefault(V->node_keys, row->pending_node, idx);
+  Py_DECREF(idx);
+  if (!k) return -1;
+  row->node = (uint32_t)PyLong_AsUnsignedLong(k);
+  return 0;
+}
+
+/* ---- parallel row pass ---------------------------------------------------------------------
+ * Large batches are encoded by worker threads while the calling thread keeps the GIL and waits,
+ * so no Python code runs anywhere in the process during the pass and the evidence objects cannot
+ * change.  The workers only READ objects: type checks, PyDict_Next scans (a dict "get" is a scan
+ * matching the key's characters; a dict with any key that is not an exact str is handed back),
+ * size / digit / character reads.  They never call into CPython's lookups, comparisons,
+ * truth tests or allocators, and never touch a reference count.  A row they cannot take is
+ * marked and redone, in row order, by encode_row_serial on the calling thread, which also
+ * numbers the node keys and reads the ids -- so the result is the serial encoder's, bit for bit
+ * (tests/test_pyhost.py runs both over the same rows). */
+#include <pthread.h>
+
+typedef struct {
+  const void* data;
+  Py_ssize_t len;
+  int kind;
+  uint32_t bits;
+} WVocabEntry;
+
+typedef struct {
+  WVocabEntry* e;
+  Py_ssize_t n;
+} WVocab;
+
+/* a str-keyed vocab dict as a flat table; -1 if it has a key that is not a ready exact str or a
+ * value that is not an int in [0, 2^32) */
+static int wvocab_build(PyObject* d, WVocab* out) {
+  out->n = 0;
+  out->e = PyMem_Malloc(sizeof(WVocabEntry) * (size_t)(PyDict_GET_SIZE(d) + 1));
+  if (!out->e) return -1;
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(d, &pos, &k, &v)) {
+    if (!PyUnicode_CheckExact(k) || !PyUnicode_IS_READY(k) || !PyLong_CheckExact(v)) return -1;
+    unsigned long b = PyLong_AsUnsignedLong(v);
+    if (b == (unsigned long)-1 && PyErr_Occurred()) { PyErr_Clear(); return -1; }
+    WVocabEntry* e = &out->e[out->n++];
+    e->data = PyUnicode_DATA(k);
+    e->len = PyUnicode_GET_LENGTH(k);
+    e->kind = PyUnicode_KIND(k);
+    e->bits = (uint32_t)(b & 0xFFFFFFFFu);
+  }
+  return 0;
+}
+
+/* equal characters (two ready strs: PEP 393 keeps each in its narrowest kind, so equal strings
+ * have equal kinds) */
+static inline int w_str_eq(PyObject* a, const void* bd, Py_ssize_t blen, int bkind) {
+  if (!PyUnicode_IS_READY(a)) return -1;
+  if (PyUnicode_GET_LENGTH(a) != blen || PyUnicode_KIND(a) != bkind) return 0;
+  return memcmp(PyUnicode_DATA(a), bd, (size_t)blen * (size_t)bkind) == 0;
+}
+static inline int w_eq_obj(PyObject* a, PyObject* b) {   /* b: one of our interned strs */
+  if (a == b) return 1;
+  return w_str_eq(a, PyUnicode_DATA(b), PyUnicode_GET_LENGTH(b), PyUnicode_KIND(b));
+}
+
+/* dict.get of n <= 8 keys (our interned strs, hashes cached) by one scan of an exact dict's
+ * entries with their stored hashes.  A lookup compares only the entries whose hash equals the
+ * key's, so only those are looked at: an exact ready str is matched by its characters; any
+ * other key object there -- whose __eq__ the lookup would call -- hands the row over (1). */
+static int w_get(PyObject* d, PyObject* const* keys, int n, PyObject** out) {
+  Py_hash_t kh[8];
+  for (int j = 0; j < n; ++j) {
+    out[j] = NULL;
+    kh[j] = ((PyASCIIObject*)keys[j])->hash;
+  }
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  Py_hash_t h;
+  while (_PyDict_Next(d, &pos, &k, &v, &h)) {
+    for (int j = 0; j < n; ++j) {
+      if (h != kh[j]) continue;
+      if (k != keys[j]) {
+        if (!PyUnicode_CheckExact(k)) return 1;
+        const int eq = w_eq_obj(k, keys[j]);
+        if (eq < 0) return 1;
+        if (!eq) continue;
+      }
+      out[j] = v;
+      break;
+    }
+  }
+  return 0;
+}
+
+/* truth value of a plain value, by reading it (bool / int / float / str / list / dict / None) */
+static inline int w_truthy(PyObject* o) {
+  if (o == NULL || o == Py_None) return 0;
+  if (PyBool_Check(o)) return o == Py_True;
+  if (PyLong_CheckExact(o)) return Py_SIZE(o) != 0;
+  if (PyFloat_CheckExact(o)) return PyFloat_AS_DOUBLE(o) != 0.0;
+  if (PyUnicode_CheckExact(o)) return PyUnicode_GET_LENGTH(o) != 0;
+  if (PyList_CheckExact(o)) return PyList_GET_SIZE(o) != 0;
+  if (PyDict_CheckExact(o)) return PyDict_GET_SIZE(o) != 0;
+  return -1;
+}
+static inline int w_eq_str(PyObject* o, PyObject* s) {
+  if (o == NULL || !PyUnicode_CheckExact(o)) return 0;
+  return w_eq_obj(o, s);      /* -1: not ready (hand over) */
+}
+/* plain number (int / bool / float) `op` a small int constant c: 1 / 0 (exact, as Python) */
+static inline int w_num_cmp(PyObject* o, long c, int op) {
+  if (PyFloat_CheckExact(o)) {
+    const double x = PyFloat_AS_DOUBLE(o), y = (double)c;   /* small c: exact */
+    return op == Py_GT ? x > y : x == y;
+  }
+  int ovf = 0;
+  const long long x = PyLong_AsLongLongAndOverflow(o, &ovf);   /* exact int / bool: reads digits */
+  if (ovf) return op == Py_GT ? ovf > 0 : 0;
+  return op == Py_GT ? x > c : x == c;
+}
+/* vocab bits of a key: 0 absent; -1 hand over (a key that is not an exact str) */
+static inline int64_t w_vocab_bits(const WVocab* V, PyObject* key) {
+  if (!hashable_plain(key)) return -1;
+  if (!PyUnicode_CheckExact(key) || !PyUnicode_IS_READY(key)) return -1;
+  const Py_ssize_t len = PyUnicode_GET_LENGTH(key);
+  const int kind = PyUnicode_KIND(key);
+  const void* d = PyUnicode_DATA(key);
+  for (Py_ssize_t i = 0; i < V->n; ++i)
+    if (V->e[i].len == len && V->e[i].kind == kind &&
+        memcmp(V->e[i].data, d, (size_t)len * (size_t)kind) == 0)
+      return V->e[i].bits;
+  return 0;
+}
+/* `s in q` for an ASCII constant s: 1 / 0 */
+static int w_contains(PyObject* q, PyObject* s) {
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(q), m = PyUnicode_GET_LENGTH(s);
+  const Py_UCS1* sd = PyUnicode_1BYTE_DATA(s);
+  const int kind = PyUnicode_KIND(q);
+  const void* qd = PyUnicode_DATA(q);
+  for (Py_ssize_t i = 0; i + m <= n; ++i) {
+    Py_ssize_t j = 0;
+    while (j < m && PyUnicode_READ(kind, qd, i + j) == sd[j]) ++j;
+    if (j == m) return 1;
+  }
+  return 0;
+}
+
+typedef struct {
+  WVocab waiting, terminated, patterns;
+} WVocabs;
+
+static PyObject* K_EV[2];      /* evidence_type, data */
+static PyObject* K_POD[6];     /* waiting, terminated, restart, node_name, conditions, phase */
+static PyObject* K_COND[1];    /* type */
+static PyObject* K_READY[2];   /* status, reason */
+static PyObject* K_LOG[2];     /* patterns_found, error_count */
+static PyObject* K_METRIC[3];  /* query_name, is_anomalous, current_value */
+static PyObject* K_NODE[2];    /* name, conditions */
+
+static int w_pod(PyObject* d, const WVocabs* V, Row* r) {
+  PyObject* o[6];
+  if (w_get(d, K_POD, 6, o)) return 1;
+  PyObject *wr = o[0], *tr = o[1], *rc = o[2], *nn = o[3], *conds = o[4], *ph = o[5];
+  if (!plain(wr) || !plain(tr) || !plain(nn)) return 1;
+  if (rc != NULL && !is_num(rc)) return 1;
+  const int wr_t = w_truthy(wr), tr_t = w_truthy(tr);
+  if (wr_t < 0 || tr_t < 0) return 1;
+  if (wr_t) {
+    int64_t b = w_vocab_bits(&V->waiting, wr);
+    if (b < 0) return 1;
+    r->vocab |= (uint32_t)b;
+  }
+  if (tr_t) {
+    int64_t b = w_vocab_bits(&V->terminated, tr);
+    if (b < 0) return 1;
+    r->vocab |= (uint32_t)b;
+  }
+  const int has_issue = wr_t || tr_t || (rc != NULL && w_num_cmp(rc, 0, Py_GT) == 1);
+  const int nn_t = w_truthy(nn);
+  if (nn_t < 0) return 1;
+  if (nn_t && has_issue) {
+    if (!hashable_plain(nn)) return 1;
+    r->pending_node = nn;
+  }
+  PyObject* ready = NULL;
+  if (conds != NULL) {
+    if (!PyList_CheckExact(conds)) return 1;
+    const Py_ssize_t n = PyList_GET_SIZE(conds);
+    for (Py_ssize_t i = 0; i < n && ready == NULL; ++i) {
+      PyObject* c = PyList_GET_ITEM(conds, i);
+      if (!PyDict_CheckExact(c)) return 1;
+      PyObject* t;
+      if (w_get(c, K_COND, 1, &t) || !plain(t)) return 1;
+      const int eq = w_eq_str(t, s_ready);
+      if (eq < 0) return 1;
+      if (eq) ready = c;
+    }
+  }
+  if (ready != NULL && PyDict_GET_SIZE(ready) > 0) {
+    PyObject* rr[2];
+    if (w_get(ready, K_READY, 2, rr) || !plain(rr[0])) return 1;
+    const int st_true = w_eq_str(rr[0], s_true);
+    if (st_true < 0) return 1;
+    if (!st_true) {
+      if (!plain(ph)) return 1;
+      const int running = w_eq_str(ph, s_running);
+      if (running < 0) return 1;
+      if (running) {
+        r->flags |= F_NOT_READY;
+        if (!plain(rr[1])) return 1;
+        const int cnr = w_eq_str(rr[1], s_cnr);
+        if (cnr < 0) return 1;
+        if (cnr) r->flags |= F_READINESS_FAIL;
+      }
+    }
+  }
+  return 0;
+}
+
+static int w_flag(PyObject* d, PyObject* key, uint32_t bit, Row* r) {
+  PyObject* v;
+  if (w_get(d, &key, 1, &v) || !plain(v)) return 1;
+  const int t = w_truthy(v);
+  if (t < 0) return 1;
+  if (t) r->flags |= bit;
+  return 0;
+}
+
+static int w_log(PyObject* d, const WVocabs* V, Row* r) {
+  PyObject* o[2];
+  if (w_get(d, K_LOG, 2, o)) return 1;
+  PyObject *pf = o[0], *ec = o[1];
+  if (pf != NULL) {
+    if (!PyList_CheckExact(pf)) return 1;
+    const Py_ssize_t n = PyList_GET_SIZE(pf);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      int64_t b = w_vocab_bits(&V->patterns, PyList_GET_ITEM(pf, i));
+      if (b < 0) return 1;
+      r->vocab |= (uint32_t)b;
+    }
+  }
+  if (ec == NULL) return 0;
+  if (PyFloat_CheckExact(ec)) {
+    const double e = PyFloat_AS_DOUBLE(ec);
+    if (!(isfinite(e) && floor(e) == e && fabs(e) < INT_LIMIT)) r->flags |= F_ERR_FLOAT;
+    r->err = e;
+  } else if (PyLong_CheckExact(ec) || PyBool_Check(ec)) {
+    int overflow = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(ec, &overflow);
+    if (overflow) return 1;
+    if (v >= (long long)INT_LIMIT || v <= -(long long)INT_LIMIT) r->flags |= F_ERR_FLOAT;
+    r->err = (double)v;
+  } else {
+    return 1;
+  }
+  if (r->err == 0.0) r->err = 0.0;
+  return 0;
+}
+
+static int w_metric(PyObject* d, Row* r) {
+  PyObject* o[3];
+  if (w_get(d, K_METRIC, 3, o)) return 1;
+  PyObject *q = o[0], *an = o[1], *cv = o[2];
+  if (q != NULL && (!PyUnicode_CheckExact(q) || !PyUnicode_IS_READY(q))) return 1;
+  if (!plain(an) || !plain(cv)) return 1;
+  if (q == NULL) return 0;
+  const int an_t = w_truthy(an), cv_t = w_truthy(cv);
+  if (an_t < 0 || cv_t < 0) return 1;
+  if (w_contains(q, s_memory) && an_t) {
+    if (cv != NULL && cv != Py_None) {
+      if (!is_num(cv)) {
+        if (cv_t) return 1;
+      } else if (cv_t && w_num_cmp(cv, 90, Py_GT) == 1) {
+        r->flags |= F_MEMORY_HIGH;
+      }
+    }
+  }
+  if (w_contains(q, s_hpa) && w_contains(q, s_max)) {
+    if (cv != NULL && is_num(cv) && w_num_cmp(cv, 1, Py_EQ) == 1) r->flags |= F_HPA_AT_MAX;
+  }
+  if (w_contains(q, s_latency)) {
+    if (cv != NULL) {
+      if (!is_num(cv)) return 1;
+      if (w_num_cmp(cv, 1, Py_GT) == 1) r->flags |= F_LATENCY_HIGH;
+    }
+  }
+  return 0;
+}
+
+static int w_node(PyObject* d, Row* r) {
+  PyObject* o[2];
+  PyObject *ready = NULL, *st = NULL;
+  if (w_get(d, K_NODE, 2, o)) return 1;
+  PyObject *name = o[0], *conds = o[1];
+  if (conds != NULL) {
+    if (!PyDict_CheckExact(conds)) return 1;
+    if (w_get(conds, &k_ready_key, 1, &ready)) return 1;
+    if (ready != NULL) {
+      if (!PyDict_CheckExact(ready)) return 1;
+      if (w_get(ready, K_READY, 1, &st) || !plain(st)) return 1;
+    }
+  }
+  const int st_true = w_eq_str(st, s_true);
+  if (st_true < 0) return 1;
+  if (!st_true) {
+    if (name != NULL && !hashable_plain(name)) return 1;
+    r->flags |= F_NODE_ISSUE;
+  }
+  return 0;
+}
+
+/* 0 = encoded, 1 = redo on the calling thread */
+static int w_row(PyObject* ev, const WVocabs* V, Row* row) {
+  if (!PyDict_CheckExact(ev)) return 1;
+  PyObject* o[2];
+  if (w_get(ev, K_EV, 2, o)) return 1;
+  PyObject *t = o[0], *data = o[1];
+  if (t == NULL || t == Py_None) return 0;                     /* no processor: nothing */
+  if (!PyUnicode_CheckExact(t)) return 1;
+  int ty = T_NONE;
+  for (int i = T_POD; i <= T_NODE; ++i) {
+    const int eq = w_eq_obj(t, s_type_names[i]);
+    if (eq < 0) return 1;
+    if (eq) { ty = i; break; }
+  }
+  if (ty == T_NONE) return 0;                                  /* unknown type: nothing */
+  if (data == NULL || !PyDict_CheckExact(data)) return 1;      /* (missing data: serially) */
+  switch (ty) {
+    case T_POD: return w_pod(data, V, row);
+    case T_DEPLOY: return w_flag(data, k_recent, F_RECENT_DEPLOY, row);
+    case T_IMAGE: return w_flag(data, k_image_changed, F_IMAGE_CHANGED, row);
+    case T_LOG: return w_log(data, V, row);
+    case T_METRIC: return w_metric(data, row);
+    case T_NODE: return w_node(data, row);
+  }
+  return 1;
+}
+
+typedef struct {
+  PyObject* const* lists;    /* the evidence lists (exact lists; their items are read in place) */
+  const int64_t* base;       /* first row of each incident */
+  Py_ssize_t i0, i1;         /* this worker's incidents */
+  const WVocabs* V;
+  uint32_t *flags, *vocab;
+  double* err;
+  PyObject** pend;           /* per row: the node name to number (borrowed) or NULL */
+  PyObject** ids5;           /* per incident: its first five rows' ids (borrowed; NULL = none) */
+  uint8_t* redo;             /* per row: 1 = encode on the calling thread */
+} WJob;
+
+static void* w_main(void* arg) {
+  const WJob* J = (const WJob*)arg;
+  for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
+    PyObject* evs = J->lists[i];
+    const Py_ssize_t n = PyList_GET_SIZE(evs);
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      const Py_ssize_t r = J->base[i] + j;
+      PyObject* ev = PyList_GET_ITEM(evs, j);
+      Row row = {0, 0, NO_NODE, 0.0, NULL};
+      int redo = w_row(ev, J->V, &row);
+      if (!redo && j < 5 && w_get(ev, &k_id, 1, &J->ids5[5 * i + j])) redo = 1;
+      J->redo[r] = (uint8_t)redo;
+      J->flags[r] = row.flags;
+      J->vocab[r] = row.vocab;
+      J->err[r] = row.err;
+      J->pend[r] = row.pending_node;
+    }
+  }
+  return NULL;
+}
+
+/* A persistent pool of worker threads (created on first use, up to PAR_MAX_THREADS - 1; the
+ * calling thread runs job 0): a call hands out its jobs and waits for them, instead of creating
+ * and joining threads every time.  A forked child starts without the parent's threads: the
+ * pool is rebuilt there on first use. */
+#define PAR_MAX_THREADS 64
+static struct {
+  pthread_mutex_t mu;
+  pthread_cond_t go, done;
+  int n;                          /* threads in the pool */
+  unsigned long gen;              /* incremented per call */
+  int pending;                    /* jobs not finished in this call */
+  int njobs;
+  WJob* jobs;                     /* jobs[1..njobs) for the pool threads */
+} pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, NULL};
+
+typedef struct { int id; } PoolArg;
+static PoolArg pool_args[PAR_MAX_THREADS];
+
+static void* pool_main(void* arg) {
+  const int id = ((PoolArg*)arg)->id;      /* runs job `id` of each call that has one */
+  unsigned long seen = 0;
+  pthread_mutex_lock(&pool.mu);
+  for (;;) {
+    while (pool.gen == seen) pthread_cond_wait(&pool.go, &pool.mu);
+    seen = pool.gen;
+    if (id < pool.njobs) {
+      WJob* j = &pool.jobs[id];
+      pthread_mutex_unlock(&pool.mu);
+      w_main(j);
+      pthread_mutex_lock(&pool.mu);
+      if (--pool.pending == 0) pthread_cond_signal(&pool.done);
+    }
+  }
+  return NULL;
+}
+
+static void pool_after_fork(void) {
+  pthread_mutex_init(&pool.mu, NULL);
+  pthread_cond_init(&pool.go, NULL);
+  pthread_cond_init(&pool.done, NULL);
+  pool.n = 0;
+  pool.pending = 0;
+}
+
+/* run jobs[0..n): jobs[1..) on the pool (grown as needed), jobs[0] here; returns when all are done */
+static void pool_run(WJob* jobs, int n) {
+  pthread_mutex_lock(&pool.mu);
+  while (pool.n < n - 1) {
+    pthread_t t;
+    pool_args[pool.n + 1].id = pool.n + 1;
+    if (pthread_create(&t, NULL, pool_main, &pool_args[pool.n + 1]) != 0) break;
+    pthread_detach(t);
+    ++pool.n;
+  }
+  const int m = pool.n + 1 < n ? pool.n + 1 : n;      /* jobs the pool can take */
+  pool.jobs = jobs;
+  pool.njobs = m;
+  pool.pending = m - 1;
+  ++pool.gen;
+  pthread_cond_broadcast(&pool.go);
+  pthread_mutex_unlock(&pool.mu);
+  w_main(&jobs[0]);
+  for (int t = m; t < n; ++t) w_main(&jobs[t]);       /* jobs no thread could be created for */
+  pthread_mutex_lock(&pool.mu);
+  while (pool.pending > 0) pthread_cond_wait(&pool.done, &pool.mu);
+  pool.njobs = 0;
+  pthread_mutex_unlock(&pool.mu);
+}
+
+static int intern_worker_keys(void) {
+  pthread_atfork(NULL, NULL, pool_after_fork);
+  K_EV[0] = k_type; K_EV[1] = k_data;
+  K_POD[0] = k_waiting; K_POD[1] = k_terminated; K_POD[2] = k_restart; K_POD[3] = k_node_name;
+  K_POD[4] = k_conditions; K_POD[5] = k_phase;
+  K_COND[0] = k_ctype;
+  K_READY[0] = k_status; K_READY[1] = k_reason;
+  K_LOG[0] = k_patterns; K_LOG[1] = k_error_count;
+  K_METRIC[0] = k_query; K_METRIC[1] = k_anomalous; K_METRIC[2] = k_current;
+  K_NODE[0] = k_name; K_NODE[1] = k_conditions;
+  /* w_get compares entry hashes with these keys' cached hashes */
+  PyObject* all[] = {k_type, k_data, k_waiting, k_terminated, k_restart, k_node_name, k_conditions,
+                     k_phase, k_ctype, k_status, k_reason, k_patterns, k_error_count, k_query,
+                     k_anomalous, k_current, k_name, k_ready_key, k_recent, k_image_changed};
+  for (size_t i = 0; i < sizeof(all) / sizeof(all[0]); ++i)
+    if (PyObject_Hash(all[i]) == -1) return -1;
+  return 0;
+}
+
 /* encode_rows(evidence_lists, waiting, terminated, patterns, node_keys, slow_row,
- *             flags, vocab, node, err, seg_off) -> (first-five-ids lists, rows handed over)
- * Output buffers are writable contiguous arrays sized by the caller (sum of len(evidence)). */
+ *             flags, vocab, node, err, seg_off[, threads]) -> (first-five-ids lists, rows handed over)
+ * Output buffers are writable contiguous arrays sized by the caller (sum of len(evidence)).
+ * threads > 1 and enough rows: the parallel row pass above, then the serial completion. */
+#define PAR_MIN_ROWS 4096
 static PyObject* encode_rows(PyObject* self, PyObject* args) {
   PyObject *lists, *slow_row;
   Vocab V;
+  int threads = 1;
   Py_buffer bf = {0}, bv = {0}, bn = {0}, be = {0}, bs = {0};
-  if (!PyArg_ParseTuple(args, "OO!O!O!O!Ow*w*w*w*w*", &lists, &PyDict_Type, &V.waiting,
+  if (!PyArg_ParseTuple(args, "OO!O!O!O!Ow*w*w*w*w*|i", &lists, &PyDict_Type, &V.waiting,
                         &PyDict_Type, &V.terminated, &PyDict_Type, &V.patterns, &PyDict_Type,
-                        &V.node_keys, &slow_row, &bf, &bv, &bn, &be, &bs))
+                        &V.node_keys, &slow_row, &bf, &bv, &bn, &be, &bs, &threads))
     return NULL;
   PyObject* result = NULL;
   PyObject* seq = NULL;
   PyObject* ids = NULL;
+  int64_t* base = NULL;
+  PyObject** pend = NULL;
+  PyObject** ids5 = NULL;
+  uint8_t* redo = NULL;
+  WVocabs WV = {{NULL, 0}, {NULL, 0}, {NULL, 0}};
   Py_ssize_t n_slow = 0;
   uint32_t* flags = (uint32_t*)bf.buf;
   uint32_t* vocab = (uint32_t*)bv.buf;
@@ -323,12 +863,49 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
   }
   ids = PyList_New(B);
   if (!ids) goto done;
+  /* the parallel pass: every evidence list an exact list, enough rows, the vocab tables flat */
+  int par = threads > 1;
+  Py_ssize_t total = 0;
+  for (Py_ssize_t i = 0; par && i < B; ++i) {
+    PyObject* evs = PySequence_Fast_GET_ITEM(seq, i);
+    if (!PyList_CheckExact(evs)) par = 0;
+    else total += PyList_GET_SIZE(evs);
+  }
+  if (par && (total < PAR_MIN_ROWS || total > cap)) par = 0;
+  if (par && (wvocab_build(V.waiting, &WV.waiting) || wvocab_build(V.terminated, &WV.terminated) ||
+              wvocab_build(V.patterns, &WV.patterns))) {
+    if (PyErr_Occurred()) goto done;             /* (allocation failure) */
+    par = 0;
+  }
+  if (par) {
+    base = PyMem_Malloc(sizeof(int64_t) * (size_t)(B + 1));
+    pend = PyMem_Malloc(sizeof(PyObject*) * (size_t)total);
+    ids5 = PyMem_Calloc((size_t)B * 5, sizeof(PyObject*));
+    redo = PyMem_Malloc((size_t)total);
+    if (!base || !pend || !ids5 || !redo) { PyErr_NoMemory(); goto done; }
+    base[0] = 0;
+    for (Py_ssize_t i = 0; i < B; ++i) base[i + 1] = base[i] + PyList_GET_SIZE(PySequence_Fast_GET_ITEM(seq, i));
+    if (threads > PAR_MAX_THREADS) threads = PAR_MAX_THREADS;
+    WJob jobs[PAR_MAX_THREADS];
+    /* incident ranges of about total / threads rows each */
+    Py_ssize_t i = 0;
+    for (int t = 0; t < threads; ++t) {
+      const int64_t goal = (int64_t)((total * (t + 1)) / threads);
+      const Py_ssize_t i0 = i;
+      while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
+      jobs[t] = (WJob){PySequence_Fast_ITEMS(seq), base, i0, i, &WV, flags, vocab, err, pend, ids5, redo};
+    }
+    /* (the GIL stays held: no Python code runs while the workers read) */
+    pool_run(jobs, threads);
+  }
+  /* serial pass (or the completion of the parallel one), in row order */
   Py_ssize_t r = 0;
+  int python_ran = 0;                 /* a slow row ran Python: re-read later rows serially */
   seg[0] = 0;
   for (Py_ssize_t i = 0; i < B; ++i) {
     PyObject* evs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, i), "evidence is not iterable");
     if (!evs) goto done;
-    Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
     PyObject* first = PyList_New(0);
     if (!first) { Py_DECREF(evs); goto done; }
     PyList_SET_ITEM(ids, i, first);
@@ -338,74 +915,38 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
         Py_DECREF(evs);
         goto done;
       }
-      PyObject* ev = PySequence_Fast_GET_ITEM(evs, j);
-      Row row = {0, 0, NO_NODE, 0.0, NULL};
+      const int want_id = PyList_GET_SIZE(first) < 5;
+      Row row;
       PyObject* ev_id = NULL;
-      int slow = 1;
-      if (PyDict_CheckExact(ev)) {
-        PyObject *t, *data;
-        /* evidence_ids[:5] reads only the first five rows' ids (an exact dict's get of a str
-         * key cannot raise or run user code, so skipping the rest changes nothing) */
-        const int want_id = PyList_GET_SIZE(first) < 5;
-        if (!(want_id && dget(ev, k_id, &ev_id)) && !dget(ev, k_type, &t) && !dget(ev, k_data, &data)) {
-          int ty = type_of(t);
-          if (ty == T_NONE) {
-            slow = hashable_plain(t == NULL ? Py_None : t) ? 0 : 1;
-          } else if (ty > 0 && data != NULL && PyDict_CheckExact(data)) {
-            switch (ty) {
-              case T_POD: slow = enc_pod(data, &V, &row); break;
-              case T_DEPLOY: slow = enc_flag(data, k_recent, F_RECENT_DEPLOY, &row); break;
-              case T_IMAGE: slow = enc_flag(data, k_image_changed, F_IMAGE_CHANGED, &row); break;
-              case T_LOG: slow = enc_log(data, &V, &row); break;
-              case T_METRIC: slow = enc_metric(data, &row); break;
-              case T_NODE: slow = enc_node(data, &row); break;
-            }
-          } else if (ty > 0 && data == NULL) {
-            /* ev.get("data", {}) -> {}: every get misses */
-            PyObject* empty = PyDict_New();
-            if (!empty) { Py_DECREF(evs); goto done; }
-            switch (ty) {
-              case T_POD: slow = enc_pod(empty, &V, &row); break;
-              case T_DEPLOY: slow = 0; break;
-              case T_IMAGE: slow = 0; break;
-              case T_LOG: slow = enc_log(empty, &V, &row); break;
-              case T_METRIC: slow = enc_metric(empty, &row); break;
-              case T_NODE: slow = enc_node(empty, &row); break;
-            }
-            Py_DECREF(empty);
-          }
-        }
-      }
-      if (!slow && row.pending_node != NULL) {
-        PyObject* idx = PyLong_FromSsize_t(PyDict_GET_SIZE(V.node_keys));
-        if (!idx) { Py_DECREF(evs); goto done; }
-        PyObject* k = PyDict_SetDefault(V.node_keys, row.pending_node, idx);
-        Py_DECREF(idx);
-        if (!k) { Py_DECREF(evs); goto done; }
-        row.node = (uint32_t)PyLong_AsUnsignedLong(k);
-      }
       PyObject* slow_res = NULL;
-      if (slow) {                                /* the Python encoder: same result or raise */
-        ++n_slow;
-        slow_res = PyObject_CallOneArg(slow_row, ev);
-        if (!slow_res) { Py_DECREF(evs); goto done; }
-        unsigned int f, v, k;
-        double e;
-        PyObject* sid;
-        if (!PyArg_ParseTuple(slow_res, "OIIId", &sid, &f, &v, &k, &e)) {
-          Py_DECREF(slow_res);
+      /* the worker's encoding, unless Python has run since the pass (it could have changed the
+       * evidence: from then on every row is encoded here again) */
+      if (par && !python_ran && !redo[r]) {
+        row.flags = flags[r];
+        row.vocab = vocab[r];
+        row.node = NO_NODE;
+        row.err = err[r];
+        row.pending_node = pend[r];
+        if (want_id) ev_id = ids5[5 * i + j];
+      } else {
+        const Py_ssize_t before = n_slow;
+        if (encode_row_serial(PySequence_Fast_GET_ITEM(evs, j), &V, slow_row, want_id, &row,
+                              &ev_id, &slow_res, &n_slow) < 0) {
           Py_DECREF(evs);
           goto done;
         }
-        ev_id = sid;
-        row.flags = f; row.vocab = v; row.node = k; row.err = e;
+        if (n_slow != before) python_ran = 1;
+      }
+      if (resolve_node(&V, &row) < 0) {
+        Py_XDECREF(slow_res);
+        Py_DECREF(evs);
+        goto done;
       }
       flags[r] = row.flags;
       vocab[r] = row.vocab;
       node[r] = row.node;
       err[r] = row.err;
-      if (PyList_GET_SIZE(first) < 5 &&
-          PyList_Append(first, ev_id == NULL ? Py_None : ev_id) < 0) {
+      if (want_id && PyList_Append(first, ev_id == NULL ? Py_None : ev_id) < 0) {
         Py_XDECREF(slow_res);
         Py_DECREF(evs);
         goto done;
@@ -420,6 +961,13 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
 done:
   Py_XDECREF(ids);
   Py_XDECREF(seq);
+  PyMem_Free(base);
+  PyMem_Free(pend);
+  PyMem_Free(ids5);
+  PyMem_Free(redo);
+  PyMem_Free(WV.waiting.e);
+  PyMem_Free(WV.terminated.e);
+  PyMem_Free(WV.patterns.e);
   PyBuffer_Release(&bf); PyBuffer_Release(&bv); PyBuffer_Release(&bn);
   PyBuffer_Release(&be); PyBuffer_Release(&bs);
   return result;
@@ -467,6 +1015,7 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
     return NULL;
   PyObject* out = NULL;
   PyObject* gen_by = NULL;
+  PyObject** tmpl = NULL;
   Py_ssize_t R = PyTuple_GET_SIZE(templates), S = R + 1;
   Py_ssize_t B = PyList_GET_SIZE(inc_ids);
   const uint8_t* n_hyp = (const uint8_t*)bn.buf;
@@ -495,6 +1044,47 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
   }
   gen_by = PyUnicode_InternFromString("rules_engine");
   if (!gen_by) goto done;
+  /* One template dict per slot with every key in the reference's order and the values shared
+   * by all of that slot's hypotheses; each hypothesis is a copy of it (a combined-table dict
+   * copy: one allocation, no per-key insertion or resize) with its own values then put in
+   * place -- the keys keep their positions, so the dict is the one built key by key. */
+  tmpl = PyMem_Calloc((size_t)S, sizeof(PyObject*));
+  if (!tmpl) { PyErr_NoMemory(); goto done; }
+  for (Py_ssize_t slot = 0; slot < S; ++slot) {
+    PyObject* h = tmpl[slot] = _PyDict_NewPresized(14);
+    if (!h) goto done;
+    int bad;
+    if (slot == R) {
+      PyObject* u = unknown;
+      bad = PyDict_SetItem(h, h_id, Py_None) < 0 || PyDict_SetItem(h, h_incident, Py_None) < 0 ||
+            PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(u, 0)) < 0 ||
+            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(u, 1)) < 0 ||
+            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(u, 2)) < 0 ||
+            PyDict_SetItem(h, h_confidence, PyTuple_GET_ITEM(u, 3)) < 0 ||
+            PyDict_SetItem(h, h_rank, PyTuple_GET_ITEM(u, 4)) < 0 ||
+            PyDict_SetItem(h, h_support_ids, Py_None) < 0 ||
+            PyDict_SetItem(h, h_actions, Py_None) < 0 ||
+            PyDict_SetItem(h, h_generated_by, PyTuple_GET_ITEM(u, 6)) < 0 ||
+            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(u, 7)) < 0 ||
+            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(u, 8)) < 0 ||
+            PyDict_SetItem(h, h_strength, PyTuple_GET_ITEM(u, 9)) < 0;
+    } else {
+      PyObject* t = PyTuple_GET_ITEM(templates, slot);
+      bad = PyDict_SetItem(h, h_id, Py_None) < 0 || PyDict_SetItem(h, h_incident, Py_None) < 0 ||
+            PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(t, 0)) < 0 ||
+            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(t, 1)) < 0 ||
+            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(t, 2)) < 0 ||
+            PyDict_SetItem(h, h_confidence, Py_None) < 0 ||
+            PyDict_SetItem(h, h_rank, i_zero) < 0 ||
+            PyDict_SetItem(h, h_support_ids, Py_None) < 0 ||
+            PyDict_SetItem(h, h_actions, Py_None) < 0 ||
+            PyDict_SetItem(h, h_generated_by, gen_by) < 0 ||
+            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(t, 4)) < 0 ||
+            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(t, 5)) < 0 ||
+            PyDict_SetItem(h, h_strength, Py_None) < 0;
+    }
+    if (bad || (ranked && PyDict_SetItem(h, h_final, Py_None) < 0)) goto done;
+  }
   out = PyList_New(B);
   if (!out) goto done;
   for (Py_ssize_t i = 0; i < B; ++i) {
@@ -514,37 +1104,19 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
         PyErr_SetString(PyExc_ValueError, "assemble: slot out of range or random bytes short");
         goto fail;
       }
-      PyObject* h = PyDict_New();
+      PyObject* h = PyDict_Copy(tmpl[slot]);
       if (!h) goto fail;
       PyList_SET_ITEM(lst, p, h);
       if (set_steal(h, h_id, uuid4_str(rnd + 16 * used++)) < 0) goto fail;
       if (PyDict_SetItem(h, h_incident, iid) < 0) goto fail;
+      if (set_steal(h, h_support_ids, PyList_GetSlice(eids, 0, PY_SSIZE_T_MAX)) < 0) goto fail;
       if (slot == R) {                          /* _create_unknown_hypothesis (:457-478) */
-        PyObject* u = unknown;
-        if (PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(u, 0)) < 0 ||
-            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(u, 1)) < 0 ||
-            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(u, 2)) < 0 ||
-            PyDict_SetItem(h, h_confidence, PyTuple_GET_ITEM(u, 3)) < 0 ||
-            PyDict_SetItem(h, h_rank, PyTuple_GET_ITEM(u, 4)) < 0 ||
-            set_steal(h, h_support_ids, PyList_GetSlice(eids, 0, PY_SSIZE_T_MAX)) < 0 ||
-            set_steal(h, h_actions, PyList_GetSlice(PyTuple_GET_ITEM(u, 5), 0, PY_SSIZE_T_MAX)) < 0 ||
-            PyDict_SetItem(h, h_generated_by, PyTuple_GET_ITEM(u, 6)) < 0 ||
-            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(u, 7)) < 0 ||
-            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(u, 8)) < 0 ||
-            PyDict_SetItem(h, h_strength, PyTuple_GET_ITEM(u, 9)) < 0)
+        if (set_steal(h, h_actions, PyList_GetSlice(PyTuple_GET_ITEM(unknown, 5), 0, PY_SSIZE_T_MAX)) < 0)
           goto fail;
       } else {                                  /* _create_hypothesis (:235-262) */
         PyObject* t = PyTuple_GET_ITEM(templates, slot);
-        if (PyDict_SetItem(h, h_category, PyTuple_GET_ITEM(t, 0)) < 0 ||
-            PyDict_SetItem(h, h_title, PyTuple_GET_ITEM(t, 1)) < 0 ||
-            PyDict_SetItem(h, h_description, PyTuple_GET_ITEM(t, 2)) < 0 ||
-            set_steal(h, h_confidence, PyFloat_FromDouble(conf[i * S + slot])) < 0 ||
-            PyDict_SetItem(h, h_rank, i_zero) < 0 ||
-            set_steal(h, h_support_ids, PyList_GetSlice(eids, 0, PY_SSIZE_T_MAX)) < 0 ||
+        if (set_steal(h, h_confidence, PyFloat_FromDouble(conf[i * S + slot])) < 0 ||
             set_steal(h, h_actions, PyList_GetSlice(PyTuple_GET_ITEM(t, 3), 0, PY_SSIZE_T_MAX)) < 0 ||
-            PyDict_SetItem(h, h_generated_by, gen_by) < 0 ||
-            PyDict_SetItem(h, h_rule_id, PyTuple_GET_ITEM(t, 4)) < 0 ||
-            PyDict_SetItem(h, h_support_count, PyTuple_GET_ITEM(t, 5)) < 0 ||
             set_steal(h, h_strength, PyFloat_FromDouble(strength[i * S + slot])) < 0)
           goto fail;
       }
@@ -559,6 +1131,9 @@ static PyObject* assemble(PyObject* self, PyObject* args) {
 fail:
   Py_CLEAR(out);
 done:
+  if (tmpl)
+    for (Py_ssize_t slot = 0; slot < S; ++slot) Py_XDECREF(tmpl[slot]);
+  PyMem_Free(tmpl);
   Py_XDECREF(gen_by);
   PyBuffer_Release(&bn); PyBuffer_Release(&bo); PyBuffer_Release(&bc);
   PyBuffer_Release(&bfs); PyBuffer_Release(&bst); PyBuffer_Release(&brnd);
@@ -807,6 +1382,6 @@ static PyMethodDef methods[] = {
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_egr_pyhost", NULL, -1, methods};
 
 PyMODINIT_FUNC PyInit__egr_pyhost(void) {
-  if (intern_all() < 0 || intern_seeds() < 0) return NULL;
+  if (intern_all() < 0 || intern_seeds() < 0 || intern_worker_keys() < 0) return NULL;
   return PyModule_Create(&module);
 }

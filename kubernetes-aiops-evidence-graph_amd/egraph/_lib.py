@@ -175,7 +175,9 @@ def _load_pyhost():
     import importlib.machinery
     import importlib.util
     import sysconfig
-    path = PKG_ROOT / "lib" / ("_egr_pyhost" + sysconfig.get_config_var("EXT_SUFFIX"))
+    name = "_egr_pyhost" + sysconfig.get_config_var("EXT_SUFFIX")
+    # $EGRAPH_PYHOST_DIR: an A/B build of the extension (scripts/, never set in production)
+    path = Path(os.environ.get("EGRAPH_PYHOST_DIR", PKG_ROOT / "lib")) / name
     if not path.is_file():
         raise ImportError(f"{path.name} not found in {path.parent}; build it with "
                           f"`make -C {PKG_ROOT}`")

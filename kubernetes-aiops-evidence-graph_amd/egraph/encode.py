@@ -17,6 +17,8 @@ the reference raises.  `encode_batch_py` is the all-Python encoder the tests che
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -177,12 +179,33 @@ def _columns_native(evidence_lists):
             buf[o + 8 * n:o + 12 * n].view(np.uint32), err, seg)
 
 
-def encode_batch(evidence_lists: list[list[dict]], cat: Catalog) -> EncodedBatch:
-    """Encode B evidence lists (one per incident) into batch columns (native row encoder)."""
+def encode_threads() -> int:
+    """Worker threads of the native encoder's parallel row pass ($EGRAPH_ENCODE_THREADS, else
+    this process's CPU share, capped at 16; 1 = serial).  The pass applies to batches of at
+    least 4096 rows; single incidents always encode on the calling thread."""
+    global _THREADS
+    if _THREADS is None:
+        env = os.environ.get("EGRAPH_ENCODE_THREADS")
+        if env:
+            _THREADS = max(1, int(env))
+        else:
+            share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+            _THREADS = max(1, min(16, share))
+    return _THREADS
+
+
+_THREADS = None
+
+
+def encode_batch(evidence_lists: list[list[dict]], cat: Catalog, threads: int | None = None
+                 ) -> EncodedBatch:
+    """Encode B evidence lists (one per incident) into batch columns (native row encoder;
+    `threads` workers for large batches, default encode_threads())."""
     enc = _RowEncoder(cat)
     flags, vocab, node, err, seg_off = _columns_native(evidence_lists)
     ids, _ = L.pyhost.encode_rows(evidence_lists, enc.waiting, enc.terminated, enc.patterns,
-                                  enc.node_keys, enc.row, flags, vocab, node, err, seg_off)
+                                  enc.node_keys, enc.row, flags, vocab, node, err, seg_off,
+                                  encode_threads() if threads is None else threads)
     return EncodedBatch(flags, vocab, node, err, seg_off, ids)
 
 

@@ -201,6 +201,37 @@ def test_native_encoder_edge_rows_match_python():
     assert 5 <= n_slow <= 20
 
 
+def _encode_threads(lists, threads):
+    from egraph import catalog
+    from egraph.encode import encode_batch
+    return encode_batch(lists, catalog.default(), threads=threads)
+
+
+@pytest.mark.parametrize("threads", [2, 7])
+def test_parallel_row_pass_matches_python(threads):
+    """The worker threads' read-only row pass (csrc/pyhost.c): fuzz rows, the edge rows (dict
+    subclasses, non-str keys, objects with __eq__ / __bool__, NaN, huge ints, odd types) spread
+    over a batch past the pass's 4096-row minimum, and synthetic cluster incidents -- bit for bit
+    the Python encoder, with the same node-key numbering and ids."""
+    from egraph import catalog, synth
+    from egraph.encode import encode_batch_py
+    cat = catalog.default()
+    rng = random.Random(23)
+    edge = _edge_rows()
+    lists = [evidence_fuzz.random_evidence(rng) for _ in range(400)]
+    for _ in range(300):
+        lists.append(rng.sample(edge, 5) + evidence_fuzz.random_evidence(rng, 4))
+    cl = synth.build_cluster(synth.ClusterConfig(pods=600, namespaces=4, nodes=12,
+                                                 deployments=60, services=40, seed=3))
+    lists += [c.evidence for c in synth.make_incidents(cl, 40, seed=5)]
+    lists += [[]]
+    rng.shuffle(lists)
+    a = _encode_threads(lists, threads)
+    assert a.n_rows > 4096
+    _same(a, encode_batch_py(lists, cat))
+    _same(a, _encode_threads(lists, 1))
+
+
 BAD_ROWS = [
     ({"evidence_type": "kubernetes_pod", "data": {"restart_count": None}}, TypeError),
     ({"evidence_type": "kubernetes_pod", "data": {"restart_count": "3"}}, TypeError),
@@ -225,6 +256,14 @@ BAD_ROWS = [
     ({"evidence_type": ["kubernetes_pod"]}, TypeError),
     ("not a dict", AttributeError),
 ]
+
+
+@pytest.mark.parametrize("row,exc", BAD_ROWS)
+def test_parallel_row_pass_raises_what_python_raises(row, exc):
+    good = {"id": "ok", "evidence_type": "deploy_change", "data": {"is_recent_change": True}}
+    lists = [[good] * 10 for _ in range(500)] + [[good, row, good]]
+    with pytest.raises(exc):
+        _encode_threads(lists, 4)
 
 
 @pytest.mark.parametrize("row,exc", BAD_ROWS)
