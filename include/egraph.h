@@ -343,11 +343,15 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
 typedef struct egr_frontier egr_frontier;
 
 /* Narrow (top-k-only) frontiers: give the columns that overflow the narrow LDS table (more than
- * 1536 members) a second chance in the wide LDS table (4608 members) before the global-memory
+ * 1152 members) a second chance in the wide LDS table (4608 members) before the global-memory
  * variant, on a persistent grid of `blocks` workgroups (0 = off, the default; graphs whose
  * 3-hop neighbourhoods are small never overflow and skip the launch).  Takes effect from the
  * next egr_frontier_run (capture it into a graph after setting it).                       */
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
+/* Narrow frontiers with the retry on: `on` != 0 sends EVERY column straight to the wide grid
+ * (for graphs where most columns overflow the narrow table, e.g. the dense C4: the narrow
+ * attempt would be wasted work).  Same results; takes effect from the next egr_frontier_run. */
+int egr_frontier_set_wide_first(egr_frontier* f, int32_t on);
 
 int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,
                         int64_t pool_entries, egr_frontier** out);

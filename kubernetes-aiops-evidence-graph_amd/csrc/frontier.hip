@@ -147,6 +147,7 @@ namespace fr_wide {
 #define FR_KV 0
 #define FR_HUBCHAIN 1
 #define FR_DBUF 0
+#define FR_MEDIUM 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -157,6 +158,7 @@ namespace fr_wide {
 #undef FR_KV
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_MEDIUM
 }  // namespace fr_wide
 
 namespace fr_narrow {
@@ -170,6 +172,9 @@ namespace fr_narrow {
 #ifndef EGR_FR_NARROW_LSNEW
 #define EGR_FR_NARROW_LSNEW 0
 #endif
+#ifndef EGR_FR_NARROW_MEDIUM   // rows of 5..16 entries four per wave (frontier_body.h LMAX)
+#define EGR_FR_NARROW_MEDIUM 0
+#endif
 #ifndef EGR_FR_NARROW_DBUF   // two slot-indexed score buffers, no copy phase (+2.5 %, abdb)
 #define EGR_FR_NARROW_DBUF 1
 #endif
@@ -182,6 +187,7 @@ namespace fr_narrow {
 #define FR_KV EGR_FR_NARROW_KV
 #define FR_HUBCHAIN EGR_FR_HUBCHAIN
 #define FR_DBUF EGR_FR_NARROW_DBUF
+#define FR_MEDIUM EGR_FR_NARROW_MEDIUM
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -192,6 +198,7 @@ namespace fr_narrow {
 #undef FR_KV
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_MEDIUM
 }  // namespace fr_narrow
 
 // The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
@@ -209,6 +216,7 @@ namespace fr_fallback {
 #define FR_KV 0
 #define FR_HUBCHAIN 2
 #define FR_DBUF 0
+#define FR_MEDIUM 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -219,6 +227,7 @@ namespace fr_fallback {
 #undef FR_KV
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_MEDIUM
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
@@ -426,6 +435,9 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
   bool big_geom = false;          // global variant in 256-thread workgroups (egr_frontier_set_retry)
+  bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
+                                  // wide retry grid over every column (egr_frontier_set_wide_first)
+  uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
   int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
                                   // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
   int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
@@ -518,7 +530,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
       (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 7)) ||
       (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
-      (rc = dalloc(&f->ovf, 2 * (size_t)n_cols + 4)) ||
+      (rc = dalloc(&f->ovf, 2 * (size_t)n_cols + 4)) || (rc = dalloc(&f->all_n, 1)) ||
       (rc = dalloc(&f->gkeys, gcap * f->nbig)) || (rc = dalloc(&f->gs, gcap * f->nbig)) ||
       (rc = dalloc(&f->gfl, gcap * f->nbig)) || (rc = dalloc(&f->gneed, gcap * f->nbig)) || (rc = dalloc(&f->gsnew, (size_t)V * f->nbig)) ||
       (rc = dalloc(&f->gmlist, (size_t)V * f->nbig)) ||
@@ -544,8 +556,10 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   {
     std::vector<uint32_t> id((size_t)n_cols);
     for (int i = 0; i < n_cols; ++i) id[i] = (uint32_t)i;
+    const uint32_t nb = (uint32_t)n_cols;
     if (hipMemcpy(f->ident, id.data(), (size_t)n_cols * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(f->order, id.data(), (size_t)n_cols * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(f->order, id.data(), (size_t)n_cols * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(f->all_n, &nb, 4, hipMemcpyHostToDevice) != hipSuccess) {
       egr_frontier_free(f);
       return egr::fail(EGR_EDEVICE, "egr_frontier_create: order init failed");
     }
@@ -571,6 +585,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->mem_off);
   dfree(f->mem_cnt);
   dfree(f->ovf);
+  dfree(f->all_n);
   dfree(f->gkeys);
   dfree(f->gs);
   dfree(f->gsnew);
@@ -702,11 +717,21 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
                        : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
     an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
-    hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
-    EGR_CHECK_LAUNCH();
-    if (rb > 0)
+    if (f->wide_first && rb > 0) {
+      // most columns overflow the narrow table: every column goes straight to the wide grid,
+      // in launch order (the narrow kernel, which also zeroes the seed counters, is skipped)
+      FArgs aw = a;
+      aw.retry_list = a.order;
+      aw.retry_n = f->all_n;
       hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
-                         dim3(fr_wide::FT), 0, st, a);
+                         dim3(fr_wide::FT), 0, st, aw);
+    } else {
+      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
+      EGR_CHECK_LAUNCH();
+      if (rb > 0)
+        hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
+                           dim3(fr_wide::FT), 0, st, a);
+    }
   } else {
     hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
   }
@@ -724,7 +749,13 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   EGR_CHECK_LAUNCH();
   f->ran = true;
   f->ctr_clean = false;
-  f->cnt_clean = true;
+  f->cnt_clean = !(f->narrow && f->wide_first && f->retry_blocks > 0);   // (see above)
+  return EGR_OK;
+}
+
+int egr_frontier_set_wide_first(egr_frontier* f, int32_t on) {
+  if (!f) return egr::fail(EGR_EINVAL, "egr_frontier_set_wide_first: NULL frontier");
+  f->wide_first = on != 0;
   return EGR_OK;
 }
 

@@ -13,7 +13,12 @@ constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
 constexpr uint32_t LLIMIT = FR_LLIMIT;      // members before a column overflows (load 0.75)
 constexpr int LPPT = LCAP / FT;             // slots cleared per thread
-constexpr int LMAX = 16;                    // rows up to this many entries run one lane per row
+// FR_MEDIUM: rows of up to LMAX = 4 entries run one lane per row; rows of 5..16 entries
+// ("medium") run four at a time across the wave, 16 lanes each (most rows are short: with one
+// lane per row up to 16 entries, a chunk probed 3-4 rounds of 4 keys for a median row of 2-3
+// entries); without it rows of up to 16 entries run one lane per row.
+constexpr int LMAX = FR_MEDIUM ? 4 : 16;     // rows up to this many entries run one lane per row
+constexpr int MMAX = 16;                     // FR_MEDIUM: rows up to this many entries run 4 per wave
 constexpr int LB = 4;                       // keys probed together per lane
 constexpr int BLOOM_LOG = FR_BLOOM_LOG;
 constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys in one read
@@ -21,6 +26,7 @@ constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candida
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
 constexpr bool DBUF = FR_DBUF;
+static_assert(!FR_MEDIUM || FR_HUBCHAIN >= 2, "FR_MEDIUM chains through the per-wave LDS scratch");
 static_assert(!(FR_DBUF && (FR_KV || FR_LSNEW)), "FR_DBUF replaces the member-indexed pull results");
 
 
@@ -330,6 +336,7 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
 //   EGR_FR_HUBCHAIN 0: over the present entries only, v_readlane at a ballot-chosen lane
 //   EGR_FR_HUBCHAIN 1: every entry, unrolled by 8 with immediate lane indices
 //   EGR_FR_HUBCHAIN 2: the pairs go through the wave's LDS scratch and lane m runs the chain
+//   EGR_FR_HUBCHAIN 3: as 2 over the present entries' pairs only (compacted in lane order)
 //                      from 16-B LDS reads (one lane, 4-cycle dependent fmas)
 __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32_t rem, int m,
                                           float& hacc, float2* chain) {
@@ -348,7 +355,7 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
 #pragma unroll
     for (int y = 0; y < 8; ++y) hacc = fmaf(readlane_f(xw, y0 + y), readlane_f(x, y0 + y), hacc);
   }
-#else
+#elif FR_HUBCHAIN == 2
   (void)present;
   chain[lane] = make_float2(present ? w : 0.f, x);
   __builtin_amdgcn_wave_barrier();
@@ -360,8 +367,42 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
     for (int y0 = 0; y0 < n2; y0 += 4) {
       float4 p[4];
 #pragma unroll
-      for (int y = 0; y < 4; ++y) p[y] = c4[y0 + y];     // (past n2: stale pairs of lanes >= rem,
-#pragma unroll                                           //  all (0, +0) or beyond the chain)
+      for (int y = 0; y < 4; ++y) p[y] = c4[y0 + y];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        if (y0 + y < n2) {
+          a = fmaf(p[y].x, p[y].y, a);
+          a = fmaf(p[y].z, p[y].w, a);
+        }
+      }
+    }
+    hacc = a;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#else
+  // EGR_FR_HUBCHAIN 3: the present entries' pairs are compacted into the wave's LDS scratch in
+  // lane (= CSR) order and lane m chains over those only (an absent entry's term is exact +0
+  // and skipping it changes no bit, as in light_row); a hub row with few members costs a short
+  // chain.  An odd count is padded with (0, +0).
+  (void)rem;
+  const uint64_t pm = __ballot(present);
+  const int np = __popcll(pm);
+  const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+  if (present) chain[at] = make_float2(w, x);
+  if (lane == 63 && (np & 1)) chain[np] = make_float2(0.f, 0.f);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane == m && np > 0) {
+    const float4* c4 = reinterpret_cast<const float4*>(chain);
+    const int n2 = (np + 1) / 2;
+    float a = hacc;
+    for (int y0 = 0; y0 < n2; y0 += 4) {
+      float4 p[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) p[y] = c4[y0 + y];     // (pairs past n2: read, unused)
+#pragma unroll
       for (int y = 0; y < 4; ++y) {
         if (y0 + y < n2) {
           a = fmaf(p[y].x, p[y].y, a);
@@ -514,8 +555,70 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     float acc = 0.f;
     light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
     tk.tick(1);
+#if FR_MEDIUM
+    // medium rows, four at a time: lane j takes entry j & 15 of the (j >> 4)-th row of the
+    // group; the pairs go through the wave's LDS scratch (row r at [16r, 16r + 16)) and each
+    // row's owner lane runs its fmaf chain over them (absent entries as (0, +0): exact)
+    for (uint64_t mids = __ballot(!light && deg <= (uint32_t)MMAX); mids;) {
+      int mr[4];
+      int nr = 0;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        mr[y] = mids ? __ffsll((long long)mids) - 1 : 0;
+        if (mids) {
+          mids &= mids - 1;
+          ++nr;
+        }
+      }
+      const int r = lane >> 4, xe = lane & 15;
+      uint32_t re0 = 0u, rdeg = 0u, rkind = 0u;
+      int myg = -1;                                   // this lane's group, if it owns a row
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        if (y < nr) {
+          const uint32_t ye0 = __builtin_amdgcn_readlane(e0, mr[y]);
+          const uint32_t ydeg = __builtin_amdgcn_readlane(deg, mr[y]);
+          const uint32_t ykind = __builtin_amdgcn_readlane(kind, mr[y]);
+          if (r == y) {
+            re0 = ye0;
+            rdeg = ydeg;
+            rkind = ykind;
+          }
+          if (lane == mr[y]) myg = y;
+        }
+      }
+      const bool act = r < nr && (uint32_t)xe < rdeg;
+      const uint2 ce = act ? A.cv[re0 + xe] : make_uint2(0u, 0u);
+      const int q = act ? tab_find<GT>(t, ce.x) : -1;
+      {
+        const bool pull_any = __ballot((rkind & K_PULL) != 0) != 0;
+        if (pull_any) {
+          chain[lane] = make_float2(q >= 0 ? __uint_as_float(ce.y) : 0.f, q >= 0 ? t.sc(q) : 0.f);
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          if (myg >= 0 && (kind & K_PULL)) {
+            const float4* c4 = reinterpret_cast<const float4*>(chain + 16 * myg);
+            const int n2 = (int)((deg + 1) / 2);      // (an odd row's last pair: (0, +0))
+            float a = 0.f;
+#pragma unroll
+            for (int y = 0; y < MMAX / 2; ++y) {
+              if (y < n2) {
+                const float4 pq = c4[y];
+                a = fmaf(pq.x, pq.y, a);
+                a = fmaf(pq.z, pq.w, a);
+              }
+            }
+            acc = a;
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+      }
+      if ((rkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, ce.x, q, rkind, h);
+    }
+#endif
 #if EGR_FR_HUBPF == 0
-    uint64_t heavy = __ballot(!light);
+    uint64_t heavy = __ballot(!light && (!FR_MEDIUM || deg > (uint32_t)MMAX));
     while (heavy) {
       const int m = __ffsll((long long)heavy) - 1;
       heavy &= heavy - 1;
@@ -545,7 +648,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
 #else
     // hub rows, one at a time across the wave, 64 entries per segment; the next segment's
     // (or the next hub's first segment's) entries are loaded before this one is probed
-    uint64_t heavy = __ballot(!light);
+    uint64_t heavy = __ballot(!light && (!FR_MEDIUM || deg > (uint32_t)MMAX));
     if (heavy) {
       int m = __ffsll((long long)heavy) - 1;
       heavy &= heavy - 1;
@@ -659,7 +762,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
 
 struct Shared {
   uint32_t count, ovf, item, chunk;
-#if FR_HUBCHAIN == 2
+#if FR_HUBCHAIN >= 2
   float2 chain[NWAVES][64];     // hub-row chain pairs, one row per wave
 #define SH_CHAIN (&sh.chain[0][0])
 #else

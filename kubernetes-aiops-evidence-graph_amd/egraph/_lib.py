@@ -125,6 +125,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_run": (C.c_int, [P, P, I32, I32, P, P, P]),
     "egr_frontier_stats": (C.c_int, [P, P, P]),
     "egr_frontier_set_retry": (C.c_int, [P, I32]),
+    "egr_frontier_set_wide_first": (C.c_int, [P, I32]),
     "egr_frontier_read_scores": (C.c_int, [P, P, P]),
     "egr_frontier_phase_times": (C.c_int, [P, P, I64, P]),
     "egr_frontier_read_reach": (C.c_int, [P, P, P]),

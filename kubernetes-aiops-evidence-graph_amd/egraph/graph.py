@@ -506,6 +506,7 @@ class Frontier:
         self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
         self.retry_blocks = 0
+        self.wide_first = False
         self._adapt_calls = 0
 
     def __del__(self):
@@ -543,9 +544,19 @@ class Frontier:
         L.check(L.lib.egr_frontier_set_retry(self._h, int(blocks)), "egr_frontier_set_retry")
         self.retry_blocks = int(blocks)
 
+    def set_wide_first(self, on: bool) -> None:
+        """With the retry on: every column straight to the wide table (egr_frontier_set_wide_first)."""
+        L.check(L.lib.egr_frontier_set_wide_first(self._h, int(bool(on))), "egr_frontier_set_wide_first")
+        self.wide_first = bool(on)
+
+    # a run in which more than this fraction of the columns overflowed the narrow table switches
+    # to wide-first (the narrow attempt of such columns is wasted work)
+    WIDE_FIRST_FRACTION = 0.5
+
     def adapt(self, stats: dict | None = None) -> bool:
         """After a run: turn the wide retry on if that run had overflowing columns (graphs with
-        large 3-hop neighbourhoods, e.g. the dense C4).  Returns True if it changed."""
+        large 3-hop neighbourhoods, e.g. the dense C4), and send every column straight to the
+        wide table if most of them overflowed.  Returns True if it changed."""
         if self.retry_blocks != 0 or self.pool_entries >= 0:
             return False
         self._adapt_calls += 1
@@ -554,6 +565,8 @@ class Frontier:
         st = self.stats() if stats is None else stats
         if st["overflowed"] > 0:
             self.set_retry(min(self.RETRY_BLOCKS, self.B))
+            if st["overflowed"] > self.WIDE_FIRST_FRACTION * self.B:
+                self.set_wide_first(True)
             return True
         return False
 

@@ -220,6 +220,14 @@ def test_c4_frontier_b256(c4):
         assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
         if run == 0:
             assert fr.stats()["overflowed"] > 0 and fr.adapt() and fr.retry_blocks > 0
+    # most C4 columns overflow the narrow table: adapt() chose wide-first (every column straight
+    # to the wide grid); the narrow-then-retry path and wide-first give the same top-k
+    assert fr.wide_first
+    fr.set_wide_first(False)
+    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+    ids, sco = fr.run(_dev(src), hops=3, exclude_label=g.labels().index("Incident"))
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids, err_msg="narrow + retry")
+    assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
 
 
 @pytest.mark.parametrize("P", [2, 4])
