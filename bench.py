@@ -115,7 +115,7 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
                             [(fr, rules, seeds, sources)] + [(None, enc, seeds, sources)] * (pipeline - 1))
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
-    return dict(graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
+    return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 lanes=lanes, tick=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence)
 
@@ -423,6 +423,19 @@ def _traffic(name: str):
     return None
 
 
+def _frontier_traffic(ctx, B: int):
+    """Bytes past L2 per frontier launch (profiles/pmc_frontier_calibrated.json), when this run
+    is the workload the counters were collected on; else None."""
+    pmc = REPO / "profiles" / "pmc_frontier_calibrated.json"
+    if not pmc.is_file():
+        return None
+    d = json.loads(pmc.read_text())
+    w = d.get("workload", {})
+    if w.get("config") != ctx.get("config") or w.get("batch") != B:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
 def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
     # SURVEY §8d compulsory bytes of one propagation hop: CSR (col + type) once, row_ptr,
     # scores read once and written once; gathers beyond the one compulsory read are not counted
@@ -496,12 +509,14 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
                                        "(egr_frontier_run: reach + propagation + top-k)",
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": achieved / HBM_PEAK_GBS,
-             # not HBM-bound: the 12-MB CSR stays in the Infinity Cache and the column state in
-             # LDS; FETCH_SIZE is calibrated only for 16-B coalesced streams (MI355X_MICROARCH
-             # HBM section) and counts Infinity-Cache hits, so for these 8-B gathers it is no
-             # HBM byte count (profiles/pmc_frontier.json keeps the raw counters)
-             "traffic": None, "traffic_note": "uncalibrated for 8-B gathers; Infinity-Cache "
-                                              "resident working set (DESIGN.md §4)",
+             # bytes fetched past L2 per launch from the committed counter passes at the bench
+             # workload (C3, B = 1024): TCC_EA0_RDREQ x 128 B, the request size calibrated for
+             # this kernel's 8-B gathers by scripts/calib_gather.hip, + the write requests.
+             # Infinity-Cache hits count as fetched: an upper bound on HBM bytes.
+             "traffic": _frontier_traffic(ctx, B),
+             "traffic_note": "TCC_EA0_RDREQ x 128 B (calibrated: profiles/r02_calib_gather.txt) + "
+                             "write requests, profiles/pmc_frontier_calibrated.json; counts "
+                             "Infinity-Cache hits (C3 CSR resident there): upper bound on HBM bytes",
              "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes,
              # with batches in flight, launches overlap: per batch the GPU delivers nbytes
              # in one step's wall time
