@@ -73,9 +73,36 @@ class SeedCandidates:
         flat, count, col, val = _lib.pyhost.seed_candidates(evidence_lists, _row)
         self.n_cols = len(evidence_lists)
         self.flat = flat
-        self.count = np.frombuffer(count, np.int64)
-        self.col = np.frombuffer(col, np.uint32)
-        self.val = np.frombuffer(val, np.float64).astype(np.float32)
+        # (no seeding row at all: the native call returns None for the empty buffers)
+        self.count = np.frombuffer(count or b"", np.int64)
+        self.col = np.frombuffer(col or b"", np.uint32)
+        self.val = np.frombuffer(val or b"", np.float64).astype(np.float32)
+
+    @classmethod
+    def _of(cls, n_cols: int, flat: list, count, col, val) -> "SeedCandidates":
+        o = cls.__new__(cls)
+        o.n_cols, o.flat, o.count, o.col, o.val = n_cols, flat, count, col, val
+        return o
+
+    @classmethod
+    def per_column(cls, evidence_lists: list[list[dict]]) -> list["SeedCandidates"]:
+        """One SeedCandidates per evidence list, from ONE native pass over all of them."""
+        sc = cls(evidence_lists)
+        n = sc.n_cols
+        rb = np.searchsorted(sc.col, np.arange(n + 1, dtype=np.uint32))       # rows per column
+        fb = np.concatenate([[0], np.cumsum(sc.count)])[rb]                   # flat ids per column
+        return [cls._of(1, sc.flat[fb[b]:fb[b + 1]], sc.count[rb[b]:rb[b + 1]],
+                        np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]])
+                for b in range(n)]
+
+    @classmethod
+    def combine(cls, parts: list["SeedCandidates"]) -> "SeedCandidates":
+        """The single-column candidates `parts` as the columns 0..len(parts)-1 of one batch."""
+        rows = [len(p.count) for p in parts]
+        return cls._of(len(parts), [i for p in parts for i in p.flat],
+                       np.concatenate([p.count for p in parts]) if parts else np.zeros(0, np.int64),
+                       np.repeat(np.arange(len(parts), dtype=np.uint32), rows),
+                       np.concatenate([p.val for p in parts]) if parts else np.zeros(0, np.float32))
 
     def attach(self, graph, pending: list | None = None):
         """(vertex u32, column u32, strength f32) triples: each row attaches to its first

@@ -114,25 +114,27 @@ class StormEngine:
 
     def _reseed(self, handles: list[int]) -> None:
         """(Re)attach the evidence rows of these incidents to the current graph: their
-        candidate ids are extracted once per incident (native, egraph/seeds.py) and looked up
-        in ONE graph call for all of them."""
+        candidate ids are extracted once per incident (native, egraph/seeds.py; the incidents
+        without them in ONE pass) and all of them are looked up and attached in ONE batch."""
         xs = [self.incidents[h] for h in handles]
-        for x in xs:
-            if x.cand is None:
-                x.cand = SeedCandidates([x.evidence])
-        flat = [i for x in xs for i in x.cand.flat]
-        found = self.g.lookup(flat) if flat else np.zeros(0, np.int64)
-        off = 0
-        for x in xs:
-            n = len(x.cand.flat)
-            pend: list = []
-            x.sv, _, x.ss = x.cand.attach_found(found[off:off + n], pend)
-            off += n
+        need = [x for x in xs if x.cand is None]
+        if need:
+            for x, c in zip(need, SeedCandidates.per_column([x.evidence for x in need])):
+                x.cand = c
+        if not xs:
+            return
+        cand = SeedCandidates.combine([x.cand for x in xs])
+        found = self.g.lookup(cand.flat) if cand.flat else np.zeros(0, np.int64)
+        pend: list = []
+        sv, col, ss = cand.attach_found(found, pend)
+        cut = np.searchsorted(col, np.arange(len(xs) + 1, dtype=np.uint32))
+        for j, x in enumerate(xs):
+            x.sv, x.ss = sv[cut[j]:cut[j + 1]], ss[cut[j]:cut[j + 1]]
             for pid in x.pending:
                 hs = self._pending.get(pid)
                 if hs is not None:
                     hs.discard(x.handle)
-            x.pending = pend[0]
+            x.pending = pend[j] if pend else set()
             for pid in x.pending:
                 self._pending.setdefault(pid, set()).add(x.handle)
 
@@ -172,8 +174,9 @@ class StormEngine:
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
-            for j, x in enumerate(part):
-                x.top_ids, x.top_scores = ids[j].copy(), scores[j].copy()
+            # each incident keeps row views of this launch's (fresh) host arrays
+            for x, i_row, s_row in zip(part, ids, scores):
+                x.top_ids, x.top_scores = i_row, s_row
                 x.ranked_at = self.ticks
 
     def tick(self, keys: list[str], now_ms: int, make_case: Callable[[int, int], StormCase],

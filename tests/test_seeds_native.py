@@ -135,3 +135,31 @@ def test_seed_candidates_attach_unchanged():
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x, y)
     assert p1 == p2
+
+
+def test_per_column_and_combined_attach_match_one_incident_at_a_time():
+    """The storm's batched reseed (egraph/storm.py _reseed): candidates of many incidents from
+    one native pass (SeedCandidates.per_column) and one attach over all of them (combine) give
+    each incident the seeds and pending ids of its own SeedCandidates([evidence]).attach."""
+    import numpy as np
+    from egraph import synth
+    from egraph.seeds import SeedCandidates
+    cl = synth.build_cluster(synth.ClusterConfig(pods=600, namespaces=4, nodes=12,
+                                                 deployments=60, services=40, seed=3))
+    lists = [c.evidence for c in synth.make_incidents(cl, 40, seed=5)] + [[]]
+    per = SeedCandidates.per_column(lists)
+    rng = np.random.default_rng(0)
+    singles = [SeedCandidates([ev]) for ev in lists]
+    for p, s in zip(per, singles):
+        assert p.flat == s.flat and np.array_equal(p.count, s.count)
+        assert np.array_equal(p.val, s.val) and np.array_equal(p.col, s.col)
+    found_one = [rng.integers(-1, 50, len(s.flat)) for s in singles]   # -1 = not in the graph
+    comb = SeedCandidates.combine(per)
+    pend: list = []
+    sv, col, ss = comb.attach_found(np.concatenate(found_one) if comb.flat else np.zeros(0, np.int64), pend)
+    cut = np.searchsorted(col, np.arange(len(lists) + 1, dtype=np.uint32))
+    for j, s in enumerate(singles):
+        p1: list = []
+        v1, _, s1 = s.attach_found(found_one[j], p1)
+        assert np.array_equal(sv[cut[j]:cut[j + 1]], v1) and np.array_equal(ss[cut[j]:cut[j + 1]], s1)
+        assert pend[j] == p1[0]
