@@ -128,6 +128,16 @@ struct FArgs {
 #ifndef EGR_FR_COPYU
 #define EGR_FR_COPYU 0
 #endif
+// light rows load two CSR entries per 16-B load and a row_ptr pair in one 8-B load
+#ifndef EGR_FR_PAIRLOAD        // +1-3 % at three batches in flight (profiles/r02_ab_frontier_session3.txt)
+#define EGR_FR_PAIRLOAD 1
+#endif
+// rows of up to this many entries run one lane per row (longer ones across the wave)
+#ifndef EGR_FR_LMAX
+#define EGR_FR_LMAX 12
+#endif
+struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
+struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr[v + 1]
 // narrow table slots hold (key, score) side by side: a probe returns the score (frontier_body.h)
 #ifndef EGR_FR_NARROW_KV
 #define EGR_FR_NARROW_KV 0

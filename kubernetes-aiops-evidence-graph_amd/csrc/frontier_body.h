@@ -17,7 +17,8 @@ constexpr int LPPT = LCAP / FT;             // slots cleared per thread
 // ("medium") run four at a time across the wave, 16 lanes each (most rows are short: with one
 // lane per row up to 16 entries, a chunk probed 3-4 rounds of 4 keys for a median row of 2-3
 // entries); without it rows of up to 16 entries run one lane per row.
-constexpr int LMAX = FR_MEDIUM ? 4 : 16;     // rows up to this many entries run one lane per row
+constexpr int LMAX = FR_MEDIUM ? 4 : EGR_FR_LMAX;   // rows up to this many entries run one lane per row
+static_assert(LMAX % 4 == 0 && LMAX <= 16, "light rows: whole probe batches of LB = 4");
 constexpr int MMAX = 16;                     // FR_MEDIUM: rows up to this many entries run 4 per wave
 constexpr int LB = 4;                       // keys probed together per lane
 constexpr int BLOOM_LOG = FR_BLOOM_LOG;
@@ -287,6 +288,20 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
                                           uint32_t kind, int h, float& acc, Ticker& tk) {
   uint32_t c[LMAX];
   float w[LMAX];
+#if EGR_FR_PAIRLOAD
+  // two entries per 16-B load (8-B aligned: gfx950 global loads need only dword alignment);
+  // the second entry of an odd row's last pair lies past the row -- read (the CSR arrays carry
+  // two entries of padding) but never used: the probes and the chain stop at dl
+#pragma unroll
+  for (int x = 0; x < LMAX; x += 2) {
+    Pair2 ce = {0u, 0u, 0u, 0u};
+    if ((uint32_t)x < dl) ce = *reinterpret_cast<const Pair2*>(A.cv + e0 + x);
+    c[x] = ce.c0;
+    w[x] = __uint_as_float(ce.v0);
+    c[x + 1] = ce.c1;
+    w[x + 1] = __uint_as_float(ce.v1);
+  }
+#else
 #pragma unroll
   for (int x = 0; x < LMAX; ++x) {
     uint2 ce = make_uint2(0u, 0u);
@@ -294,6 +309,7 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     c[x] = ce.x;
     w[x] = __uint_as_float(ce.y);
   }
+#endif
   tk.tick(4);
 #pragma unroll
   for (int sb = 0; sb < LMAX / LB; ++sb) {
@@ -519,8 +535,14 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     }
 #endif
     if (ch.kind) {
+#if EGR_FR_PAIRLOAD
+      const RowPair rp = *reinterpret_cast<const RowPair*>(A.row_ptr + v);   // one 8-B load
+      ch.e0 = rp.e0;
+      ch.e1 = rp.e1;
+#else
       ch.e0 = A.row_ptr[v];
       ch.e1 = A.row_ptr[v + 1];
+#endif
     }
     return ch;
   };
@@ -801,9 +823,12 @@ __device__ __forceinline__ uint64_t rescan_best(const FArgs& A, const Tab<GT>& t
 // Per-wave top-k into sh.top[wave][0..k) (k wave-wide max rounds, no block barrier).
 template <bool GT>
 __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shared& sh, uint32_t n,
-                                          uint8_t maxd) {
+                                          uint8_t maxd, int b = -1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if constexpr (!GT) {
+    // diagnostics (profiling on): per-wave time of the candidate loads and of the k rounds
+    const bool prof = A.prof && b >= 0;
+    const uint64_t tp0 = prof ? wall_clock64() : 0;
     uint64_t kk[MPT];
 #pragma unroll
     for (int j = 0; j < MPT; ++j) {
@@ -811,12 +836,17 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
       kk[j] = i < n ? cand_key<GT>(A, t, t.mlist[i], maxd) : 0ull;
     }
     auto best = [&]() {
-      uint64_t b = 0;
+      uint64_t bb = 0;
 #pragma unroll
-      for (int j = 0; j < MPT; ++j) b = kk[j] > b ? kk[j] : b;
-      return b;
+      for (int j = 0; j < MPT; ++j) bb = kk[j] > bb ? kk[j] : bb;
+      return bb;
     };
     uint64_t lb = best();
+    uint64_t tp1 = 0;
+    if (prof) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      tp1 = wall_clock64();
+    }
     for (int q = 0; q < A.k; ++q) {
       const uint64_t wb = wave_max_u64(lb);
       if (lane == 0) sh.top[wave][q] = wb;
@@ -830,6 +860,11 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
           if (kk[j] == wb) kk[j] = 0;
         lb = best();
       }
+    }
+    if (prof && lane == 0) {
+      const uint64_t tp2 = wall_clock64();
+      A.prof[((size_t)b * PROF_SLOTS + 36) * PROF_W + 1 + wave] = tp1 - tp0;
+      A.prof[((size_t)b * PROF_SLOTS + 37) * PROF_W + 1 + wave] = tp2 - tp1;
     }
   } else {
     uint64_t lb = rescan_best<GT>(A, t, n, maxd, ~0ull);
@@ -877,7 +912,7 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
   const uint32_t n = cnt;
   // top-k over the reach set: each wave its own k best, then wave 0 merges the NWAVES lists
   const int lane = tid & 63, wave = tid >> 6;
-  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1));
+  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1), b);
   wstamp();
   __syncthreads();
   if (wave == 0) {

@@ -999,7 +999,7 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
   int rc = EGR_OK;
   if ((rc = dalloc(&s->row_ptr, V + 1)) || (rc = dalloc(&s->col, 2 * E)) ||
       (rc = dalloc(&s->meta, 2 * E)) || (rc = dalloc(&s->val, 2 * E)) ||
-      (rc = dalloc(&s->cv, 2 * E)) || (rc = dalloc(&s->vlabel, V))) {
+      (rc = dalloc(&s->cv, 2 * E + 2)) || (rc = dalloc(&s->vlabel, V))) {
     egr_snapshot_free(s);
     return rc;
   }
@@ -1345,7 +1345,7 @@ int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const ui
   s->NE = NE;
   int rc = EGR_OK;
   if ((rc = dalloc(&s->row_ptr, V + 1)) || (rc = dalloc(&s->col, NE)) || (rc = dalloc(&s->meta, NE)) ||
-      (rc = dalloc(&s->val, NE)) || (rc = dalloc(&s->cv, NE)) || (rc = dalloc(&s->vlabel, V))) {
+      (rc = dalloc(&s->val, NE)) || (rc = dalloc(&s->cv, NE + 2)) || (rc = dalloc(&s->vlabel, V))) {
     egr_snapshot_free(s);
     return rc;
   }

@@ -200,7 +200,7 @@ int ensure(egr_snapshot* s, SnapUpdate* u, int64_t Vn, int64_t NEn, int64_t m2) 
     dfree(u->cv);
     u->cap_e = 0;
     if ((rc = dalloc(&u->col, c)) || (rc = dalloc(&u->meta, c)) || (rc = dalloc(&u->val, c)) ||
-        (rc = dalloc(&u->cv, c)))
+        (rc = dalloc(&u->cv, c + 2)))
       return rc;
     u->cap_e = c;
   }

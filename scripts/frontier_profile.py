@@ -76,6 +76,10 @@ def main():
               " / store / light loads / light probes / light chain / light inserts / hub loads / "
               "hub probes / hub chain / hub inserts:",
               " / ".join(f"{sub[:, k, :].mean():.2f}" for k in range(12)))
+    tk = wv[:, 36:38, :]
+    if (tk > 0).any():
+        print("top-k, per wave (us): candidate keys (LDS) %.2f / k wave-max rounds %.2f"
+              % (tk[:, 0, :].mean(), tk[:, 1, :].mean()))
     q = np.percentile(members, [50, 90, 99, 99.9, 100])
     print("members per column: mean %.0f p50 %d p90 %d p99 %d p99.9 %d max %d; > 768: %.1f %%, "
           "> 1024: %.1f %%" % (members.mean(), *q, 100 * (members > 768).mean(),
