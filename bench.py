@@ -785,8 +785,10 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 400 for the incident-sharded rank workload, whose "
+                         "step is ~0.07 ms; 20 for the storm and the edge-cut graph)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 10 / 3)")
     ap.add_argument("--config", default="C3", choices=["C2", "C3", "C4"])
     ap.add_argument("--batch", type=int, default=1024, help="incidents per GPU per step")
     ap.add_argument("--hops", type=int, default=3)
@@ -820,6 +822,11 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=20,
                     help="isolated frontier launches timed after the run for the roofline")
     args = ap.parse_args()
+    short = args.workload == "rank" and args.shard == "incidents"
+    if args.steps is None:
+        args.steps = 400 if short else 20
+    if args.warmup is None:
+        args.warmup = 10 if short else 3
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
