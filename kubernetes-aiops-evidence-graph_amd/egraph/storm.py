@@ -174,6 +174,7 @@ class StormEngine:
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
+            fr.adapt()              # overflowing columns: the wide-table retry from the next call on
             # each incident keeps row views of this launch's (fresh) host arrays
             for x, i_row, s_row in zip(part, ids, scores):
                 x.top_ids, x.top_scores = i_row, s_row
