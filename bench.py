@@ -129,15 +129,20 @@ def build_lanes(snap, B: int, max_seeds: int, k: int, pipeline: int, pool_entrie
     from egraph import catalog
     from egraph.rca import RulesDeviceBatch
     lanes = []
-    for fr, rules, seeds, sources in inputs:
+    # $EGRAPH_BENCH_LANE_STREAMS=S (A/B): the lanes share S stream pairs round-robin (lanes on
+    # one stream run their batches in order); default: a pair per lane
+    share = int(os.environ.get("EGRAPH_BENCH_LANE_STREAMS", "0") or 0)
+    pairs: list = []
+    for i, (fr, rules, seeds, sources) in enumerate(inputs):
         if fr is None:
             fr = snap.frontier(B, max_seeds=max_seeds, k=k, pool_entries=pool_entries)
         if not isinstance(rules, RulesDeviceBatch):
             rules = RulesDeviceBatch(rules, catalog.default(), dev)
-        lanes.append(dict(frontier=fr, rules=rules, seeds=seeds, sources=sources,
-                          main=torch.cuda.Stream(dev) if pipeline > 1 else None,
-                          side=(None if os.environ.get("EGRAPH_BENCH_ONE_STREAM")
-                                else torch.cuda.Stream(dev))))
+        if share <= 0 or len(pairs) < share:
+            pairs.append((torch.cuda.Stream(dev) if pipeline > 1 else None,
+                          None if os.environ.get("EGRAPH_BENCH_ONE_STREAM") else torch.cuda.Stream(dev)))
+        main, side = pairs[i % share] if share > 0 else pairs[-1]
+        lanes.append(dict(frontier=fr, rules=rules, seeds=seeds, sources=sources, main=main, side=side))
     return lanes
 
 
