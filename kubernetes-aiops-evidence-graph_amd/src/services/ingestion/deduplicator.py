@@ -14,6 +14,11 @@ Table keys: a 32-character hex fingerprint (the normalizer's output) is its own 
 other string is keyed by the first 16 bytes of its SHA-256 (computed on the GPU).  Incident id
 strings are interned into u32 handles here on the host.
 
+Memory: the table compacts itself (expired keys drop out); the host keeps one interned id
+string per incident ever registered (`_ids`, about 100 B each) until `reset()` -- a service that
+opens 100k incidents a day holds ~10 MB after a day.  Recycling the handles of expired keys
+needs a device-side remap of the table's incident column (not built).
+
 Additive batch entry point: `ingest_batch` runs the webhook loop of
 src/services/ingestion/main.py:141-170 (check -> create -> register, in payload order) for a
 whole batch in three kernels (egr_dedup_ingest).
