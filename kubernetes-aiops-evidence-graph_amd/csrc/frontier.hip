@@ -132,6 +132,10 @@ struct FArgs {
 #ifndef EGR_FR_PAIRLOAD        // +1-3 % at three batches in flight (profiles/r02_ab_frontier_session3.txt)
 #define EGR_FR_PAIRLOAD 1
 #endif
+// a lane keeps the row_ptr pairs of its first EGR_FR_ROWCACHE chunks' members across walks
+#ifndef EGR_FR_ROWCACHE
+#define EGR_FR_ROWCACHE 0
+#endif
 // rows of up to this many entries run one lane per row (longer ones across the wave)
 #ifndef EGR_FR_LMAX
 #define EGR_FR_LMAX 12

@@ -449,9 +449,22 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
 // time across the whole wave: 64 entries loaded and probed per round, the fmaf chain over the
 // present entries in lane (= CSR) order with v_readlane operands (every lane computes the
 // same chain; the owner keeps it).
+// EGR_FR_ROWCACHE: a lane's (row start, row end) of the members of its first RC chunks, kept
+// in registers from walk to walk (static striping gives a member the same wave, chunk and lane
+// in every walk of a column), so a member's row_ptr pair is loaded once per column instead of
+// once per walk.  e0 = ~0u: not loaded yet.
+constexpr int RC = (EGR_FR_ROWCACHE && EGR_FR_DYN == 0) ? EGR_FR_ROWCACHE : 0;
+struct RowCache {
+  uint32_t e0[RC > 0 ? RC : 1], e1[RC > 0 ? RC : 1];
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int j = 0; j < (RC > 0 ? RC : 1); ++j) e0[j] = ~0u, e1[j] = 0u;
+  }
+};
+
 template <bool GT, Phase PH>
 __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int h, Work& work,
-                                          int b = -1) {
+                                          int b, RowCache& rc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
   Ticker tk;
@@ -536,9 +549,29 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
 #endif
     if (ch.kind) {
 #if EGR_FR_PAIRLOAD
-      const RowPair rp = *reinterpret_cast<const RowPair*>(A.row_ptr + v);   // one 8-B load
-      ch.e0 = rp.e0;
-      ch.e1 = rp.e1;
+      bool hit = false;
+      if constexpr (!GT && RC > 0) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j)
+          if (c == (uint32_t)j && rc.e0[j] != ~0u) {
+            ch.e0 = rc.e0[j];
+            ch.e1 = rc.e1[j];
+            hit = true;
+          }
+      }
+      if (!hit) {
+        const RowPair rp = *reinterpret_cast<const RowPair*>(A.row_ptr + v);   // one 8-B load
+        ch.e0 = rp.e0;
+        ch.e1 = rp.e1;
+        if constexpr (!GT && RC > 0) {
+#pragma unroll
+          for (int j = 0; j < RC; ++j)
+            if (c == (uint32_t)j) {
+              rc.e0[j] = rp.e0;
+              rc.e1[j] = rp.e1;
+            }
+        }
+      }
 #else
       ch.e0 = A.row_ptr[v];
       ch.e1 = A.row_ptr[v + 1];
@@ -1081,7 +1114,9 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   stamp();
   if (ovf) return false;
   // the seeds' neighbours are the members pulled at hop 0
-  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1);
+  RowCache rc;
+  rc.clear();
+  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1, rc);
   wstamp();
   ovf = phase_sync(sh, cnt);
   stamp();
@@ -1094,7 +1129,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       Tab<GT> th = t;
       th.s = sbuf[h & 1];
       th.snew = sbuf[(h + 1) & 1];
-      row_phase<GT, PULL>(A, th, cnt, h, work, h == hops - 1 ? b : -1);
+      row_phase<GT, PULL>(A, th, cnt, h, work, h == hops - 1 ? b : -1, rc);
       wstamp();
       ovf = phase_sync(sh, cnt);
       stamp();
@@ -1108,7 +1143,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   for (int h = 0; h < hops; ++h) {
     // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
     const uint32_t n0 = cnt;
-    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
+    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1, rc);
     wstamp();
     ovf = phase_sync(sh, cnt);
     stamp();
