@@ -351,6 +351,65 @@ static int encode_row_serial(PyObject* ev, const Vocab* V, PyObject* slow_row, i
   return 0;
 }
 
+/* First-seen numbering of node names without the Python dict (the parallel pass's completion):
+ * an open-addressing map over (content hash, name) -> index.  Equal only for equal characters of
+ * ready exact strs -- exactly dict equality for such keys.  `materialize` writes the numbering
+ * into node_keys (index order) when the dict has to take over or at the end. */
+typedef struct {
+  uint64_t* h;
+  PyObject** key;
+  uint32_t* idx;
+  PyObject** by_idx;         /* names in index order */
+  size_t cap, n;
+} NodeMap;
+
+static int nodemap_init(NodeMap* m, size_t want) {
+  m->cap = 64;
+  while (m->cap < 2 * want + 2) m->cap *= 2;
+  m->n = 0;
+  m->h = PyMem_Calloc(m->cap, sizeof(uint64_t));
+  m->key = PyMem_Calloc(m->cap, sizeof(PyObject*));
+  m->idx = PyMem_Calloc(m->cap, sizeof(uint32_t));
+  m->by_idx = PyMem_Calloc(want + 1, sizeof(PyObject*));
+  if (!m->h || !m->key || !m->idx || !m->by_idx) { PyErr_NoMemory(); return -1; }
+  return 0;
+}
+static void nodemap_free(NodeMap* m) {
+  PyMem_Free(m->h); PyMem_Free(m->key); PyMem_Free(m->idx); PyMem_Free(m->by_idx);
+}
+static inline int same_str(PyObject* a, PyObject* b) {
+  return a == b || (PyUnicode_GET_LENGTH(a) == PyUnicode_GET_LENGTH(b) &&
+                    PyUnicode_KIND(a) == PyUnicode_KIND(b) &&
+                    memcmp(PyUnicode_DATA(a), PyUnicode_DATA(b),
+                           (size_t)PyUnicode_GET_LENGTH(a) * (size_t)PyUnicode_KIND(a)) == 0);
+}
+/* the name's index, inserting it (capacity: at most `want` distinct names, checked by caller) */
+static uint32_t nodemap_get(NodeMap* m, uint64_t h, PyObject* name) {
+  size_t i = (size_t)(h ^ (h >> 29)) & (m->cap - 1);
+  for (;;) {
+    if (m->h[i] == 0) {
+      m->h[i] = h;
+      m->key[i] = name;
+      m->idx[i] = (uint32_t)m->n;
+      m->by_idx[m->n] = name;
+      return (uint32_t)m->n++;
+    }
+    if (m->h[i] == h && same_str(m->key[i], name)) return m->idx[i];
+    i = (i + 1) & (m->cap - 1);
+  }
+}
+static int nodemap_materialize(NodeMap* m, PyObject* node_keys) {
+  for (size_t j = 0; j < m->n; ++j) {
+    PyObject* v = PyLong_FromSize_t(j);
+    if (!v) return -1;
+    const int rc = PyDict_SetItem(node_keys, m->by_idx[j], v);
+    Py_DECREF(v);
+    if (rc < 0) return -1;
+  }
+  m->n = 0;
+  return 0;
+}
+
 /* node_keys.setdefault(name, len(node_keys)) -> the row's node key (a name seen before is a
  * plain lookup: no index object is built for it) */
 static int resolve_node(const Vocab* V, Row* row) {
@@ -700,6 +759,18 @@ static int w_row(PyObject* ev, const WVocabs* V, Row* row) {
   return 1;
 }
 
+/* FNV-1a over a ready exact str's kind, length and characters (never 0); 0 for anything else.
+ * Equal strs have equal kinds (PEP 393), so equal strs hash equal. */
+static inline uint64_t w_str_hash(PyObject* o) {
+  if (!PyUnicode_CheckExact(o) || !PyUnicode_IS_READY(o)) return 0u;
+  const Py_ssize_t len = PyUnicode_GET_LENGTH(o);
+  const int kind = PyUnicode_KIND(o);
+  const unsigned char* p = (const unsigned char*)PyUnicode_DATA(o);
+  uint64_t h = 1469598103934665603ull ^ (uint64_t)kind ^ ((uint64_t)len << 8);
+  for (Py_ssize_t i = 0; i < len * kind; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h ? h : 1u;
+}
+
 typedef struct {
   PyObject* const* lists;    /* the evidence lists (exact lists; their items are read in place) */
   const int64_t* base;       /* first row of each incident */
@@ -708,6 +779,7 @@ typedef struct {
   uint32_t *flags, *vocab;
   double* err;
   PyObject** pend;           /* per row: the node name to number (borrowed) or NULL */
+  uint64_t* phash;           /* per row with a node name: its characters' hash (0: not a str) */
   PyObject** ids5;           /* per incident: its first five rows' ids (borrowed; NULL = none) */
   uint8_t* redo;             /* per row: 1 = encode on the calling thread */
 } WJob;
@@ -728,6 +800,7 @@ static void* w_main(void* arg) {
       J->vocab[r] = row.vocab;
       J->err[r] = row.err;
       J->pend[r] = row.pending_node;
+      J->phash[r] = (!redo && row.pending_node != NULL) ? w_str_hash(row.pending_node) : 0u;
     }
   }
   return NULL;
@@ -840,6 +913,9 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
   PyObject* ids = NULL;
   int64_t* base = NULL;
   PyObject** pend = NULL;
+  uint64_t* phash = NULL;
+  NodeMap nm = {NULL, NULL, NULL, NULL, 0, 0};
+  int use_map = 0;                  /* node numbering in the C map (until the dict takes over) */
   PyObject** ids5 = NULL;
   uint8_t* redo = NULL;
   WVocabs WV = {{NULL, 0}, {NULL, 0}, {NULL, 0}};
@@ -880,6 +956,8 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
   if (par) {
     base = PyMem_Malloc(sizeof(int64_t) * (size_t)(B + 1));
     pend = PyMem_Malloc(sizeof(PyObject*) * (size_t)total);
+    phash = PyMem_Malloc(sizeof(uint64_t) * (size_t)total);
+    if (!phash) { PyErr_NoMemory(); goto done; }
     ids5 = PyMem_Calloc((size_t)B * 5, sizeof(PyObject*));
     redo = PyMem_Malloc((size_t)total);
     if (!base || !pend || !ids5 || !redo) { PyErr_NoMemory(); goto done; }
@@ -893,10 +971,19 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
       const int64_t goal = (int64_t)((total * (t + 1)) / threads);
       const Py_ssize_t i0 = i;
       while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
-      jobs[t] = (WJob){PySequence_Fast_ITEMS(seq), base, i0, i, &WV, flags, vocab, err, pend, ids5, redo};
+      jobs[t] = (WJob){PySequence_Fast_ITEMS(seq), base, i0, i, &WV, flags, vocab, err, pend, phash,
+                       ids5, redo};
     }
     /* (the GIL stays held: no Python code runs while the workers read) */
     pool_run(jobs, threads);
+    /* node names are numbered in a C map keyed by the workers' content hashes while no Python
+     * code runs and node_keys starts empty (encode_batch's fresh dict) */
+    if (PyDict_GET_SIZE(V.node_keys) == 0) {
+      size_t np = 0;
+      for (Py_ssize_t q = 0; q < total; ++q) np += pend[q] != NULL && !redo[q];
+      if (nodemap_init(&nm, np) < 0) goto done;
+      use_map = 1;
+    }
   }
   /* serial pass (or the completion of the parallel one), in row order */
   Py_ssize_t r = 0;
@@ -928,7 +1015,20 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
         row.err = err[r];
         row.pending_node = pend[r];
         if (want_id) ev_id = ids5[5 * i + j];
+        if (use_map && row.pending_node != NULL) {
+          if (phash[r] != 0) {
+            row.node = nodemap_get(&nm, phash[r], row.pending_node);
+            row.pending_node = NULL;
+          } else {                       /* a name that is not a str: the dict takes over */
+            if (nodemap_materialize(&nm, V.node_keys) < 0) { Py_DECREF(evs); goto done; }
+            use_map = 0;
+          }
+        }
       } else {
+        if (use_map) {                   /* the serial encoder numbers through the dict */
+          if (nodemap_materialize(&nm, V.node_keys) < 0) { Py_DECREF(evs); goto done; }
+          use_map = 0;
+        }
         const Py_ssize_t before = n_slow;
         if (encode_row_serial(PySequence_Fast_GET_ITEM(evs, j), &V, slow_row, want_id, &row,
                               &ev_id, &slow_res, &n_slow) < 0) {
@@ -957,12 +1057,16 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
     Py_DECREF(evs);
     seg[i + 1] = r;
   }
+  if (use_map && nodemap_materialize(&nm, V.node_keys) < 0) goto done;   /* node_keys as the
+                                                                            serial pass fills it */
   result = Py_BuildValue("(On)", ids, n_slow);
 done:
   Py_XDECREF(ids);
   Py_XDECREF(seq);
   PyMem_Free(base);
   PyMem_Free(pend);
+  PyMem_Free(phash);
+  nodemap_free(&nm);
   PyMem_Free(ids5);
   PyMem_Free(redo);
   PyMem_Free(WV.waiting.e);

@@ -125,7 +125,41 @@ class RulesRunner:
     def _d(self, name) -> int:
         return self.dbuf.data_ptr() + self.off[name][0]
 
+    def input_views(self, rows: int, B: int):
+        """(flags, vocab, node, err, seg_off) arrays inside the buffer the next launch of this
+        size reads its inputs from: an encoder writing into them saves launch() the staging
+        copy (launch() recognises them and skips it)."""
+        if B == 1 and rows <= self.SMALL_ROWS:
+            # (a single small incident travels in the kernel's arguments; its outputs land
+            # where these inputs would sit, so it gets arrays of its own)
+            return (np.empty(rows, np.uint32), np.empty(rows, np.uint32), np.empty(rows, np.uint32),
+                    np.empty(rows, np.float64), np.empty(B + 1, np.int64))
+        off, _, total = self._layout(rows, B)
+        if rows <= self.ZERO_COPY_ROWS:
+            if self.mapped is None or self.mapped.nbytes < total:
+                self.mapped = MappedBuffer(max(total, 1 << 20))
+                self._small_out = None
+            h = self.mapped.np
+        else:
+            self._ensure(rows, B)
+            h = self.hbuf.numpy()
+
+        def v(name, dt, n):
+            o = off[name][0]
+            return h[o:o + n * np.dtype(dt).itemsize].view(dt)
+        return (v("flags", np.uint32, rows), v("vocab", np.uint32, rows), v("node", np.uint32, rows),
+                v("err", np.float64, rows), v("seg", np.int64, B + 1))
+
+    def _staged_in_place(self, enc: EncodedBatch, h) -> bool:
+        """The encoded columns already sit where this launch reads them (input_views)."""
+        base = h.ctypes.data
+        return all(len(a) == 0 or a.ctypes.data == base + self.off[name][0]
+                   for name, a in (("flags", enc.flags), ("vocab", enc.vocab), ("node", enc.node),
+                                   ("err", enc.err), ("seg", enc.seg_off)))
+
     def _stage_inputs(self, enc: EncodedBatch) -> None:
+        if self._staged_in_place(enc, self.hnp):
+            return
         for name, arr, dt in (("flags", enc.flags, np.uint32), ("vocab", enc.vocab, np.uint32),
                               ("node", enc.node, np.uint32), ("err", enc.err, np.float64),
                               ("seg", enc.seg_off, np.int64)):
@@ -310,7 +344,8 @@ class RulesBatcher:
         # encode: the whole batch at once; if a row raises, call by call, so that only the
         # calls whose evidence makes the reference raise get the exception
         try:
-            encs = [encode_batch([ev for c in calls for ev in c.evidence_lists], self.cat)]
+            encs = [encode_batch([ev for c in calls for ev in c.evidence_lists], self.cat,
+                                 out=self.runner.input_views)]
             ok = calls
         except Exception:
             encs, ok = [], []

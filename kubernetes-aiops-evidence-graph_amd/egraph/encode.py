@@ -197,12 +197,17 @@ def encode_threads() -> int:
 _THREADS = None
 
 
-def encode_batch(evidence_lists: list[list[dict]], cat: Catalog, threads: int | None = None
-                 ) -> EncodedBatch:
+def encode_batch(evidence_lists: list[list[dict]], cat: Catalog, threads: int | None = None,
+                 out=None) -> EncodedBatch:
     """Encode B evidence lists (one per incident) into batch columns (native row encoder;
-    `threads` workers for large batches, default encode_threads())."""
+    `threads` workers for large batches, default encode_threads()).  `out(rows, B)`, if given,
+    returns the five column arrays to write into (e.g. a launch's pinned staging buffer)."""
     enc = _RowEncoder(cat)
-    flags, vocab, node, err, seg_off = _columns_native(evidence_lists)
+    if out is not None:
+        flags, vocab, node, err, seg_off = out(sum(len(ev) for ev in evidence_lists),
+                                               len(evidence_lists))
+    else:
+        flags, vocab, node, err, seg_off = _columns_native(evidence_lists)
     ids, _ = L.pyhost.encode_rows(evidence_lists, enc.waiting, enc.terminated, enc.patterns,
                                   enc.node_keys, enc.row, flags, vocab, node, err, seg_off,
                                   encode_threads() if threads is None else threads)

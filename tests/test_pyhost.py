@@ -342,3 +342,25 @@ def test_native_assembly_matches_python_dicts(ranked):
             # fresh lists per dict: mutating one must not touch the catalog or a sibling
             assert h["recommended_actions"] is not w["recommended_actions"]
     assert len(ids) == sum(len(h) for h in got)
+
+
+@pytest.mark.parametrize("odd", ["none", "int_name", "dict_subclass"])
+def test_parallel_node_numbering_matches_python(odd):
+    """The parallel pass numbers node names in its own map while every name is a str; an int
+    name or a row the serial encoder takes hands the numbering to node_keys mid-batch -- the
+    numbering stays the Python encoder's first-seen order either way."""
+    from egraph import catalog
+    from egraph.encode import encode_batch_py
+    rng = random.Random(31)
+    pod = lambda name: {"evidence_type": "kubernetes_pod",                     # noqa: E731
+                        "data": {"restart_count": 1, "node_name": name}}
+    lists = [[pod(f"node-{rng.randrange(300)}") for _ in range(12)] for _ in range(500)]
+    if odd == "int_name":
+        lists[250][3] = pod(7)
+        lists[251][0] = pod(7.0)                     # == 7: the same dict key
+    elif odd == "dict_subclass":
+        lists[250][3] = {"evidence_type": "kubernetes_pod",
+                         "data": _Dict(restart_count=1, node_name="node-new")}
+    a = _encode_threads(lists, 4)
+    assert a.n_rows > 4096
+    _same(a, encode_batch_py(lists, catalog.default()))
