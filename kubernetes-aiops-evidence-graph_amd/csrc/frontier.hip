@@ -132,6 +132,10 @@ struct FArgs {
 #ifndef EGR_FR_PAIRLOAD        // +1-3 % at three batches in flight (profiles/r02_ab_frontier_session3.txt)
 #define EGR_FR_PAIRLOAD 1
 #endif
+// hub-row segments of 128 entries, two per lane (frontier_body.h HUBPAIR)
+#ifndef EGR_FR_HUBPAIR
+#define EGR_FR_HUBPAIR 0
+#endif
 // a lane keeps the row_ptr pairs of its first EGR_FR_ROWCACHE chunks' members across walks
 #ifndef EGR_FR_ROWCACHE
 #define EGR_FR_ROWCACHE 0

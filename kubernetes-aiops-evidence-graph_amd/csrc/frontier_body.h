@@ -27,6 +27,11 @@ constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candida
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
 constexpr bool DBUF = FR_DBUF;
+// EGR_FR_HUBPAIR: hub-row segments of 128 entries, two per lane from one 16-B load (half the
+// lanes' address lookups of the one-entry-per-lane segments); chain pairs via LDS as in
+// FR_HUBCHAIN 2, 128 per wave
+constexpr bool HUBPAIR = EGR_FR_HUBPAIR && FR_HUBCHAIN == 2 && !FR_MEDIUM;
+constexpr int CHAIN_W = HUBPAIR ? 128 : 64;         // chain scratch pairs per wave
 static_assert(!FR_MEDIUM || FR_HUBCHAIN >= 2, "FR_MEDIUM chains through the per-wave LDS scratch");
 static_assert(!(FR_DBUF && (FR_KV || FR_LSNEW)), "FR_DBUF replaces the member-indexed pull results");
 
@@ -478,7 +483,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   const bool reach_lvl = h + REACH_AHEAD + 1 <= A.hops;
   const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
   const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
-  float2* const chain = t.chain ? t.chain + wave * 64 : nullptr;
+  float2* const chain = t.chain ? t.chain + wave * CHAIN_W : nullptr;
   auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
   // Work split.  A walk is cut into chunks of 64 members; chunk c holds the members
   // c + nch * lane (nch = number of chunks), so vertices inserted together (e.g. the incident's
@@ -681,6 +686,52 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       const uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
       const uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
       float hacc = 0.f;
+      if constexpr (HUBPAIR) {
+        for (uint32_t base = 0; base < hdeg; base += 128) {
+          const uint32_t j = base + 2u * lane;
+          const bool a0 = j < hdeg, a1 = j + 1u < hdeg;
+          Pair2 ce = {0u, 0u, 0u, 0u};
+          if (a0) ce = *reinterpret_cast<const Pair2*>(A.cv + he0 + j);   // (+1 past: padding)
+          const uint32_t keys[2] = {ce.c0, ce.c1};
+          int q[2];
+          float xs[2];
+          find_batch<GT, 2>(t, keys, a1 ? 2u : (a0 ? 1u : 0u), q, xs);
+          if (hkind & K_PULL) {
+            // (w, x) of both entries in lane order = CSR order; absent entries as (0, +0)
+            reinterpret_cast<float4*>(chain)[lane] =
+                make_float4(q[0] >= 0 ? __uint_as_float(ce.v0) : 0.f, q[0] >= 0 ? t.sc(q[0]) : 0.f,
+                            q[1] >= 0 ? __uint_as_float(ce.v1) : 0.f, q[1] >= 0 ? t.sc(q[1]) : 0.f);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == m) {
+              const float4* c4 = reinterpret_cast<const float4*>(chain);
+              const int n4 = (int)((min(hdeg - base, 128u) + 1) / 2);
+              float a = hacc;
+              for (int y0 = 0; y0 < n4; y0 += 4) {
+                float4 pq[4];
+#pragma unroll
+                for (int y = 0; y < 4; ++y) pq[y] = c4[y0 + y];
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                  if (y0 + y < n4) {
+                    a = fmaf(pq[y].x, pq[y].y, a);
+                    a = fmaf(pq[y].z, pq[y].w, a);
+                  }
+                }
+              }
+              hacc = a;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          }
+          if (hkind & (K_REACH | K_PROP)) {
+            if (a0) grow_entry<GT>(t, ce.c0, q[0], hkind, h);
+            if (a1) grow_entry<GT>(t, ce.c1, q[1], hkind, h);
+          }
+        }
+        if (lane == m) acc = hacc;
+        continue;
+      }
       for (uint32_t base = 0; base < hdeg; base += 64) {
         const uint32_t j = base + lane;
         const bool act = j < hdeg;
@@ -818,7 +869,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
 struct Shared {
   uint32_t count, ovf, item, chunk;
 #if FR_HUBCHAIN >= 2
-  float2 chain[NWAVES][64];     // hub-row chain pairs, one row per wave
+  float2 chain[NWAVES][CHAIN_W];   // hub-row chain pairs, one row per wave
 #define SH_CHAIN (&sh.chain[0][0])
 #else
 #define SH_CHAIN nullptr
