@@ -88,7 +88,8 @@ struct FArgs {
   const uint32_t* retry_list;   // the retry kernel's input list, count and work counter
   const uint32_t* retry_n;
   uint32_t* retry_next;         // (unused: the retry kernel takes entry blockIdx.x)
-  float* lsnew;                 // [B][LLIMIT] pull results of the LDS variant (by member index)
+  float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
+                                // narrow (FR_DBUF): the seeds' values by slot
   // global tables (one per resident workgroup of the fallback kernel)
   uint32_t* gkeys;              // [nbig][gcap]
   float* gs;                    // [nbig][gcap]
@@ -124,7 +125,7 @@ struct FArgs {
 #ifndef EGR_FR_LBLOOM
 #define EGR_FR_LBLOOM 1
 #endif
-// the copy after a pull: 1 = a thread's members' loads issued together (unrolled over MPT)
+// the copy after a pull (single-buffer tables): 1 = a thread's members' loads issued together
 #ifndef EGR_FR_COPYU
 #define EGR_FR_COPYU 0
 #endif

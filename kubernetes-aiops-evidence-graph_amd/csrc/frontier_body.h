@@ -38,7 +38,7 @@ static_assert(!(FR_DBUF && (FR_KV || FR_LSNEW)), "FR_DBUF replaces the member-in
 
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
 // insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
-// index.
+// index (FR_DBUF: the second score buffer, by slot).
 // FR_KV: the LDS table stores slot p's key at keys[2p] and its score at keys[2p+1], so the
 // probe that finds a key (a 32-B bucket read) also returns its score; otherwise keys[p], s[p].
 template <bool GT>
