@@ -56,6 +56,7 @@ struct FArgs {
   const uint32_t* row_ptr;
   const uint2* cv;             // (col, val bits) per CSR entry
   const uint8_t* vlabel;
+  const uint32_t* xbits;       // EGR_FR_XBITS: bit v = vertex v carries the excluded label
   uint32_t V;
   int B, hops, k, exclude;
   int prune;                   // no member pool: the last hop pulls the candidates only
@@ -136,6 +137,11 @@ struct FArgs {
 // hub-row segments of 128 entries, two per lane (frontier_body.h HUBPAIR)
 #ifndef EGR_FR_HUBPAIR
 #define EGR_FR_HUBPAIR 0
+#endif
+// the last walk tests the excluded label in a V-bit map built once per (label, snapshot
+// version) instead of gathering vlabel bytes: 1/8 of the bytes, mostly L1 hits
+#ifndef EGR_FR_XBITS
+#define EGR_FR_XBITS 0
 #endif
 // a lane keeps the row_ptr pairs of its first EGR_FR_ROWCACHE chunks' members across walks
 #ifndef EGR_FR_ROWCACHE
@@ -436,6 +442,19 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
   for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[order_bin(cost[c], cmax, c, V, xcd)], 1u)] = (uint32_t)c;
 }
 
+// bit v of bits = (vlabel[v] == label), one 32-vertex word per thread
+__global__ void excl_bits_kernel(const uint8_t* __restrict__ vlabel, uint32_t V, int32_t label,
+                                 uint32_t* bits) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (V + 31u) / 32u) return;
+  uint32_t b = 0;
+  for (uint32_t j = 0; j < 32u; ++j) {
+    const uint32_t v = w * 32u + j;
+    if (v < V && (int32_t)vlabel[v] == label) b |= 1u << j;
+  }
+  bits[w] = b;
+}
+
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                     const float* __restrict__ sval, int64_t n, uint32_t V, int B,
                                     uint32_t* cursor, uint32_t* out_v, float* out_s) {
@@ -454,6 +473,10 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
   bool big_geom = false;          // global variant in 256-thread workgroups (egr_frontier_set_retry)
+  uint32_t* xbits = nullptr;      // EGR_FR_XBITS: excluded-label bit map ([vmax / 32 + 1] words)
+  int32_t xbits_label = -1;       // ... built for this label, snapshot version and V
+  uint64_t xbits_version = ~0ull;
+  int64_t xbits_V = -1;
   bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
                                   // wide retry grid over every column (egr_frontier_set_wide_first)
   uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
@@ -605,6 +628,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->mem_cnt);
   dfree(f->ovf);
   dfree(f->all_n);
+  dfree(f->xbits);
   dfree(f->gkeys);
   dfree(f->gs);
   dfree(f->gsnew);
@@ -677,7 +701,26 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   a.row_ptr = s->row_ptr;
   a.cv = s->cv;
   a.vlabel = s->vlabel;
+  a.xbits = nullptr;
   a.V = (uint32_t)s->V;
+#if EGR_FR_XBITS
+  if (f->narrow && exclude_label >= 0) {
+    if (!f->xbits) {
+      const int rc = dalloc(&f->xbits, (size_t)f->vmax / 32 + 1);
+      if (rc) return rc;
+    }
+    if (f->xbits_label != exclude_label || f->xbits_version != s->version || f->xbits_V != s->V) {
+      const uint32_t words = (uint32_t)((s->V + 31) / 32);
+      hipLaunchKernelGGL(excl_bits_kernel, dim3((words + 255) / 256), dim3(256), 0, st, s->vlabel,
+                         (uint32_t)s->V, exclude_label, f->xbits);
+      EGR_CHECK_LAUNCH();
+      f->xbits_label = exclude_label;
+      f->xbits_version = s->version;
+      f->xbits_V = s->V;
+    }
+    a.xbits = f->xbits;
+  }
+#endif
   a.B = f->B;
   a.hops = hops;
   a.k = f->k;

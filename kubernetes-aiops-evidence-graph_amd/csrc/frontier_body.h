@@ -542,7 +542,11 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
             atomicAnd(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), ~((1u << par) << ((p & 3u) * 8u)));
           ch.p = p;
           if (f & FL_SEED) ch.s0 = t.s0g[p];
+#if EGR_FR_XBITS
+          if (mark_excl && is_cand(f) && ((A.xbits[v >> 5] >> (v & 31u)) & 1u)) ch.p |= 0x1FFu << 16;
+#else
           if (mark_excl && is_cand(f)) ch.p |= (0x100u | A.vlabel[v]) << 16;   // candidate | label
+#endif
         }
       }
     }
@@ -811,7 +815,11 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         // = the copy (pulled ? acc : +0) then the seed add (+ s0): the same fadd, bit for bit
         // (s0 is +0 for a non-seed, and r + +0 == r: r is never -0)
         t.snew[p] = ((kind & K_PULL) ? acc : 0.f) + cur.s0;
+#if EGR_FR_XBITS
+        if (mark_excl && (cur.p >> 16) == 0x1FFu)    // (an excluded candidate, from the bit map)
+#else
         if (mark_excl && (cur.p >> 16) == (0x100u | (uint8_t)A.exclude))
+#endif
           atomicOr(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), (uint32_t)NEED_EXCL << ((p & 3u) * 8u));
       }
     } else if constexpr (PH == PULL) {
