@@ -114,6 +114,25 @@ class SeedCandidates:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
         return self.attach_found(graph.lookup(self.flat), pending)
 
+    def attach_found_idx(self, found: np.ndarray):
+        """attach_found's triples plus, as flat candidate indices and their columns, the
+        candidates ranked before each row's attached one (all of an unattached row's) -- the
+        ids whose creation would re-attach a row (egraph/storm.py indexes them by hash)."""
+        if not self.flat:
+            z = np.zeros(0, np.int64)
+            return (np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32), z,
+                    np.zeros(0, np.uint32))
+        found = np.asarray(found).astype(np.int64)
+        n = len(self.flat)
+        starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])
+        pos = np.where(found >= 0, np.arange(n), n)
+        first = np.minimum.reduceat(pos, starts)
+        ok = first < n
+        before = np.flatnonzero(np.arange(n) < np.repeat(np.where(ok, first, n), self.count))
+        row_of = np.repeat(np.arange(len(self.count)), self.count)
+        return (found[first[ok]].astype(np.uint32), self.col[ok], self.val[ok], before,
+                self.col[row_of[before]])
+
     def attach_found(self, found: np.ndarray, pending: list | None = None):
         """attach() with the graph lookup of self.flat already done (callers batch it)."""
         if pending is not None:

@@ -70,7 +70,6 @@ class OpenIncident:
     vertex: int = -1
     sv: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))    # seed vertices
     ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
-    pending: set = field(default_factory=set)
     cand: SeedCandidates | None = None     # its rows' attachment candidates (computed once)
     top_ids: np.ndarray | None = None      # [k] u32 vertex ids, NO_NODE padded
     top_scores: np.ndarray | None = None   # [k] f32
@@ -92,7 +91,14 @@ class StormEngine:
         self.rank, self.world = (rank, comm.P) if comm is not None else (0, 1)
         self.dedup = ShardedDedup(self.table, comm, rank) if comm is not None else None
         self.incidents: list[OpenIncident] = []
-        self._pending: dict[str, set[int]] = {}
+        # pending-id index: (hash of a candidate id ranked before a row's attached one, incident
+        # handle, generation); an entry is live while its generation is the incident's current
+        # one.  A hash match only ever adds an incident to the re-attached set (a spurious
+        # match re-attaches and re-ranks it exactly: harmless).
+        self._pend_h = np.zeros(0, np.int64)
+        self._pend_o = np.zeros(0, np.int64)
+        self._pend_g = np.zeros(0, np.int64)
+        self._gen = np.zeros(0, np.int64)
         self._frontiers: dict[int, object] = {}
         self.ticks = 0
         # (vertex, incident) pairs the affected test reads: incident vertices and seed vertices
@@ -125,18 +131,47 @@ class StormEngine:
             return
         cand = SeedCandidates.combine([x.cand for x in xs])
         found = self.g.lookup(cand.flat) if cand.flat else np.zeros(0, np.int64)
-        pend: list = []
-        sv, col, ss = cand.attach_found(found, pend)
+        sv, col, ss, before, bcol = cand.attach_found_idx(found)
         cut = np.searchsorted(col, np.arange(len(xs) + 1, dtype=np.uint32))
         for j, x in enumerate(xs):
             x.sv, x.ss = sv[cut[j]:cut[j + 1]], ss[cut[j]:cut[j + 1]]
-            for pid in x.pending:
-                hs = self._pending.get(pid)
-                if hs is not None:
-                    hs.discard(x.handle)
-            x.pending = pend[j] if pend else set()
-            for pid in x.pending:
-                self._pending.setdefault(pid, set()).add(x.handle)
+        # the incidents' pending ids: their earlier entries retire (generation bump)
+        hs = np.array([x.handle for x in xs], np.int64)
+        top = int(hs.max()) + 1
+        if top > len(self._gen):
+            self._gen = np.concatenate([self._gen, np.zeros(max(top - len(self._gen), 1024), np.int64)])
+        self._gen[hs] += 1
+        if len(before):
+            flat = cand.flat
+            h = np.fromiter((hash(flat[i]) for i in before), np.int64, len(before))
+            order = np.argsort(h, kind="stable")
+            h, oh = h[order], hs[bcol.astype(np.int64)[order]]
+            # merge into the hash-sorted index (O(entries), no re-sort of the resident part)
+            at = np.searchsorted(self._pend_h, h)
+            self._pend_h = np.insert(self._pend_h, at, h)
+            self._pend_o = np.insert(self._pend_o, at, oh)
+            self._pend_g = np.insert(self._pend_g, at, self._gen[oh])
+            if len(self._pend_h) > 4096:              # drop retired entries once they dominate
+                live = self._pend_g == self._gen[self._pend_o]
+                if live.sum() * 2 < len(live):
+                    self._pend_h, self._pend_o, self._pend_g = (
+                        self._pend_h[live], self._pend_o[live], self._pend_g[live])
+
+    def _pending_hit(self, ids: list) -> set:
+        """Incidents with a live pending entry whose hash matches one of these ids: a binary
+        search of the ids' hashes in the hash-sorted index, then the runs of equal hashes."""
+        if not ids or not len(self._pend_h):
+            return set()
+        q = np.fromiter((hash(v) for v in ids), np.int64, len(ids))
+        lo = np.searchsorted(self._pend_h, q, "left")
+        n = np.searchsorted(self._pend_h, q, "right") - lo
+        tot = int(n.sum())
+        if not tot:
+            return set()
+        ix = np.repeat(lo - (np.cumsum(n) - n), n) + np.arange(tot)
+        o = self._pend_o[ix]
+        o = o[self._pend_g[ix] == self._gen[o]]
+        return set(np.unique(o).tolist())
 
     def _check_parts(self, xs: list[OpenIncident]) -> tuple[torch.Tensor, torch.Tensor]:
         v = np.concatenate([np.array([max(x.vertex, 0) for x in xs], np.int64)] +
@@ -248,11 +283,8 @@ class StormEngine:
         new_handles = [h for h in new_handles if self.owns(h)]
         affected = set(new_handles)
         reseed = set()
-        if n_old:
-            for vid in new_ids:                          # rows that would attach differently now
-                hs = self._pending.get(vid)
-                if hs:
-                    reseed.update(hs)
+        if n_old:                                        # rows that would attach differently now
+            reseed = {h for h in self._pending_hit(new_ids) if h < n_old}
         if (n_v or n_e) and n_old and self.hops >= 1:
             s2, d2, _ = self.g.export_edges(E0, n_e)
             touched = np.unique(np.concatenate([np.arange(V0, V0 + n_v, dtype=np.int64),

@@ -163,3 +163,44 @@ def test_per_column_and_combined_attach_match_one_incident_at_a_time():
         v1, _, s1 = s.attach_found(found_one[j], p1)
         assert np.array_equal(sv[cut[j]:cut[j + 1]], v1) and np.array_equal(ss[cut[j]:cut[j + 1]], s1)
         assert pend[j] == p1[0]
+
+
+def test_attach_found_idx_matches_pending_sets():
+    """The storm's hashed pending index is fed by attach_found_idx: its (flat index, column)
+    pairs name exactly the candidate ids attach_found puts in each column's pending set."""
+    import numpy as np
+    from egraph import synth
+    from egraph.seeds import SeedCandidates
+    cl = synth.build_cluster(synth.ClusterConfig(pods=600, namespaces=4, nodes=12,
+                                                 deployments=60, services=40, seed=3))
+    lists = [c.evidence for c in synth.make_incidents(cl, 30, seed=9)]
+    sc = SeedCandidates(lists)
+    found = np.random.default_rng(1).integers(-1, 40, len(sc.flat))
+    pend: list = []
+    v1, c1, s1 = sc.attach_found(found, pend)
+    v2, c2, s2, before, bcol = sc.attach_found_idx(found)
+    assert np.array_equal(v1, v2) and np.array_equal(c1, c2) and np.array_equal(s1, s2)
+    got = [set() for _ in lists]
+    for i, c in zip(before, bcol):
+        got[int(c)].add(sc.flat[int(i)])
+    assert got == pend
+
+
+def test_storm_pending_index_lookup():
+    """StormEngine._pending_hit over a hash-sorted index with duplicate hashes and retired
+    generations (host logic only; no device)."""
+    import types
+    import numpy as np
+    from egraph.storm import StormEngine
+    rng = np.random.default_rng(4)
+    ids = [f"pod/ns/p{i}" for i in range(300)]
+    ent = [(ids[int(rng.integers(300))], int(rng.integers(40)), int(rng.integers(3))) for _ in range(2000)]
+    gen = rng.integers(0, 3, 40)
+    h = np.array([hash(e[0]) for e in ent], np.int64)
+    o = np.array([e[1] for e in ent], np.int64)
+    g = np.array([e[2] for e in ent], np.int64)
+    k = np.argsort(h, kind="stable")
+    eng = types.SimpleNamespace(_pend_h=h[k], _pend_o=o[k], _pend_g=g[k], _gen=gen)
+    for q in ([], ids[:1], ids[::7], ["absent"], ids):
+        want = {e[1] for e in ent if e[0] in set(q) and e[2] == gen[e[1]]}
+        assert StormEngine._pending_hit(eng, q) == want
