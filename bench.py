@@ -32,6 +32,7 @@ scaling).  `--partitions P` on one GPU runs P partitions in one process (device-
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -318,7 +319,6 @@ def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
             lat.append(time.perf_counter() - t0)
         return lat
 
-    import gc
     asyncio.run(single())                                          # warm
     gc.collect()               # (both single-call loops start from a collected heap)
     lat = np.array(asyncio.run(single())) * 1e6
@@ -728,7 +728,7 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
         from egraph.shard import TorchComm
         comm = TorchComm()
     eng = StormEngine(g, device=dev, hops=args.hops, k=args.k, dedup_capacity=1 << 17,
-                      comm=comm, rank=rank)
+                      comm=comm, rank=rank, keep_evidence=args.storm_keep_evidence)
     per_tick = args.storm_rate // 60
     n_tick = per_tick * world
     log(f"[rank {rank}] built {args.config} + storm: V={g.num_vertices} keys={args.storm_keys} "
@@ -736,6 +736,22 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
     now = 1_790_000_000_000
     stats = []
     mine = np.arange(rank, n_tick, world, dtype=np.int64)
+    # cyclic-GC time inside the timed part of a tick (not while the collector stand-in runs)
+    gc_t = [0.0, 0.0, False]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t[0] = time.perf_counter()
+        elif not gc_t[2]:
+            gc_t[1] += time.perf_counter() - gc_t[0]
+    gc.callbacks.append(_gc_cb)
+
+    def make_case(h, i):
+        gc_t[2] = True
+        try:
+            return wl.make_case(h, i)
+        finally:
+            gc_t[2] = False
     for i in range(args.warmup + args.steps):
         now += 1000
         keys = wl.alerts(n_tick)
@@ -746,9 +762,11 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
             import torch.distributed as dist
             dist.barrier()
         a = time.perf_counter()
-        st = eng.tick(local, now, wl.make_case, topology=topo, seq=mine if world > 1 else None)
+        gc_t[1] = 0.0
+        st = eng.tick(local, now, make_case, topology=topo, seq=mine if world > 1 else None)
         torch.cuda.synchronize(dev)
         st["wall_ms"] = (time.perf_counter() - a) * 1e3 - st["collect_ms"]
+        st["gc_ms"] = gc_t[1] * 1e3
         if world > 1:
             import torch.distributed as dist
             st["wall_ms"] = max_over_ranks(dist, st["wall_ms"], dev)
@@ -773,6 +791,7 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
                    "tick_ms_p50": float(np.percentile(wall, 50)),
                    "tick_ms_p99": float(np.percentile(wall, 99)),
                    "stage_ms_mean": stage,
+                   "gc_ms_per_tick": float(np.mean([s_["gc_ms"] for s_ in stats])),
                    "new_incidents_per_tick": float(np.mean([s_["new_incidents"] for s_ in stats])),
                    "affected_per_tick": float(np.mean([s_["affected"] for s_ in stats])),
                    "open_incidents_end": stats[-1]["open_incidents"],
@@ -821,6 +840,8 @@ def main():
     ap.add_argument("--storm-rate", type=int, default=100_000, help="alerts per minute")
     ap.add_argument("--storm-keys", type=int, default=10_000)
     ap.add_argument("--storm-events", type=int, default=100, help="topology events per tick")
+    ap.add_argument("--storm-keep-evidence", action="store_true",
+                    help="A/B: the engine keeps every incident's evidence rows (no release)")
     ap.add_argument("--no-graph", action="store_true",
                     help="frontier: enqueue each batch eagerly instead of replaying the lane's "
                          "captured HIP graph")

@@ -68,6 +68,8 @@ class EvidenceGraph:
         h = C.c_void_p()
         L.check(L.lib.egr_graph_create(C.byref(h)), "egr_graph_create")
         self._h = h
+        self._label_names: list[str] = []
+        self._type_names: list[str] = []
         self.node_props: dict[tuple[str, str], dict] = {}
         self.vertex_of: dict[tuple[str, str], int] = {}      # (label, id) -> vertex
         self.edge_props: dict[tuple[str, str, str], dict] = {}
@@ -158,20 +160,22 @@ class EvidenceGraph:
     def num_edges(self) -> int:
         return int(L.lib.egr_graph_num_edges(self._h))
 
-    def _names(self, count_fn, name_fn) -> list[str]:
-        out = []
-        for i in range(count_fn(self._h)):
+    def _names(self, cache: list, count_fn, name_fn) -> list[str]:
+        # label / type numbers are interned in creation order and never renumbered: only the
+        # names added since the last call are fetched
+        for i in range(len(cache), count_fn(self._h)):
             n = name_fn(self._h, i, None, 0)
             buf = C.create_string_buffer(max(int(n), 1))
             name_fn(self._h, i, buf, n)
-            out.append(buf.raw[:n].decode())
-        return out
+            cache.append(buf.raw[:n].decode())
+        return list(cache)
 
     def labels(self) -> list[str]:
-        return self._names(L.lib.egr_graph_num_labels, L.lib.egr_graph_label_name)
+        return self._names(self._label_names, L.lib.egr_graph_num_labels, L.lib.egr_graph_label_name)
 
     def rel_types(self) -> list[str]:
-        return self._names(L.lib.egr_graph_num_rel_types, L.lib.egr_graph_rel_type_name)
+        return self._names(self._type_names, L.lib.egr_graph_num_rel_types,
+                           L.lib.egr_graph_rel_type_name)
 
     def vertex_id(self, v: int) -> str:
         n = L.lib.egr_graph_vertex_id(self._h, v, None, 0)
@@ -203,6 +207,12 @@ class EvidenceGraph:
         L.check(L.lib.egr_graph_export(self._h, _addr(vl), _addr(es), _addr(ed), _addr(et)),
                 "egr_graph_export")
         return vl, es, ed, et
+
+    def vertex_labels(self, first: int = 0) -> np.ndarray:
+        """u8 labels of vertices [first, V) (no edge copy)."""
+        vl = np.empty(max(self.num_vertices, 1), np.uint8)
+        L.check(L.lib.egr_graph_export(self._h, _addr(vl), None, None, None), "egr_graph_export")
+        return vl[first:self.num_vertices]
 
     def export_edges(self, first: int, n: int | None = None) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Edges [first, first + n) in creation order (what MERGE batches appended since)."""
@@ -291,10 +301,10 @@ class Snapshot:
         V, E = graph.num_vertices, graph.num_edges
         if V == V0 and E == E0:
             return 0, 0
-        vl, _, _, _ = graph.export()
+        vl = graph.vertex_labels(V0)
         es, ed, et = graph.export_edges(E0, E - E0)
         with torch.cuda.device(self.dev):
-            self.update(to_device(np.ascontiguousarray(vl[V0:]), self.dev),
+            self.update(to_device(np.ascontiguousarray(vl), self.dev),
                         to_device(es.view(np.uint32), self.dev), to_device(ed.view(np.uint32), self.dev),
                         to_device(et, self.dev), graph.weight_array(self.weights), stream)
         self.synced_edges = E

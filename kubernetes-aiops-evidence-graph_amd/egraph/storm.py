@@ -66,7 +66,7 @@ class StormCase:
 class OpenIncident:
     handle: int
     incident_id: str
-    evidence: list
+    evidence: list | None     # released once its candidates are extracted (keep_evidence=False)
     vertex: int = -1
     sv: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))    # seed vertices
     ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
@@ -81,8 +81,12 @@ class StormEngine:
 
     def __init__(self, graph: EvidenceGraph, *, device=None, hops: int = 3, k: int = 10,
                  ttl_ms: int = 4 * 3600 * 1000, dedup_capacity: int = 1 << 16, weights=None,
-                 comm=None, rank: int = 0):
+                 comm=None, rank: int = 0, keep_evidence: bool = False):
         self.g = graph
+        # an incident's evidence rows are read once, to extract its attachment candidates
+        # (SeedCandidates): afterwards only the candidates are kept (and other ranks' incidents
+        # never keep them), so the open incidents hold no per-row Python objects
+        self.keep_evidence = keep_evidence
         self.snap = graph.snapshot(weights, device)
         self.dev = self.snap.dev
         self.hops, self.k, self.ttl_ms = hops, k, ttl_ms
@@ -127,6 +131,8 @@ class StormEngine:
         if need:
             for x, c in zip(need, SeedCandidates.per_column([x.evidence for x in need])):
                 x.cand = c
+                if not self.keep_evidence:
+                    x.evidence = None
         if not xs:
             return
         cand = SeedCandidates.combine([x.cand for x in xs])
@@ -247,7 +253,8 @@ class StormEngine:
             case = make_case(h, int(i))
             t_collect += time.perf_counter() - tc
             assert h == len(self.incidents), "incident handles are dense and ordered"
-            self.incidents.append(OpenIncident(h, case.incident_id, case.evidence))
+            self.incidents.append(OpenIncident(h, case.incident_id, case.evidence
+                                               if self.keep_evidence or self.owns(h) else None))
             new_handles.append(h)
             for vid, lab in case.entities:
                 ids.append(vid)

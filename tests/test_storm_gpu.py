@@ -39,7 +39,7 @@ def test_storm_ticks_match_full_recompute_and_oracle():
     g.merge_edges(c.src, c.dst, c.types)
     wl = synth.StormWorkload(c, n_keys=900, seed=5, events_per_incident=10)
     ttl_s = 20
-    eng = StormEngine(g, hops=3, k=8, ttl_ms=ttl_s * 1000, dedup_capacity=4096)
+    eng = StormEngine(g, hops=3, k=8, ttl_ms=ttl_s * 1000, dedup_capacity=4096, keep_evidence=True)
     store = AO.TTLStore()
     now = 1_000_000
     saw_partial = False
