@@ -193,9 +193,14 @@ class EvidenceGraph:
 
     def lookup(self, ids: Sequence[str]) -> np.ndarray:
         """First vertex carrying each id (-1 if none)."""
-        b, o = str_blob(ids)
-        out = np.empty(len(ids), np.int32)
-        L.check(L.lib.egr_graph_lookup(self._h, b, _addr(o), len(ids), _addr(out)), "egr_graph_lookup")
+        return self.lookup_blob(*str_blob(ids))
+
+    def lookup_blob(self, blob: bytes, off: np.ndarray) -> np.ndarray:
+        """lookup() of ids given as a utf-8 blob + int64 offsets [n+1] (str_blob's form)."""
+        off = np.ascontiguousarray(off, np.int64)
+        out = np.empty(len(off) - 1, np.int32)
+        L.check(L.lib.egr_graph_lookup(self._h, blob, _addr(off), len(out), _addr(out)),
+                "egr_graph_lookup")
         return out
 
     def export(self) -> tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:

@@ -73,36 +73,69 @@ class SeedCandidates:
         flat, count, col, val = _lib.pyhost.seed_candidates(evidence_lists, _row)
         self.n_cols = len(evidence_lists)
         self.flat = flat
+        self.keys = None
         # (no seeding row at all: the native call returns None for the empty buffers)
         self.count = np.frombuffer(count or b"", np.int64)
         self.col = np.frombuffer(col or b"", np.uint32)
         self.val = np.frombuffer(val or b"", np.float64).astype(np.float32)
 
     @classmethod
-    def _of(cls, n_cols: int, flat: list, count, col, val) -> "SeedCandidates":
+    def _of(cls, n_cols: int, flat: list | None, count, col, val, keys=None) -> "SeedCandidates":
         o = cls.__new__(cls)
         o.n_cols, o.flat, o.count, o.col, o.val = n_cols, flat, count, col, val
+        o.keys = keys
         return o
 
+    @property
+    def n_flat(self) -> int:
+        return len(self.flat) if self.flat is not None else len(self.keys[2])
+
+    def _flat_keys(self):
+        """(utf-8 blob, int64 offsets [n+1], int64 Python hashes [n]) of the flat ids: what a
+        blob graph lookup and the storm's pending index read, computed once per batch."""
+        from .graph import str_blob
+        b, o = str_blob(self.flat)
+        return b, o, np.fromiter(map(hash, self.flat), np.int64, len(self.flat))
+
     @classmethod
-    def per_column(cls, evidence_lists: list[list[dict]]) -> list["SeedCandidates"]:
-        """One SeedCandidates per evidence list, from ONE native pass over all of them."""
+    def per_column(cls, evidence_lists: list[list[dict]], keys: bool = False) -> list["SeedCandidates"]:
+        """One SeedCandidates per evidence list, from ONE native pass over all of them.  With
+        `keys`, each also carries its ids' blob / offsets / hashes (for combine(with_flat=False))
+        and drops the per-id str list."""
         sc = cls(evidence_lists)
         n = sc.n_cols
         rb = np.searchsorted(sc.col, np.arange(n + 1, dtype=np.uint32))       # rows per column
         fb = np.concatenate([[0], np.cumsum(sc.count)])[rb]                   # flat ids per column
-        return [cls._of(1, sc.flat[fb[b]:fb[b + 1]], sc.count[rb[b]:rb[b + 1]],
-                        np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]])
-                for b in range(n)]
+        if not keys:
+            return [cls._of(1, sc.flat[fb[b]:fb[b + 1]], sc.count[rb[b]:rb[b + 1]],
+                            np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]])
+                    for b in range(n)]
+        blob, off, hs = sc._flat_keys()
+        out = []
+        for b in range(n):
+            f0, f1 = fb[b], fb[b + 1]
+            k = (blob[off[f0]:off[f1]], off[f0:f1 + 1] - off[f0], hs[f0:f1])
+            out.append(cls._of(1, None, sc.count[rb[b]:rb[b + 1]],
+                               np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]], k))
+        return out
 
     @classmethod
-    def combine(cls, parts: list["SeedCandidates"]) -> "SeedCandidates":
-        """The single-column candidates `parts` as the columns 0..len(parts)-1 of one batch."""
+    def combine(cls, parts: list["SeedCandidates"], with_flat: bool = True) -> "SeedCandidates":
+        """The single-column candidates `parts` as the columns 0..len(parts)-1 of one batch.
+        with_flat=False joins the parts' keys (per_column(keys=True)) instead of their id lists."""
         rows = [len(p.count) for p in parts]
-        return cls._of(len(parts), [i for p in parts for i in p.flat],
-                       np.concatenate([p.count for p in parts]) if parts else np.zeros(0, np.int64),
-                       np.repeat(np.arange(len(parts), dtype=np.uint32), rows),
-                       np.concatenate([p.val for p in parts]) if parts else np.zeros(0, np.float32))
+        count = np.concatenate([p.count for p in parts]) if parts else np.zeros(0, np.int64)
+        col = np.repeat(np.arange(len(parts), dtype=np.uint32), rows)
+        val = np.concatenate([p.val for p in parts]) if parts else np.zeros(0, np.float32)
+        if with_flat:
+            return cls._of(len(parts), [i for p in parts for i in p.flat], count, col, val)
+        if not parts:
+            return cls._of(0, None, count, col, val, (b"", np.zeros(1, np.int64), np.zeros(0, np.int64)))
+        lens = np.array([len(p.keys[0]) for p in parts], np.int64)
+        base = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        off = np.concatenate([np.zeros(1, np.int64)] + [p.keys[1][1:] + base[j] for j, p in enumerate(parts)])
+        keys = (b"".join(p.keys[0] for p in parts), off, np.concatenate([p.keys[2] for p in parts]))
+        return cls._of(len(parts), None, count, col, val, keys)
 
     def attach(self, graph, pending: list | None = None):
         """(vertex u32, column u32, strength f32) triples: each row attaches to its first
@@ -110,20 +143,22 @@ class SeedCandidates:
         candidate ids ranked before the attached one (all, for an unattached row)."""
         if pending is not None:
             pending[:] = [set() for _ in range(self.n_cols)]
-        if not self.flat:
+        if not self.n_flat:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
+        if self.flat is None:
+            return self.attach_found(graph.lookup_blob(*self.keys[:2]), pending)
         return self.attach_found(graph.lookup(self.flat), pending)
 
     def attach_found_idx(self, found: np.ndarray):
         """attach_found's triples plus, as flat candidate indices and their columns, the
         candidates ranked before each row's attached one (all of an unattached row's) -- the
         ids whose creation would re-attach a row (egraph/storm.py indexes them by hash)."""
-        if not self.flat:
+        if not self.n_flat:
             z = np.zeros(0, np.int64)
             return (np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32), z,
                     np.zeros(0, np.uint32))
         found = np.asarray(found).astype(np.int64)
-        n = len(self.flat)
+        n = self.n_flat
         starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])
         pos = np.where(found >= 0, np.arange(n), n)
         first = np.minimum.reduceat(pos, starts)
@@ -137,8 +172,10 @@ class SeedCandidates:
         """attach() with the graph lookup of self.flat already done (callers batch it)."""
         if pending is not None:
             pending[:] = [set() for _ in range(self.n_cols)]
-        if not self.flat:
+        if not self.n_flat:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32)
+        if pending is not None and self.flat is None:
+            raise ValueError("pending id sets need the id list (combine(with_flat=True))")
         found = np.asarray(found).astype(np.int64)
         n = len(self.flat)
         starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])

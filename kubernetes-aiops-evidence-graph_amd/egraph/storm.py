@@ -129,14 +129,15 @@ class StormEngine:
         xs = [self.incidents[h] for h in handles]
         need = [x for x in xs if x.cand is None]
         if need:
-            for x, c in zip(need, SeedCandidates.per_column([x.evidence for x in need])):
+            for x, c in zip(need, SeedCandidates.per_column([x.evidence for x in need], keys=True)):
                 x.cand = c
                 if not self.keep_evidence:
                     x.evidence = None
         if not xs:
             return
-        cand = SeedCandidates.combine([x.cand for x in xs])
-        found = self.g.lookup(cand.flat) if cand.flat else np.zeros(0, np.int64)
+        cand = SeedCandidates.combine([x.cand for x in xs], with_flat=False)
+        blob, off, hashes = cand.keys
+        found = self.g.lookup_blob(blob, off) if cand.n_flat else np.zeros(0, np.int64)
         sv, col, ss, before, bcol = cand.attach_found_idx(found)
         cut = np.searchsorted(col, np.arange(len(xs) + 1, dtype=np.uint32))
         for j, x in enumerate(xs):
@@ -148,8 +149,7 @@ class StormEngine:
             self._gen = np.concatenate([self._gen, np.zeros(max(top - len(self._gen), 1024), np.int64)])
         self._gen[hs] += 1
         if len(before):
-            flat = cand.flat
-            h = np.fromiter((hash(flat[i]) for i in before), np.int64, len(before))
+            h = hashes[before]
             order = np.argsort(h, kind="stable")
             h, oh = h[order], hs[bcol.astype(np.int64)[order]]
             # merge into the hash-sorted index (O(entries), no re-sort of the resident part)

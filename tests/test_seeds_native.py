@@ -204,3 +204,35 @@ def test_storm_pending_index_lookup():
     for q in ([], ids[:1], ids[::7], ["absent"], ids):
         want = {e[1] for e in ent if e[0] in set(q) and e[2] == gen[e[1]]}
         assert StormEngine._pending_hit(eng, q) == want
+
+
+def test_keyed_candidates_match_flat_ones():
+    """per_column(keys=True) + combine(with_flat=False) (the storm's reseed form: utf-8 blob,
+    offsets and hashes instead of str lists) name the same ids in the same order, and attach
+    identically, as the str-list form -- including non-ASCII names and empty columns."""
+    import numpy as np
+    from egraph import synth
+    from egraph.graph import str_blob
+    from egraph.seeds import SeedCandidates
+    cl = synth.build_cluster(synth.ClusterConfig(pods=400, namespaces=3, nodes=8,
+                                                 deployments=40, services=30, seed=5))
+    lists = [c.evidence for c in synth.make_incidents(cl, 20, seed=2)]
+    lists[3] = []
+    lists[7] = [dict(lists[7][0], entity_name="pé-テ")] + lists[7][1:]
+    flat = SeedCandidates.combine(SeedCandidates.per_column(lists))
+    keyed = SeedCandidates.combine(SeedCandidates.per_column(lists, keys=True), with_flat=False)
+    pick = [2, 0, 7, 3, 5]
+    part_f = SeedCandidates.combine([SeedCandidates.per_column(lists)[i] for i in pick])
+    part_k = SeedCandidates.combine([SeedCandidates.per_column(lists, keys=True)[i] for i in pick],
+                                    with_flat=False)
+    for f, k in ((flat, keyed), (part_f, part_k)):
+        b, o = str_blob(f.flat)
+        assert k.keys[0] == b and np.array_equal(k.keys[1], o)
+        assert np.array_equal(k.keys[2], np.array([hash(x) for x in f.flat], np.int64))
+        assert k.n_flat == f.n_flat and np.array_equal(k.count, f.count)
+        assert np.array_equal(k.col, f.col) and np.array_equal(k.val, f.val)
+        found = np.random.default_rng(3).integers(-1, 30, f.n_flat)
+        for a, c in zip(f.attach_found_idx(found), k.attach_found_idx(found)):
+            assert np.array_equal(a, c)
+    empty = SeedCandidates.combine([], with_flat=False)
+    assert empty.n_flat == 0 and len(empty.attach_found_idx(np.zeros(0))[0]) == 0
