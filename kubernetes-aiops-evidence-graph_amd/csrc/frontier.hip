@@ -140,6 +140,11 @@ struct FArgs {
 #endif
 // the last walk tests the excluded label in a V-bit map built once per (label, snapshot
 // version) instead of gathering vlabel bytes: 1/8 of the bytes, mostly L1 hits
+#ifndef EGR_FR_TOPK_SORT
+// per-wave top-k: each lane sorts its candidate keys once, so the round's winner lane only
+// shifts its registers instead of rescanning them (narrow kernels, MPT <= 8)
+#define EGR_FR_TOPK_SORT 1
+#endif
 #ifndef EGR_FR_XBITS
 #define EGR_FR_XBITS 0
 #endif

@@ -933,12 +933,41 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
       for (int j = 0; j < MPT; ++j) bb = kk[j] > bb ? kk[j] : bb;
       return bb;
     };
-    uint64_t lb = best();
+    constexpr bool SORTED = EGR_FR_TOPK_SORT && MPT <= 8;
+    if constexpr (SORTED) {
+      // descending odd-even transposition sort of the lane's keys (MPT passes)
+#pragma unroll
+      for (int pass = 0; pass < MPT; ++pass)
+#pragma unroll
+        for (int j = pass & 1; j + 1 < MPT; j += 2) {
+          const uint64_t x = kk[j], y = kk[j + 1];
+          const bool sw = y > x;
+          kk[j] = sw ? y : x;
+          kk[j + 1] = sw ? x : y;
+        }
+    }
+    uint64_t lb = SORTED ? kk[0] : best();
     uint64_t tp1 = 0;
     if (prof) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       tp1 = wall_clock64();
     }
+    if constexpr (SORTED) {
+      for (int q = 0; q < A.k; ++q) {
+        const uint64_t wb = wave_max_u64(lb);
+        if (lane == 0) sh.top[wave][q] = wb;
+        if (wb == 0) {
+          for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+          break;
+        }
+        if (lb == wb) {                      // keys are distinct: one lane, its head taken
+#pragma unroll
+          for (int j = 0; j + 1 < MPT; ++j) kk[j] = kk[j + 1];
+          kk[MPT - 1] = 0;
+          lb = kk[0];
+        }
+      }
+    } else
     for (int q = 0; q < A.k; ++q) {
       const uint64_t wb = wave_max_u64(lb);
       if (lane == 0) sh.top[wave][q] = wb;
