@@ -145,6 +145,11 @@ struct FArgs {
 // shifts its registers instead of rescanning them (narrow kernels, MPT <= 8)
 #define EGR_FR_TOPK_SORT 1
 #endif
+#ifndef EGR_FR_TOPK_EARLY
+// sorted top-k: rounds per wave before the workgroup-wide threshold that lets waves stop early
+// (0 = every wave runs k rounds)
+#define EGR_FR_TOPK_EARLY 0
+#endif
 #ifndef EGR_FR_XBITS
 #define EGR_FR_XBITS 0
 #endif

@@ -953,12 +953,14 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
       tp1 = wall_clock64();
     }
     if constexpr (SORTED) {
-      for (int q = 0; q < A.k; ++q) {
-        const uint64_t wb = wave_max_u64(lb);
+      // one round: the wave's next best key into sh.top[wave][q]; false once the wave has no
+      // candidate left (the rest of its list zero-filled)
+      auto round = [&](int q, uint64_t& wb) {
+        wb = wave_max_u64(lb);
         if (lane == 0) sh.top[wave][q] = wb;
         if (wb == 0) {
           for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
-          break;
+          return false;
         }
         if (lb == wb) {                      // keys are distinct: one lane, its head taken
 #pragma unroll
@@ -966,7 +968,40 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
           kk[MPT - 1] = 0;
           lb = kk[0];
         }
+        return true;
+      };
+#if EGR_FR_TOPK_EARLY > 0
+      // R1 rounds per wave, then T = the k-th largest of the NWAVES * R1 keys emitted (0 if
+      // fewer): k keys >= T exist, so a wave stops as soon as its last key is <= T -- its
+      // remaining keys are below T and cannot rank in the top k (the merge ranks every emitted
+      // key; lists end zero-filled)
+      constexpr int R1 = EGR_FR_TOPK_EARLY;
+      static_assert(NWAVES * R1 <= 64, "one emitted key per lane");
+      const int r1 = R1 < A.k ? R1 : A.k;
+      uint64_t wb = 0;
+      bool live = true;
+      for (int q = 0; q < r1 && live; ++q) live = round(q, wb);
+      __syncthreads();
+      if (r1 < A.k) {
+        const uint64_t c = lane < NWAVES * r1 ? sh.top[lane / r1][lane % r1] : 0ull;
+        uint32_t rank = 0;
+        for (int w = 0; w < NWAVES; ++w)
+          for (int r = 0; r < r1; ++r) rank += sh.top[w][r] > c;
+        const uint64_t at = __ballot(c != 0 && rank == (uint32_t)(A.k - 1));
+        const int src = at ? __ffsll((long long)at) - 1 : 0;
+        const uint32_t tlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c, src);
+        const uint32_t thi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(c >> 32), src);
+        const uint64_t T = at ? ((uint64_t)thi << 32) | tlo : 0ull;
+        int q = r1;
+        for (; q < A.k && live && wb > T; ++q) live = round(q, wb);
+        if (live)
+          for (int r = q + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
       }
+#else
+      uint64_t wb;
+      for (int q = 0; q < A.k; ++q)
+        if (!round(q, wb)) break;
+#endif
     } else
     for (int q = 0; q < A.k; ++q) {
       const uint64_t wb = wave_max_u64(lb);
