@@ -761,12 +761,17 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
+        import resource
+        f0 = resource.getrusage(resource.RUSAGE_SELF)
         a = time.perf_counter()
         gc_t[1] = 0.0
         st = eng.tick(local, now, make_case, topology=topo, seq=mine if world > 1 else None)
         torch.cuda.synchronize(dev)
         st["wall_ms"] = (time.perf_counter() - a) * 1e3 - st["collect_ms"]
         st["gc_ms"] = gc_t[1] * 1e3
+        f1 = resource.getrusage(resource.RUSAGE_SELF)
+        st["minflt"] = f1.ru_minflt - f0.ru_minflt          # (collector stand-in included)
+        st["invol_cs"] = f1.ru_nivcsw - f0.ru_nivcsw
         if world > 1:
             import torch.distributed as dist
             st["wall_ms"] = max_over_ranks(dist, st["wall_ms"], dev)
@@ -792,6 +797,8 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
                    "tick_ms_p99": float(np.percentile(wall, 99)),
                    "stage_ms_mean": stage,
                    "gc_ms_per_tick": float(np.mean([s_["gc_ms"] for s_ in stats])),
+                   "minor_faults_per_tick": float(np.mean([s_["minflt"] for s_ in stats])),
+                   "involuntary_switches_per_tick": float(np.mean([s_["invol_cs"] for s_ in stats])),
                    "new_incidents_per_tick": float(np.mean([s_["new_incidents"] for s_ in stats])),
                    "affected_per_tick": float(np.mean([s_["affected"] for s_ in stats])),
                    "open_incidents_end": stats[-1]["open_incidents"],
