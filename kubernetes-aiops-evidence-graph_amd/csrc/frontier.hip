@@ -145,6 +145,10 @@ struct FArgs {
 // shifts its registers instead of rescanning them (narrow kernels, MPT <= 8)
 #define EGR_FR_TOPK_SORT 1
 #endif
+#ifndef EGR_FR_TOPK_SORT_MAX
+// largest candidate-register count per thread sorted (narrow: 5; wide: 9)
+#define EGR_FR_TOPK_SORT_MAX 8
+#endif
 #ifndef EGR_FR_TOPK_EARLY
 // sorted top-k: rounds per wave before the workgroup-wide threshold that lets waves stop early
 // (0 = every wave runs k rounds)

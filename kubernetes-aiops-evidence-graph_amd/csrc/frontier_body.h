@@ -933,7 +933,7 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
       for (int j = 0; j < MPT; ++j) bb = kk[j] > bb ? kk[j] : bb;
       return bb;
     };
-    constexpr bool SORTED = EGR_FR_TOPK_SORT && MPT <= 8;
+    constexpr bool SORTED = EGR_FR_TOPK_SORT && MPT <= EGR_FR_TOPK_SORT_MAX;
     if constexpr (SORTED) {
       // descending odd-even transposition sort of the lane's keys (MPT passes)
 #pragma unroll
