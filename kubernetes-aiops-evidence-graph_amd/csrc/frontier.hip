@@ -146,8 +146,8 @@ struct FArgs {
 #define EGR_FR_TOPK_SORT 1
 #endif
 #ifndef EGR_FR_TOPK_SORT_MAX
-// largest candidate-register count per thread sorted (narrow: 5; wide: 9)
-#define EGR_FR_TOPK_SORT_MAX 8
+// largest candidate-register count per thread sorted (narrow kernel 5, wide kernel 9: both)
+#define EGR_FR_TOPK_SORT_MAX 9
 #endif
 #ifndef EGR_FR_TOPK_EARLY
 // sorted top-k: rounds per wave before the workgroup-wide threshold that lets waves stop early
