@@ -1,35 +1,25 @@
 // Frontier engine: the whole graph stage of one incident column -- apoc-style k-hop reach
 // (A8, src/database/neo4j.py:169-202), typed k-hop propagation (A9) and the
-// per-incident top-k -- in ONE workgroup, with the incident's state in an LDS hash table.
+// per-incident top-k -- in ONE workgroup, with the incident's state in LDS.
 //
 // Why: a column's scores are non-zero only within `hops` hops of its seeds.  On the 100k-pod
-// graph that is ~1.9k of 229k vertices after 3 hops (0.8 %), so the dense [V x B] sweep of
-// propagate.hip spends >99 % of its HBM bytes on exact zeros.  Here a workgroup keeps only the
-// touched vertices: key = vertex id, s = current score, fl = reach depth + 1 (0 = not reached).
+// graph that is ~600 of 229k vertices (0.3 %), so the dense [V x B] sweep of propagate.hip
+// spends >99 % of its HBM bytes on exact zeros.  Here a workgroup keeps only the vertices the
+// column needs.
 //
-// Exactness (bit-identical to the dense plan and to oracle/egraph_oracle.c): for every member
-// v the pull  s'[v] = sum_{e in row v, CSR order} fmaf(val_e, s[col_e], acc)  then  s'[v] + s0[v]
-// is the dense recurrence with the terms of non-members skipped; a non-member's dense value is
-// exactly +0 and fmaf(w, +0, acc) == acc for finite w and acc != -0 (acc starts at +0 and can
-// never become -0 under round-to-nearest), so skipping them changes no bit.  Members are
-// (seeds) U (N(u) for every member u with s[u] != 0) U (reach set), which contains every
-// vertex whose dense value can be non-zero.
+// Exactness (bit-identical to the dense plan and to oracle/egraph_oracle.c): for a vertex v the
+// chain  sum_{e in row v, CSR order} fmaf(val_e, s[col_e], acc)  then  + s0[v]  is the dense
+// recurrence with the terms of vertices whose value is exactly +0 skipped; fmaf(w, +0, acc) ==
+// acc for finite w and acc != -0 (acc starts at +0 and can never become -0 under
+// round-to-nearest), so skipping them changes no bit.
 //
-// Work layout: a hop is two phases over the member list, GROW (the reach level and the
-// expansion of the non-zero members insert their neighbours) and PULL (the members an
-// expansion touched recompute their score).  A wave takes 64 members at a time: a row of <= 16
-// entries is one lane's, which loads and probes all its entries at once and runs the in-order
-// fmaf chain in registers; a longer (hub) row is taken by the whole wave, 64 entries per round,
-// with the chain run over v_readlane operands.  Top-k packs (score, vertex) into one u64 key:
-// each wave extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
-//
-// Capacity: two instantiations of the kernels (frontier_body.h).  The wide one (member-pool
-// runs, every member's score exact) holds 6144 slots in ~78 KB of LDS, 8-wave workgroups, two
-// per CU; the narrow one (pruned top-k runs: ~0.6k members per column on C3) holds 1536 slots
-// and two score buffers in 30 KB, 4-wave workgroups, five per CU.  A column with more members than the table's limit
-// is flagged and redone by the global-memory variant of the same code (a table of >= 2V slots
-// per resident workgroup, never overflows), launched unconditionally right after (it drains an
-// empty work list at once).
+// Two engines:
+//   * frontier_local.h -- top-k-only runs (pool_entries = -1: GraphService, the storm, the
+//     bench): discover the column's member set and its member-restricted local CSR once, then
+//     propagate over it in LDS.  A persistent grid pulls columns from a device work counter.
+//   * frontier_body.h -- hop by hop over an LDS (or, for columns too large for LDS, a global-
+//     memory) hash table: member-pool runs (every member's score kept for the read functions)
+//     and the second chances of columns the local kernel hands on.
 #include <algorithm>
 #include <type_traits>
 #include <vector>
@@ -42,231 +32,50 @@ using egr::dfree;
 
 namespace {
 
-constexpr uint32_t EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t NO_NODE = EGR_NO_NODE;
-constexpr int KMAXF = 16;
-constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
-constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
-constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
-constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
-constexpr int MAX_HOPS = 60;
-constexpr int PROF_SLOTS = 40;
+#include "frontier_common.h"
 
-struct FArgs {
-  const uint32_t* row_ptr;
-  const uint2* cv;             // (col, val bits) per CSR entry
-  const uint8_t* vlabel;
-  const uint32_t* xbits;       // EGR_FR_XBITS: bit v = vertex v carries the excluded label
-  uint32_t V;
-  int B, hops, k, exclude;
-  int prune;                   // no member pool: the last hop pulls the candidates only
-  const uint32_t* seed_ptr;    // [B+1] per column
-  const uint32_t* seed_vert;   // grouped by column, any order, duplicates allowed
-  const float* seed_val;       // (duplicates are max-combined in the kernel, as fmaxf)
-  uint2* seed_rep;             // per seed entry: (slot, s0 bits) of a vertex's representative
-  const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
-  const uint32_t* order;       // [B] launch order: workgroup i runs column order[i] (costly first)
-  uint32_t* xq;                // xcd: [0..8] region queue offsets into order, [9..16] queue heads
-  int xcd;                     // workgroups take their column from their XCD's region queue
-  uint32_t* seed_cnt;          // [2B] seed counters / costs, zeroed per column once consumed
-  uint32_t* out_ids;           // [B*k]
-  float* out_scores;
-  // member pool: every column's (vertex, score, depth+1) after the last hop
-  uint32_t* pool_v;
-  float* pool_s;
-  uint8_t* pool_d;
-  unsigned long long pool_cap;
-  unsigned long long* pool_ctr;
-  unsigned long long* mem_off;  // [B]
-  uint32_t* mem_cnt;            // [B], EGR_NO_NODE = not kept (pool full)
-  // overflow work list
-  uint32_t* ovf_list;           // where an LDS kernel hands on its overflowing columns
-  uint32_t* ovf_n;
-  uint32_t* ovf_next;           // the global-memory variant's work counter (over ovf_list)
-  uint32_t ovf_cap;             // ovf_list entries; further overflowing columns go to spill_*
-  uint32_t* spill_list;
-  uint32_t* spill_n;
-  const uint32_t* retry_list;   // the retry kernel's input list, count and work counter
-  const uint32_t* retry_n;
-  uint32_t* retry_next;         // (unused: the retry kernel takes entry blockIdx.x)
-  float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
-                                // narrow (FR_DBUF): the seeds' values by slot
-  // global tables (one per resident workgroup of the fallback kernel)
-  uint32_t* gkeys;              // [nbig][gcap]
-  float* gs;                    // [nbig][gcap]
-  uint8_t* gfl;                 // [nbig][gcap]
-  uint8_t* gneed;               // [nbig][gcap]
-  uint32_t* gmlist;             // [nbig][V]
-  float* gsnew;                 // [nbig][V]
-  uint32_t gcap;
-  unsigned long long* prof;     // [B][PROF_SLOTS] wall-clock stamps per phase, or nullptr
-  // [0] CSR entries gathered by pulls (col + val), [1] entries read by expansions (col),
-  // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed, [5] member keys
-  // outside the graph (a guard compiled in with -DEGR_FR_GUARDS; 0 otherwise)
-  unsigned long long* stats;
-};
+namespace fr_local {
+#include "frontier_local.h"
+}  // namespace fr_local
 
-// A/B switches of the frontier kernels (defaults = the shipped configuration)
-// walk chunking (frontier_body.h row_phase): 0 = static striping over the waves, 1 = chunks
-// taken from an LDS counter, members strided over the chunks, 2 = the same, contiguous chunks
-#ifndef EGR_FR_DYN
-#define EGR_FR_DYN 0
-#endif
-// hub rows: 1 = the next 64-entry segment's loads issued before the current one is probed
-#ifndef EGR_FR_HUBPF
-#define EGR_FR_HUBPF 0
-#endif
-// hub-row fmaf chains of the narrow kernel (frontier_body.h hub_chain): 0 = ballot loop over
-// the present entries, 1 = unrolled v_readlane chain over every entry, 2 = pairs through LDS,
-// one lane chains (2: +4 % at three batches in flight, profiles/r02_ab_hubchain.txt)
-#ifndef EGR_FR_HUBCHAIN
-#define EGR_FR_HUBCHAIN 2
-#endif
-// light rows probe the Bloom filter before the buckets (0: straight to the buckets)
-#ifndef EGR_FR_LBLOOM
-#define EGR_FR_LBLOOM 1
-#endif
-// the copy after a pull (single-buffer tables): 1 = a thread's members' loads issued together
-#ifndef EGR_FR_COPYU
-#define EGR_FR_COPYU 0
-#endif
-// light rows load two CSR entries per 16-B load and a row_ptr pair in one 8-B load
-#ifndef EGR_FR_PAIRLOAD        // +1-3 % at three batches in flight (profiles/r02_ab_frontier_session3.txt)
-#define EGR_FR_PAIRLOAD 1
-#endif
-// hub-row segments of 128 entries, two per lane (frontier_body.h HUBPAIR)
-#ifndef EGR_FR_HUBPAIR
-#define EGR_FR_HUBPAIR 0
-#endif
-// the last walk tests the excluded label in a V-bit map built once per (label, snapshot
-// version) instead of gathering vlabel bytes: 1/8 of the bytes, mostly L1 hits
-#ifndef EGR_FR_TOPK_SORT
-// per-wave top-k: each lane sorts its candidate keys once, so the round's winner lane only
-// shifts its registers instead of rescanning them (narrow kernels, MPT <= 8)
-#define EGR_FR_TOPK_SORT 1
-#endif
-#ifndef EGR_FR_TOPK_SORT_MAX
-// largest candidate-register count per thread sorted (narrow kernel 5, wide kernel 9: both)
-#define EGR_FR_TOPK_SORT_MAX 9
-#endif
-#ifndef EGR_FR_TOPK_EARLY
-// sorted top-k: rounds per wave before the workgroup-wide threshold that lets waves stop early
-// (0 = every wave runs k rounds)
-#define EGR_FR_TOPK_EARLY 0
-#endif
-#ifndef EGR_FR_XBITS
-#define EGR_FR_XBITS 0
-#endif
-// a lane keeps the row_ptr pairs of its first EGR_FR_ROWCACHE chunks' members across walks
-#ifndef EGR_FR_ROWCACHE
-#define EGR_FR_ROWCACHE 0
-#endif
-// rows of up to this many entries run one lane per row (longer ones across the wave)
-#ifndef EGR_FR_LMAX
-#define EGR_FR_LMAX 12
-#endif
-struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
-struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr[v + 1]
-// narrow table slots hold (key, score) side by side: a probe returns the score (frontier_body.h)
-#ifndef EGR_FR_NARROW_KV
-#define EGR_FR_NARROW_KV 0
-#endif
-
-// Two instantiations of the kernels (frontier_body.h): the wide table keeps every member of a
-// column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
-// one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
-// 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
+// Two instantiations of the hop-by-hop kernels (frontier_body.h).  The wide table keeps every
+// member of a column (member-pool runs: exact scores for every member, ~1.9k per column on C3)
+// and serves the wide-table second chance of columns the local kernel hands on.
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144
 #define FR_LLIMIT 4608
 #define FR_BLOOM_LOG 16
 #define FR_WAVES_PER_EU 4
-#define FR_LSNEW 0
-#define FR_KV 0
 #define FR_HUBCHAIN 1
-#define FR_DBUF 0
-#define FR_MEDIUM 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_LSNEW
-#undef FR_KV
 #undef FR_HUBCHAIN
-#undef FR_DBUF
-#undef FR_MEDIUM
 }  // namespace fr_wide
 
-namespace fr_narrow {
-#ifndef EGR_FR_NARROW_FT   // build-time knobs for A/B builds (scripts/ab_lib.sh)
-#define EGR_FR_NARROW_FT 256
-#define EGR_FR_NARROW_LCAP 1536
-#define EGR_FR_NARROW_LLIMIT 1152
-#define EGR_FR_NARROW_BLOOM_LOG 15
-#define EGR_FR_NARROW_WAVES_PER_EU 5
-#endif
-#ifndef EGR_FR_NARROW_LSNEW
-#define EGR_FR_NARROW_LSNEW 0
-#endif
-#ifndef EGR_FR_NARROW_MEDIUM   // rows of 5..16 entries four per wave (frontier_body.h LMAX)
-#define EGR_FR_NARROW_MEDIUM 0
-#endif
-#ifndef EGR_FR_NARROW_DBUF   // two slot-indexed score buffers, no copy phase (+2.5 %, abdb)
-#define EGR_FR_NARROW_DBUF 1
-#endif
-#define FR_FT EGR_FR_NARROW_FT
-#define FR_LCAP EGR_FR_NARROW_LCAP
-#define FR_LLIMIT EGR_FR_NARROW_LLIMIT
-#define FR_BLOOM_LOG EGR_FR_NARROW_BLOOM_LOG
-#define FR_WAVES_PER_EU EGR_FR_NARROW_WAVES_PER_EU
-#define FR_LSNEW EGR_FR_NARROW_LSNEW
-#define FR_KV EGR_FR_NARROW_KV
-#define FR_HUBCHAIN EGR_FR_HUBCHAIN
-#define FR_DBUF EGR_FR_NARROW_DBUF
-#define FR_MEDIUM EGR_FR_NARROW_MEDIUM
-#include "frontier_body.h"
-#undef FR_FT
-#undef FR_LCAP
-#undef FR_LLIMIT
-#undef FR_BLOOM_LOG
-#undef FR_WAVES_PER_EU
-#undef FR_LSNEW
-#undef FR_KV
-#undef FR_HUBCHAIN
-#undef FR_DBUF
-#undef FR_MEDIUM
-}  // namespace fr_narrow
-
-// The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
-// every narrow run and nearly always finds no overflowing column; a one-wave workgroup is
-// dispatched as soon as a single SIMD has room, instead of waiting behind the other batch in
-// flight for a CU to drain (scripts/ab_global.sh).  Only frontier_global_kernel is launched
-// from this instantiation.
+// The global-memory fallback's launch geometry: one wave per workgroup.  Its grid is launched
+// after every run and nearly always finds no overflowing column; a one-wave workgroup is
+// dispatched as soon as a single SIMD has room, instead of waiting behind another batch in
+// flight for a CU to drain (profiles/r01_ab_fallback_geom.txt).  Only frontier_global_kernel
+// is launched from this instantiation.
 namespace fr_fallback {
 #define FR_FT 64
 #define FR_LCAP 256
 #define FR_LLIMIT 192
 #define FR_BLOOM_LOG 10
 #define FR_WAVES_PER_EU 4
-#define FR_LSNEW 0
-#define FR_KV 0
 #define FR_HUBCHAIN 2
-#define FR_DBUF 0
-#define FR_MEDIUM 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_LSNEW
-#undef FR_KV
 #undef FR_HUBCHAIN
-#undef FR_DBUF
-#undef FR_MEDIUM
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
@@ -296,9 +105,11 @@ __global__ void scatter_reach_kernel(const uint32_t* __restrict__ pool_v,
     if (pool_d[o + i]) atomicOr(&out[(size_t)(b >> 6) * V + pool_v[o + i]], 1ull << (b & 63));
 }
 
-// seeds grouped by column without a sort: count, one-block scan, scatter.  Seeds usually arrive
-// grouped by column, so a wave's lanes form runs of equal columns: one atomic per run (the run's
-// first lane adds the run length; the others take their rank in the run).
+// Seeds as (vertex, column, value) triples in any order (egr_frontier_set_seeds) are grouped
+// by column without a sort: count, one-block scan, scatter.  Seeds usually arrive grouped by
+// column, so a wave's lanes form runs of equal columns: one atomic per run (the run's first
+// lane adds the run length; the others take their rank in the run).  Callers whose seeds are
+// grouped already pass the column offsets instead (egr_frontier_run_grouped: no kernels).
 struct SeedRun {
   bool ok;
   uint32_t col, leader, rank, len;
@@ -333,7 +144,7 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 // atomic per run of equal columns (a segmented sum over an inclusive wave scan).
 __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                   int64_t n, uint32_t V, int B, const uint32_t* __restrict__ row_ptr,
-                                  uint32_t* cnt, uint32_t* cost, uint32_t* cmax) {
+                                  uint32_t* cnt, uint32_t* cost) {
   const SeedRun r = seed_run(sv, sc, n, V, B);
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -354,60 +165,35 @@ __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_
   if (r.ok && r.rank == 0) {
     atomicAdd(&cnt[r.col], r.len);
     atomicAdd(&cost[r.col], hi - (r.leader > 0 ? lo : 0u));
-    if (cmax) atomicMax(&cmax[r.col], sv[i]);   // the column's graph region (xcd launch order)
   }
 }
 
 // ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]); order = the
 // columns by descending cost bucket (a log-scale counting sort: longest-processing-time-first
-// launch order, so the costly columns do not start in the last round).  One block of SCAN_T
-// threads, each owning a contiguous run of columns.  SCAN_T is 256 (one wave per SIMD), not
-// 1024: the block is launched while the other batch in flight holds the CUs, and a small block
-// is dispatched as soon as one workgroup of that batch finishes.
+// launch order, so the costly columns do not start in the last round); the run's counters and
+// overflow lists are zeroed.  One block of SCAN_T threads, each owning a contiguous run of
+// columns.
 constexpr int COST_BUCKETS = 64;
-#ifndef EGR_SCAN_T          // build-time knob for A/B builds
-#define EGR_SCAN_T 256
-#endif
-constexpr int SCAN_T = EGR_SCAN_T;
+constexpr int SCAN_T = 256;
+constexpr int CTL_WORDS = 9;      // u64: [0] pool, [1..6] stats, [7..8] four u32 list counters
 
 __device__ __forceinline__ int cost_bucket(uint32_t cost) {
   const int lg = (int)(__log2f((float)cost + 1.0f) * 3.0f);
   return COST_BUCKETS - 1 - min(COST_BUCKETS - 1, lg);
 }
 
-// XCD-aware launch (EGRAPH_FRONTIER_XCD=1): the columns are split into XCD_REGIONS queues by
-// the graph region of their largest seed vertex (vertices are laid out namespace by namespace,
-// so a region is a run of namespaces), each queue in cost order; a workgroup takes the next
-// column of its own XCD's queue (HW_REG_XCC_ID), then of the others.  The CSR rows a column
-// reads then mostly stay in one XCD's L2.  Placement changes only speed, never results.
-constexpr int XCD_REGIONS = 8;
-constexpr int NBINS = XCD_REGIONS * COST_BUCKETS;
-static_assert(NBINS % SCAN_T == 0, "seed scan bins");
-
-__device__ __forceinline__ int order_bin(uint32_t cost, const uint32_t* cmax, int c, uint32_t V,
-                                         int xcd) {
-  const int r = xcd ? (int)min((uint64_t)XCD_REGIONS - 1, (uint64_t)cmax[c] * XCD_REGIONS / V) : 0;
-  return r * COST_BUCKETS + cost_bucket(cost);
-}
-
-static bool xcd_queues() {
-  static const bool on = getenv("EGRAPH_FRONTIER_XCD") && atoi(getenv("EGRAPH_FRONTIER_XCD")) != 0;
-  return on;
-}
-
 __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
                                                          const uint32_t* __restrict__ cost,
-                                                         uint32_t* order, unsigned long long* ctr,
-                                                         uint32_t* ovf, const uint32_t* cmax,
-                                                         uint32_t V, int xcd, uint32_t* xq) {
+                                                         uint32_t* order, unsigned long long* ctl) {
   __shared__ uint32_t part[SCAN_T];
-  __shared__ uint32_t hist[NBINS];
+  __shared__ uint32_t hist[COST_BUCKETS];
   const int tid = threadIdx.x;
   const int per = (B + SCAN_T - 1) / SCAN_T;
   const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
   uint32_t sum = 0;
   for (int c = c0; c < c1; ++c) sum += cnt[c];
   part[tid] = sum;
+  if (tid < COST_BUCKETS) hist[tid] = 0;
   __syncthreads();
   for (int off = 1; off < SCAN_T; off <<= 1) {   // Hillis-Steele inclusive scan of the run sums
     const uint32_t x = tid >= off ? part[tid - off] : 0u;
@@ -423,50 +209,19 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
     run += x;
   }
   if (tid == SCAN_T - 1) ptr[B] = part[SCAN_T - 1];
-  if (tid < 7) ctr[tid] = 0;      // the next run's pool / stats counters and overflow list
-  if (tid < 4) ovf[tid] = 0;
-  // launch order: by (graph region, cost bucket); one region only unless xcd
-  for (int i = tid; i < NBINS; i += SCAN_T) hist[i] = 0;
+  if (tid < CTL_WORDS) ctl[tid] = 0;    // the next run's pool / stats counters and list counters
+  for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
   __syncthreads();
-  for (int c = c0; c < c1; ++c) atomicAdd(&hist[order_bin(cost[c], cmax, c, V, xcd)], 1u);
-  __syncthreads();
-  // exclusive scan of the NBINS bins: each thread owns BPT consecutive bins
-  constexpr int BPT = NBINS / SCAN_T;
-  uint32_t own = 0;
-  for (int j = 0; j < BPT; ++j) own += hist[tid * BPT + j];
-  __syncthreads();
-  part[tid] = own;
-  __syncthreads();
-  for (int off = 1; off < SCAN_T; off <<= 1) {
-    const uint32_t x = tid >= off ? part[tid - off] : 0u;
-    __syncthreads();
-    part[tid] += x;
-    __syncthreads();
-  }
-  uint32_t acc = tid ? part[tid - 1] : 0u;
-  for (int j = 0; j < BPT; ++j) {
-    const uint32_t x = hist[tid * BPT + j];
-    hist[tid * BPT + j] = acc;
-    acc += x;
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int j = 0; j < COST_BUCKETS; ++j) {
+      const uint32_t x = hist[j];
+      hist[j] = acc;
+      acc += x;
+    }
   }
   __syncthreads();
-  if (xcd && tid <= XCD_REGIONS) xq[tid] = tid < XCD_REGIONS ? hist[tid * COST_BUCKETS] : (uint32_t)B;
-  if (xcd && tid < XCD_REGIONS) xq[XCD_REGIONS + 1 + tid] = 0;
-  __syncthreads();
-  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[order_bin(cost[c], cmax, c, V, xcd)], 1u)] = (uint32_t)c;
-}
-
-// bit v of bits = (vlabel[v] == label), one 32-vertex word per thread
-__global__ void excl_bits_kernel(const uint8_t* __restrict__ vlabel, uint32_t V, int32_t label,
-                                 uint32_t* bits) {
-  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= (V + 31u) / 32u) return;
-  uint32_t b = 0;
-  for (uint32_t j = 0; j < 32u; ++j) {
-    const uint32_t v = w * 32u + j;
-    if (v < V && (int32_t)vlabel[v] == label) b |= 1u << j;
-  }
-  bits[w] = b;
+  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
@@ -482,31 +237,46 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
   out_s[base + r.rank] = sval[i];
 }
 
+// resident workgroups of the local kernel on this device (its persistent grid)
+int local_slots(int device) {
+  static int cached[64] = {0};
+  if (device < 0 || device >= 64) return 1024;
+  if (!cached[device]) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fr_local::frontier_local_kernel,
+                                                     fr_local::FT, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = fr_local::WAVES_PER_EU;
+      cus = 256;
+    }
+    cached[device] = std::max(1, per_cu) * std::max(1, cus);
+  }
+  return cached[device];
+}
+
 }  // namespace
 
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
-  bool big_geom = false;          // global variant in 256-thread workgroups (egr_frontier_set_retry)
-  uint32_t* xbits = nullptr;      // EGR_FR_XBITS: excluded-label bit map ([vmax / 32 + 1] words)
-  int32_t xbits_label = -1;       // ... built for this label, snapshot version and V
-  uint64_t xbits_version = ~0ull;
-  int64_t xbits_V = -1;
-  bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
-                                  // wide retry grid over every column (egr_frontier_set_wide_first)
+  bool big_geom = false;          // global variant in 512-thread workgroups (egr_frontier_set_retry)
+  bool wide_first = false;        // top-k frontier whose columns mostly overflow the local table:
+                                  // straight to the wide grid (egr_frontier_set_wide_first)
   uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
-  int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
+  int32_t retry_blocks = -1;      // wide-table second chance for local overflows: grid size
                                   // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
   int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
                                   // for incremental snapshot updates)
   int B = 0, k = 0, nbig = 0;
-  bool narrow = false;            // no member pool: the narrow-table kernels (fr_narrow)
+  bool narrow = false;            // no member pool: the local kernel (top-k only)
+  int local_grid = 0;             // the local kernel's persistent grid
   int64_t max_seeds = 0;
   uint32_t gcap = 0;
   int64_t n_seeds = 0;
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
-  uint32_t* seed_cnt = nullptr;   // [3B+24]: per-column counts, then scatter cursors; costs; max seed vertex; xq
+  uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; costs
   uint32_t* order = nullptr;      // [B] launch order of the columns
-  uint32_t* ident = nullptr;      // [B] 0..B-1 ($EGRAPH_FRONTIER_NO_ORDER: launch in column order)
+  uint32_t* ident = nullptr;      // [B] 0..B-1
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
   uint2* seed_rep = nullptr;
@@ -514,24 +284,27 @@ struct egr_frontier {
   float* pool_s = nullptr;
   uint8_t* pool_d = nullptr;
   unsigned long long pool_cap = 0;
-  unsigned long long* ctr = nullptr;   // [0] pool, [1..5] stats
+  // [0] pool counter, [1..6] stats, then (as u32) the overflow-list counters: [14] n and [15]
+  // next of the list the global-memory variant drains, [16] n of the list the wide retry drains
+  unsigned long long* ctl = nullptr;
+  uint32_t* lists = nullptr;      // [2B]: the global variant's list, the wide retry's list
+  uint32_t* qctl = nullptr;       // the local kernel's work counter and exit count
+  uint2* lspill = nullptr;        // the local kernel's local-CSR entries past its LDS
   unsigned long long* mem_off = nullptr;
   uint32_t* mem_cnt = nullptr;
-  // [0] n, [1] next of the list the global-memory variant drains, [2] n, [3] next of the narrow
-  // kernel's list the wide retry drains, [4..4+B) and [4+B..4+2B) the two lists
-  uint32_t* ovf = nullptr;
   uint32_t* gkeys = nullptr;
   float* gs = nullptr;
   float* gsnew = nullptr;
   float* lsnew = nullptr;
-  unsigned long long* prof = nullptr;   // [B][PROF_SLOTS] when $EGRAPH_FRONTIER_PROFILE is set
+  unsigned long long* prof = nullptr;   // [B][PROF_SLOTS][PROF_W] when $EGRAPH_FRONTIER_PROFILE is set
   uint8_t* gfl = nullptr;
   uint8_t* gneed = nullptr;
   uint32_t* gmlist = nullptr;
   bool seeds_set = false;
   bool ran = false;
   bool cnt_clean = true;          // seed_cnt is zero in stream order (the run's kernel zeroes it)
-  bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
+  bool ctl_clean = false;         // ctl zeroed by the last set_seeds, no run since
+  uint32_t last_n_seeds = 0;      // seed entries of the last run (egr_frontier_stats)
 };
 
 // default persistent grid of the wide-table second chance ($EGRAPH_FRONTIER_WIDE_RETRY, or
@@ -541,7 +314,7 @@ constexpr int RETRY_BLOCKS = 512;
 constexpr int GLOBAL_BLOCKS_BIG = 128;
 
 // stamps per profiling slot: the post-barrier stamp + one per wave of the kernel's workgroup
-static int prof_w(const egr_frontier* f) { return f->narrow ? fr_narrow::PROF_W : fr_wide::PROF_W; }
+static int prof_w(const egr_frontier* f) { return f->narrow ? fr_local::PROF_W : fr_wide::PROF_W; }
 
 extern "C" {
 
@@ -562,15 +335,11 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const int64_t vmax = std::min<int64_t>(s->V + s->V / 4 + 4096, (int64_t)EGR_NO_NODE - 1);
   f->vmax = vmax;
   const uint32_t V = (uint32_t)vmax;
-  // fallback table: 2 x nextpow2(V) slots, never more than half full
-  // top-k-only frontiers run pruned (egr_frontier_run): their columns fit the narrow table
+  // top-k-only frontiers run the local kernel; member-pool frontiers the wide hop-by-hop one
   f->narrow = pool_entries < 0;
-  const uint32_t lcap = f->narrow ? fr_narrow::LCAP : fr_wide::LCAP;
-  // pull results by member index: the narrow kernel and the wide retry index the same buffer
-  const uint32_t llimit = std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT);
-  static_assert(fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
-                "FR_DBUF: the narrow kernel keeps its seed values by slot in lsnew's column stride");
-  size_t gcap = 2 * lcap;
+  f->local_grid = f->narrow ? std::min(n_cols, local_slots(s->device)) : 0;
+  // fallback table: 2 x nextpow2(V) slots, never more than half full
+  size_t gcap = 2 * fr_wide::LCAP;
   while (gcap < 2ull * V) gcap *= 2;
   f->gcap = (uint32_t)gcap;
   f->nbig = std::min(n_cols, 32);
@@ -579,18 +348,20 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
                                  : (unsigned long long)n_cols * 4096ull + 4ull * V;
   int rc = EGR_OK;
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
-  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 3 * (size_t)n_cols + 24)) ||
+  if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
       (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
-      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 7)) ||
+      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctl, CTL_WORDS)) ||
+      (rc = dalloc(&f->lists, 2 * (size_t)n_cols)) || (rc = dalloc(&f->qctl, 2)) ||
+      (rc = dalloc(&f->lspill, (size_t)std::max(f->local_grid, 1) * fr_local::ESPILL)) ||
       (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
-      (rc = dalloc(&f->ovf, 2 * (size_t)n_cols + 4)) || (rc = dalloc(&f->all_n, 1)) ||
+      (rc = dalloc(&f->all_n, 1)) ||
       (rc = dalloc(&f->gkeys, gcap * f->nbig)) || (rc = dalloc(&f->gs, gcap * f->nbig)) ||
       (rc = dalloc(&f->gfl, gcap * f->nbig)) || (rc = dalloc(&f->gneed, gcap * f->nbig)) || (rc = dalloc(&f->gsnew, (size_t)V * f->nbig)) ||
       (rc = dalloc(&f->gmlist, (size_t)V * f->nbig)) ||
-      (rc = dalloc(&f->lsnew, (size_t)n_cols * llimit))) {
+      (rc = dalloc(&f->lsnew, (size_t)n_cols * fr_wide::LLIMIT))) {
     egr_frontier_free(f);
     return rc;
   }
@@ -604,8 +375,9 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gfl, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
-      hipMemset(f->seed_cnt, 0, (size_t)n_cols * 12) != hipSuccess ||
-      hipMemset(f->ctr, 0, 7 * 8) != hipSuccess) {
+      hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
+      hipMemset(f->qctl, 0, 8) != hipSuccess ||
+      hipMemset(f->ctl, 0, CTL_WORDS * 8) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
   }
@@ -637,12 +409,13 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->pool_v);
   dfree(f->pool_s);
   dfree(f->pool_d);
-  dfree(f->ctr);
+  dfree(f->ctl);
+  dfree(f->lists);
+  dfree(f->qctl);
+  dfree(f->lspill);
   dfree(f->mem_off);
   dfree(f->mem_cnt);
-  dfree(f->ovf);
   dfree(f->all_n);
-  dfree(f->xbits);
   dfree(f->gkeys);
   dfree(f->gs);
   dfree(f->gsnew);
@@ -654,13 +427,19 @@ void egr_frontier_free(egr_frontier* f) {
   delete f;
 }
 
-
 static int frontier_outgrown(const egr_frontier* f, const char* what) {
   return egr::fail(EGR_ESTATE, std::string(what) + ": the snapshot grew past the " +
                    std::to_string(f->vmax) + " vertices this frontier was sized for; create a new one");
 }
 
 int64_t egr_frontier_max_vertices(const egr_frontier* f) { return f ? f->vmax : -1; }
+
+int egr_frontier_shape(const egr_frontier* f, int32_t* n_cols, int32_t* k) {
+  if (!f) return egr::fail(EGR_EINVAL, "egr_frontier_shape: NULL frontier");
+  if (n_cols) *n_cols = f->B;
+  if (k) *k = f->k;
+  return EGR_OK;
+}
 
 int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const uint32_t* seed_col,
                            const float* seed_val, int64_t n_seeds, void* stream) {
@@ -673,18 +452,16 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   const uint32_t V = (uint32_t)f->s->V;
   hipStream_t st = (hipStream_t)stream;
   // counting sort by column: count, one-block exclusive scan, scatter (order within a column
-  // is arbitrary; the kernel max-combines duplicates).  Invalid triples are dropped.
-  if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 12, st));
+  // is arbitrary; the kernels max-combine duplicates).  Invalid triples are dropped.
+  if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 8, st));
   const unsigned g = (unsigned)((std::max<int64_t>(n_seeds, 1) + 255) / 256);
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_count_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
-                       n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B,
-                       xcd_queues() ? f->seed_cnt + 2 * f->B : nullptr);
+                       n_seeds, V, f->B, f->s->row_ptr, f->seed_cnt, f->seed_cnt + f->B);
     EGR_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, f->seed_cnt, f->B, f->seed_ptr,
-                     f->seed_cnt + f->B, f->order, f->ctr, f->ovf, f->seed_cnt + 2 * f->B, V,
-                     xcd_queues(), f->seed_cnt + 3 * f->B);
+                     f->seed_cnt + f->B, f->order, f->ctl);
   EGR_CHECK_LAUNCH();
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_scatter_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
@@ -694,7 +471,125 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   f->n_seeds = n_seeds;
   f->seeds_set = true;
   f->cnt_clean = false;
-  f->ctr_clean = true;
+  f->ctl_clean = true;
+  return EGR_OK;
+}
+
+// One run over seeds grouped by column (seed_ptr [B+1] into seed_v / seed_s, n entries).
+// `sorted` = the seeds came from egr_frontier_set_seeds (its counters are consumed by the
+// kernels and its scan zeroed the run's counters).
+static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_v,
+                             const float* seed_s, int64_t n_seeds, bool sorted,
+                             const uint32_t* source_vertex, int32_t hops, int32_t exclude_label,
+                             uint32_t* out_ids, float* out_scores, hipStream_t st) {
+  const egr_snapshot* s = f->s;
+  if (!(sorted && f->ctl_clean)) EGR_HIP(hipMemsetAsync(f->ctl, 0, CTL_WORDS * 8, st));
+  uint32_t* const lc = reinterpret_cast<uint32_t*>(f->ctl + 7);   // list counters
+  FArgs a{};
+  a.row_ptr = s->row_ptr;
+  a.cv = s->cv;
+  a.vlabel = s->vlabel;
+  a.V = (uint32_t)s->V;
+  a.B = f->B;
+  a.hops = hops;
+  a.k = f->k;
+  a.exclude = exclude_label;
+  a.prune = (f->pool_cap == 0 && !getenv("EGRAPH_FRONTIER_NO_PRUNE")) ? 1 : 0;
+  a.seed_ptr = seed_ptr;
+  a.seed_vert = seed_v;
+  a.seed_val = seed_s;
+  a.n_seeds = (uint32_t)n_seeds;
+  a.seed_rep = f->seed_rep;
+  a.sources = source_vertex;
+  a.order = sorted ? f->order : f->ident;
+  a.seed_cnt = sorted ? f->seed_cnt : nullptr;
+  a.qhead = f->qctl;
+  a.qdone = f->qctl + 1;
+  a.out_ids = out_ids;
+  a.out_scores = out_scores;
+  a.pool_v = f->pool_v;
+  a.pool_s = f->pool_s;
+  a.pool_d = f->pool_d;
+  a.pool_cap = f->pool_cap;
+  a.pool_ctr = f->ctl;
+  a.mem_off = f->mem_off;
+  a.mem_cnt = f->mem_cnt;
+  a.ovf_n = lc;
+  a.ovf_next = lc + 1;
+  a.ovf_list = f->lists;
+  a.ovf_cap = (uint32_t)f->B;
+  a.spill_list = a.ovf_list;
+  a.spill_n = a.ovf_n;
+  a.retry_n = lc + 2;
+  a.retry_list = f->lists + f->B;
+  a.lsnew = f->lsnew;
+  a.lspill = f->lspill;
+  a.gkeys = f->gkeys;
+  a.gs = f->gs;
+  a.gsnew = f->gsnew;
+  a.gfl = f->gfl;
+  a.gneed = f->gneed;
+  a.gmlist = f->gmlist;
+  a.gcap = f->gcap;
+  a.prof = f->prof;
+  if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
+  a.stats = f->ctl + 1;
+  bool zeroed_counters = !sorted;
+  const bool global_only = getenv("EGRAPH_FRONTIER_GLOBAL_ONLY") != nullptr;
+  if (global_only) {
+    // (tests: every column through the global-memory variant, as if every LDS kernel had
+    // handed it on)
+    a.ovf_list = const_cast<uint32_t*>(a.order);
+    a.ovf_n = f->all_n;
+  } else if (f->narrow) {
+    // the local kernel; a column it hands on goes to the wide-table second chance when that
+    // is on (egr_frontier_set_retry / $EGRAPH_FRONTIER_WIDE_RETRY, or when most columns of a
+    // graph overflow: wide-first), else straight to the global-memory variant.  Runs without
+    // pruning ($EGRAPH_FRONTIER_NO_PRUNE, an A/B knob) and hop counts past the local kernel's
+    // levels take the wide grid for every column.
+    const int32_t rb = f->retry_blocks >= 0 ? f->retry_blocks
+                       : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
+    const bool all_wide = (f->wide_first && rb > 0) || !a.prune || hops > fr_local::MAXH;
+    FArgs aw = a;
+    aw.prof = nullptr;    // the wide kernels' stamp layout differs: only the local pass is profiled
+    if (all_wide) {
+      aw.retry_list = a.order;
+      aw.retry_n = f->all_n;
+      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel,
+                         dim3(std::min(rb > 0 ? rb : RETRY_BLOCKS, f->B)), dim3(fr_wide::FT), 0,
+                         st, aw);
+      EGR_CHECK_LAUNCH();
+    } else {
+      FArgs al = a;
+      if (rb > 0) {                // hand-offs go to the wide retry's list
+        al.ovf_n = lc + 2;
+        al.ovf_list = f->lists + f->B;
+      }
+      hipLaunchKernelGGL(fr_local::frontier_local_kernel, dim3(f->local_grid), dim3(fr_local::FT),
+                         0, st, al);
+      EGR_CHECK_LAUNCH();
+      zeroed_counters = true;      // every column's counters were consumed
+      if (rb > 0) {
+        hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
+                           dim3(fr_wide::FT), 0, st, aw);
+        EGR_CHECK_LAUNCH();
+      }
+    }
+  } else {
+    hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
+    EGR_CHECK_LAUNCH();
+    zeroed_counters = true;
+  }
+  // the global-memory fallback (an empty list drains at once)
+  if (f->big_geom)
+    hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
+  else
+    hipLaunchKernelGGL(fr_fallback::frontier_global_kernel, dim3(f->nbig), dim3(fr_fallback::FT), 0, st, a);
+  EGR_CHECK_LAUNCH();
+  f->ran = true;
+  f->ctl_clean = false;
+  f->last_n_seeds = (uint32_t)n_seeds;
+  if (sorted) f->cnt_clean = zeroed_counters;
   return EGR_OK;
 }
 
@@ -705,128 +600,23 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   if (!f->seeds_set) return egr::fail(EGR_ESTATE, "egr_frontier_run: seeds not set");
   if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run");
   DeviceGuard guard(f->s->device);
-  hipStream_t st = (hipStream_t)stream;
-  const egr_snapshot* s = f->s;
-  if (!f->ctr_clean) {
-    EGR_HIP(hipMemsetAsync(f->ctr, 0, 7 * 8, st));
-    EGR_HIP(hipMemsetAsync(f->ovf, 0, 4 * 4, st));
-  }
-  FArgs a;
-  a.row_ptr = s->row_ptr;
-  a.cv = s->cv;
-  a.vlabel = s->vlabel;
-  a.xbits = nullptr;
-  a.V = (uint32_t)s->V;
-#if EGR_FR_XBITS
-  if (f->narrow && exclude_label >= 0) {
-    if (!f->xbits) {
-      const int rc = dalloc(&f->xbits, (size_t)f->vmax / 32 + 1);
-      if (rc) return rc;
-    }
-    if (f->xbits_label != exclude_label || f->xbits_version != s->version || f->xbits_V != s->V) {
-      const uint32_t words = (uint32_t)((s->V + 31) / 32);
-      hipLaunchKernelGGL(excl_bits_kernel, dim3((words + 255) / 256), dim3(256), 0, st, s->vlabel,
-                         (uint32_t)s->V, exclude_label, f->xbits);
-      EGR_CHECK_LAUNCH();
-      f->xbits_label = exclude_label;
-      f->xbits_version = s->version;
-      f->xbits_V = s->V;
-    }
-    a.xbits = f->xbits;
-  }
-#endif
-  a.B = f->B;
-  a.hops = hops;
-  a.k = f->k;
-  a.exclude = exclude_label;
-  a.prune = (f->pool_cap == 0 && !getenv("EGRAPH_FRONTIER_NO_PRUNE")) ? 1 : 0;
-  a.seed_ptr = f->seed_ptr;
-  a.seed_vert = f->seed_v;
-  a.seed_val = f->seed_s;
-  a.seed_rep = f->seed_rep;
-  a.sources = source_vertex;
-  a.order = getenv("EGRAPH_FRONTIER_NO_ORDER") ? f->ident : f->order;
-  a.xcd = (xcd_queues() && a.order == f->order) ? 1 : 0;
-  a.xq = f->seed_cnt + 3 * f->B;
-  a.seed_cnt = f->seed_cnt;
-  a.out_ids = out_ids;
-  a.out_scores = out_scores;
-  a.pool_v = f->pool_v;
-  a.pool_s = f->pool_s;
-  a.pool_d = f->pool_d;
-  a.pool_cap = f->pool_cap;
-  a.pool_ctr = f->ctr;
-  a.mem_off = f->mem_off;
-  a.mem_cnt = f->mem_cnt;
-  a.ovf_n = f->ovf;
-  a.ovf_next = f->ovf + 1;
-  a.ovf_list = f->ovf + 4;
-  a.ovf_cap = (uint32_t)f->B;
-  a.spill_list = a.ovf_list;
-  a.spill_n = a.ovf_n;
-  a.retry_n = f->ovf + 2;
-  a.retry_next = f->ovf + 3;
-  a.retry_list = f->ovf + 4 + f->B;
-  a.gkeys = f->gkeys;
-  a.gs = f->gs;
-  a.gsnew = f->gsnew;
-  a.gfl = f->gfl;
-  a.gneed = f->gneed;
-  a.gmlist = f->gmlist;
-  a.gcap = f->gcap;
-  a.lsnew = f->lsnew;
-  a.prof = f->prof;
-  if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
-  a.stats = f->ctr + 1;
-  // narrow: its overflowing columns go to the global-memory variant -- or, with the wide retry
-  // on (egr_frontier_set_retry / $EGRAPH_FRONTIER_WIDE_RETRY), to a persistent grid of the wide
-  // LDS table first, which hands on only what overflows 4608 members.  Off by default: pruned
-  // C2 / C3 columns never overflow, and the retry's 78-KB workgroups would wait for LDS held by
-  // the other batches in flight (~30 us per run in rocprof, profiles/r01_kernel_stats_v9.csv).
-  // Graphs whose 3-hop neighbourhoods are larger (the dense C4) turn it on after a run reports
-  // overflowing columns (egraph.graph.Frontier.adapt).
-  if (f->narrow) {
-    FArgs an = a;
-    an.ovf_n = f->ovf + 2;
-    an.ovf_list = f->ovf + 4 + f->B;
-    const int32_t rb = f->retry_blocks >= 0 ? f->retry_blocks
-                       : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
-    an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
-    a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
-    if (f->wide_first && rb > 0) {
-      // most columns overflow the narrow table: every column goes straight to the wide grid,
-      // in launch order (the narrow kernel, which also zeroes the seed counters, is skipped)
-      FArgs aw = a;
-      aw.retry_list = a.order;
-      aw.retry_n = f->all_n;
-      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
-                         dim3(fr_wide::FT), 0, st, aw);
-    } else {
-      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
-      EGR_CHECK_LAUNCH();
-      if (rb > 0)
-        hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
-                           dim3(fr_wide::FT), 0, st, a);
-    }
-  } else {
-    hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
-  }
-  EGR_CHECK_LAUNCH();
-  // the overflow fallback in its one-wave geometry; $EGRAPH_FRONTIER_AB_GLOBAL=0 / 1 launches the
-  // wide (512-thread) / narrow (256-thread) instantiation instead (scripts/ab_global.sh)
-  static const int fb_env = getenv("EGRAPH_FRONTIER_AB_GLOBAL") ? atoi(getenv("EGRAPH_FRONTIER_AB_GLOBAL")) : 3;
-  const int fb_geom = f->big_geom ? 1 : fb_env;
-  if (fb_geom == 0)
-    hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
-  else if (fb_geom == 1)
-    hipLaunchKernelGGL(fr_narrow::frontier_global_kernel, dim3(f->nbig), dim3(fr_narrow::FT), 0, st, a);
-  else
-    hipLaunchKernelGGL(fr_fallback::frontier_global_kernel, dim3(f->nbig), dim3(fr_fallback::FT), 0, st, a);
-  EGR_CHECK_LAUNCH();
-  f->ran = true;
-  f->ctr_clean = false;
-  f->cnt_clean = !(f->narrow && f->wide_first && f->retry_blocks > 0);   // (see above)
-  return EGR_OK;
+  return frontier_run_impl(f, f->seed_ptr, f->seed_v, f->seed_s, f->n_seeds, true, source_vertex,
+                           hops, exclude_label, out_ids, out_scores, (hipStream_t)stream);
+}
+
+int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_vertex,
+                             const float* seed_val, int64_t n_seeds, const uint32_t* source_vertex,
+                             int32_t hops, int32_t exclude_label, uint32_t* out_ids,
+                             float* out_scores, void* stream) {
+  if (!f || !seed_ptr || !source_vertex || !out_ids || !out_scores || hops < 1 || hops > MAX_HOPS ||
+      n_seeds < 0 || n_seeds > f->max_seeds || n_seeds > (int64_t)0xFFFFFFFFu ||
+      (n_seeds > 0 && (!seed_vertex || !seed_val)))
+    return egr::fail(EGR_EINVAL, "egr_frontier_run_grouped: bad arguments (need 1 <= hops <= 60, "
+                                 "n_seeds <= the frontier's max_seeds)");
+  if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run_grouped");
+  DeviceGuard guard(f->s->device);
+  return frontier_run_impl(f, seed_ptr, seed_vertex, seed_val, n_seeds, false, source_vertex,
+                           hops, exclude_label, out_ids, out_scores, (hipStream_t)stream);
 }
 
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on) {
@@ -839,7 +629,7 @@ int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
   if (!f || blocks < 0) return egr::fail(EGR_EINVAL, "egr_frontier_set_retry: bad arguments");
   f->retry_blocks = blocks;
   // graphs that need the retry also send more columns past the wide table: the global-memory
-  // variant then gets up to GLOBAL_BLOCKS_BIG workgroups (one HBM table each) in 256-thread
+  // variant then gets up to GLOBAL_BLOCKS_BIG workgroups (one HBM table each) in 512-thread
   // workgroups instead of 32 one-wave ones
   const int want = blocks > 0 ? std::min(f->B, GLOBAL_BLOCKS_BIG) : f->nbig;
   if (want > f->nbig) {
@@ -870,25 +660,22 @@ int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
   return EGR_OK;
 }
 
-int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
-  // out8 holds 9 values (egraph.h: out9)
-  if (!f || !out8) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
+int egr_frontier_stats(const egr_frontier* f, int64_t* out9, void* stream) {
+  if (!f || !out9) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_stats: not run yet");
   DeviceGuard guard(f->s->device);
-  unsigned long long h[7];
-  uint32_t nu = 0, ng = 0;
-  EGR_HIP(hipMemcpyAsync(h, f->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
-  EGR_HIP(hipMemcpyAsync(&nu, f->seed_ptr + f->B, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
-  EGR_HIP(hipMemcpyAsync(&ng, f->ovf, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  unsigned long long h[CTL_WORDS];
+  EGR_HIP(hipMemcpyAsync(h, f->ctl, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
   EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
-  out8[8] = (int64_t)ng;     // columns the global-memory variant ranked
-  for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
-  out8[5] = (int64_t)h[0];
-  out8[6] = (int64_t)nu;
+  const uint32_t* lc = reinterpret_cast<const uint32_t*>(h + 7);
+  for (int i = 0; i < 5; ++i) out9[i] = (int64_t)h[i + 1];
+  out9[5] = (int64_t)h[0];
+  out9[6] = (int64_t)f->last_n_seeds;
+  out9[8] = (int64_t)lc[0];     // columns the global-memory variant ranked
 #ifdef EGR_FR_GUARDS
-  out8[7] = (int64_t)h[6];
+  out9[7] = (int64_t)h[6];
 #else
-  out8[7] = -1;   // the corrupt-key guard is compiled only into debug builds: not counted
+  out9[7] = -1;   // the corrupt-key guard is compiled only into debug builds: not counted
 #endif
   return EGR_OK;
 }

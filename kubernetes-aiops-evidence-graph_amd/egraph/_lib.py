@@ -123,6 +123,8 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_free": (None, [P]),
     "egr_frontier_set_seeds": (C.c_int, [P, P, P, P, I64, P]),
     "egr_frontier_run": (C.c_int, [P, P, I32, I32, P, P, P]),
+    "egr_frontier_run_grouped": (C.c_int, [P, P, P, P, I64, P, I32, I32, P, P, P]),
+    "egr_frontier_shape": (C.c_int, [P, P, P]),
     "egr_frontier_stats": (C.c_int, [P, P, P]),
     "egr_frontier_set_retry": (C.c_int, [P, I32]),
     "egr_frontier_set_wide_first": (C.c_int, [P, I32]),

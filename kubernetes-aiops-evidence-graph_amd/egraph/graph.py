@@ -503,6 +503,18 @@ class Plan:
         return out[np.lexsort((out[:, 2], out[:, 0], out[:, 1]))] if cap else out.reshape(0, 3)
 
 
+def group_seeds(vertex: np.ndarray, col: np.ndarray, val: np.ndarray, n_cols: int):
+    """(seed_ptr u32 [n_cols+1], vertex u32, val f32) of seed triples grouped by column (stable;
+    triples whose column is >= n_cols are dropped): the input of Frontier.run_grouped."""
+    col = np.asarray(col, np.int64)
+    keep = (col >= 0) & (col < n_cols)
+    order = np.argsort(col[keep], kind="stable")
+    c = col[keep][order]
+    ptr = np.searchsorted(c, np.arange(n_cols + 1)).astype(np.uint32)
+    return (ptr, np.ascontiguousarray(np.asarray(vertex, np.uint32)[keep][order]),
+            np.ascontiguousarray(np.asarray(val, np.float32)[keep][order]))
+
+
 class Frontier:
     """Per-batch frontier engine (egr_frontier_*): the same seeds / sources / top-k contract as
     Plan.run, computed per incident column over only the vertices that column touches."""
@@ -546,6 +558,21 @@ class Frontier:
         L.check(L.lib.egr_frontier_run(self._h, L.ptr(sources), hops, exclude_label,
                                        L.ptr(self.out_ids), L.ptr(self.out_scores),
                                        self._st(stream)), "egr_frontier_run")
+        return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
+
+    def run_grouped(self, seed_ptr: torch.Tensor, vertex: torch.Tensor, val: torch.Tensor,
+                    sources: torch.Tensor, hops: int = 3, exclude_label: int = -1, stream=None):
+        """One pass over seeds grouped by column (egr_frontier_run_grouped): column b's seeds are
+        entries [seed_ptr[b], seed_ptr[b+1]) of vertex / val (device tensors; group_seeds()
+        builds them from triples).  No set_seeds, no sort on the device."""
+        if sources.numel() != self.B or seed_ptr.numel() != self.B + 1:
+            raise ValueError(f"need one source vertex per column ({self.B}) and {self.B + 1} seed offsets")
+        if vertex.numel() != val.numel():
+            raise ValueError("seed arrays differ in length")
+        L.check(L.lib.egr_frontier_run_grouped(self._h, L.ptr(seed_ptr), L.ptr(vertex), L.ptr(val),
+                                               vertex.numel(), L.ptr(sources), hops, exclude_label,
+                                               L.ptr(self.out_ids), L.ptr(self.out_scores),
+                                               self._st(stream)), "egr_frontier_run_grouped")
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",

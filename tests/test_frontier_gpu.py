@@ -42,7 +42,9 @@ def _world(B, seed=11, pods=3000, nodes=60):
 
 
 def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, scores=True):
-    fr = g.snapshot().frontier(B, max_seeds=max(len(sv), 1), k=k, pool_entries=pool_entries)
+    from egraph.graph import group_seeds
+    snap = g.snapshot()
+    fr = snap.frontier(B, max_seeds=max(len(sv), 1), k=k, pool_entries=pool_entries)
     fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
     inc = g.labels().index("Incident") if exclude is None else exclude
     ids, sco = fr.run(_dev(src), hops=hops, exclude_label=inc)
@@ -55,6 +57,12 @@ def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, sc
     e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)
     np.testing.assert_array_equal(got_ids, e_ids)
     np.testing.assert_array_equal(got_sc, e_sc)
+    # the same triples grouped by column on the host (egr_frontier_run_grouped: no device sort)
+    gp, gv, gs = group_seeds(sv, sc, ss, B)
+    fg = snap.frontier(B, max_seeds=max(len(gv), 1), k=k, pool_entries=pool_entries)
+    g_ids, g_sc = fg.run_grouped(_dev(gp), _dev(gv), _dev(gs), _dev(src), hops=hops, exclude_label=inc)
+    np.testing.assert_array_equal(g_ids.cpu().numpy().view(np.uint32), e_ids)
+    assert g_sc.cpu().numpy().tobytes() == e_sc.tobytes()
     assert fr.stats().get("corrupt_keys", 0) == 0     # counted in debug (guard) builds only
     if scores:
         assert fr.read_scores().cpu().numpy().tobytes() == exp.tobytes()     # bit-identical

@@ -20,10 +20,12 @@ def test_fallback_large_star():
 
 
 def test_fallback_c3_columns(monkeypatch):
-    """Narrow table with pruning switched off: most C3 columns overflow into the fallback."""
+    """Every column of a C3 batch through the global-memory variant
+    ($EGRAPH_FRONTIER_GLOBAL_ONLY: as if the LDS kernels had handed every column on), pruned and
+    with a member pool."""
     from egraph import synth
     from egraph.graph import EvidenceGraph
-    monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
+    monkeypatch.setenv("EGRAPH_FRONTIER_GLOBAL_ONLY", "1")
     B = 48
     c = synth.build_cluster(synth.CONFIGS["C3"])
     cases = synth.make_incidents(c, B, seed=1000)
@@ -34,4 +36,5 @@ def test_fallback_c3_columns(monkeypatch):
     sv, sc, ss = synth.seeds_for_batch(g, [x.evidence for x in cases])
     src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
     fr = _check(g, sv, sc, ss, src, B, pool_entries=-1, scores=False)
-    assert fr.stats()["overflowed"] >= B // 2
+    assert fr.stats()["members"] > 0
+    _check(g, sv, sc, ss, src, B, pool_entries=0, scores=False)
