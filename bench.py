@@ -84,6 +84,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def launch_ranks(n: int) -> int:
+    """Run this command line as n ranks under torch.distributed.run (child process; the caller
+    has not touched the GPU); returns its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    log(f"bench.py: launching {n} ranks: {' '.join(cmd)} {' '.join(sys.argv[1:])}")
+    return subprocess.call(cmd + sys.argv[1:])
+
+
 def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1,
           pool_entries: int = 0):
     from egraph import catalog, synth
@@ -861,7 +875,16 @@ def main():
     if args.warmup is None:
         args.warmup = 10 if short else 3
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside a launcher: start the N ranks ourselves (one per GPU,
+        # torch.distributed.run over 127.0.0.1) before anything here touches the GPU, as a child
+        # process, and exit with its status
+        raise SystemExit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank "
+                         f"per GPU (torch.distributed.run --nproc-per-node {args.gpus}) or pass "
+                         f"--gpus {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():

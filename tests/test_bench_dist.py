@@ -78,3 +78,39 @@ def test_incident_sharded_timed_region_gloo_world_size_2():
     assert v0 == v1 and v0 > 0                          # value = all ranks' incidents / time
     assert not set(ids0) & set(ids1)                    # each rank its own incidents
     assert ok0 and ok1 and sc0 and sc1                  # each rank's top-k = the oracle's
+
+
+def test_gpus_flag_must_match_world_size(monkeypatch):
+    """`--gpus N` under a launcher with another world size is refused before any GPU call."""
+    import sys
+
+    import pytest
+
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "WORLD_SIZE=1" in str(e.value.code)
+
+
+def test_gpus_flag_launches_ranks(monkeypatch):
+    """`bench.py --gpus N` with no launcher starts N ranks under torch.distributed.run (child
+    process, 127.0.0.1 rendezvous) and exits with its status."""
+    import subprocess
+    import sys
+
+    import pytest
+
+    import bench
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "7"])
+    monkeypatch.setattr(subprocess, "call", lambda cmd: calls.append(cmd) or 3)
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 3
+    (cmd,) = calls
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
