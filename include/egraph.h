@@ -225,6 +225,10 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
                     egr_plan** out);
 void egr_plan_free(egr_plan* p);
 int egr_plan_tile_width(const egr_plan* p);
+/* the vertex count of the plan's snapshot and the plan's column count: the shape of the dense
+ * score array egr_plan_read_scores writes ([V][n_cols]) and of the reach bits egr_plan_read_reach
+ * writes ([ceil(n_cols/64)][V]); callers size their outputs by it */
+int egr_plan_shape(const egr_plan* p, int64_t* n_vertices, int32_t* n_cols);
 /* Seeds s0[v, b] = max over triples (seed_vertex, seed_col, seed_val) (device arrays). */
 int egr_plan_set_seeds(egr_plan* p, const uint32_t* seed_vertex, const uint32_t* seed_col,
                        const float* seed_val, int64_t n_seeds, void* stream);
@@ -322,20 +326,18 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
  * propagation / top-k.
  *   egr_frontier_create : pool_entries = capacity of the member pool that keeps every
  *                         column's (vertex, score, depth) for the read functions; 0 picks
- *                         n_cols*4096 + 4V; -1 = no pool (top-k only: the local kernel, which
- *                         builds each column's member-restricted subgraph once and propagates
- *                         over it in LDS; the read functions return EGR_ESTATE).  Columns that
- *                         do not fit a table or the pool are still ranked.
+ *                         n_cols*4096 + 4V; -1 = no pool (top-k only: the narrow-table kernel,
+ *                         whose last pull computes the candidates only; the read functions
+ *                         return EGR_ESTATE).  Columns that do not fit a table or the pool are
+ *                         still ranked.
  *   egr_frontier_run    : one pass; sources [n_cols] device; outputs [n_cols*k] as
  *                         egr_plan_topk (EGR_NO_NODE / -inf in unused slots).
- *   egr_frontier_stats  : synchronous; out[9] of the last run = CSR entries read with their
- *                         values (hop pulls; the local kernel: its one read of every member's
- *                         row), CSR entries read by expansions (col only), rows walked
- *                         (row_ptr pairs), members, columns handed on by an LDS kernel (the
- *                         local one and, with the retry on, the wide one), pool entries used,
- *                         seed entries given, member keys outside the graph (a device-side
- *                         guard of -DEGR_FR_GUARDS builds; -1 = not counted: release builds
- *                         compile the guard out), columns ranked by the global-memory variant.
+ *   egr_frontier_stats  : synchronous; out[9] of the last run = CSR entries gathered by
+ *                         pulls (col + val read), CSR entries read by expansions (col only),
+ *                         rows walked (row_ptr pairs), members, columns handed on by an LDS
+ *                         kernel (the narrow one and, with the retry on, the wide one), pool
+ *                         entries used, valid seed entries, -1 (reserved), columns ranked by
+ *                         the global-memory variant.
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.
@@ -344,15 +346,15 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
  * ---------------------------------------------------------------------------------------- */
 typedef struct egr_frontier egr_frontier;
 
-/* Top-k-only frontiers (pool_entries = -1, the local kernel): give the columns the local kernel
- * hands on (more than 1152 members, 128 seed vertices or 6k local entries) a second chance in
- * the wide LDS table (4608 members) before the global-memory variant, on a persistent grid of
+/* Top-k-only frontiers (pool_entries = -1, the narrow-table kernel): give the columns that
+ * overflow the narrow LDS table (more than 1152 members) a second chance in the wide LDS table
+ * (4608 members) before the global-memory variant, on a persistent grid of
  * `blocks` workgroups (0 = off, the default; graphs whose 3-hop neighbourhoods are small never
  * overflow and skip the launch).  Takes effect from the next run (capture it into a graph
  * after setting it).                                                                       */
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
 /* Top-k-only frontiers with the retry on: `on` != 0 sends EVERY column straight to the wide grid
- * (for graphs where most columns overflow the local kernel, e.g. the dense C4: the local
+ * (for graphs where most columns overflow the narrow table, e.g. the dense C4: the narrow
  * attempt would be wasted work).  Same results; takes effect from the next egr_frontier_run. */
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on);
 
@@ -367,7 +369,8 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
  * entries [seed_ptr[b], seed_ptr[b+1]) of seed_vertex / seed_val (device; seed_ptr [n_cols+1]
  * u32, clamped to n_seeds; n_seeds <= the frontier's max_seeds; duplicates max-combined,
  * out-of-range vertices dropped).  Same results as egr_frontier_set_seeds + egr_frontier_run
- * with the same triples; the pointers are read by this call's kernels only (stream order). */
+ * with the same triples; the columns start in column order (set_seeds sorts them costly-first);
+ * the pointers are read by this call's kernels only (stream order). */
 int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_vertex,
                              const float* seed_val, int64_t n_seeds, const uint32_t* source_vertex,
                              int32_t hops, int32_t exclude_label, uint32_t* out_ids,

@@ -1,25 +1,40 @@
 // Frontier engine: the whole graph stage of one incident column -- apoc-style k-hop reach
 // (A8, src/database/neo4j.py:169-202), typed k-hop propagation (A9) and the
-// per-incident top-k -- in ONE workgroup, with the incident's state in LDS.
+// per-incident top-k -- in ONE workgroup, with the incident's state in an LDS hash table.
 //
 // Why: a column's scores are non-zero only within `hops` hops of its seeds.  On the 100k-pod
-// graph that is ~600 of 229k vertices (0.3 %), so the dense [V x B] sweep of propagate.hip
-// spends >99 % of its HBM bytes on exact zeros.  Here a workgroup keeps only the vertices the
-// column needs.
+// graph that is ~1.9k of 229k vertices after 3 hops (0.8 %), so the dense [V x B] sweep of
+// propagate.hip spends >99 % of its HBM bytes on exact zeros.  Here a workgroup keeps only the
+// touched vertices: key = vertex id, s = current score, fl = reach depth + 1 (0 = not reached).
 //
-// Exactness (bit-identical to the dense plan and to oracle/egraph_oracle.c): for a vertex v the
-// chain  sum_{e in row v, CSR order} fmaf(val_e, s[col_e], acc)  then  + s0[v]  is the dense
-// recurrence with the terms of vertices whose value is exactly +0 skipped; fmaf(w, +0, acc) ==
-// acc for finite w and acc != -0 (acc starts at +0 and can never become -0 under
-// round-to-nearest), so skipping them changes no bit.
+// Exactness (bit-identical to the dense plan and to oracle/egraph_oracle.c): for every member
+// v the pull  s'[v] = sum_{e in row v, CSR order} fmaf(val_e, s[col_e], acc)  then  s'[v] + s0[v]
+// is the dense recurrence with the terms of non-members skipped; a non-member's dense value is
+// exactly +0 and fmaf(w, +0, acc) == acc for finite w and acc != -0 (acc starts at +0 and can
+// never become -0 under round-to-nearest), so skipping them changes no bit.  Members are
+// (seeds) U (N(u) for every member u with s[u] != 0) U (reach set), which contains every
+// vertex whose dense value can be non-zero.
 //
-// Two engines:
-//   * frontier_local.h -- top-k-only runs (pool_entries = -1: GraphService, the storm, the
-//     bench): discover the column's member set and its member-restricted local CSR once, then
-//     propagate over it in LDS.  A persistent grid pulls columns from a device work counter.
-//   * frontier_body.h -- hop by hop over an LDS (or, for columns too large for LDS, a global-
-//     memory) hash table: member-pool runs (every member's score kept for the read functions)
-//     and the second chances of columns the local kernel hands on.
+// Work layout: a hop is two phases over the member list, GROW (the reach level and the
+// expansion of the non-zero members insert their neighbours) and PULL (the members an
+// expansion touched recompute their score).  A wave takes 64 members at a time: a row of <= 12
+// entries is one lane's, which loads and probes all its entries at once and runs the in-order
+// fmaf chain in registers; a longer (hub) row is taken by the whole wave, 64 entries per round,
+// with the chain run over v_readlane operands.  Top-k packs (score, vertex) into one u64 key:
+// each wave extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
+//
+// Capacity: two instantiations of the kernels (frontier_body.h).  The wide one (member-pool
+// runs, every member's score exact) holds 6144 slots in ~78 KB of LDS, 8-wave workgroups, two
+// per CU; the narrow one (pruned top-k runs: ~0.6k members per column on C3) holds 1536 slots
+// and two score buffers in 30 KB, 4-wave workgroups, five per CU.  A column with more members
+// than the table's limit is flagged and redone by the global-memory variant of the same code (a
+// table of >= 2V slots per resident workgroup, never overflows), launched unconditionally right
+// after (it drains an empty work list at once).
+//
+// (Round 3 measured a two-phase alternative for top-k runs -- discover the column's member set
+// and its member-restricted local CSR first, then propagate in LDS only -- at 0.14-0.16 ms per
+// C3 step against 0.065 for this kernel: its discovery walks cost as much as the pulls they
+// replace, and hub members serialise the LDS hops; profiles/r03_ab_local_kernel.txt.)
 #include <algorithm>
 #include <type_traits>
 #include <vector>
@@ -32,15 +47,74 @@ using egr::dfree;
 
 namespace {
 
-#include "frontier_common.h"
+constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t NO_NODE = EGR_NO_NODE;
+constexpr int KMAXF = 16;
+constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
+constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
+constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
+constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
+constexpr int MAX_HOPS = 60;
+constexpr int PROF_SLOTS = 40;
 
-namespace fr_local {
-#include "frontier_local.h"
-}  // namespace fr_local
+struct FArgs {
+  const uint32_t* row_ptr;
+  const uint2* cv;             // (col, val bits) per CSR entry
+  const uint8_t* vlabel;
+  uint32_t V;
+  int B, hops, k, exclude;
+  int prune;                   // no member pool: the last hop pulls the candidates only
+  const uint32_t* seed_ptr;    // [B+1] per column
+  const uint32_t* seed_vert;   // grouped by column, any order, duplicates allowed
+  const float* seed_val;       // (duplicates are max-combined in the kernel, as fmaxf)
+  uint32_t n_seeds;            // entries in seed_vert / seed_val (seed_ptr is clamped to it)
+  uint2* seed_rep;             // per seed entry: (slot, s0 bits) of a vertex's representative
+  const uint32_t* sources;     // [B] incident vertex per column (EGR_NO_NODE: none)
+  const uint32_t* order;       // [B] launch order: workgroup i runs column order[i] (costly first)
+  uint32_t* seed_cnt;          // [2B] set_seeds' counters / costs, zeroed per column once
+                               // consumed (nullptr: grouped seeds, nothing to zero)
+  uint32_t* out_ids;           // [B*k]
+  float* out_scores;
+  // member pool: every column's (vertex, score, depth+1) after the last hop
+  uint32_t* pool_v;
+  float* pool_s;
+  uint8_t* pool_d;
+  unsigned long long pool_cap;
+  unsigned long long* pool_ctr;
+  unsigned long long* mem_off;  // [B]
+  uint32_t* mem_cnt;            // [B], EGR_NO_NODE = not kept (pool full)
+  // overflow work list
+  uint32_t* ovf_list;           // where an LDS kernel hands on its overflowing columns
+  uint32_t* ovf_n;
+  uint32_t* ovf_next;           // the global-memory variant's work counter (over ovf_list)
+  uint32_t ovf_cap;             // ovf_list entries; further overflowing columns go to spill_*
+  uint32_t* spill_list;
+  uint32_t* spill_n;
+  const uint32_t* retry_list;   // the retry kernel's input list and count (block i takes
+  const uint32_t* retry_n;      // entries i, i + gridDim.x, ...)
+  float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
+                                // narrow (FR_DBUF): the seeds' values by slot
+  // global tables (one per resident workgroup of the fallback kernel)
+  uint32_t* gkeys;              // [nbig][gcap]
+  float* gs;                    // [nbig][gcap]
+  uint8_t* gfl;                 // [nbig][gcap]
+  uint8_t* gneed;               // [nbig][gcap]
+  uint32_t* gmlist;             // [nbig][V]
+  float* gsnew;                 // [nbig][V]
+  uint32_t gcap;
+  unsigned long long* prof;     // [B][PROF_SLOTS] wall-clock stamps per phase, or nullptr
+  // [0] CSR entries gathered by pulls (col + val), [1] entries read by expansions (col),
+  // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed
+  unsigned long long* stats;
+};
 
-// Two instantiations of the hop-by-hop kernels (frontier_body.h).  The wide table keeps every
-// member of a column (member-pool runs: exact scores for every member, ~1.9k per column on C3)
-// and serves the wide-table second chance of columns the local kernel hands on.
+struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
+struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr[v + 1]
+
+// Two instantiations of the kernels (frontier_body.h): the wide table keeps every member of a
+// column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
+// one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
+// 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144
@@ -48,6 +122,8 @@ namespace fr_wide {
 #define FR_BLOOM_LOG 16
 #define FR_WAVES_PER_EU 4
 #define FR_HUBCHAIN 1
+#define FR_DBUF 0
+#define FR_KERNELS 7
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -55,13 +131,38 @@ namespace fr_wide {
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
+#undef FR_DBUF
+#undef FR_KERNELS
 }  // namespace fr_wide
 
-// The global-memory fallback's launch geometry: one wave per workgroup.  Its grid is launched
-// after every run and nearly always finds no overflowing column; a one-wave workgroup is
-// dispatched as soon as a single SIMD has room, instead of waiting behind another batch in
-// flight for a CU to drain (profiles/r01_ab_fallback_geom.txt).  Only frontier_global_kernel
-// is launched from this instantiation.
+namespace fr_narrow {
+// hub-row chains through LDS, one lane (+4 % at three batches in flight,
+// profiles/r02_ab_hubchain.txt); two slot-indexed score buffers, no copy phase (+2.5 %,
+// profiles/r02_ab_frontier_session3.txt)
+#define FR_FT 256
+#define FR_LCAP 1536
+#define FR_LLIMIT 1152
+#define FR_BLOOM_LOG 15
+#define FR_WAVES_PER_EU 5
+#define FR_HUBCHAIN 2
+#define FR_DBUF 1
+#define FR_KERNELS 1
+#include "frontier_body.h"
+#undef FR_FT
+#undef FR_LCAP
+#undef FR_LLIMIT
+#undef FR_BLOOM_LOG
+#undef FR_WAVES_PER_EU
+#undef FR_HUBCHAIN
+#undef FR_DBUF
+#undef FR_KERNELS
+}  // namespace fr_narrow
+
+// The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
+// every narrow run and nearly always finds no overflowing column; a one-wave workgroup is
+// dispatched as soon as a single SIMD has room, instead of waiting behind the other batch in
+// flight for a CU to drain (scripts/ab_global.sh).  Only frontier_global_kernel is launched
+// from this instantiation.
 namespace fr_fallback {
 #define FR_FT 64
 #define FR_LCAP 256
@@ -69,6 +170,8 @@ namespace fr_fallback {
 #define FR_BLOOM_LOG 10
 #define FR_WAVES_PER_EU 4
 #define FR_HUBCHAIN 2
+#define FR_DBUF 0
+#define FR_KERNELS 4
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -76,6 +179,8 @@ namespace fr_fallback {
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
+#undef FR_DBUF
+#undef FR_KERNELS
 }  // namespace fr_fallback
 
 // members -> dense row-major scores [V][B] / reach bits [W][V] (inspection and tests)
@@ -105,11 +210,9 @@ __global__ void scatter_reach_kernel(const uint32_t* __restrict__ pool_v,
     if (pool_d[o + i]) atomicOr(&out[(size_t)(b >> 6) * V + pool_v[o + i]], 1ull << (b & 63));
 }
 
-// Seeds as (vertex, column, value) triples in any order (egr_frontier_set_seeds) are grouped
-// by column without a sort: count, one-block scan, scatter.  Seeds usually arrive grouped by
-// column, so a wave's lanes form runs of equal columns: one atomic per run (the run's first
-// lane adds the run length; the others take their rank in the run).  Callers whose seeds are
-// grouped already pass the column offsets instead (egr_frontier_run_grouped: no kernels).
+// seeds grouped by column without a sort: count, one-block scan, scatter.  Seeds usually arrive
+// grouped by column, so a wave's lanes form runs of equal columns: one atomic per run (the run's
+// first lane adds the run length; the others take their rank in the run).
 struct SeedRun {
   bool ok;
   uint32_t col, leader, rank, len;
@@ -170,12 +273,13 @@ __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_
 
 // ptr[0..B] = exclusive scan of cnt; cnt becomes the scatter cursor (= ptr[c]); order = the
 // columns by descending cost bucket (a log-scale counting sort: longest-processing-time-first
-// launch order, so the costly columns do not start in the last round); the run's counters and
-// overflow lists are zeroed.  One block of SCAN_T threads, each owning a contiguous run of
-// columns.
+// launch order, so the costly columns do not start in the last round); the next run's counters
+// and overflow lists are zeroed.  One block of SCAN_T threads, each owning a contiguous run of
+// columns.  SCAN_T is 256 (one wave per SIMD), not 1024: the block is launched while the other
+// batches in flight hold the CUs, and a small block is dispatched as soon as one workgroup of
+// theirs finishes (profiles/r01_ab_scan_t.txt).
 constexpr int COST_BUCKETS = 64;
 constexpr int SCAN_T = 256;
-constexpr int CTL_WORDS = 9;      // u64: [0] pool, [1..6] stats, [7..8] four u32 list counters
 
 __device__ __forceinline__ int cost_bucket(uint32_t cost) {
   const int lg = (int)(__log2f((float)cost + 1.0f) * 3.0f);
@@ -184,7 +288,8 @@ __device__ __forceinline__ int cost_bucket(uint32_t cost) {
 
 __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B, uint32_t* ptr,
                                                          const uint32_t* __restrict__ cost,
-                                                         uint32_t* order, unsigned long long* ctl) {
+                                                         uint32_t* order, unsigned long long* ctr,
+                                                         uint32_t* ovf) {
   __shared__ uint32_t part[SCAN_T];
   __shared__ uint32_t hist[COST_BUCKETS];
   const int tid = threadIdx.x;
@@ -209,7 +314,8 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
     run += x;
   }
   if (tid == SCAN_T - 1) ptr[B] = part[SCAN_T - 1];
-  if (tid < CTL_WORDS) ctl[tid] = 0;    // the next run's pool / stats counters and list counters
+  if (tid < 7) ctr[tid] = 0;      // the next run's pool / stats counters and overflow lists
+  if (tid < 4) ovf[tid] = 0;
   for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
   __syncthreads();
   if (tid == 0) {
@@ -237,46 +343,27 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
   out_s[base + r.rank] = sval[i];
 }
 
-// resident workgroups of the local kernel on this device (its persistent grid)
-int local_slots(int device) {
-  static int cached[64] = {0};
-  if (device < 0 || device >= 64) return 1024;
-  if (!cached[device]) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fr_local::frontier_local_kernel,
-                                                     fr_local::FT, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
-      (void)hipGetLastError();
-      per_cu = fr_local::WAVES_PER_EU;
-      cus = 256;
-    }
-    cached[device] = std::max(1, per_cu) * std::max(1, cus);
-  }
-  return cached[device];
-}
-
 }  // namespace
 
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
   bool big_geom = false;          // global variant in 512-thread workgroups (egr_frontier_set_retry)
-  bool wide_first = false;        // top-k frontier whose columns mostly overflow the local table:
-                                  // straight to the wide grid (egr_frontier_set_wide_first)
+  bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
+                                  // wide retry grid over every column (egr_frontier_set_wide_first)
   uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
-  int32_t retry_blocks = -1;      // wide-table second chance for local overflows: grid size
+  int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
                                   // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
   int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
                                   // for incremental snapshot updates)
   int B = 0, k = 0, nbig = 0;
-  bool narrow = false;            // no member pool: the local kernel (top-k only)
-  int local_grid = 0;             // the local kernel's persistent grid
+  bool narrow = false;            // no member pool: the narrow-table kernels (fr_narrow)
   int64_t max_seeds = 0;
   uint32_t gcap = 0;
   int64_t n_seeds = 0;
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
   uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; costs
-  uint32_t* order = nullptr;      // [B] launch order of the columns
-  uint32_t* ident = nullptr;      // [B] 0..B-1
+  uint32_t* order = nullptr;      // [B] launch order of the columns (set_seeds: costly first)
+  uint32_t* ident = nullptr;      // [B] 0..B-1 (grouped runs: column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
   uint2* seed_rep = nullptr;
@@ -284,27 +371,26 @@ struct egr_frontier {
   float* pool_s = nullptr;
   uint8_t* pool_d = nullptr;
   unsigned long long pool_cap = 0;
-  // [0] pool counter, [1..6] stats, then (as u32) the overflow-list counters: [14] n and [15]
-  // next of the list the global-memory variant drains, [16] n of the list the wide retry drains
-  unsigned long long* ctl = nullptr;
-  uint32_t* lists = nullptr;      // [2B]: the global variant's list, the wide retry's list
-  uint32_t* qctl = nullptr;       // the local kernel's work counter and exit count
-  uint2* lspill = nullptr;        // the local kernel's local-CSR entries past its LDS
+  unsigned long long* ctr = nullptr;   // [0] pool, [1..5] stats
   unsigned long long* mem_off = nullptr;
   uint32_t* mem_cnt = nullptr;
+  // [0] n, [1] next of the list the global-memory variant drains, [2] n, [3] (unused) of the
+  // narrow kernel's list the wide retry drains, [4..4+B) and [4+B..4+2B) the two lists
+  uint32_t* ovf = nullptr;
   uint32_t* gkeys = nullptr;
   float* gs = nullptr;
   float* gsnew = nullptr;
   float* lsnew = nullptr;
-  unsigned long long* prof = nullptr;   // [B][PROF_SLOTS][PROF_W] when $EGRAPH_FRONTIER_PROFILE is set
+  unsigned long long* prof = nullptr;   // [B][PROF_SLOTS] when $EGRAPH_FRONTIER_PROFILE is set
   uint8_t* gfl = nullptr;
   uint8_t* gneed = nullptr;
   uint32_t* gmlist = nullptr;
   bool seeds_set = false;
   bool ran = false;
   bool cnt_clean = true;          // seed_cnt is zero in stream order (the run's kernel zeroes it)
-  bool ctl_clean = false;         // ctl zeroed by the last set_seeds, no run since
-  uint32_t last_n_seeds = 0;      // seed entries of the last run (egr_frontier_stats)
+  bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
+  int64_t last_n_seeds = -1;      // seed entries of the last grouped run (-1: the last run was
+                                  // a set_seeds run; its valid count is seed_ptr[B])
 };
 
 // default persistent grid of the wide-table second chance ($EGRAPH_FRONTIER_WIDE_RETRY, or
@@ -314,7 +400,7 @@ constexpr int RETRY_BLOCKS = 512;
 constexpr int GLOBAL_BLOCKS_BIG = 128;
 
 // stamps per profiling slot: the post-barrier stamp + one per wave of the kernel's workgroup
-static int prof_w(const egr_frontier* f) { return f->narrow ? fr_local::PROF_W : fr_wide::PROF_W; }
+static int prof_w(const egr_frontier* f) { return f->narrow ? fr_narrow::PROF_W : fr_wide::PROF_W; }
 
 extern "C" {
 
@@ -335,11 +421,15 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const int64_t vmax = std::min<int64_t>(s->V + s->V / 4 + 4096, (int64_t)EGR_NO_NODE - 1);
   f->vmax = vmax;
   const uint32_t V = (uint32_t)vmax;
-  // top-k-only frontiers run the local kernel; member-pool frontiers the wide hop-by-hop one
+  // top-k-only frontiers run pruned (egr_frontier_run): their columns fit the narrow table
   f->narrow = pool_entries < 0;
-  f->local_grid = f->narrow ? std::min(n_cols, local_slots(s->device)) : 0;
+  const uint32_t lcap = f->narrow ? fr_narrow::LCAP : fr_wide::LCAP;
+  // pull results by member index: the narrow kernel and the wide retry index the same buffer
+  const uint32_t llimit = std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT);
+  static_assert(fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
+                "FR_DBUF: the narrow kernel keeps its seed values by slot in lsnew's column stride");
   // fallback table: 2 x nextpow2(V) slots, never more than half full
-  size_t gcap = 2 * fr_wide::LCAP;
+  size_t gcap = 2 * lcap;
   while (gcap < 2ull * V) gcap *= 2;
   f->gcap = (uint32_t)gcap;
   f->nbig = std::min(n_cols, 32);
@@ -353,15 +443,13 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
-      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctl, CTL_WORDS)) ||
-      (rc = dalloc(&f->lists, 2 * (size_t)n_cols)) || (rc = dalloc(&f->qctl, 2)) ||
-      (rc = dalloc(&f->lspill, (size_t)std::max(f->local_grid, 1) * fr_local::ESPILL)) ||
+      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 7)) ||
       (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
-      (rc = dalloc(&f->all_n, 1)) ||
+      (rc = dalloc(&f->ovf, 2 * (size_t)n_cols + 4)) || (rc = dalloc(&f->all_n, 1)) ||
       (rc = dalloc(&f->gkeys, gcap * f->nbig)) || (rc = dalloc(&f->gs, gcap * f->nbig)) ||
-      (rc = dalloc(&f->gfl, gcap * f->nbig)) || (rc = dalloc(&f->gneed, gcap * f->nbig)) || (rc = dalloc(&f->gsnew, (size_t)V * f->nbig)) ||
-      (rc = dalloc(&f->gmlist, (size_t)V * f->nbig)) ||
-      (rc = dalloc(&f->lsnew, (size_t)n_cols * fr_wide::LLIMIT))) {
+      (rc = dalloc(&f->gfl, gcap * f->nbig)) || (rc = dalloc(&f->gneed, gcap * f->nbig)) ||
+      (rc = dalloc(&f->gsnew, (size_t)V * f->nbig)) || (rc = dalloc(&f->gmlist, (size_t)V * f->nbig)) ||
+      (rc = dalloc(&f->lsnew, (size_t)n_cols * llimit))) {
     egr_frontier_free(f);
     return rc;
   }
@@ -376,8 +464,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
       hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
-      hipMemset(f->qctl, 0, 8) != hipSuccess ||
-      hipMemset(f->ctl, 0, CTL_WORDS * 8) != hipSuccess) {
+      hipMemset(f->ctr, 0, 7 * 8) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
   }
@@ -409,12 +496,10 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->pool_v);
   dfree(f->pool_s);
   dfree(f->pool_d);
-  dfree(f->ctl);
-  dfree(f->lists);
-  dfree(f->qctl);
-  dfree(f->lspill);
+  dfree(f->ctr);
   dfree(f->mem_off);
   dfree(f->mem_cnt);
+  dfree(f->ovf);
   dfree(f->all_n);
   dfree(f->gkeys);
   dfree(f->gs);
@@ -452,7 +537,7 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   const uint32_t V = (uint32_t)f->s->V;
   hipStream_t st = (hipStream_t)stream;
   // counting sort by column: count, one-block exclusive scan, scatter (order within a column
-  // is arbitrary; the kernels max-combine duplicates).  Invalid triples are dropped.
+  // is arbitrary; the kernel max-combines duplicates).  Invalid triples are dropped.
   if (!f->cnt_clean) EGR_HIP(hipMemsetAsync(f->seed_cnt, 0, (size_t)f->B * 8, st));
   const unsigned g = (unsigned)((std::max<int64_t>(n_seeds, 1) + 255) / 256);
   if (n_seeds > 0) {
@@ -461,7 +546,7 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
     EGR_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(seed_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, f->seed_cnt, f->B, f->seed_ptr,
-                     f->seed_cnt + f->B, f->order, f->ctl);
+                     f->seed_cnt + f->B, f->order, f->ctr, f->ovf);
   EGR_CHECK_LAUNCH();
   if (n_seeds > 0) {
     hipLaunchKernelGGL(seed_scatter_kernel, dim3(g), dim3(256), 0, st, seed_vertex, seed_col,
@@ -471,20 +556,23 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
   f->n_seeds = n_seeds;
   f->seeds_set = true;
   f->cnt_clean = false;
-  f->ctl_clean = true;
+  f->ctr_clean = true;
   return EGR_OK;
 }
 
-// One run over seeds grouped by column (seed_ptr [B+1] into seed_v / seed_s, n entries).
-// `sorted` = the seeds came from egr_frontier_set_seeds (its counters are consumed by the
-// kernels and its scan zeroed the run's counters).
+// One run over seeds grouped by column (seed_ptr [B+1] into seed_v / seed_s, n_seeds entries).
+// `sorted` = the seeds came from egr_frontier_set_seeds: its launch order (costly columns first)
+// is used, its counters are consumed (zeroed) by the narrow kernel, and its scan zeroed the
+// run's counters.
 static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_v,
-                             const float* seed_s, int64_t n_seeds, bool sorted,
-                             const uint32_t* source_vertex, int32_t hops, int32_t exclude_label,
-                             uint32_t* out_ids, float* out_scores, hipStream_t st) {
+                             const float* seed_s, int64_t n_seeds, bool sorted, const uint32_t* source_vertex,
+                             int32_t hops, int32_t exclude_label, uint32_t* out_ids,
+                             float* out_scores, hipStream_t st) {
   const egr_snapshot* s = f->s;
-  if (!(sorted && f->ctl_clean)) EGR_HIP(hipMemsetAsync(f->ctl, 0, CTL_WORDS * 8, st));
-  uint32_t* const lc = reinterpret_cast<uint32_t*>(f->ctl + 7);   // list counters
+  if (!(sorted && f->ctr_clean)) {
+    EGR_HIP(hipMemsetAsync(f->ctr, 0, 7 * 8, st));
+    EGR_HIP(hipMemsetAsync(f->ovf, 0, 4 * 4, st));
+  }
   FArgs a{};
   a.row_ptr = s->row_ptr;
   a.cv = s->cv;
@@ -494,6 +582,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.hops = hops;
   a.k = f->k;
   a.exclude = exclude_label;
+  // ($EGRAPH_FRONTIER_NO_PRUNE: every member exact in a top-k run too -- a test hook)
   a.prune = (f->pool_cap == 0 && !getenv("EGRAPH_FRONTIER_NO_PRUNE")) ? 1 : 0;
   a.seed_ptr = seed_ptr;
   a.seed_vert = seed_v;
@@ -503,27 +592,23 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.sources = source_vertex;
   a.order = sorted ? f->order : f->ident;
   a.seed_cnt = sorted ? f->seed_cnt : nullptr;
-  a.qhead = f->qctl;
-  a.qdone = f->qctl + 1;
   a.out_ids = out_ids;
   a.out_scores = out_scores;
   a.pool_v = f->pool_v;
   a.pool_s = f->pool_s;
   a.pool_d = f->pool_d;
   a.pool_cap = f->pool_cap;
-  a.pool_ctr = f->ctl;
+  a.pool_ctr = f->ctr;
   a.mem_off = f->mem_off;
   a.mem_cnt = f->mem_cnt;
-  a.ovf_n = lc;
-  a.ovf_next = lc + 1;
-  a.ovf_list = f->lists;
+  a.ovf_n = f->ovf;
+  a.ovf_next = f->ovf + 1;
+  a.ovf_list = f->ovf + 4;
   a.ovf_cap = (uint32_t)f->B;
   a.spill_list = a.ovf_list;
   a.spill_n = a.ovf_n;
-  a.retry_n = lc + 2;
-  a.retry_list = f->lists + f->B;
-  a.lsnew = f->lsnew;
-  a.lspill = f->lspill;
+  a.retry_n = f->ovf + 2;
+  a.retry_list = f->ovf + 4 + f->B;
   a.gkeys = f->gkeys;
   a.gs = f->gs;
   a.gsnew = f->gsnew;
@@ -531,65 +616,67 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.gneed = f->gneed;
   a.gmlist = f->gmlist;
   a.gcap = f->gcap;
+  a.lsnew = f->lsnew;
   a.prof = f->prof;
   if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
-  a.stats = f->ctl + 1;
-  bool zeroed_counters = !sorted;
-  const bool global_only = getenv("EGRAPH_FRONTIER_GLOBAL_ONLY") != nullptr;
-  if (global_only) {
-    // (tests: every column through the global-memory variant, as if every LDS kernel had
+  a.stats = f->ctr + 1;
+  bool skipped_lds = false;       // no LDS kernel ran: the set_seeds counters were not consumed
+  if (getenv("EGRAPH_FRONTIER_GLOBAL_ONLY")) {
+    // (a test hook: every column through the global-memory variant, as if every LDS kernel had
     // handed it on)
     a.ovf_list = const_cast<uint32_t*>(a.order);
     a.ovf_n = f->all_n;
+    skipped_lds = true;
   } else if (f->narrow) {
-    // the local kernel; a column it hands on goes to the wide-table second chance when that
-    // is on (egr_frontier_set_retry / $EGRAPH_FRONTIER_WIDE_RETRY, or when most columns of a
-    // graph overflow: wide-first), else straight to the global-memory variant.  Runs without
-    // pruning ($EGRAPH_FRONTIER_NO_PRUNE, an A/B knob) and hop counts past the local kernel's
-    // levels take the wide grid for every column.
+    // narrow: its overflowing columns go to the global-memory variant -- or, with the wide
+    // retry on (egr_frontier_set_retry / $EGRAPH_FRONTIER_WIDE_RETRY), to a persistent grid of
+    // the wide LDS table first, which hands on only what overflows 4608 members.  Off by
+    // default: pruned C2 / C3 columns never overflow, and the retry's 78-KB workgroups would
+    // wait for LDS held by the other batches in flight (~30 us per run in rocprof,
+    // profiles/r01_kernel_stats_v9.csv).  Graphs whose 3-hop neighbourhoods are larger (the
+    // dense C4) turn it on after a run reports overflowing columns (egraph.graph.Frontier.adapt).
+    FArgs an = a;
+    an.ovf_n = f->ovf + 2;
+    an.ovf_list = f->ovf + 4 + f->B;
     const int32_t rb = f->retry_blocks >= 0 ? f->retry_blocks
                        : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
-    const bool all_wide = (f->wide_first && rb > 0) || !a.prune || hops > fr_local::MAXH;
-    FArgs aw = a;
-    aw.prof = nullptr;    // the wide kernels' stamp layout differs: only the local pass is profiled
-    if (all_wide) {
+    an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
+    a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
+    if (f->wide_first && rb > 0) {
+      // most columns overflow the narrow table: every column goes straight to the wide grid,
+      // in launch order (the narrow kernel, which also zeroes the seed counters, is skipped)
+      FArgs aw = a;
       aw.retry_list = a.order;
       aw.retry_n = f->all_n;
-      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel,
-                         dim3(std::min(rb > 0 ? rb : RETRY_BLOCKS, f->B)), dim3(fr_wide::FT), 0,
-                         st, aw);
+      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
+                         dim3(fr_wide::FT), 0, st, aw);
       EGR_CHECK_LAUNCH();
+      skipped_lds = true;
     } else {
-      FArgs al = a;
-      if (rb > 0) {                // hand-offs go to the wide retry's list
-        al.ovf_n = lc + 2;
-        al.ovf_list = f->lists + f->B;
-      }
-      hipLaunchKernelGGL(fr_local::frontier_local_kernel, dim3(f->local_grid), dim3(fr_local::FT),
-                         0, st, al);
+      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
       EGR_CHECK_LAUNCH();
-      zeroed_counters = true;      // every column's counters were consumed
       if (rb > 0) {
         hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
-                           dim3(fr_wide::FT), 0, st, aw);
+                           dim3(fr_wide::FT), 0, st, a);
         EGR_CHECK_LAUNCH();
       }
     }
   } else {
     hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
     EGR_CHECK_LAUNCH();
-    zeroed_counters = true;
   }
-  // the global-memory fallback (an empty list drains at once)
+  // the overflow fallback: one-wave workgroups (they are dispatched as soon as one SIMD has
+  // room, profiles/r01_ab_fallback_geom.txt), or 512-thread ones once the retry is on
   if (f->big_geom)
     hipLaunchKernelGGL(fr_wide::frontier_global_kernel, dim3(f->nbig), dim3(fr_wide::FT), 0, st, a);
   else
     hipLaunchKernelGGL(fr_fallback::frontier_global_kernel, dim3(f->nbig), dim3(fr_fallback::FT), 0, st, a);
   EGR_CHECK_LAUNCH();
   f->ran = true;
-  f->ctl_clean = false;
-  f->last_n_seeds = (uint32_t)n_seeds;
-  if (sorted) f->cnt_clean = zeroed_counters;
+  f->ctr_clean = false;
+  // the narrow / wide LDS kernels zero each column's set_seeds counters as they consume them;
+  // a run that skipped them leaves the counters for the next set_seeds to clear
+  if (sorted) f->cnt_clean = !skipped_lds;
   return EGR_OK;
 }
 
@@ -600,8 +687,10 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   if (!f->seeds_set) return egr::fail(EGR_ESTATE, "egr_frontier_run: seeds not set");
   if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run");
   DeviceGuard guard(f->s->device);
-  return frontier_run_impl(f, f->seed_ptr, f->seed_v, f->seed_s, f->n_seeds, true, source_vertex,
-                           hops, exclude_label, out_ids, out_scores, (hipStream_t)stream);
+  const int rc = frontier_run_impl(f, f->seed_ptr, f->seed_v, f->seed_s, f->n_seeds, true, source_vertex, hops,
+                                   exclude_label, out_ids, out_scores, (hipStream_t)stream);
+  if (rc == EGR_OK) f->last_n_seeds = -1;
+  return rc;
 }
 
 int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_vertex,
@@ -615,8 +704,10 @@ int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const ui
                                  "n_seeds <= the frontier's max_seeds)");
   if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run_grouped");
   DeviceGuard guard(f->s->device);
-  return frontier_run_impl(f, seed_ptr, seed_vertex, seed_val, n_seeds, false, source_vertex,
-                           hops, exclude_label, out_ids, out_scores, (hipStream_t)stream);
+  const int rc = frontier_run_impl(f, seed_ptr, seed_vertex, seed_val, n_seeds, false, source_vertex, hops,
+                                   exclude_label, out_ids, out_scores, (hipStream_t)stream);
+  if (rc == EGR_OK) f->last_n_seeds = n_seeds;
+  return rc;
 }
 
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on) {
@@ -629,7 +720,7 @@ int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
   if (!f || blocks < 0) return egr::fail(EGR_EINVAL, "egr_frontier_set_retry: bad arguments");
   f->retry_blocks = blocks;
   // graphs that need the retry also send more columns past the wide table: the global-memory
-  // variant then gets up to GLOBAL_BLOCKS_BIG workgroups (one HBM table each) in 512-thread
+  // variant then gets up to GLOBAL_BLOCKS_BIG workgroups (one HBM table each) in 256-thread
   // workgroups instead of 32 one-wave ones
   const int want = blocks > 0 ? std::min(f->B, GLOBAL_BLOCKS_BIG) : f->nbig;
   if (want > f->nbig) {
@@ -660,23 +751,23 @@ int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
   return EGR_OK;
 }
 
-int egr_frontier_stats(const egr_frontier* f, int64_t* out9, void* stream) {
-  if (!f || !out9) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
+int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
+  // out8 holds 9 values (egraph.h: out9)
+  if (!f || !out8) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
   if (!f->ran) return egr::fail(EGR_ESTATE, "egr_frontier_stats: not run yet");
   DeviceGuard guard(f->s->device);
-  unsigned long long h[CTL_WORDS];
-  EGR_HIP(hipMemcpyAsync(h, f->ctl, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  unsigned long long h[7];
+  uint32_t nu = 0, ng = 0;
+  EGR_HIP(hipMemcpyAsync(h, f->ctr, sizeof(h), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  if (f->last_n_seeds < 0)       // a set_seeds run: the valid entries its scan counted
+    EGR_HIP(hipMemcpyAsync(&nu, f->seed_ptr + f->B, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  EGR_HIP(hipMemcpyAsync(&ng, f->ovf, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   EGR_HIP(hipStreamSynchronize((hipStream_t)stream));
-  const uint32_t* lc = reinterpret_cast<const uint32_t*>(h + 7);
-  for (int i = 0; i < 5; ++i) out9[i] = (int64_t)h[i + 1];
-  out9[5] = (int64_t)h[0];
-  out9[6] = (int64_t)f->last_n_seeds;
-  out9[8] = (int64_t)lc[0];     // columns the global-memory variant ranked
-#ifdef EGR_FR_GUARDS
-  out9[7] = (int64_t)h[6];
-#else
-  out9[7] = -1;   // the corrupt-key guard is compiled only into debug builds: not counted
-#endif
+  out8[8] = (int64_t)ng;     // columns the global-memory variant ranked
+  for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
+  out8[5] = (int64_t)h[0];
+  out8[6] = f->last_n_seeds < 0 ? (int64_t)nu : f->last_n_seeds;
+  out8[7] = -1;   // reserved (a corrupt-key counter of earlier debug builds): not counted
   return EGR_OK;
 }
 

@@ -1,31 +1,38 @@
-// Frontier engine kernels for ONE table geometry, hop by hop (the member-pool runs and the
-// second chances of columns the local kernel hands on); included by csrc/frontier.hip once per
+// Frontier engine kernels for ONE table geometry; included by csrc/frontier.hip once per
 // geometry, each time inside its own namespace (no include guard, no includes: by design).
-//
-// Geometry of this instantiation (set by the includer): FR_FT threads per workgroup, FR_LCAP
-// LDS table slots, FR_LLIMIT members before a column overflows to the global-memory variant,
-// FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU, FR_HUBCHAIN (1: hub-row chains over
-// v_readlane operands, every lane; 2: the pairs through the wave's LDS scratch, one lane).
+// FR_KERNELS selects the kernels the geometry emits (below).
+
+// Geometry of this instantiation (set by the includer, csrc/frontier.hip):
+//   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
+//   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU,
+//   FR_HUBCHAIN (hub-row fmaf chains: 1 = v_readlane operands in every lane, 2 = the pairs
+//   through the wave's LDS scratch, one lane), FR_DBUF (1: two slot-indexed score buffers; a
+//   pull reads hop h's and writes hop h + 1's directly, seed add and need-bit clearing
+//   included, so no copy phase follows the walk; 0: pull results by member index in HBM and a
+//   copy phase).  Every combination instantiated by frontier.hip is a shipped path.
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
 constexpr uint32_t LLIMIT = FR_LLIMIT;      // members before a column overflows (load 0.75)
 constexpr int LPPT = LCAP / FT;             // slots cleared per thread
-constexpr int LMAX = 12;                    // rows up to this many entries run one lane per row
+// rows of up to LMAX entries run one lane per row (longer ones across the wave); 12 measured
+// best against 8 and 16 (profiles/r02_ab_frontier_session3.txt)
+constexpr int LMAX = 12;
+static_assert(LMAX % 4 == 0 && LMAX <= 16, "light rows: whole probe batches of LB = 4");
 constexpr int LB = 4;                       // keys probed together per lane
 constexpr int BLOOM_LOG = FR_BLOOM_LOG;
 constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys in one read
 constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
-constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
-constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
-constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
-constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
+constexpr bool DBUF = FR_DBUF;
+constexpr int CHAIN_W = 64;                 // hub-chain scratch pairs per wave (FR_HUBCHAIN 2)
+static_assert(FR_HUBCHAIN == 1 || FR_HUBCHAIN == 2, "hub-row chain scheme");
+
 
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
 // insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
-// index.
+// index (FR_DBUF: the second score buffer, by slot).
 template <bool GT>
 struct Tab {
   using MT = typename std::conditional<GT, uint32_t, uint16_t>::type;
@@ -38,15 +45,53 @@ struct Tab {
   uint32_t cap, limit;
   uint32_t* count;  // LDS
   uint32_t* ovf;    // LDS
-  uint32_t* bloom;  // LDS variant: membership filter (nullptr: none)
+  uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
   float2* chain;    // LDS: per-wave hub-chain scratch [NWAVES][64] (FR_HUBCHAIN 2), or null
+  // FR_DBUF (LDS tables): snew is the slot-indexed buffer the walk writes (hop h + 1's scores)
+  // and s0g the column's seed values by slot, in global memory (read by the seeds' pullers)
+  const float* s0g = nullptr;
 
+  __device__ __forceinline__ uint32_t key(uint32_t p) const { return keys[p]; }
+  __device__ __forceinline__ float& sc(uint32_t p) const { return s[p]; }
+  // the keys of bucket bk's 4 slots (one 16-B read)
   __device__ __forceinline__ uint4 bucket(uint32_t bk) const {
     return reinterpret_cast<const uint4*>(keys)[bk];
   }
 };
 
-__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) { return bloom_hash_bits(v, BLOOM_LOG); }
+// Buckets of 4 slots (one 16-B read), probed linearly.  A bucket fills from its first slot: an
+// insert CASes the lowest empty slot it sees and moves on only when that slot is taken, so a
+// bucket with an empty slot ends every probe sequence that passes through it.
+// Hashes use only full-rate 24-bit multiplies (a 32-bit v_mul_lo / v_mul_hi is quarter rate,
+// and every probed key pays for its hashes): the id is folded to 24 bits, multiplied by an odd
+// 24-bit constant, and 16 mixed bits are range-reduced to [0, nb) by a second 24-bit multiply.
+__device__ __forceinline__ uint32_t mix24(uint32_t v, uint32_t c) {
+  return (uint32_t)__umul24((v ^ (v >> 24)) & 0xFFFFFFu, c);
+}
+
+// (HIP's __umul24 returns a signed int: the product is taken as unsigned before the shift, or a
+// table of more than 2^15 buckets would get negative -- out of range -- start buckets.  Tables
+// of more than 2^16 buckets, the global-memory variant's on large graphs, reduce a full 32-bit
+// hash with __umulhi instead.)
+__device__ __forceinline__ uint32_t hbucket(uint32_t v, uint32_t nb) {
+  const uint32_t h = mix24(v, 0x9E3779u);
+  if (nb > 65536u) return __umulhi(h, nb);
+  return (uint32_t)__umul24((h >> 8) & 0xFFFFu, nb) >> 16;
+}
+
+// outcome of one bucket read for key v: slot (>= 0), -1 = absent, -2 = continue probing
+__device__ __forceinline__ int bucket_match(const uint4& kk, uint32_t v, uint32_t bk) {
+  if (kk.x == v) return (int)(4 * bk);
+  if (kk.y == v) return (int)(4 * bk + 1);
+  if (kk.z == v) return (int)(4 * bk + 2);
+  if (kk.w == v) return (int)(4 * bk + 3);
+  if (kk.w == EMPTY) return -1;            // slots fill in order: an empty last slot ends it
+  return -2;
+}
+
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t v) {   // BLOOM_LOG bits
+  return (mix24(v, 0xB5297Au | 1u) >> 8) & ((1u << BLOOM_LOG) - 1u);
+}
 
 // slot of v, inserting it if absent (-1: table full, or an LDS table that has overflowed)
 template <bool GT>
@@ -56,7 +101,9 @@ __device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
   for (uint32_t n = 0; n < nb; ++n) {
     // An LDS table past its member limit hands its column on (the result is discarded), so an
     // insert that has to probe past its first bucket stops there -- a table filled to the last
-    // slot would make every insert of a new key scan all its buckets.
+    // slot would make every insert of a new key scan all its buckets (the dense C4 spent ~4 ms
+    // per launch there before this exit).  Checked only past the first bucket: the common
+    // insert pays nothing.
     if constexpr (!GT) {
       if (n > 0 && *t.ovf) return -1;
     }
@@ -95,7 +142,7 @@ __device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
     const uint32_t h = bloom_hash(v);
     if (!((t.bloom[h >> 5] >> (h & 31u)) & 1u)) return -1;
   }
-  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk = hbucket(v, nb);
   for (uint32_t n = 0; n < nb; ++n) {
     const int r = bucket_match(t.bucket(bk), v, bk);
@@ -115,12 +162,28 @@ __device__ __forceinline__ bool cand_depth(uint8_t f, int hops) {
   return d != 0 && d <= (uint32_t)(hops + 1);
 }
 
+// diagnostics: per-wave sums of sub-step times (profiling builds of a phase only)
+struct Ticker {
+  bool on = false;
+  uint64_t t0 = 0;
+  uint64_t sub[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void tick(int k) {
+    if (on) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t t1 = wall_clock64();
+      sub[k] += t1 - t0;
+      t0 = t1;
+    }
+  }
+};
+
+
 // Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
 // still unresolved, so a lane's NQ probe sequences share round trips.
 template <bool GT, int NQ>
 __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
                                            int (&q)[NQ]) {
-  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
   uint32_t bk[NQ];
   uint32_t pend = 0;
 #pragma unroll
@@ -192,15 +255,17 @@ __device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q
   if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
 }
 
-// One row of dl <= LMAX entries, one lane per row: every entry is loaded in one round trip
-// (two entries per 16-B load; the CSR arrays carry two entries of padding for an odd row's
-// last pair), probed LB keys at a time (lockstep), then the in-order fmaf chain runs in
-// registers (K_PULL) and the absent neighbours are inserted (K_REACH / K_PROP).
+// One row of dl <= LMAX entries, one lane per row: every entry is loaded in one round trip,
+// probed LB keys at a time (lockstep), then the in-order fmaf chain runs in registers (K_PULL)
+// and the absent neighbours are inserted (K_REACH / K_PROP).
 template <bool GT>
 __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
-                                          uint32_t kind, int h, float& acc) {
+                                          uint32_t kind, int h, float& acc, Ticker& tk) {
   uint32_t c[LMAX];
   float w[LMAX];
+  // two entries per 16-B load (8-B aligned: gfx950 global loads need only dword alignment);
+  // the second entry of an odd row's last pair lies past the row -- read (the CSR arrays carry
+  // two entries of padding) but never used: the probes and the chain stop at dl
 #pragma unroll
   for (int x = 0; x < LMAX; x += 2) {
     Pair2 ce = {0u, 0u, 0u, 0u};
@@ -210,6 +275,7 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     c[x + 1] = ce.c1;
     w[x + 1] = __uint_as_float(ce.v1);
   }
+  tk.tick(4);
 #pragma unroll
   for (int sb = 0; sb < LMAX / LB; ++sb) {
     if (!__any(dl > (uint32_t)(sb * LB))) continue;   // (continue, not break: keeps it unrolled)
@@ -219,28 +285,41 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
     int q[LB];
     find_batch<GT, LB>(t, key, nq, q);
+    tk.tick(5);
     if (kind & K_PULL) {
+      float xs[LB];
+#pragma unroll
+      for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
 #pragma unroll
       for (int x = 0; x < LB; ++x)
-        if (q[x] >= 0) acc = fmaf(w[sb * LB + x], t.s[q[x]], acc);   // absent: skipped (exact)
+        if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
     }
+    tk.tick(6);
     if (kind & (K_REACH | K_PROP)) {
 #pragma unroll
       for (int x = 0; x < LB; ++x)
         if ((uint32_t)x < nq) grow_entry<GT>(t, key[x], q[x], kind, h);
     }
+    tk.tick(7);
   }
+}
+
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 
 // The in-order fmaf chain of one hub-row segment: lane j holds entry j's (w, x) (x of an
 // absent neighbour is +0: fmaf(w, +0, acc) == acc for finite w and acc != -0, so running the
 // chain over every entry equals running it over the present ones).  `rem` = entries left in
-// the row (>= 1, wave-uniform); the result is in every lane (HUBCHAIN 1) or in lane m (2).
+// the row (>= 1, wave-uniform); the result is in every lane (FR_HUBCHAIN 1) or in lane m (2).
+//   FR_HUBCHAIN 1: every entry, unrolled by 8 with immediate lane indices
+//   FR_HUBCHAIN 2: the pairs go through the wave's LDS scratch and lane m runs the chain from
+//                  16-B LDS reads (one lane, 4-cycle dependent fmas)
 __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32_t rem, int m,
                                           float& hacc, float2* chain) {
   const int lane = threadIdx.x & 63;
 #if FR_HUBCHAIN == 1
-  (void)m; (void)chain; (void)lane;
+  (void)present; (void)m; (void)chain; (void)lane;
   const float xw = present ? w : 0.f;
   const int n = (int)min(rem, 64u);
   for (int y0 = 0; y0 < n; y0 += 8) {
@@ -248,6 +327,7 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
     for (int y = 0; y < 8; ++y) hacc = fmaf(readlane_f(xw, y0 + y), readlane_f(x, y0 + y), hacc);
   }
 #else
+  (void)present;
   chain[lane] = make_float2(present ? w : 0.f, x);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -279,59 +359,79 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
 //         hop 0; the incident vertex inserts its neighbours at depth 1.
 //   PULL (hop h): a member pulled at h (`need` bit h & 1, or a seed) recomputes its score:
 //         its sum over its row, CSR order, of val * s[neighbour] (non-members skipped: exact,
-//         see frontier.hip) -> snew[member index]; unless h is the last hop it also inserts
-//         its neighbours and marks them `need` for h + 1 (a superset of the expansion of the
-//         non-zero members: harmless).  Members at reach depth h + 2 insert their neighbours
-//         with depth h + 3 in the same walk (reach runs two walks ahead of the pulls, so with
-//         A.prune the last pull skips every member outside the candidate set: their final
-//         scores are never read).  Insertions during the pass are exact: a new member's score
-//         is +0, so a pull that sees it or not reads the same term.
+//         see the file comment) -> snew[member index]; unless h is the last hop it also
+//         inserts its neighbours and marks them `need` for h + 1 (a superset of the expansion
+//         of the non-zero members: harmless).  Members at reach depth h + 1 insert their
+//         neighbours with depth h + 2 in the same walk (reach runs one walk ahead of the
+//         pulls, so with A.prune the last pull skips every member outside the candidate set:
+//         their final scores are never read).  Insertions during the pass are exact: a new
+//         member's score is +0, so a pull that sees it or not reads the same term.
 // Rows of <= LMAX entries run one lane per row (light_row); longer rows (hubs) run one at a
-// time across the whole wave: 64 entries loaded and probed per round.  Wave w walks chunks
-// k = 0, 1, ... holding members w + NWAVES * (lane + 64 k): vertices inserted together (the
-// incident's Node hubs, all reached at one level) spread over the waves.
+// time across the whole wave: 64 entries loaded and probed per round, the fmaf chain over the
+// present entries in lane (= CSR) order with v_readlane operands (every lane computes the
+// same chain; the owner keeps it).
 template <bool GT, Phase PH>
-__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int h, Work& work) {
+__device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint32_t n, int h, Work& work,
+                                          int b) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
+  Ticker tk;
+  tk.on = A.prof && b >= 0;
+  if (tk.on) tk.t0 = wall_clock64();
   const bool prop_next = h + 1 < A.hops;
   const uint32_t par = (uint32_t)h & 1u;
+  // walk h (SEEDS: h = -1) expands the members at depth h + REACH_AHEAD into reach level
+  // h + REACH_AHEAD + 1: every level <= hops exists before the walk of hop hops - 2 starts
   const uint32_t reach_fl = (uint32_t)(h + REACH_AHEAD + 1);   // fl of the expanded depth
   const bool reach_lvl = h + REACH_AHEAD + 1 <= A.hops;
   const bool prune_now = PH == PULL && A.prune && h == A.hops - 1;
   const uint32_t noins = (A.prune && h == A.hops - 2) ? K_NOINS : 0u;
-  float2* const chain = t.chain ? t.chain + wave * 64 : nullptr;
+  float2* const chain = t.chain ? t.chain + wave * CHAIN_W : nullptr;
+  auto is_cand = [&](uint8_t f) { return cand_depth(f, A.hops); };
+  // Work split.  A walk is cut into chunks of FT members, striped over the waves: wave w walks
+  // chunks k = 0, 1, ... holding members w + NWAVES * (lane + 64 k), so vertices inserted
+  // together (e.g. the incident's Node hubs, all reached at one level) spread over different
+  // waves.  The next chunk's selection and row_ptr loads are issued before the current chunk is
+  // walked (a member's kind cannot change during the pass: see the comment above).
+  // FR_DBUF pulls (DW): every member of the walk writes its hop h + 1 score into the other
+  // buffer (0 when not pulled, + s0 for a seed), clears its hop-h need bit and, after the last
+  // pull, gets NEED_EXCL when it is a candidate carrying the excluded label.
+  constexpr bool DW = DBUF && !GT && PH == PULL;
+  const bool last_pull = h == A.hops - 1;
+  const bool mark_excl = DW && last_pull && A.exclude >= 0;
+  constexpr uint32_t NOP = 0xFFFFFFFFu;
   struct Chunk {
     uint32_t i, kind, e0, e1;
+    uint32_t p;      // DW: the member's slot | (0x100 | label) << 16 for a candidate (NOP: none)
+    float s0;        // DW: the member's seed value (0 unless a seed)
   };
   const uint32_t nch = (n + FT - 1) / FT;
+  auto member_of = [&](uint32_t c) { return wave + NWAVES * (lane + 64u * c); };
   auto fetch = [&](uint32_t c) {
-    Chunk ch{wave + NWAVES * (lane + 64u * c), 0u, 0u, 0u};
+    Chunk ch{member_of(c), 0u, 0u, 0u, NOP, 0.f};
     uint32_t v = 0;
     if (c < nch && ch.i < n) {
       uint32_t p = t.mlist[ch.i];
-#ifdef EGR_FR_GUARDS   // debug builds: count and skip corrupt member slots / keys
-      if (p >= t.cap) {
-        atomicAdd(&A.stats[5], 1ull);
-        p = 0;
-      }
-#endif
-      v = t.keys[p];
+      v = t.key(p);
       const uint8_t f = t.fl[p];
       if (reach_lvl && (f & FL_DEPTH) == reach_fl) ch.kind |= K_REACH;
       if constexpr (PH == SEEDS) {
         if (f & FL_SEED) ch.kind |= K_PROP | noins;
       } else {
         const uint32_t nd = t.need[p];
-        if ((((nd >> par) & 1u) || (f & FL_SEED)) && (!prune_now || cand_depth(f, A.hops)))
+        if ((((nd >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
           ch.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
+        if constexpr (DW) {
+          // the hop-h bit is consumed here (the copy phase of the single-buffer scheme cleared
+          // it); expansions of this walk set the other parity's bit of the same word
+          if (((nd >> par) & 1u) && !last_pull)
+            atomicAnd(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), ~((1u << par) << ((p & 3u) * 8u)));
+          ch.p = p;
+          if (f & FL_SEED) ch.s0 = t.s0g[p];
+          if (mark_excl && is_cand(f)) ch.p |= (0x100u | A.vlabel[v]) << 16;   // candidate | label
+        }
       }
     }
-#ifdef EGR_FR_GUARDS
-    if (ch.kind && v >= A.V) {   // a member key outside the graph: table corruption, counted
-      atomicAdd(&A.stats[5], 1ull);
-      ch.kind = 0;
-    }
-#endif
     if (ch.kind) {
       const RowPair rp = *reinterpret_cast<const RowPair*>(A.row_ptr + v);   // one 8-B load
       ch.e0 = rp.e0;
@@ -340,21 +440,23 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     return ch;
   };
   Chunk nxt = fetch(0);
-  for (uint32_t c = 0; c < nch; ++c) {
+  for (uint32_t c_cur = 0; c_cur < nch; ++c_cur) {
     if constexpr (!GT) {
       if (*t.ovf) break;        // overflowed LDS table: the column is redone elsewhere
     }
     const Chunk cur = nxt;
-    nxt = fetch(c + 1);
+    nxt = fetch(c_cur + 1);
     const uint32_t i = cur.i, kind = cur.kind, e0 = cur.e0, deg = cur.e1 - cur.e0;
     if (kind) {
       ++work.rows;
       if (kind & K_PULL) work.pull += deg;
       else work.expand += deg;
     }
+    tk.tick(0);
     const bool light = deg <= (uint32_t)LMAX;
     float acc = 0.f;
-    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc);
+    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
+    tk.tick(1);
     uint64_t heavy = __ballot(!light);
     while (heavy) {
       const int m = __ffsll((long long)heavy) - 1;
@@ -368,26 +470,86 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         const bool act = j < hdeg;
         const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
         const uint32_t u = ce.x;
+        tk.tick(8);
         const int q = act ? tab_find<GT>(t, u) : -1;
+        tk.tick(9);
         if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
-          const float x = q >= 0 ? t.s[q] : 0.f;
+          const float x = q >= 0 ? t.sc(q) : 0.f;
           hub_chain(w, x, q >= 0, hdeg - base, m, hacc, chain);
         }
+        tk.tick(10);
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
+        tk.tick(11);
       }
       if (lane == m) acc = hacc;
     }
-    if constexpr (PH == PULL) {
+    tk.tick(2);
+    if constexpr (DW) {
+      if (cur.p != NOP) {
+        const uint32_t p = cur.p & 0xFFFFu;
+        // = the copy (pulled ? acc : +0) then the seed add (+ s0): the same fadd, bit for bit
+        // (s0 is +0 for a non-seed, and r + +0 == r: r is never -0)
+        t.snew[p] = ((kind & K_PULL) ? acc : 0.f) + cur.s0;
+        if (mark_excl && (cur.p >> 16) == (0x100u | (uint8_t)A.exclude))
+          atomicOr(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), (uint32_t)NEED_EXCL << ((p & 3u) * 8u));
+      }
+    } else if constexpr (PH == PULL) {
       if (kind & K_PULL) t.snew[i] = acc;
     }
+    tk.tick(3);
   }
+  if (tk.on && lane == 0)
+    for (int k = 0; k < 12; ++k)
+      A.prof[((size_t)b * PROF_SLOTS + 24 + k) * PROF_W + 1 + wave] = tk.sub[k];
+}
+
+// ---- top-k keys: (score desc, vertex asc) as one u64, larger = better, 0 = none -----------
+__device__ __forceinline__ uint64_t topk_key(float s, uint32_t v) {
+  const uint32_t f = __float_as_uint(s);
+  const uint32_t o = (f & 0x80000000u) ? ~f : (f | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)~v;
+}
+
+__device__ __forceinline__ void topk_unkey(uint64_t k, float& s, uint32_t& v) {
+  if (k == 0) {
+    s = -INFINITY;
+    v = NO_NODE;
+    return;
+  }
+  const uint32_t o = (uint32_t)(k >> 32);
+  s = __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+  v = ~(uint32_t)k;
+}
+
+// wave-wide max of a u32 with DPP row ops (quad perms, half / full row mirror, row broadcasts
+// 15 and 31), result from lane 63; every lane gets it
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0xB1, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x4E, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x141, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x140, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
+// wave-wide max of a u64 key: the max high word, then the max low word among its holders (a
+// second reduction only when several lanes hold that high word: scores are mostly distinct)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+  const uint32_t hi = (uint32_t)(k >> 32);
+  const uint32_t mh = wave_max_u32(hi);
+  const uint64_t holders = __ballot(hi == mh);
+  const uint32_t ml = (holders & (holders - 1))
+                          ? wave_max_u32(hi == mh ? (uint32_t)k : 0u)
+                          : (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, __ffsll((long long)holders) - 1);
+  return ((uint64_t)mh << 32) | ml;
 }
 
 struct Shared {
   uint32_t count, ovf, item;
-#if FR_HUBCHAIN >= 2
-  float2 chain[NWAVES][64];   // hub-row chain pairs, one row per wave
+#if FR_HUBCHAIN == 2
+  float2 chain[NWAVES][CHAIN_W];   // hub-row chain pairs, one row per wave
 #define SH_CHAIN (&sh.chain[0][0])
 #else
 #define SH_CHAIN nullptr
@@ -404,10 +566,10 @@ __device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, u
   if (p >= t.cap) return 0;
   const uint8_t f = t.fl[p] & FL_DEPTH;
   if (f < 1 || f > maxd) return 0;
-  const uint32_t v = t.keys[p];
+  const uint32_t v = t.key(p);
   if (v >= A.V) return 0;
   if (A.exclude >= 0 && (t.need[p] & NEED_EXCL)) return 0;   // marked after the last pull
-  return topk_key(t.s[p], v);
+  return topk_key(t.sc(p), v);
 }
 
 // This thread's best candidate key strictly below `bound` (global variant: rescans).
@@ -422,20 +584,60 @@ __device__ __forceinline__ uint64_t rescan_best(const FArgs& A, const Tab<GT>& t
   return b;
 }
 
-// Per-wave top-k into sh.top[wave][0..k): the LDS table keeps every candidate of a thread in
-// MPT sorted registers (frontier_common.h); the global variant rescans for each round.
+// Per-wave top-k into sh.top[wave][0..k) (k wave-wide max rounds, no block barrier).
 template <bool GT>
 __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shared& sh, uint32_t n,
-                                          uint8_t maxd) {
+                                          uint8_t maxd, int b = -1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if constexpr (!GT) {
+    // diagnostics (profiling on): per-wave time of the candidate loads and of the k rounds
+    const bool prof = A.prof && b >= 0;
+    const uint64_t tp0 = prof ? wall_clock64() : 0;
     uint64_t kk[MPT];
 #pragma unroll
     for (int j = 0; j < MPT; ++j) {
       const uint32_t i = threadIdx.x + j * FT;
       kk[j] = i < n ? cand_key<GT>(A, t, t.mlist[i], maxd) : 0ull;
     }
-    wave_topk_sorted<MPT>(kk, A.k, sh.top[wave]);
+    // descending odd-even transposition sort of the lane's keys (MPT passes): the round's
+    // winner lane then only shifts its registers (profiles/r02_ab_topk_sort.txt)
+    static_assert(MPT <= 9, "sorted candidate registers");
+#pragma unroll
+    for (int pass = 0; pass < MPT; ++pass)
+#pragma unroll
+      for (int j = pass & 1; j + 1 < MPT; j += 2) {
+        const uint64_t x = kk[j], y = kk[j + 1];
+        const bool sw = y > x;
+        kk[j] = sw ? y : x;
+        kk[j + 1] = sw ? x : y;
+      }
+    uint64_t lb = kk[0];
+    uint64_t tp1 = 0;
+    if (prof) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      tp1 = wall_clock64();
+    }
+    // one round: the wave's next best key into sh.top[wave][q]; stop once the wave has no
+    // candidate left (the rest of its list zero-filled)
+    for (int q = 0; q < A.k; ++q) {
+      const uint64_t wb = wave_max_u64(lb);
+      if (lane == 0) sh.top[wave][q] = wb;
+      if (wb == 0) {                         // uniform: no candidate left in this wave
+        for (int r = q + 1 + lane; r < A.k; r += 64) sh.top[wave][r] = 0;
+        break;
+      }
+      if (lb == wb) {                        // keys are distinct: one lane, its head taken
+#pragma unroll
+        for (int j = 0; j + 1 < MPT; ++j) kk[j] = kk[j + 1];
+        kk[MPT - 1] = 0;
+        lb = kk[0];
+      }
+    }
+    if (prof && lane == 0) {
+      const uint64_t tp2 = wall_clock64();
+      A.prof[((size_t)b * PROF_SLOTS + 36) * PROF_W + 1 + wave] = tp1 - tp0;
+      A.prof[((size_t)b * PROF_SLOTS + 37) * PROF_W + 1 + wave] = tp2 - tp1;
+    }
   } else {
     uint64_t lb = rescan_best<GT>(A, t, n, maxd, ~0ull);
     for (int q = 0; q < A.k; ++q) {
@@ -452,7 +654,8 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
 
 // Phase boundary: a barrier, then the member count and overflow flag every thread sees, then a
 // second barrier.  Reading them after a single barrier races with the next phase's inserts by
-// faster waves: a late wave could see an overflow set by the others and leave alone.
+// faster waves: a late wave could see an overflow the others missed and leave alone, and the
+// rest would walk a member list longer than the table's limit.
 __device__ __forceinline__ bool phase_sync(Shared& sh, uint32_t& cnt) {
   __syncthreads();
   cnt = sh.count;
@@ -473,11 +676,50 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
     ++slot;
   };
+  auto wstamp = [&]() {
+    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
+  };
   const uint32_t n = cnt;
+  // top-k over the reach set: each wave its own k best, then wave 0 merges the NWAVES lists
   const int lane = tid & 63, wave = tid >> 6;
-  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1));
+  wave_topk<GT>(A, t, sh, n, (uint8_t)(hops + 1), b);
+  wstamp();
   __syncthreads();
-  if (wave == 0) merge_topk<NWAVES>(sh.top, A.k, b, A.out_ids, A.out_scores);
+  if (wave == 0) {
+    // merge by rank: each of the NWAVES * k candidates counts the candidates above it (keys
+    // are distinct: a member is in one wave's list) and lands at its rank; the slots past the
+    // number of candidates get EGR_NO_NODE / -inf
+    uint64_t c[2];
+    uint32_t nnz = 0;
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int cc = lane + 64 * y, w = cc / KMAXF, r = cc % KMAXF;
+      c[y] = (w < NWAVES && r < A.k) ? sh.top[w][r] : 0ull;
+      nnz += (uint32_t)__popcll(__ballot(c[y] != 0));
+    }
+    uint32_t rank[2] = {0u, 0u};
+    for (int w = 0; w < NWAVES; ++w)
+      for (int r = 0; r < A.k; ++r) {
+        const uint64_t o = sh.top[w][r];
+        rank[0] += o > c[0];
+        rank[1] += o > c[1];
+      }
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      if (c[y] != 0 && rank[y] < (uint32_t)A.k) {
+        float sc;
+        uint32_t v;
+        topk_unkey(c[y], sc, v);
+        A.out_ids[(size_t)b * A.k + rank[y]] = v;
+        A.out_scores[(size_t)b * A.k + rank[y]] = sc;
+      }
+    }
+    for (uint32_t q = nnz + lane; q < (uint32_t)A.k; q += 64) {
+      A.out_ids[(size_t)b * A.k + q] = NO_NODE;
+      A.out_scores[(size_t)b * A.k + q] = -INFINITY;
+    }
+  }
   stamp();
   // members -> pool (coalesced by member index)
   if (tid == 0) sh.base = A.pool_cap ? atomicAdd(A.pool_ctr, (unsigned long long)n) : 0ull;
@@ -500,8 +742,8 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
   if (keep) {
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
-      A.pool_v[base + i] = t.keys[p];
-      A.pool_s[base + i] = t.s[p];
+      A.pool_v[base + i] = t.key(p);
+      A.pool_s[base + i] = t.sc(p);
       A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
     }
   }
@@ -525,11 +767,16 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   const int hops = A.hops;
   Work work;
   // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
+  // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
   int slot = 0;
   auto stamp = [&]() {
     if (A.prof && tid == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
     ++slot;
+  };
+  auto wstamp = [&]() {
+    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+      A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   stamp();
   // The incident vertex and its row (reach level 1) are loaded first: their latency hides
@@ -543,8 +790,9 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   // slot's 0 lies below every float's image, -inf included) -- fmaxf, like the dense plan's
   // seed prep.  Pass 2: one entry per vertex claims it, turns the slot back into the float and
   // records (slot, s0) for the per-hop seed add; thread 0 also inserts the incident vertex.
-  const uint32_t ns = A.n_seeds;
-  const uint32_t sb = min(A.seed_ptr[b], ns), se = max(sb, min(A.seed_ptr[b + 1], ns));
+  // (offsets clamped to the entries given: egr_frontier_run_grouped takes them from the caller)
+  const uint32_t sb = min(A.seed_ptr[b], A.n_seeds);
+  const uint32_t se = max(sb, min(A.seed_ptr[b + 1], A.n_seeds));
   auto ord = [](float f) {
     const uint32_t u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -558,30 +806,31 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   for (uint32_t i = i0; i < se; i += FT) {
     const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
     const float x = i == i0 ? x0 : A.seed_val[i];
-    if (v >= A.V) continue;
+    if (v >= A.V) continue;          // (grouped seeds: out-of-range vertices are dropped)
     const int q = tab_insert<GT>(t, v);
     if (q >= 0) {
-      atomicMax(reinterpret_cast<unsigned int*>(t.s + q), ord(x));
+      atomicMax(reinterpret_cast<unsigned int*>(&t.s[q]), ord(x));
       atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
                (uint32_t)FL_SEED << (((uint32_t)q & 3u) * 8u));
     }
   }
   __syncthreads();
   for (uint32_t i = i0; i < se; i += FT) {
-    const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
-    const int q = v < A.V ? tab_find<GT>(t, v) : -1;
+    const int q = tab_find<GT>(t, i == i0 ? v0 : A.seed_vert[i]);
     uint2 r = make_uint2(NO_NODE, 0u);
     if (q >= 0) {
       const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;
       const uint32_t old = atomicOr(reinterpret_cast<uint32_t*>(t.fl) + ((uint32_t)q >> 2),
                                     (uint32_t)FL_CLAIM << sh8);
       if (!((old >> sh8) & FL_CLAIM)) {        // the claimer alone touches the value now
-        const float s0 = unord(*reinterpret_cast<unsigned int*>(t.s + q));
-        t.s[q] = s0;
+        const float s0 = unord(*reinterpret_cast<unsigned int*>(&t.s[q]));
+        t.sc(q) = s0;
         r = make_uint2((uint32_t)q, __float_as_uint(s0));
+        if constexpr (DBUF && !GT) const_cast<float*>(t.s0g)[q] = s0;   // read by its pullers
       }
     }
-    A.seed_rep[i] = r;
+    if constexpr (!(DBUF && !GT)) A.seed_rep[i] = r;
+    else (void)r;
   }
   if (tid == 0 && src_ok) {       // (a find of a seed is unaffected by concurrent inserts)
     const int q = tab_insert<GT>(t, src);
@@ -600,19 +849,41 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
       if (q >= 0 && (t.fl[q] & FL_DEPTH) == 0) t.fl[q] |= 2;   // every writer writes this
     }
   }
+  wstamp();
   uint32_t cnt;
   bool ovf = phase_sync(sh, cnt);
   stamp();
   if (ovf) return false;
   // the seeds' neighbours are the members pulled at hop 0
-  row_phase<GT, SEEDS>(A, t, cnt, -1, work);
+  row_phase<GT, SEEDS>(A, t, cnt, -1, work, -1);
+  wstamp();
   ovf = phase_sync(sh, cnt);
   stamp();
   if (ovf) return false;
+  if constexpr (DBUF && !GT) {
+    // two slot-indexed score buffers: pull h reads t.s / t.snew alternately and writes the
+    // other one (the copy, the seed add and the excluded-label marks happen in the walk)
+    float* const sbuf[2] = {t.s, t.snew};
+    for (int h = 0; h < hops; ++h) {
+      Tab<GT> th = t;
+      th.s = sbuf[h & 1];
+      th.snew = sbuf[(h + 1) & 1];
+      row_phase<GT, PULL>(A, th, cnt, h, work, h == hops - 1 ? b : -1);
+      wstamp();
+      ovf = phase_sync(sh, cnt);
+      stamp();
+      if (ovf) return false;
+      stamp();                      // (an empty copy phase: the profile's slots keep their meaning)
+    }
+    Tab<GT> tf = t;
+    tf.s = sbuf[hops & 1];
+    return finish_column<GT>(A, tf, sh, b, cnt, work, slot);
+  }
   for (int h = 0; h < hops; ++h) {
     // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
     const uint32_t n0 = cnt;
-    row_phase<GT, PULL>(A, t, n0, h, work);
+    row_phase<GT, PULL>(A, t, n0, h, work, h == hops - 1 ? b : -1);
+    wstamp();
     ovf = phase_sync(sh, cnt);
     stamp();
     if (ovf) return false;
@@ -627,23 +898,26 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     // this thread's first seed entry: its load is issued beside the copy's loads
     const uint32_t ir = sb + tid;
     const uint2 r0 = ir < se ? A.seed_rep[ir] : make_uint2(NO_NODE, 0u);
-    for (uint32_t i = tid; i < n; i += FT) {
-      const uint32_t p = t.mlist[i];
-      if (p >= t.cap) continue;
-      const uint8_t f = t.fl[p];
-      const uint8_t lab = (mark_excl && cand_depth(f, hops)) ? A.vlabel[t.keys[p]] : 0xFF;
-      const uint8_t nd = t.need[p];
-      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) && (!prune_now || cand_depth(f, hops));
-      t.s[p] = pulled ? t.snew[i] : 0.f;
+    auto copy_one = [&](uint32_t i, uint32_t p, uint8_t nd, uint8_t f, float sn, uint8_t lab) {
+      const bool pulled = i < n0 && ((nd & bit) || (f & FL_SEED)) &&
+                          (!prune_now || cand_depth(f, hops));
+      t.sc(p) = pulled ? sn : 0.f;
       uint8_t nn = nd & ~bit;
       if (mark_excl && cand_depth(f, hops) && lab == (uint8_t)A.exclude) nn |= NEED_EXCL;
       if (nn != nd) t.need[p] = nn;
+    };
+      for (uint32_t i = tid; i < n; i += FT) {
+        const uint32_t p = t.mlist[i];
+        if (p >= t.cap) continue;
+        const uint8_t f = t.fl[p];
+        const uint8_t lab = (mark_excl && cand_depth(f, hops)) ? A.vlabel[t.key(p)] : 0xFF;
+        copy_one(i, p, t.need[p], f, i < n0 ? t.snew[i] : 0.f, lab);
     }
     __syncthreads();
-    if (r0.x != NO_NODE) t.s[r0.x] = t.s[r0.x] + __uint_as_float(r0.y);
+    if (r0.x != NO_NODE) t.sc(r0.x) = t.sc(r0.x) + __uint_as_float(r0.y);
     for (uint32_t i = ir + FT; i < se; i += FT) {
       const uint2 r = A.seed_rep[i];
-      if (r.x != NO_NODE) t.s[r.x] = t.s[r.x] + __uint_as_float(r.y);
+      if (r.x != NO_NODE) t.sc(r.x) = t.sc(r.x) + __uint_as_float(r.y);
     }
     __syncthreads();
     stamp();
@@ -659,7 +933,16 @@ struct LdsTab {
   uint32_t needw[LCAP / 4];
   uint16_t mlist[LLIMIT];
   uint32_t bloom[BLOOM_WORDS];
+#if FR_DBUF
+  float s2[LCAP];              // the second slot-indexed score buffer (FR_DBUF)
+#endif
 };
+#define LDS_S_PTR L.s
+#if FR_DBUF
+#define LSNEW_PTR L.s2
+#else
+#define LSNEW_PTR (A.lsnew + (size_t)b * LLIMIT)
+#endif
 
 // One column in the LDS table: clear, run, and on overflow hand the column on (A.ovf_list).
 __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh) {
@@ -669,6 +952,9 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   for (int i = 0; i < LPPT; ++i) {
     L.keys[tid + i * FT] = EMPTY;
     L.s[tid + i * FT] = 0.f;
+#if FR_DBUF
+    L.s2[tid + i * FT] = 0.f;
+#endif
   }
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.flw[i] = 0;
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.needw[i] = 0;
@@ -678,9 +964,9 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
-  Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom,
-               SH_CHAIN};
+  Tab<false> t{L.keys, LDS_S_PTR, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
+               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN,
+               A.lsnew + (size_t)b * LCAP};   // (FR_DBUF: seed values by slot; LCAP <= lsnew's stride)
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
@@ -689,23 +975,28 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   }
 }
 
+// The kernels this geometry launches (FR_KERNELS: 1 = frontier_lds_kernel, 2 =
+// frontier_lds_retry_kernel, 4 = frontier_global_kernel).
+#if FR_KERNELS & 1
 // One workgroup per column, in launch order (A.order).
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
 void frontier_lds_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
   const int b = (int)A.order[blockIdx.x];
-  if (threadIdx.x == 0 && A.seed_cnt) {   // the sorting path's counters: consumed
-    A.seed_cnt[b] = 0;
+  if (threadIdx.x == 0 && A.seed_cnt) {   // the sort's seed counters are consumed: leave them
+    A.seed_cnt[b] = 0;                      // zero for the next set_seeds
     A.seed_cnt[A.B + b] = 0;
   }
   lds_column(A, b, L, sh);
 }
+#endif
 
-// Second chance: a persistent grid over the columns another kernel handed on (A.retry_list,
-// *A.retry_n entries): block i takes entries i, i + gridDim.x, ...; those that overflow this
-// table too go on to the global-memory variant.  Every block leaves once the list is drained
-// (an empty list: at once).
+#if FR_KERNELS & 2
+// Second chance: a persistent grid over the columns another geometry's LDS kernel handed on
+// (A.retry_list, *A.retry_n entries): block i takes entries i, i + gridDim.x, ...; those that
+// overflow this table too go on to the global-memory variant.  Every block leaves once the
+// list is drained (an empty list: at once).
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
 void frontier_lds_retry_kernel(const FArgs A) {
   __shared__ LdsTab L;
@@ -716,7 +1007,9 @@ void frontier_lds_retry_kernel(const FArgs A) {
     __syncthreads();              // the next column clears the table this one used
   }
 }
+#endif
 
+#if FR_KERNELS & 4
 // Persistent fallback: each workgroup owns one global table and drains the overflow list.
 __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   __shared__ Shared sh;
@@ -752,11 +1045,14 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
       const uint32_t p = t.mlist[i];
       if (p >= cap) continue;
       t.keys[p] = EMPTY;
-      t.s[p] = 0.f;
+      t.sc(p) = 0.f;
       t.fl[p] = 0;
       t.need[p] = 0;
     }
     __syncthreads();
   }
 }
+#endif
+#undef LSNEW_PTR
 #undef SH_CHAIN
+#undef LDS_S_PTR

@@ -1132,6 +1132,13 @@ void egr_plan_free(egr_plan* p) {
 
 int egr_plan_tile_width(const egr_plan* p) { return p ? p->TW : -1; }
 
+int egr_plan_shape(const egr_plan* p, int64_t* n_vertices, int32_t* n_cols) {
+  if (!p) return egr::fail(EGR_EINVAL, "egr_plan_shape: NULL plan");
+  if (n_vertices) *n_vertices = p->s->V;
+  if (n_cols) *n_cols = p->B;
+  return EGR_OK;
+}
+
 
 static int plan_stale(const egr_plan* p, const char* what) {
   return egr::fail(EGR_ESTATE, std::string(what) +
@@ -1450,6 +1457,14 @@ int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const int width = reach ? p->W : p->Bpad;
+  // a score entry packs (row-in-segment * width + column) into the high 32 bits: refuse a
+  // segment whose index range would wrap (the reach format keeps two words and has no limit)
+  if (!reach)
+    for (int q = 0; q < P; ++q)
+      if ((uint64_t)(seg[q + 1] - seg[q]) * (uint64_t)width >= (1ull << 32))
+        return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse: a peer segment of " +
+                         std::to_string(seg[q + 1] - seg[q]) + " rows x " + std::to_string(width) +
+                         " columns exceeds the 2^32 entry index of the score format");
   if ((size_t)n + 1 > p->sx_cap) {
     dfree(p->sx_off);
     p->sx_cap = 0;

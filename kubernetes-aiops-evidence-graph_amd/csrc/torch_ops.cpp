@@ -18,6 +18,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <string>
 #include <tuple>
 
 #include "egraph.h"
@@ -39,6 +40,24 @@ void need(const at::Tensor& t, at::ScalarType st, const char* name) {
   TORCH_CHECK_VALUE(t.is_cuda(), name, " must be a device (HIP) tensor");
   TORCH_CHECK_VALUE(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", need ", st);
   TORCH_CHECK_VALUE(t.is_contiguous(), name, " must be contiguous");
+}
+
+// the engine's own sizes: every op checks the caller's arguments against them, because the C
+// calls read and write by the engine's sizes (a mismatch would be an out-of-bounds access)
+void check_frontier_shape(const egr_frontier* f, int64_t n_cols, int64_t k) {
+  int32_t B = 0, K = 0;
+  check_rc(egr_frontier_shape(f, &B, &K), "egraph::frontier_run (shape)");
+  TORCH_CHECK_VALUE(n_cols == B && k == K, "egraph::frontier_run: the frontier was created for ",
+                    B, " columns and k = ", K, ", got n_cols = ", n_cols, ", k = ", k);
+}
+
+void check_plan_shape(const egr_plan* p, int64_t n_vertices, int64_t n_cols, const char* what) {
+  int64_t V = 0;
+  int32_t B = 0;
+  check_rc(egr_plan_shape(p, &V, &B), what);
+  TORCH_CHECK_VALUE(n_vertices == V && (n_cols < 0 || n_cols == B), what, ": the plan is for ", V,
+                    " vertices and ", B, " columns, got n_vertices = ", n_vertices,
+                    n_cols >= 0 ? ", n_cols = " : "", n_cols >= 0 ? std::to_string(n_cols) : "");
 }
 
 template <class T>
@@ -105,6 +124,7 @@ std::tuple<at::Tensor, at::Tensor> frontier_run(int64_t frontier, const at::Tens
   const int64_t n = seed_vertex.numel();
   TORCH_CHECK_VALUE(seed_col.numel() == n && seed_val.numel() == n, "seed arrays differ in length");
   TORCH_CHECK_VALUE(sources.numel() == n_cols, "need one source vertex per column");
+  check_frontier_shape(f, n_cols, k);
   void* st = cur_stream(sources);
   at::Tensor ids = at::empty({n_cols, k}, sources.options());
   at::Tensor scores = at::empty({n_cols, k}, seed_val.options());
@@ -130,6 +150,7 @@ at::Tensor propagate(int64_t plan, const at::Tensor& seed_vertex, const at::Tens
   const int64_t n = seed_vertex.numel();
   TORCH_CHECK_VALUE(seed_col.numel() == n && seed_val.numel() == n, "seed arrays differ in length");
   TORCH_CHECK_VALUE(hops >= 1, "hops must be >= 1");
+  check_plan_shape(p, n_vertices, n_cols, "egraph::propagate");
   void* st = cur_stream(seed_val);
   check_rc(egr_plan_set_seeds(p, reinterpret_cast<const uint32_t*>(seed_vertex.data_ptr<int32_t>()),
                               reinterpret_cast<const uint32_t*>(seed_col.data_ptr<int32_t>()),
@@ -146,6 +167,7 @@ at::Tensor reach(int64_t plan, const at::Tensor& sources, int64_t n_vertices, in
   auto* p = handle<egr_plan>(plan, "plan");
   need(sources, at::kInt, "sources");
   TORCH_CHECK_VALUE(hops >= 0, "hops must be >= 0");
+  check_plan_shape(p, n_vertices, sources.numel(), "egraph::reach");
   void* st = cur_stream(sources);
   check_rc(egr_plan_set_sources(p, reinterpret_cast<const uint32_t*>(sources.data_ptr<int32_t>()), st),
            "egraph::reach (sources)");
@@ -167,6 +189,11 @@ std::tuple<at::Tensor, at::Tensor> topk(int64_t snapshot, const at::Tensor& scor
   const int64_t B = scores.size(1);
   TORCH_CHECK_VALUE(reach_bits.size(0) == (B + 63) / 64 && reach_bits.size(1) == scores.size(0),
                     "reach_bits must be [ceil(B/64), V] for scores [V, B]");
+  int64_t V = 0, nnz = 0;
+  check_rc(egr_snapshot_info(s, &V, &nnz), "egraph::topk (shape)");
+  TORCH_CHECK_VALUE(scores.size(0) == V, "egraph::topk: scores has ", scores.size(0),
+                    " rows, the snapshot ", V, " vertices");
+  TORCH_CHECK_VALUE(k >= 1 && k <= 16, "egraph::topk: need 1 <= k <= 16");
   at::Tensor ids = at::empty({B, k}, scores.options().dtype(at::kInt));
   at::Tensor out = at::empty({B, k}, scores.options());
   check_rc(egr_topk(s, scores.data_ptr<float>(),

@@ -99,6 +99,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_plan_create": (C.c_int, [P, I32, I64, I32, C.POINTER(P)]),
     "egr_plan_free": (None, [P]),
     "egr_plan_tile_width": (C.c_int, [P]),
+    "egr_plan_shape": (C.c_int, [P, P, P]),
     "egr_plan_set_seeds": (C.c_int, [P, P, P, P, I64, P]),
     "egr_plan_set_sources": (C.c_int, [P, P, P]),
     "egr_plan_hop": (C.c_int, [P, P]),

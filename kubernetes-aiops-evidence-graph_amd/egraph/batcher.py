@@ -359,26 +359,52 @@ class RulesBatcher:
         if not ok:
             return
         enc = concat(encs)
+        self.launches += 1
         try:
-            self.launches += 1
             res = await self.runner.run(enc)
+        except asyncio.CancelledError:
+            # the task that launched this batch was cancelled (e.g. an activity timeout) while
+            # its kernel runs: finish the launch here -- the next launch reuses its buffers --
+            # and serve the other calls of the batch, then let the cancellation through
+            try:
+                self.runner.event.synchronize()
+                res = self.runner.results()
+            except BaseException as e:                      # noqa: BLE001 (re-raised below)
+                self._fail(ok, e)
+                raise
+            self._finish(ok, enc, res)
+            raise
         except Exception as e:                              # noqa: BLE001 (device failure)
-            for c in ok:
-                if not c.fut.done():
-                    c.fut.set_exception(e)
+            self._fail(ok, e)
             return
-        with gc_paused():
-            if len(ok) == 1:               # (a lone call: its lists are the whole result)
-                c = ok[0]
-                lists = hypothesis_lists(self.cat, res, c.incident_ids, enc.evidence_ids, c.ranked)
-                if not c.ranked:
-                    FUSED.register(self.cat, res, lists, range(len(lists)))
-                if not c.fut.done():
-                    c.fut.set_result(lists)
-                return
-            # incident rows of every call, then one native assembly per ranking mode
-            starts = np.cumsum([0] + [len(c.incident_ids) for c in ok])
-            self._deliver(ok, starts, enc, res)
+        self._finish(ok, enc, res)
+
+    @staticmethod
+    def _fail(calls: list, e: BaseException) -> None:
+        for c in calls:
+            if not c.fut.done():
+                c.fut.set_exception(e)
+
+    def _finish(self, ok: list, enc: EncodedBatch, res: RulesResult) -> None:
+        """Deliver a finished launch's lists; a failure while assembling them goes to every call
+        still waiting (none is left pending)."""
+        try:
+            with gc_paused():
+                if len(ok) == 1:               # (a lone call: its lists are the whole result)
+                    c = ok[0]
+                    lists = hypothesis_lists(self.cat, res, c.incident_ids, enc.evidence_ids, c.ranked)
+                    if not c.ranked:
+                        FUSED.register(self.cat, res, lists, range(len(lists)))
+                    if not c.fut.done():
+                        c.fut.set_result(lists)
+                    return
+                # incident rows of every call, then one native assembly per ranking mode
+                starts = np.cumsum([0] + [len(c.incident_ids) for c in ok])
+                self._deliver(ok, starts, enc, res)
+        except BaseException as e:                          # noqa: BLE001
+            self._fail(ok, e)
+            if not isinstance(e, Exception):
+                raise
 
     def _deliver(self, ok: list, starts, enc: EncodedBatch, res: RulesResult) -> None:
         for ranked in (False, True):

@@ -338,6 +338,9 @@ def _exchange_sparse_py(runs: list[RankRun], comm, what: str) -> None:
         local = (row - seg_t[peer]) * width + (nz % width)       # index inside the peer's segment
         counts = torch.bincount(peer, minlength=len(r.lg.send_counts)).cpu().tolist()
         if what == "scores":
+            if int(np.diff(seg).max(initial=0)) * width >= 1 << 32:
+                raise ValueError("sparse score exchange: a peer segment's (row, column) index "
+                                 "exceeds 2^32 (rows x columns); use the dense halo")
             vbits = flat[nz].view(torch.int32).to(torch.int64) & 0xFFFFFFFF
             payload = (local << 32) | vbits
             n_per = [c for c in counts]

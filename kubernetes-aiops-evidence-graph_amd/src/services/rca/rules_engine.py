@@ -16,6 +16,9 @@ fallback: without a ROCm GPU the call raises RuntimeError.
 """
 from __future__ import annotations
 
+import asyncio
+import weakref
+
 from egraph import catalog as _catalog
 from egraph.batcher import RulesBatcher
 from src.models import HypothesisCategory
@@ -28,16 +31,28 @@ DIAGNOSIS_RULES = [
 ]
 
 
+# id(catalog) -> (weak ref to the catalog, {event loop (weak) -> {device: batcher}}).  A batcher
+# lives as long as its catalog and its loop: a new catalog that reuses a dead one's id() gets a
+# batcher of its own (never the old rule table), and a loop that closed mid-launch (asyncio.run
+# in tests, a worker restart) leaves no busy batcher behind for the next loop to wait on.
 _BATCHERS: dict = {}
 
 
 def _batcher(catalog: _catalog.Catalog, device) -> RulesBatcher:
-    """The process-wide batcher of a (catalog, device): concurrent activities share it, so
-    calls that overlap in time go out in one launch."""
-    key = (id(catalog), str(device))
-    b = _BATCHERS.get(key)
+    """The batcher of a (catalog, running event loop, device): concurrent activities of one
+    worker loop share it, so calls that overlap in time go out in one launch."""
+    key = id(catalog)
+    ent = _BATCHERS.get(key)
+    if ent is None or ent[0]() is not catalog:
+        ent = _BATCHERS[key] = (weakref.ref(catalog, lambda _r, k=key: _BATCHERS.pop(k, None)),
+                                weakref.WeakKeyDictionary())
+    loop = asyncio.get_running_loop()
+    per_dev = ent[1].get(loop)
+    if per_dev is None:
+        per_dev = ent[1][loop] = {}
+    b = per_dev.get(str(device))
     if b is None:
-        b = _BATCHERS[key] = RulesBatcher(catalog, device)
+        b = per_dev[str(device)] = RulesBatcher(catalog, device)
     return b
 
 

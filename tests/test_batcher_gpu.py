@@ -70,13 +70,15 @@ def test_concurrent_calls_coalesce_and_match_golden(golden):
             return rk.rank(await eng.generate_hypotheses(inc, case["evidence"]))
         return (await eng.rank_incidents_batch([inc], [case["evidence"]]))[0]
 
-    async def go():
-        return await asyncio.gather(*[one(i, c) for i, c in enumerate(cases)])
-
     from egraph.ranker import FUSED
-    b = RE._batcher(eng.catalog, eng.device)
-    l0, c0, h0 = b.launches, b.calls, FUSED.hits
-    out = asyncio.run(go())
+    h0 = FUSED.hits
+
+    async def go():
+        b = RE._batcher(eng.catalog, eng.device)          # (one batcher per event loop)
+        return b, await asyncio.gather(*[one(i, c) for i, c in enumerate(cases)])
+
+    b, out = asyncio.run(go())
+    l0, c0 = 0, 0
     assert b.calls - c0 == len(cases)
     assert b.launches - l0 < len(cases) // 4            # coalesced
     assert FUSED.hits - h0 == len(cases) // 2           # rank() reused the kernel's ranking
@@ -103,3 +105,58 @@ def test_error_raises_in_its_own_call_only(golden):
         assert strip == rca_oracle.generate("g", c["evidence"])
     for c, r in zip(bad, out[len(good):]):
         assert isinstance(r, BaseException) and type(r).__name__ == c["raises"], c["name"]
+
+
+def test_cancelled_launcher_leaves_the_batch_intact(golden):
+    """The call that launched a batch is cancelled (an activity timeout) while its kernel runs:
+    the calls coalesced behind it still get the reference's dicts, and the next launch, which
+    reuses the same buffers, is correct too."""
+    import rca_oracle
+    from src.services.rca import rules_engine as RE
+    eng = RE.RulesEngine()
+    cases = golden["rules"]["cases"][:48]
+
+    def strip(hs):
+        return [{k: v for k, v in h.items() if k != "id"} for h in hs]
+
+    async def go():
+        first = asyncio.ensure_future(eng.generate_hypotheses(_Inc("c"), cases[0]["evidence"]))
+        rest = [asyncio.ensure_future(eng.generate_hypotheses(_Inc("c"), c["evidence"]))
+                for c in cases[1:]]
+        await asyncio.sleep(0)            # `first` has launched and yields while its kernel runs
+        first.cancel()
+        got = await asyncio.gather(*rest)
+        after = await eng.rank_incidents_batch([_Inc("c")] * 8, [c["evidence"] for c in cases[:8]])
+        try:
+            await first
+        except asyncio.CancelledError:
+            pass
+        return first, got, after
+
+    first, got, after = asyncio.run(go())
+    assert first.cancelled()
+    for c, r in zip(cases[1:], got):
+        assert strip(r) == rca_oracle.generate("c", c["evidence"]), c["name"]
+    for c, r in zip(cases[:8], after):
+        assert strip(r) == strip(rca_oracle.rca("c", c["evidence"])), c["name"]
+
+
+def test_batchers_follow_catalog_and_loop():
+    """A batcher belongs to one catalog object and one event loop: a new loop gets a fresh,
+    idle batcher, and a catalog's batcher is never handed to another catalog."""
+    from egraph import catalog
+    from src.services.rca import rules_engine as RE
+
+    async def get(cat):
+        return RE._batcher(cat, None)
+
+    c1 = catalog.default()
+    b1 = asyncio.run(get(c1))
+    b2 = asyncio.run(get(c1))
+    assert b1 is not b2 and not b2.busy
+
+    async def same_loop():
+        return RE._batcher(c1, None) is RE._batcher(c1, None)
+    assert asyncio.run(same_loop())
+    c2 = catalog.Catalog(**{f: getattr(c1, f) for f in c1.__dataclass_fields__})
+    assert asyncio.run(get(c2)).cat is c2
