@@ -50,6 +50,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
+# (A/B) seeds grouped by column on the host at setup: the step runs egr_frontier_run_grouped
+GROUPED = os.environ.get("EGRAPH_BENCH_GROUPED")
 
 
 def max_over_ranks(dist, x: float, dev) -> float:
@@ -132,7 +134,7 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     inc_label = g.labels().index("Incident")
     return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 lanes=lanes, tick=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
-                evidence=evidence)
+                evidence=evidence, incident_ids=[str(x.incident["id"]) for x in cases])
 
 
 def build_lanes(snap, B: int, max_seeds: int, k: int, pipeline: int, pool_entries: int, dev,
@@ -157,7 +159,18 @@ def build_lanes(snap, B: int, max_seeds: int, k: int, pipeline: int, pool_entrie
             pairs.append((torch.cuda.Stream(dev) if pipeline > 1 else None,
                           None if os.environ.get("EGRAPH_BENCH_ONE_STREAM") else torch.cuda.Stream(dev)))
         main, side = pairs[i % share] if share > 0 else pairs[-1]
-        lanes.append(dict(frontier=fr, rules=rules, seeds=seeds, sources=sources, main=main, side=side))
+        lane = dict(frontier=fr, rules=rules, seeds=seeds, sources=sources, main=main, side=side)
+        if GROUPED:
+            # seeds grouped by column on the host (egr_frontier_run_grouped: no device sort)
+            from egraph.graph import group_seeds, launch_order
+            gp, gv, gs = group_seeds(*(a.cpu().numpy() for a in seeds), B)
+            lane["grouped"] = tuple(torch.from_numpy(x).to(dev) for x in
+                                    (gp.view(np.int32), gv.view(np.int32), gs))
+            lane["order"] = None
+            if GROUPED == "order":
+                rp = snap.download()["row_ptr"]
+                lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
+        lanes.append(lane)
     return lanes
 
 
@@ -194,15 +207,21 @@ def lane_step(lane, hops: int, inc_label: int, ev=None, fork_join: bool = False)
             lane["rules"].launch()
     else:
         lane["rules"].launch()
-    fr.set_seeds(*lane["seeds"])
+    def run():
+        if "grouped" in lane:
+            fr.run_grouped(*lane["grouped"], lane["sources"], hops, inc_label, order=lane["order"])
+        else:
+            fr.run(lane["sources"], hops, inc_label)
+    if "grouped" not in lane:
+        fr.set_seeds(*lane["seeds"])
     if ev is not None:
         a, b = ev.pop()
         a.record()
-        fr.run(lane["sources"], hops, inc_label)
+        run()
         b.record()
         ev.done.append((a, b))
     else:
-        fr.run(lane["sources"], hops, inc_label)
+        run()
     if side is not None and fork_join:
         cur.wait_stream(side)
 
@@ -382,6 +401,52 @@ def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
                                    "in flight at once; the batcher coalesces them"}}
 
 
+def dropin_graph(ctx, dev, hops: int, k: int, reps: int = 5) -> dict:
+    """The graph half of the drop-in end to end (host buffers; reported beside `value`, never as
+    it): activities.rank_root_causes_batch on the bench batch -- evidence dicts in, seed
+    attachment on the host (egraph.seeds.seeds_for_batch), seed upload, the frontier through
+    torch.ops.egraph.frontier_run, download, ranked root-cause entity dicts out -- over the
+    bench's own graph and snapshot installed in GraphService (src/database/graph.py)."""
+    import asyncio
+
+    from egraph.seeds import seeds_for_batch
+    from src.database import GraphService
+    from src.services.workflow import activities
+    GraphService.reset()
+    GraphService._graph, GraphService._snapshot, GraphService.device = ctx["graph"], ctx["snap"], dev
+    data = [{"incident": {"id": i}, "evidence": {"evidence": ev}, "k": k}
+            for i, ev in zip(ctx["incident_ids"], ctx["evidence"])]
+
+    async def go(n):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            out = await activities.rank_root_causes_batch(data)
+            ts.append(time.perf_counter() - t0)
+        return ts, out
+
+    asyncio.run(go(1))                                            # warm (frontier creation)
+    ts, out = asyncio.run(go(reps))
+    # the host seed attachment alone (the largest host stage)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        seeds_for_batch(ctx["graph"], ctx["evidence"])
+    t_seed = (time.perf_counter() - t0) / reps
+    best = min(ts)
+    # the same batch's ids from the bench's own frontier (lane 0 ran the same evidence): the
+    # drop-in's entities must be the engine's top-k
+    g = ctx["graph"]
+    ids0 = ctx["lanes"][0]["frontier"].out_ids.view(len(data), k).cpu().numpy().view(np.uint32)
+    same = all([e["id"] for e in row] == [g.vertex_id(int(v)) for v in ids0[b] if v != 0xFFFFFFFF]
+               for b, row in enumerate(out))
+    GraphService.reset()
+    return {"value": len(data) / best, "unit": "incidents/s", "ms_per_batch": best * 1e3,
+            "incidents": len(data), "seed_attach_ms": t_seed * 1e3, "matches_engine_topk": same,
+            "what": "activities.rank_root_causes_batch: evidence dicts -> host seed attachment -> "
+                    "torch.ops.egraph.frontier_run (3-hop propagation + reach + top-k) -> ranked "
+                    "root-cause entity dicts"}
+
+
 def cpu_baseline(ctx, hops: int, k: int, threads: int, seconds: float = 8.0) -> dict:
     """The same step on the host cores: oracle/egraph_oracle.c's rules restatement plus
     orc_frontier (the frontier engine's algorithm per column: touched vertices only, pruned last
@@ -484,11 +549,16 @@ def roofline_probe(ctx, hops: int, reps: int) -> float:
     ms = []
     torch.cuda.synchronize()
     for _ in range(max(reps, 1)):
-        fr.set_seeds(*lane["seeds"])
+        if "grouped" not in lane:
+            fr.set_seeds(*lane["seeds"])
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         a.record()
-        fr.run(lane["sources"], hops, ctx["inc_label"])
+        if "grouped" in lane:
+            fr.run_grouped(*lane["grouped"], lane["sources"], hops, ctx["inc_label"],
+                           order=lane["order"])
+        else:
+            fr.run(lane["sources"], hops, ctx["inc_label"])
         b.record()
         b.synchronize()
         ms.append(a.elapsed_time(b))
@@ -1007,6 +1077,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(ctx, args.hops, args.k, threads)
     if rank == 0 and args.engine == "frontier" and not args.no_dropin:
         out["dropin_rules"] = dropin_rules(ctx, dev)
+        out["dropin_graph"] = dropin_graph(ctx, dev, args.hops, args.k)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

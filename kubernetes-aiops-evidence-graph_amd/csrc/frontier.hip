@@ -565,7 +565,7 @@ int egr_frontier_set_seeds(egr_frontier* f, const uint32_t* seed_vertex, const u
 // is used, its counters are consumed (zeroed) by the narrow kernel, and its scan zeroed the
 // run's counters.
 static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_v,
-                             const float* seed_s, int64_t n_seeds, bool sorted, const uint32_t* source_vertex,
+                             const float* seed_s, int64_t n_seeds, bool sorted, const uint32_t* order, const uint32_t* source_vertex,
                              int32_t hops, int32_t exclude_label, uint32_t* out_ids,
                              float* out_scores, hipStream_t st) {
   const egr_snapshot* s = f->s;
@@ -590,7 +590,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.n_seeds = (uint32_t)n_seeds;
   a.seed_rep = f->seed_rep;
   a.sources = source_vertex;
-  a.order = sorted ? f->order : f->ident;
+  a.order = sorted ? f->order : order ? order : f->ident;
   a.seed_cnt = sorted ? f->seed_cnt : nullptr;
   a.out_ids = out_ids;
   a.out_scores = out_scores;
@@ -687,14 +687,15 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
   if (!f->seeds_set) return egr::fail(EGR_ESTATE, "egr_frontier_run: seeds not set");
   if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run");
   DeviceGuard guard(f->s->device);
-  const int rc = frontier_run_impl(f, f->seed_ptr, f->seed_v, f->seed_s, f->n_seeds, true, source_vertex, hops,
+  const int rc = frontier_run_impl(f, f->seed_ptr, f->seed_v, f->seed_s, f->n_seeds, true, nullptr, source_vertex, hops,
                                    exclude_label, out_ids, out_scores, (hipStream_t)stream);
   if (rc == EGR_OK) f->last_n_seeds = -1;
   return rc;
 }
 
 int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_vertex,
-                             const float* seed_val, int64_t n_seeds, const uint32_t* source_vertex,
+                             const float* seed_val, int64_t n_seeds, const uint32_t* order,
+                             const uint32_t* source_vertex,
                              int32_t hops, int32_t exclude_label, uint32_t* out_ids,
                              float* out_scores, void* stream) {
   if (!f || !seed_ptr || !source_vertex || !out_ids || !out_scores || hops < 1 || hops > MAX_HOPS ||
@@ -704,7 +705,7 @@ int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const ui
                                  "n_seeds <= the frontier's max_seeds)");
   if (f->s->V > f->vmax) return frontier_outgrown(f, "egr_frontier_run_grouped");
   DeviceGuard guard(f->s->device);
-  const int rc = frontier_run_impl(f, seed_ptr, seed_vertex, seed_val, n_seeds, false, source_vertex, hops,
+  const int rc = frontier_run_impl(f, seed_ptr, seed_vertex, seed_val, n_seeds, false, order, source_vertex, hops,
                                    exclude_label, out_ids, out_scores, (hipStream_t)stream);
   if (rc == EGR_OK) f->last_n_seeds = n_seeds;
   return rc;

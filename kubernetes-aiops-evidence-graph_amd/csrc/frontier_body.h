@@ -984,6 +984,7 @@ void frontier_lds_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
   const int b = (int)A.order[blockIdx.x];
+  if (b < 0 || b >= A.B) return;          // (a caller's order that is no permutation)
   if (threadIdx.x == 0 && A.seed_cnt) {   // the sort's seed counters are consumed: leave them
     A.seed_cnt[b] = 0;                      // zero for the next set_seeds
     A.seed_cnt[A.B + b] = 0;

@@ -124,7 +124,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_free": (None, [P]),
     "egr_frontier_set_seeds": (C.c_int, [P, P, P, P, I64, P]),
     "egr_frontier_run": (C.c_int, [P, P, I32, I32, P, P, P]),
-    "egr_frontier_run_grouped": (C.c_int, [P, P, P, P, I64, P, I32, I32, P, P, P]),
+    "egr_frontier_run_grouped": (C.c_int, [P, P, P, P, I64, P, P, I32, I32, P, P, P]),
     "egr_frontier_shape": (C.c_int, [P, P, P]),
     "egr_frontier_stats": (C.c_int, [P, P, P]),
     "egr_frontier_set_retry": (C.c_int, [P, I32]),

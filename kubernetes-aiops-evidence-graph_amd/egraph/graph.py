@@ -72,6 +72,7 @@ class EvidenceGraph:
         self._type_names: list[str] = []
         self.node_props: dict[tuple[str, str], dict] = {}
         self.vertex_of: dict[tuple[str, str], int] = {}      # (label, id) -> vertex
+        self._ids: list[str] = []                           # vertex -> id (creation order)
         self.edge_props: dict[tuple[str, str, str], dict] = {}
 
     def __del__(self):
@@ -94,9 +95,11 @@ class EvidenceGraph:
         out = np.empty(len(ids), np.int32)
         L.check(L.lib.egr_graph_merge_nodes(self._h, ib, _addr(io), lb, _addr(lo), len(ids),
                                             _addr(out)), "egr_graph_merge_nodes")
-        vo = self.vertex_of
+        vo, idl = self.vertex_of, self._ids
         for i, lab, v in zip(ids, labels, out.tolist()):
             vo[(lab, i)] = v
+            if v == len(idl):                 # a new vertex (numbered in creation order)
+                idl.append(i)
         return out
 
     def merge_edges(self, src: Sequence[str], dst: Sequence[str], types: Sequence[str]) -> int:
@@ -178,6 +181,8 @@ class EvidenceGraph:
                            L.lib.egr_graph_rel_type_name)
 
     def vertex_id(self, v: int) -> str:
+        if 0 <= v < len(self._ids):
+            return self._ids[v]
         n = L.lib.egr_graph_vertex_id(self._h, v, None, 0)
         if n < 0:
             raise IndexError(v)
@@ -186,7 +191,13 @@ class EvidenceGraph:
         return buf.raw[:n].decode()
 
     def vertex_ids(self) -> list[str]:
-        return [self.vertex_id(v) for v in range(self.num_vertices)]
+        """The id of every vertex, by vertex index (a list kept by merge_nodes; rebuilt from
+        the native graph if it ever disagrees with it)."""
+        V = self.num_vertices
+        if len(self._ids) != V:
+            self._ids = []
+            self._ids = [self.vertex_id(v) for v in range(V)]
+        return self._ids
 
     def vertex_ids_set(self) -> set[str]:
         return {i for (_, i) in self.vertex_of}
@@ -515,6 +526,21 @@ def group_seeds(vertex: np.ndarray, col: np.ndarray, val: np.ndarray, n_cols: in
             np.ascontiguousarray(np.asarray(val, np.float32)[keep][order]))
 
 
+def launch_order(seed_ptr: np.ndarray, vertex: np.ndarray, row_ptr: np.ndarray) -> np.ndarray:
+    """u32 [n_cols]: the columns costliest first (cost = sum over the column's seeds of
+    1 + the seed vertex's degree, the predictor egr_frontier_set_seeds sorts by), ties in column
+    order -- the longest-processing-time-first launch order for Frontier.run_grouped."""
+    ptr = np.asarray(seed_ptr, np.int64)
+    v = np.asarray(vertex, np.int64)
+    rp = np.asarray(row_ptr, np.int64)
+    ok = v < len(rp) - 1
+    deg = np.zeros(len(v), np.int64)
+    deg[ok] = rp[v[ok] + 1] - rp[v[ok]] + 1
+    csum = np.concatenate([[0], np.cumsum(deg)])
+    cost = csum[ptr[1:]] - csum[ptr[:-1]]
+    return np.argsort(-cost, kind="stable").astype(np.uint32)
+
+
 class Frontier:
     """Per-batch frontier engine (egr_frontier_*): the same seeds / sources / top-k contract as
     Plan.run, computed per incident column over only the vertices that column touches."""
@@ -561,7 +587,8 @@ class Frontier:
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     def run_grouped(self, seed_ptr: torch.Tensor, vertex: torch.Tensor, val: torch.Tensor,
-                    sources: torch.Tensor, hops: int = 3, exclude_label: int = -1, stream=None):
+                    sources: torch.Tensor, hops: int = 3, exclude_label: int = -1, stream=None,
+                    order: torch.Tensor | None = None):
         """One pass over seeds grouped by column (egr_frontier_run_grouped): column b's seeds are
         entries [seed_ptr[b], seed_ptr[b+1]) of vertex / val (device tensors; group_seeds()
         builds them from triples).  No set_seeds, no sort on the device."""
@@ -569,8 +596,12 @@ class Frontier:
             raise ValueError(f"need one source vertex per column ({self.B}) and {self.B + 1} seed offsets")
         if vertex.numel() != val.numel():
             raise ValueError("seed arrays differ in length")
+        if order is not None and order.numel() != self.B:
+            raise ValueError(f"order needs {self.B} entries")
         L.check(L.lib.egr_frontier_run_grouped(self._h, L.ptr(seed_ptr), L.ptr(vertex), L.ptr(val),
-                                               vertex.numel(), L.ptr(sources), hops, exclude_label,
+                                               vertex.numel(),
+                                               L.ptr(order) if order is not None else None,
+                                               L.ptr(sources), hops, exclude_label,
                                                L.ptr(self.out_ids), L.ptr(self.out_scores),
                                                self._st(stream)), "egr_frontier_run_grouped")
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)

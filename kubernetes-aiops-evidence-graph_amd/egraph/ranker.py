@@ -133,9 +133,24 @@ class FusedRanks:
         self.hits = self.misses = 0
 
     def register(self, cat, res, lists: list[list[dict]], rows) -> None:
-        """lists[j] = the unranked dicts of result row rows[j] (confidence order)."""
-        recs = [(hyps[0]["id"], (tuple(h["id"] for h in hyps), cat, res, int(i)))
-                for hyps, i in zip(lists, rows) if hyps]
+        """lists[j] = the unranked dicts of result row rows[j] (confidence order).  The rows'
+        fields are converted to Python numbers here, once per launch (whole arrays), so that
+        rank() -- called once per list, often one list per call -- does no numpy work."""
+        rows = list(rows)
+        if not rows:
+            return
+        sel = np.asarray(rows, np.int64)
+        conf = res.confidence[sel].tolist()
+        strength = res.strength[sel].tolist()
+        final = res.final_score[sel].tolist()
+        oconf = res.order_conf[sel].tolist()
+        orank = res.order_rank[sel].tolist()
+        recs = []
+        for j, hyps in enumerate(lists):
+            if hyps:
+                n = len(hyps)
+                recs.append((hyps[0]["id"], (tuple(h["id"] for h in hyps), cat, oconf[j][:n],
+                                              conf[j], strength[j], final[j], orank[j][:n])))
         with self.lock:
             for key, rec in recs:
                 self.recs[key] = rec
@@ -151,11 +166,7 @@ class FusedRanks:
         if rec is None or len(hyps) != len(rec[0]):
             self.misses += 1
             return None
-        ids, cat, res, i = rec
-        n = len(ids)
-        # the result row as Python numbers, one conversion per array (not per element)
-        slots = res.order_conf[i, :n].tolist()
-        conf, strength = res.confidence[i].tolist(), res.strength[i].tolist()
+        ids, cat, slots, conf, strength, final, orank = rec
         R, rules, u = cat.n_rules, cat.rules, cat.unknown
         for h, hid, slot in zip(hyps, ids, slots):
             if not isinstance(h, dict) or h.get("id") != hid:
@@ -172,13 +183,13 @@ class FusedRanks:
                 self.misses += 1
                 return None
         self.hits += 1
-        final = res.final_score[i].tolist()
-        pos = {slot: p for p, slot in enumerate(slots)}
-        for h, slot in zip(hyps, slots):
+        pos = {}
+        for p, (h, slot) in enumerate(zip(hyps, slots)):
             h["final_score"] = final[slot]
-        out = [hyps[pos[s]] for s in res.order_rank[i, :n].tolist()]
-        for q, h in enumerate(out):
-            h["rank"] = q + 1
+            pos[slot] = p
+        out = [hyps[pos[s]] for s in orank]
+        for q, h in enumerate(out, 1):
+            h["rank"] = q
         return out
 
 

@@ -165,19 +165,18 @@ class GraphService:
         # torch.ops.egraph.frontier_run: the registered custom op (seeds + run of the frontier)
         ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
                                        to_device(ss, dev), src, hops, inc)
-        ids = ids.cpu().numpy().view("uint32")
-        scores = scores.cpu().numpy()
+        ids = ids.cpu().numpy().view("uint32").tolist()
+        scores = scores.cpu().numpy().tolist()
         fr.adapt()              # overflowing columns: the wide-table retry from the next call on
-        vlabel, _, _, _ = g.export()
+        vlabel = g.vertex_labels().tolist()
+        vid = g.vertex_ids()
         out = []
-        for b in range(len(keys)):
+        for irow, srow in zip(ids, scores):
             row = []
-            for r in range(k):
-                v = int(ids[b, r])
+            for r, (v, sc) in enumerate(zip(irow, srow)):
                 if v == 0xFFFFFFFF:
                     break
-                row.append({"id": g.vertex_id(v), "labels": [labels[vlabel[v]]],
-                            "score": float(scores[b, r]), "rank": r + 1})
+                row.append({"id": vid[v], "labels": [labels[vlabel[v]]], "score": sc, "rank": r + 1})
             out.append(row)
         return out
 
@@ -214,7 +213,7 @@ class GraphService:
             plan.reach_hop()
         bits = plan.read_reach().cpu().numpy().view("uint64")
         labels = g.labels()
-        vlabel, _, _, _ = g.export()
+        vlabel = g.vertex_labels()
         rtypes = g.rel_types()
         out = []
         for b, k in enumerate(keys):

@@ -42,7 +42,7 @@ def _world(B, seed=11, pods=3000, nodes=60):
 
 
 def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, scores=True):
-    from egraph.graph import group_seeds
+    from egraph.graph import group_seeds, launch_order
     snap = g.snapshot()
     fr = snap.frontier(B, max_seeds=max(len(sv), 1), k=k, pool_entries=pool_entries)
     fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
@@ -61,6 +61,13 @@ def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, sc
     gp, gv, gs = group_seeds(sv, sc, ss, B)
     fg = snap.frontier(B, max_seeds=max(len(gv), 1), k=k, pool_entries=pool_entries)
     g_ids, g_sc = fg.run_grouped(_dev(gp), _dev(gv), _dev(gs), _dev(src), hops=hops, exclude_label=inc)
+    np.testing.assert_array_equal(g_ids.cpu().numpy().view(np.uint32), e_ids)
+    assert g_sc.cpu().numpy().tobytes() == e_sc.tobytes()
+    # ... started costliest-first (a caller-given launch order changes no bit)
+    order = launch_order(gp, gv, g.csr()["row_ptr"])
+    assert sorted(order.tolist()) == list(range(B))
+    g_ids, g_sc = fg.run_grouped(_dev(gp), _dev(gv), _dev(gs), _dev(src), hops=hops, exclude_label=inc,
+                                 order=_dev(order))
     np.testing.assert_array_equal(g_ids.cpu().numpy().view(np.uint32), e_ids)
     assert g_sc.cpu().numpy().tobytes() == e_sc.tobytes()
     assert fr.stats().get("corrupt_keys", 0) == 0     # counted in debug (guard) builds only
