@@ -50,8 +50,11 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
-# (A/B) seeds grouped by column on the host at setup: the step runs egr_frontier_run_grouped
-GROUPED = os.environ.get("EGRAPH_BENCH_GROUPED")
+# --seed-input (main sets it): "grouped" = the seed triples arrive grouped by incident with
+# their column offsets and a costliest-first launch order (the host's seed attachment emits
+# them incident by incident; egr_frontier_run_grouped); "sort" = unordered triples, sorted by
+# column on the device in every step (egr_frontier_set_seeds: count, scan, scatter)
+GROUPED = "order"
 
 
 def max_over_ranks(dist, x: float, dev) -> float:
@@ -257,7 +260,17 @@ def step_graph(ctx, hops: int, ev=None):
     lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
     ctx["tick"] += 1
     with torch.cuda.stream(lane["cap_stream"]):
-        lane["graph"].replay()
+        if ev is not None:
+            # HIP events on the lane's stream around the replay: its span on the GPU (from its
+            # first kernel's start to its last kernel's end, the wait for CUs held by the other
+            # batches in flight included)
+            a, b = ev.pop()
+            a.record()
+            lane["graph"].replay()
+            b.record()
+            ev.done.append((a, b))
+        else:
+            lane["graph"].replay()
     return lane
 
 
@@ -937,6 +950,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="frontier: enqueue each batch eagerly instead of replaying the lane's "
                          "captured HIP graph")
+    ap.add_argument("--seed-input", default="grouped", choices=["grouped", "sort"],
+                    help="grouped: seeds grouped by incident + launch order as resident input "
+                         "(egr_frontier_run_grouped); sort: device counting sort per step")
     ap.add_argument("--roofline-reps", type=int, default=20,
                     help="isolated frontier launches timed after the run for the roofline")
     args = ap.parse_args()
@@ -958,6 +974,8 @@ def main():
                          f"--gpus {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    global GROUPED
+    GROUPED = "order" if args.seed_input == "grouped" else None
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
     # EGRAPH_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device); the
@@ -1007,7 +1025,7 @@ def main():
             run_step(ctx, args.hops)
         torch.cuda.synchronize(dev)
 
-    events: list = EventPool(args.steps) if args.engine == "frontier" and not graphs else []
+    events: list = EventPool(args.steps) if args.engine == "frontier" else []
     elapsed = timed_steps(lambda: run_step(ctx, args.hops, events), args.steps, dist, rank,
                           lambda: torch.cuda.synchronize(dev), dev)
 
@@ -1025,7 +1043,18 @@ def main():
         roof["isolated_launches"] = args.roofline_reps
         rules_iso = rules_probe(ctx)
         if timed:
-            roof["avg_launch_ms_in_flight"] = float(np.mean([a.elapsed_time(b) for a, b in timed]))
+            spans = np.array([a.elapsed_time(b) for a, b in timed])
+            # in the timed region: each batch's span on its lane's stream (graph replay: the
+            # whole captured batch; eager: the frontier run), their sum per step, and the mean
+            # number of batches in flight (sum of spans / wall time) -- so the isolated launch
+            # time, the overlap and ms_per_step can be reconciled from this line alone
+            roof["in_region"] = {
+                "what": "graph replay span (rules + frontier + fallback)" if graphs
+                        else "egr_frontier_run span",
+                "span_ms_mean": float(spans.mean()), "span_ms_p50": float(np.median(spans)),
+                "span_ms_sum_per_step": float(spans.sum() / args.steps),
+                "batches_in_flight_mean": float(spans.sum() / (elapsed * 1e3)),
+                "isolated_launch_ms_over_step_ms": launch_ms / ms}
         out_graph = graphs
     else:
         launch_ms = float(np.mean([a.elapsed_time(b) for a, b in timed]))
@@ -1060,6 +1089,9 @@ def main():
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
             "batches_in_flight": args.pipeline if args.engine == "frontier" else 1,
             "hip_graph_replay": out_graph,
+            "seed_input": ("grouped by incident + column offsets + costliest-first launch order, "
+                           "resident (egr_frontier_run_grouped)" if GROUPED and args.engine == "frontier"
+                           else "unordered triples, device counting sort per step"),
         },
         "roofline": roof,
     }

@@ -108,8 +108,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("P,sparse", [(2, True), (2, False)])
+@pytest.mark.parametrize("P,sparse", [(2, True), (2, False), (8, True)])
 def test_partitioned_protocol_gloo_world_size_2(P, sparse):
+    """(P = 8: the 8-GPU layout of the edge-cut path, every peer pair exchanging.)"""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -134,3 +134,46 @@ def test_partitioned_two_processes_one_gpu():
         assert own.tobytes() == exp[gids].tobytes()
         np.testing.assert_array_equal(ids, e_ids.astype(np.int64))
         np.testing.assert_array_equal(scores, e_sc)
+
+
+def test_partitioned_c4_eight_partitions():
+    """BASELINE C4 (the 1.09M-vertex graph with its dense Event / LogPattern / MetricAnomaly
+    links, ~10M CSR entries) edge-cut into 8 partitions in one process: the 8-GPU layout of
+    bench.py --shard graph.  Owned scores bit-identical to the unpartitioned oracle recurrence,
+    merged top-k equal to the unpartitioned top-k."""
+    from egraph import shard, synth
+    from egraph.graph import Snapshot
+    P, B, k = 8, 16, 8
+    c = synth.build_cluster(synth.CONFIGS["C4"])
+    cases = synth.make_incidents(c, B, seed=1000)
+    synth.add_incidents(c, cases)
+    g = synth.build_graph(c)
+    sv, sc, ss = synth.seeds_for_batch(g, [x.evidence for x in cases])
+    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+    csr = g.csr()
+    vl = g.vertex_labels()
+    V = g.num_vertices
+    assert V > 1_000_000 and len(csr["col"]) > 9_000_000
+    inc = g.labels().index("Incident")
+    owner = shard.partition_vertices(csr["row_ptr"], vl, g.labels(), P)
+    runs = []
+    for r in range(P):
+        lg = shard.build_local(csr, vl, owner, r, P)
+        snap = Snapshot.from_csr(lg.row_ptr, lg.col, lg.meta, lg.val, lg.vlabel, g.labels())
+        lv, lc, ls = shard.local_seeds(lg, V, sv, sc, ss)
+        plan = snap.plan(B, max_seeds=max(len(lv), 1), k=k)
+        plan.set_seeds(_dev(lv), _dev(lc), _dev(ls))
+        plan.set_sources(_dev(shard.local_sources(lg, V, src)))
+        runs.append(shard.RankRun(lg, plan, torch.device("cuda", 0)))
+        runs[-1].snap = snap
+    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k, sparse=True)
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)
+    assert sum(r.lg.n_owned for r in runs) == V
+    for run, (ids, scores) in zip(runs, out):
+        lg = run.lg
+        got = run.eng.read_scores().cpu().numpy()[: lg.n_owned]
+        assert got.tobytes() == exp[lg.gid[: lg.n_owned]].tobytes()        # bit-identical
+        np.testing.assert_array_equal(ids.cpu().numpy(), e_ids.astype(np.int64))
+        np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
