@@ -163,18 +163,25 @@ def build_lanes(snap, B: int, max_seeds: int, k: int, pipeline: int, pool_entrie
                           None if os.environ.get("EGRAPH_BENCH_ONE_STREAM") else torch.cuda.Stream(dev)))
         main, side = pairs[i % share] if share > 0 else pairs[-1]
         lane = dict(frontier=fr, rules=rules, seeds=seeds, sources=sources, main=main, side=side)
-        if GROUPED:
-            # seeds grouped by column on the host (egr_frontier_run_grouped: no device sort)
-            from egraph.graph import group_seeds, launch_order
-            gp, gv, gs = group_seeds(*(a.cpu().numpy() for a in seeds), B)
-            lane["grouped"] = tuple(torch.from_numpy(x).to(dev) for x in
-                                    (gp.view(np.int32), gv.view(np.int32), gs))
-            lane["order"] = None
-            if GROUPED == "order":
-                rp = snap.download()["row_ptr"]
-                lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
+        set_lane_seeds(lane, seeds, B, snap, dev)
         lanes.append(lane)
     return lanes
+
+
+def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) -> None:
+    """A lane's seed input: the device triples, and for --seed-input grouped their grouping by
+    column (offsets) and the costliest-first launch order, built on the host."""
+    lane["seeds"] = seeds
+    lane.pop("grouped", None)
+    lane["order"] = None
+    if GROUPED:
+        from egraph.graph import group_seeds, launch_order
+        gp, gv, gs = group_seeds(*(a.cpu().numpy() for a in seeds), B)
+        lane["grouped"] = tuple(torch.from_numpy(x).to(dev) for x in
+                                (gp.view(np.int32), gv.view(np.int32), gs))
+        if GROUPED == "order":
+            rp = row_ptr if row_ptr is not None else snap.download()["row_ptr"]
+            lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
 
 
 _GRAPH_NAME = {"C2": "10k-pod", "C3": "100k-pod", "C4": "400k-pod (1M-vertex)"}

@@ -68,8 +68,12 @@ def _check_rules(res, enc):
     assert res.confidence.tobytes() == exp["confidence"].tobytes()
 
 
-def test_bench_config_c3_pipelined_lanes():
+@pytest.mark.parametrize("seed_input", ["order", None])
+def test_bench_config_c3_pipelined_lanes(seed_input, monkeypatch):
+    """bench.py's C3 step exactly: three lanes, six different batches, seeds as grouped input
+    with a launch order (the default) or sorted on the device (--seed-input sort)."""
     import bench
+    monkeypatch.setattr(bench, "GROUPED", seed_input)
     from egraph import catalog
     from egraph.encode import encode_batch
     from egraph.rca import RulesDeviceBatch
@@ -90,11 +94,13 @@ def test_bench_config_c3_pipelined_lanes():
                               [(None, x["rules"], x["seeds"], x["sources"]) for x in inputs[:P]])
     assert all(ln["frontier"].pool_entries == -1 for ln in lanes)
     ctx = dict(lanes=lanes, tick=0, inc_label=inc)
+    row_ptr = g.csr()["row_ptr"]
     got = [(torch.empty(B * k, dtype=torch.int32, device=dev),
             torch.empty(B * k, dtype=torch.float32, device=dev)) for _ in range(n_batches)]
     for i, x in enumerate(inputs):                  # bench.step_frontier, one batch per step
         lane = ctx["lanes"][ctx["tick"] % P]
-        lane.update(seeds=x["seeds"], sources=x["sources"], rules=x["rules"])
+        lane.update(sources=x["sources"], rules=x["rules"])
+        bench.set_lane_seeds(lane, x["seeds"], B, snap, dev, row_ptr)
         lane = bench.step_frontier(ctx, hops)
         with torch.cuda.stream(lane["main"]):       # the lane's outputs before its next batch
             got[i][0].copy_(lane["frontier"].out_ids)
