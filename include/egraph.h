@@ -187,6 +187,11 @@ int64_t egr_graph_vertex_id(const egr_graph* g, int64_t v, char* buf, int64_t ca
 /* first vertex (lowest index) whose id equals each query id, -1 if none */
 int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
                      int32_t* out_vertex);
+/* egr_graph_lookup of ONE id given as bytes (len bytes, not NUL-terminated): the first vertex
+ * carrying it, -1 if none (or bad arguments).  Read-only: safe from several threads at once
+ * while no merge runs (the native seed attachment calls it from its worker threads; the
+ * reference resolves these ids with Cypher MATCH ... {id: $id}, src/database/neo4j.py:145-167). */
+int32_t egr_graph_find(const egr_graph* g, const char* id, int64_t len);
 /* vertex labels [V] and edge list (src, dst, type) [E] in creation order */
 int egr_graph_export(const egr_graph* g, uint8_t* vertex_label, int32_t* edge_src,
                      int32_t* edge_dst, uint8_t* edge_type);

@@ -11,6 +11,7 @@
 //          the relation silently.
 // Properties are not stored here: the Python GraphService mirror keeps them (last write wins).
 #include <algorithm>
+#include <cstring>
 #include <numeric>
 #include <string>
 #include <string_view>
@@ -26,6 +27,15 @@ struct egr_graph {
   std::vector<std::string> vid;          // vertex id strings, creation order
   std::vector<uint8_t> vlabel;
   std::unordered_map<std::string, std::vector<int32_t>> by_id;  // id -> vertices, creation order
+  // id -> first vertex, open addressing over the id bytes (egr_graph_find): a lookup hashes the
+  // caller's bytes in place (no std::string per query) and compares them with vid[v].  Read-only
+  // between merges, so concurrent finds are safe while no merge runs.
+  struct IdSlot {
+    uint32_t tag;   // high hash bits | 1 (0 = empty)
+    int32_t v;
+  };
+  std::vector<IdSlot> idx;
+  size_t idx_n = 0;
   std::vector<int32_t> esrc, edst;
   std::vector<uint8_t> etype;
   struct EdgeKey {
@@ -54,6 +64,64 @@ int intern(std::vector<std::string>& names, std::unordered_map<std::string, int>
   names.emplace_back(s);
   idx.emplace(names.back(), i);
   return i;
+}
+
+// 64-bit hash of an id's bytes, 8 at a time (a multiply-xorshift mix per word)
+inline uint64_t id_hash(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xFF51AFD7ED558CCDull);
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h = (h ^ (w * 0xC4CEB9FE1A85EC53ull)) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    p += 8;
+    n -= 8;
+  }
+  if (n) {
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = (h ^ (w * 0xC4CEB9FE1A85EC53ull)) * 0x9E3779B97F4A7C15ull;
+  }
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
+}
+
+void idx_put(egr_graph* g, const std::string& id, int32_t v) {
+  if (2 * (g->idx_n + 1) > g->idx.size()) {         // grow to keep the load at most 1/2
+    std::vector<egr_graph::IdSlot> old;
+    old.swap(g->idx);
+    g->idx.assign(std::max<size_t>(1024, 2 * old.size()), egr_graph::IdSlot{0u, -1});
+    const size_t m = g->idx.size() - 1;
+    for (const auto& e : old) {
+      if (!e.tag) continue;
+      const std::string& s = g->vid[e.v];
+      size_t i = (size_t)id_hash(s.data(), s.size()) & m;
+      while (g->idx[i].tag) i = (i + 1) & m;
+      g->idx[i] = e;
+    }
+  }
+  const uint64_t h = id_hash(id.data(), id.size());
+  const size_t m = g->idx.size() - 1;
+  size_t i = (size_t)h & m;
+  while (g->idx[i].tag) i = (i + 1) & m;
+  g->idx[i] = egr_graph::IdSlot{(uint32_t)(h >> 32) | 1u, v};
+  ++g->idx_n;
+}
+
+inline int32_t idx_find(const egr_graph* g, const char* p, size_t n) {
+  if (g->idx.empty()) return -1;
+  const uint64_t h = id_hash(p, n);
+  const uint32_t tag = (uint32_t)(h >> 32) | 1u;
+  const size_t m = g->idx.size() - 1;
+  for (size_t i = (size_t)h & m;; i = (i + 1) & m) {
+    const egr_graph::IdSlot e = g->idx[i];
+    if (!e.tag) return -1;
+    if (e.tag == tag) {
+      const std::string& s = g->vid[e.v];
+      if (s.size() == n && memcmp(s.data(), p, n) == 0) return e.v;
+    }
+  }
 }
 
 inline std::string_view str_at(const char* blob, const int64_t* off, int64_t i) {
@@ -99,6 +167,7 @@ int egr_graph_merge_nodes(egr_graph* g, const char* id_blob, const int64_t* id_o
       v = (int32_t)g->vid.size();
       g->vid.emplace_back(id);
       g->vlabel.push_back((uint8_t)lab);
+      if (vs.empty()) idx_put(g, g->vid.back(), v);   // the id's first vertex
       vs.push_back(v);
     }
     if (out_vertex) out_vertex[i] = v;
@@ -190,13 +259,14 @@ int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, i
                      int32_t* out_vertex) {
   if (!g || n < 0 || (n > 0 && (!blob || !off || !out_vertex)))
     return egr::fail(EGR_EINVAL, "egr_graph_lookup: bad arguments");
-  std::string key;
-  for (int64_t i = 0; i < n; ++i) {
-    key.assign(str_at(blob, off, i));
-    auto it = g->by_id.find(key);
-    out_vertex[i] = (it == g->by_id.end() || it->second.empty()) ? -1 : it->second.front();
-  }
+  for (int64_t i = 0; i < n; ++i)
+    out_vertex[i] = idx_find(g, blob + off[i], (size_t)(off[i + 1] - off[i]));
   return EGR_OK;
+}
+
+int32_t egr_graph_find(const egr_graph* g, const char* id, int64_t len) {
+  if (!g || len < 0 || (len > 0 && !id)) return -1;
+  return idx_find(g, id, (size_t)len);
 }
 
 int egr_graph_export(const egr_graph* g, uint8_t* vertex_label, int32_t* edge_src,

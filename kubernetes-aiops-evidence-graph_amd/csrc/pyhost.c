@@ -808,9 +808,11 @@ static void* w_main(void* arg) {
 
 /* A persistent pool of worker threads (created on first use, up to PAR_MAX_THREADS - 1; the
  * calling thread runs job 0): a call hands out its jobs and waits for them, instead of creating
- * and joining threads every time.  A forked child starts without the parent's threads: the
- * pool is rebuilt there on first use. */
+ * and joining threads every time.  A job is `fn(jobs + i * job_size)`: the rules encoder's row
+ * pass (w_main) and the seed attachment's (s_main) share the pool.  A forked child starts
+ * without the parent's threads: the pool is rebuilt there on first use. */
 #define PAR_MAX_THREADS 64
+typedef void* (*JobFn)(void*);
 static struct {
   pthread_mutex_t mu;
   pthread_cond_t go, done;
@@ -818,8 +820,11 @@ static struct {
   unsigned long gen;              /* incremented per call */
   int pending;                    /* jobs not finished in this call */
   int njobs;
-  WJob* jobs;                     /* jobs[1..njobs) for the pool threads */
-} pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, NULL};
+  JobFn fn;
+  char* jobs;                     /* job i at jobs + i * job_size (pool threads run 1..njobs) */
+  size_t job_size;
+} pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0, 0,
+          NULL, NULL, 0};
 
 typedef struct { int id; } PoolArg;
 static PoolArg pool_args[PAR_MAX_THREADS];
@@ -832,9 +837,10 @@ static void* pool_main(void* arg) {
     while (pool.gen == seen) pthread_cond_wait(&pool.go, &pool.mu);
     seen = pool.gen;
     if (id < pool.njobs) {
-      WJob* j = &pool.jobs[id];
+      const JobFn fn = pool.fn;
+      void* j = pool.jobs + (size_t)id * pool.job_size;
       pthread_mutex_unlock(&pool.mu);
-      w_main(j);
+      fn(j);
       pthread_mutex_lock(&pool.mu);
       if (--pool.pending == 0) pthread_cond_signal(&pool.done);
     }
@@ -850,8 +856,10 @@ static void pool_after_fork(void) {
   pool.pending = 0;
 }
 
-/* run jobs[0..n): jobs[1..) on the pool (grown as needed), jobs[0] here; returns when all are done */
-static void pool_run(WJob* jobs, int n) {
+/* run fn over jobs[0..n): jobs[1..) on the pool (grown as needed), jobs[0] here; returns when
+ * all are done */
+static void pool_run_fn(JobFn fn, void* jobs_v, size_t job_size, int n) {
+  char* jobs = (char*)jobs_v;
   pthread_mutex_lock(&pool.mu);
   while (pool.n < n - 1) {
     pthread_t t;
@@ -861,19 +869,23 @@ static void pool_run(WJob* jobs, int n) {
     ++pool.n;
   }
   const int m = pool.n + 1 < n ? pool.n + 1 : n;      /* jobs the pool can take */
+  pool.fn = fn;
   pool.jobs = jobs;
+  pool.job_size = job_size;
   pool.njobs = m;
   pool.pending = m - 1;
   ++pool.gen;
   pthread_cond_broadcast(&pool.go);
   pthread_mutex_unlock(&pool.mu);
-  w_main(&jobs[0]);
-  for (int t = m; t < n; ++t) w_main(&jobs[t]);       /* jobs no thread could be created for */
+  fn(jobs);
+  for (int t = m; t < n; ++t) fn(jobs + (size_t)t * job_size);   /* jobs no thread could be created for */
   pthread_mutex_lock(&pool.mu);
   while (pool.pending > 0) pthread_cond_wait(&pool.done, &pool.mu);
   pool.njobs = 0;
   pthread_mutex_unlock(&pool.mu);
 }
+
+static void pool_run(WJob* jobs, int n) { pool_run_fn(w_main, jobs, sizeof(WJob), n); }
 
 static int intern_worker_keys(void) {
   pthread_atfork(NULL, NULL, pool_after_fork);
@@ -1257,6 +1269,10 @@ static PyObject *a_ns, *a_name, *a_strength, *a_involved, *a_kind, *a_namespace,
     *t_metric, *s_empty, *s_node_lc, *s_colon, *p_pod, *p_deploy, *p_node, *p_hpa, *p_config,
     *p_logpattern, *p_service, *p_metric, *p_event, *kind_cache;
 
+static PyObject* K_SEED[5];    /* evidence_type, entity_namespace, entity_name, data, signal_strength */
+static PyObject* K_INV[1];     /* involved_object */
+static PyObject* K_OBJ[3];     /* kind, name, namespace */
+
 static int intern_seeds(void) {
 #define S(var, text) if (!(var = PyUnicode_InternFromString(text))) return -1
   S(a_ns, "entity_namespace"); S(a_name, "entity_name"); S(a_strength, "signal_strength");
@@ -1271,6 +1287,13 @@ static int intern_seeds(void) {
 #undef S
   if (!(kind_cache = PyDict_New())) return -1;
   if (!(a_half = PyFloat_FromDouble(0.5))) return -1;
+  K_SEED[0] = k_type; K_SEED[1] = a_ns; K_SEED[2] = a_name; K_SEED[3] = k_data; K_SEED[4] = a_strength;
+  K_INV[0] = a_involved;
+  K_OBJ[0] = a_kind; K_OBJ[1] = k_name; K_OBJ[2] = a_namespace;
+  PyObject* hk[] = {k_type, a_ns, a_name, k_data, a_strength, a_involved, a_kind, k_name, a_namespace,
+                    t_pod, t_deploy, t_dchange, t_ichange, t_node, t_hpa, t_config, t_event, t_log, t_metric};
+  for (size_t i = 0; i < sizeof(hk) / sizeof(hk[0]); ++i)   /* w_get reads the cached hashes */
+    if (PyObject_Hash(hk[i]) == -1) return -1;
   return 0;
 }
 
@@ -1476,8 +1499,362 @@ done:
   return result;
 }
 
+/* ---- seed attachment in one native pass (egraph/seeds.py seeds_for_batch) ------------------
+ * seed_attach(evidence_lists, slow, find, graph[, threads]) -> (vertex u32, column u32,
+ * strength f32) bytes: SeedCandidates(evidence_lists).attach(graph) without building a Python
+ * str per candidate id.  Each row's candidate ids (seeds.attach_ids) are formatted as UTF-8 into
+ * a scratch buffer and resolved by `find` (the address of libegraph's egr_graph_find, `graph` its
+ * egr_graph*): the first id present wins; rows with no id present, no candidate or a strength
+ * <= 0 seed nothing.
+ * Large batches run the row pass on the worker pool while the calling thread keeps the GIL (as
+ * encode_rows does): the workers take a row only when every value it reads is an exact dict /
+ * ASCII str / None / bool / float / int (no user code, nothing raises) and hand every other row
+ * back; the calling thread redoes those in row order through the serial path (cand_ids, or the
+ * Python statement `slow` = seeds._row, which raises what the reference expression raises), and
+ * once Python has run it redoes every later row too.  The graph must not change during the call
+ * (GraphService holds its lock). */
+typedef int32_t (*FindFn)(const void* g, const char* id, int64_t len);
+
+
+typedef struct {
+  char b[448];
+  size_t n;
+  int ovf;
+} IdBuf;
+
+static inline void ib_put(IdBuf* B, const char* p, size_t n) {
+  if (B->n + n > sizeof(B->b)) { B->ovf = 1; return; }
+  memcpy(B->b + B->n, p, n);
+  B->n += n;
+}
+
+/* str(o) as bytes for the values a worker formats: an ASCII exact str, None (also a missing
+ * key), True / False.  -1: the serial path formats it. */
+static inline int w_part(PyObject* o, const char** p, Py_ssize_t* n) {
+  if (o == NULL || o == Py_None) { *p = "None"; *n = 4; return 0; }
+  if (PyUnicode_CheckExact(o)) {
+    if (!PyUnicode_IS_READY(o) || !PyUnicode_IS_ASCII(o)) return -1;
+    *p = (const char*)PyUnicode_1BYTE_DATA(o);
+    *n = PyUnicode_GET_LENGTH(o);
+    return 0;
+  }
+  if (o == Py_True) { *p = "True"; *n = 4; return 0; }
+  if (o == Py_False) { *p = "False"; *n = 5; return 0; }
+  return -1;
+}
+
+enum { ST_POD, ST_DEPLOY, ST_DCHANGE, ST_ICHANGE, ST_NODE, ST_HPA, ST_CONFIG, ST_EVENT, ST_LOG,
+       ST_METRIC, ST_N };
+static PyObject** seed_types[ST_N] = {&t_pod, &t_deploy, &t_dchange, &t_ichange, &t_node, &t_hpa,
+                                      &t_config, &t_event, &t_log, &t_metric};
+
+/* resolve prefix + a [+ ":" + b]: 1 = found (*v), 0 = absent, -1 = id too long (hand over) */
+static inline int s_try(FindFn find, const void* g, const char* pre, size_t pn, const char* a,
+                        size_t an, const char* b, Py_ssize_t bn, int32_t* v) {
+  IdBuf B;
+  B.n = 0;
+  B.ovf = 0;
+  ib_put(&B, pre, pn);
+  ib_put(&B, a, an);
+  if (bn >= 0) {
+    ib_put(&B, ":", 1);
+    ib_put(&B, b, (size_t)bn);
+  }
+  if (B.ovf) return -1;
+  *v = find(g, B.b, (int64_t)B.n);
+  return *v >= 0;
+}
+
+/* One row on a worker: 0 = done (*vout = the attached vertex or NO_NODE), 1 = hand over */
+static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float* sout) {
+  *vout = NO_NODE;
+  if (!PyDict_CheckExact(ev)) return 1;
+  PyObject* o[5];
+  if (w_get(ev, K_SEED, 5, o)) return 1;
+  PyObject *t = o[0], *ns = o[1], *name = o[2], *data = o[3], *st = o[4];
+  /* float(ev.get("signal_strength", 0.5)): evaluated for every row (seeds._row) */
+  double sv;
+  if (st == NULL) sv = 0.5;
+  else if (PyFloat_CheckExact(st)) sv = PyFloat_AS_DOUBLE(st);
+  else if (PyBool_Check(st)) sv = st == Py_True ? 1.0 : 0.0;
+  else if (PyLong_CheckExact(st)) {
+    int ovf = 0;
+    const long long x = PyLong_AsLongLongAndOverflow(st, &ovf);
+    if (ovf) return 1;
+    sv = (double)x;                 /* round to nearest, as float(int) */
+  } else return 1;
+  if (t == NULL || t == Py_None) return 0;                       /* no candidate */
+  if (!PyUnicode_CheckExact(t)) return 1;
+  if (data != NULL && data != Py_None && !PyDict_CheckExact(data)) return 1;
+  const char *a, *b;
+  Py_ssize_t an, bn;
+  if (w_part(ns, &a, &an) || w_part(name, &b, &bn)) return 1;
+  int ty = -1;
+  for (int i = 0; i < ST_N; ++i) {
+    const int eq = w_eq_obj(t, *seed_types[i]);
+    if (eq < 0) return 1;
+    if (eq) { ty = i; break; }
+  }
+  if (ty < 0) return 0;                                          /* any other type: none */
+  if (sv <= 0.0) return 0;                                       /* `s <= 0` (NaN seeds) */
+  int32_t v = -1;
+  int r = 0;
+#define TRY(pre, x, xn, y, yn) do {                                              \
+    r = s_try(find, g, pre, sizeof(pre) - 1, x, (size_t)(xn), y, yn, &v);      \
+    if (r < 0) return 1;                                                       \
+    if (r > 0) goto found;                                                     \
+  } while (0)
+  switch (ty) {
+    case ST_POD: TRY("pod:", a, an, b, bn); break;
+    case ST_DEPLOY: case ST_DCHANGE: case ST_ICHANGE: TRY("deployment:", a, an, b, bn); break;
+    case ST_NODE: TRY("node:", b, bn, NULL, -1); break;
+    case ST_HPA: TRY("hpa:", a, an, b, bn); break;
+    case ST_CONFIG: TRY("configmap:", a, an, b, bn); break;
+    case ST_LOG:
+      TRY("logpattern:", a, an, b, bn);
+      TRY("service:", a, an, b, bn);
+      TRY("deployment:", a, an, b, bn);
+      break;
+    case ST_METRIC: TRY("metric:", a, an, b, bn); break;
+    case ST_EVENT: {
+      PyObject* obj = NULL;
+      if (data != NULL && data != Py_None && PyDict_GET_SIZE(data) > 0 && w_get(data, K_INV, 1, &obj))
+        return 1;
+      if (obj != NULL && obj != Py_None && !PyDict_CheckExact(obj)) return 1;
+      if (obj != NULL && (obj == Py_None || PyDict_GET_SIZE(obj) == 0)) obj = NULL;
+      PyObject *kind = NULL, *oname = NULL, *ons = NULL;
+      if (obj != NULL) {
+        PyObject* q[3];
+        if (w_get(obj, K_OBJ, 3, q)) return 1;
+        kind = q[0]; oname = q[1]; ons = q[2];
+      }
+      TRY("event:", a, an, b, bn);
+      /* kind = str(obj.get("kind", "")).lower() (ASCII here: lower() is per-byte) */
+      const char* kp = "";
+      Py_ssize_t kn = 0;
+      if (kind != NULL && w_part(kind, &kp, &kn)) return 1;
+      char kl[64];
+      if (kn >= (Py_ssize_t)sizeof(kl)) return 1;
+      for (Py_ssize_t i = 0; i < kn; ++i) kl[i] = (char)((kp[i] >= 'A' && kp[i] <= 'Z') ? kp[i] + 32 : kp[i]);
+      const char *op, *sp;
+      Py_ssize_t on, sn;
+      if (w_part(oname, &op, &on)) return 1;                      /* obj.get('name') */
+      if (ons == NULL) { sp = a; sn = an; }                        /* obj.get('namespace', ns) */
+      else if (w_part(ons, &sp, &sn)) return 1;
+      if (kn == 4 && memcmp(kl, "node", 4) == 0) {
+        TRY("node:", op, on, NULL, -1);
+      } else if (kn > 0) {
+        IdBuf B;
+        B.n = 0;
+        B.ovf = 0;
+        ib_put(&B, kl, (size_t)kn);
+        ib_put(&B, ":", 1);
+        ib_put(&B, sp, (size_t)sn);
+        ib_put(&B, ":", 1);
+        ib_put(&B, op, (size_t)on);
+        if (B.ovf) return 1;
+        v = find(g, B.b, (int64_t)B.n);
+        if (v >= 0) goto found;
+      }
+      break;
+    }
+  }
+#undef TRY
+  return 0;
+found:
+  *vout = (uint32_t)v;
+  *sout = (float)sv;
+  return 0;
+}
+
+typedef struct {
+  PyObject* const* lists;
+  const int64_t* base;
+  Py_ssize_t i0, i1;
+  FindFn find;
+  const void* g;
+  uint32_t* vert;
+  float* val;
+  uint8_t* redo;
+} SJob;
+
+static void* s_main(void* arg) {
+  const SJob* J = (const SJob*)arg;
+  for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
+    PyObject* evs = J->lists[i];
+    const Py_ssize_t n = PyList_GET_SIZE(evs);
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      const Py_ssize_t r = J->base[i] + j;
+      J->val[r] = 0.f;
+      J->redo[r] = (uint8_t)s_row(PyList_GET_ITEM(evs, j), J->find, J->g, &J->vert[r], &J->val[r]);
+    }
+  }
+  return NULL;
+}
+
+/* One row on the calling thread (GIL held): cand_ids, or the Python statement. */
+static int s_row_serial(PyObject* ev, PyObject* slow, FindFn find, const void* g, uint32_t* vout,
+                        float* sout, int* ran_python) {
+  *vout = NO_NODE;
+  PyObject* ids = PyList_New(0);
+  if (!ids) return -1;
+  double sv = 0.0;
+  int fast = 0;
+  if (PyDict_CheckExact(ev)) {
+    PyObject* st;
+    fast = cand_ids(ev, ids);
+    if (fast == 1) {
+      if (dget(ev, a_strength, &st)) fast = 0;
+      else if (st == NULL) sv = 0.5;
+      else if (PyFloat_CheckExact(st)) sv = PyFloat_AS_DOUBLE(st);
+      else if (PyLong_CheckExact(st) || PyBool_Check(st)) {
+        sv = PyLong_AsDouble(st);
+        if (sv == -1.0 && PyErr_Occurred()) { PyErr_Clear(); fast = 0; }
+      } else fast = 0;
+    }
+  }
+  if (fast < 0) { Py_DECREF(ids); return -1; }
+  if (!fast) {                                   /* the Python statement decides (or raises) */
+    Py_DECREF(ids);
+    *ran_python = 1;
+    PyObject* r = PyObject_CallOneArg(slow, ev);
+    if (!r) return -1;
+    if (!PyArg_ParseTuple(r, "Od", &ids, &sv) || !PyList_Check(ids)) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "seed_attach: bad slow row");
+      Py_DECREF(r);
+      return -1;
+    }
+    Py_INCREF(ids);
+    Py_DECREF(r);
+  }
+  const Py_ssize_t k = PyList_GET_SIZE(ids);
+  int rc = 0;
+  if (k > 0 && !(sv <= 0.0)) {
+    for (Py_ssize_t i = 0; i < k; ++i) {
+      PyObject* x = PyList_GET_ITEM(ids, i);
+      Py_ssize_t n;
+      const char* u = PyUnicode_Check(x) ? PyUnicode_AsUTF8AndSize(x, &n) : NULL;
+      if (!u) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "seed_attach: candidate id is not a str");
+        rc = -1;
+        break;
+      }
+      const int32_t v = find(g, u, (int64_t)n);
+      if (v >= 0) {
+        *vout = (uint32_t)v;
+        *sout = (float)sv;
+        break;
+      }
+    }
+  }
+  Py_DECREF(ids);
+  return rc;
+}
+
+static PyObject* seed_attach(PyObject* self, PyObject* args) {
+  PyObject *lists, *slow;
+  unsigned long long find_addr, g_addr;
+  int threads = 1;
+  if (!PyArg_ParseTuple(args, "OOKK|i", &lists, &slow, &find_addr, &g_addr, &threads)) return NULL;
+  const FindFn find = (FindFn)(uintptr_t)find_addr;
+  const void* g = (const void*)(uintptr_t)g_addr;
+  if (!find || !g) {
+    PyErr_SetString(PyExc_ValueError, "seed_attach: NULL find function or graph");
+    return NULL;
+  }
+  PyObject* seq = PySequence_Fast(lists, "evidence_lists must be a sequence");
+  if (!seq) return NULL;
+  PyObject* result = NULL;
+  int64_t* base = NULL;
+  uint32_t *wv = NULL, *ov = NULL, *oc = NULL;
+  float *wval = NULL, *os = NULL;
+  uint8_t* redo = NULL;
+  Py_ssize_t nout = 0, cap = 0;
+  const Py_ssize_t B = PySequence_Fast_GET_SIZE(seq);
+  int par = threads > 1;
+  Py_ssize_t total = 0;
+  for (Py_ssize_t i = 0; par && i < B; ++i) {
+    PyObject* evs = PySequence_Fast_GET_ITEM(seq, i);
+    if (!PyList_CheckExact(evs)) par = 0;
+    else total += PyList_GET_SIZE(evs);
+  }
+  if (par && total < PAR_MIN_ROWS) par = 0;
+  if (par) {
+    base = PyMem_Malloc(sizeof(int64_t) * (size_t)(B + 1));
+    wv = PyMem_Malloc(sizeof(uint32_t) * (size_t)total);
+    wval = PyMem_Malloc(sizeof(float) * (size_t)total);
+    redo = PyMem_Malloc((size_t)total);
+    if (!base || !wv || !wval || !redo) { PyErr_NoMemory(); goto done; }
+    base[0] = 0;
+    for (Py_ssize_t i = 0; i < B; ++i) base[i + 1] = base[i] + PyList_GET_SIZE(PySequence_Fast_GET_ITEM(seq, i));
+    if (threads > PAR_MAX_THREADS) threads = PAR_MAX_THREADS;
+    SJob jobs[PAR_MAX_THREADS];
+    Py_ssize_t i = 0;
+    for (int t = 0; t < threads; ++t) {
+      const int64_t goal = (int64_t)((total * (t + 1)) / threads);
+      const Py_ssize_t i0 = i;
+      while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
+      jobs[t] = (SJob){PySequence_Fast_ITEMS(seq), base, i0, i, find, g, wv, wval, redo};
+    }
+    pool_run_fn(s_main, jobs, sizeof(SJob), threads);   /* (the GIL stays held) */
+  }
+  {
+    int ran_python = 0;
+    Py_ssize_t r = 0;
+    for (Py_ssize_t i = 0; i < B; ++i) {
+      PyObject* evs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, i), "evidence is not iterable");
+      if (!evs) goto done;
+      const Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
+      for (Py_ssize_t j = 0; j < n; ++j, ++r) {
+        uint32_t v;
+        float x = 0.f;
+        if (par && !ran_python && !redo[r]) {
+          v = wv[r];
+          x = wval[r];
+        } else if (!par && !ran_python &&
+                   s_row(PySequence_Fast_GET_ITEM(evs, j), find, g, &v, &x) == 0) {
+          /* (a small batch: the worker's row function on this thread) */
+        } else if (s_row_serial(PySequence_Fast_GET_ITEM(evs, j), slow, find, g, &v, &x, &ran_python) < 0) {
+          Py_DECREF(evs);
+          goto done;
+        }
+        if (v == NO_NODE) continue;
+        if (nout == cap) {
+          cap = cap ? 2 * cap : 4096;
+          uint32_t* v2 = PyMem_Realloc(ov, cap * sizeof(uint32_t));
+          if (v2) ov = v2;
+          uint32_t* c2 = PyMem_Realloc(oc, cap * sizeof(uint32_t));
+          if (c2) oc = c2;
+          float* s2 = PyMem_Realloc(os, cap * sizeof(float));
+          if (s2) os = s2;
+          if (!v2 || !c2 || !s2) { PyErr_NoMemory(); Py_DECREF(evs); goto done; }
+        }
+        ov[nout] = v;
+        oc[nout] = (uint32_t)i;
+        os[nout] = x;
+        ++nout;
+      }
+      Py_DECREF(evs);
+    }
+  }
+  result = Py_BuildValue("(y#y#y#)", (const char*)ov, nout * (Py_ssize_t)sizeof(uint32_t),
+                         (const char*)oc, nout * (Py_ssize_t)sizeof(uint32_t), (const char*)os,
+                         nout * (Py_ssize_t)sizeof(float));
+done:
+  PyMem_Free(base);
+  PyMem_Free(wv);
+  PyMem_Free(wval);
+  PyMem_Free(redo);
+  PyMem_Free(ov);
+  PyMem_Free(oc);
+  PyMem_Free(os);
+  Py_DECREF(seq);
+  return result;
+}
+
 static PyMethodDef methods[] = {
     {"seed_candidates", seed_candidates, METH_VARARGS, "evidence rows -> seed attachment candidates"},
+    {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},
     {"assemble", assemble, METH_VARARGS, "kernel outputs -> hypothesis dicts"},
     {"flag_bits", flag_bits, METH_NOARGS, "the EGR_F_* bits and EGR_NO_NODE compiled in"},

@@ -190,10 +190,29 @@ class SeedCandidates:
         return (found[first[ok]].astype(np.uint32), self.col[ok], self.val[ok])
 
 
+def attach_native(graph, evidence_lists: list[list[dict]], threads: int | None = None):
+    """SeedCandidates(evidence_lists).attach(graph) in one native pass (csrc/pyhost.c
+    seed_attach): candidate ids are formatted as bytes and resolved by egr_graph_find, on the
+    encoder's worker pool for large batches, with no Python str built per id.  Rows whose values
+    are not plain built-ins are handed to `_row` (the Python statement), in row order."""
+    import ctypes as C
+
+    from . import _lib
+    from .encode import encode_threads
+    find = C.cast(_lib.lib.egr_graph_find, C.c_void_p).value
+    v, c, s = _lib.pyhost.seed_attach(evidence_lists, _row, find, graph.handle.value,
+                                      encode_threads() if threads is None else threads)
+    return (np.frombuffer(v, np.uint32).copy(), np.frombuffer(c, np.uint32).copy(),
+            np.frombuffer(s, np.float32).copy())
+
+
 def seeds_for_batch(graph, evidence_lists: list[list[dict]], pending: list | None = None):
     """(vertex u32, column u32, strength f32) triples for a batch: each row attaches to the
     first of its candidate ids present in the graph; unattached rows are dropped.
     `pending` (optional, a list) receives per column the set of candidate ids ranked before the
     one attached (all of them for an unattached row): the vertices whose later creation would
-    re-attach a row -- the alert storm's re-rank trigger (egraph/storm.py)."""
+    re-attach a row -- the alert storm's re-rank trigger (egraph/storm.py).  Without `pending`
+    the attachment runs in one native pass (attach_native)."""
+    if pending is None:
+        return attach_native(graph, evidence_lists)
     return SeedCandidates(evidence_lists).attach(graph, pending)

@@ -29,6 +29,7 @@ from __future__ import annotations
 import asyncio
 import threading
 
+import numpy as np
 import torch
 
 from egraph import ops
@@ -165,18 +166,21 @@ class GraphService:
         # torch.ops.egraph.frontier_run: the registered custom op (seeds + run of the frontier)
         ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
                                        to_device(ss, dev), src, hops, inc)
-        ids = ids.cpu().numpy().view("uint32").tolist()
+        ids = ids.cpu().numpy().view("uint32")
         scores = scores.cpu().numpy().tolist()
         fr.adapt()              # overflowing columns: the wide-table retry from the next call on
-        vlabel = g.vertex_labels().tolist()
+        # the ranked vertices' labels by numpy indexing (no per-vertex list of the whole graph)
+        lab = np.zeros(ids.shape, np.uint8)
+        ok = ids != 0xFFFFFFFF
+        lab[ok] = g.vertex_labels()[ids[ok]]
         vid = g.vertex_ids()
         out = []
-        for irow, srow in zip(ids, scores):
+        for irow, srow, lrow in zip(ids.tolist(), scores, lab.tolist()):
             row = []
-            for r, (v, sc) in enumerate(zip(irow, srow)):
+            for r, v in enumerate(irow):
                 if v == 0xFFFFFFFF:
                     break
-                row.append({"id": vid[v], "labels": [labels[vlabel[v]]], "score": sc, "rank": r + 1})
+                row.append({"id": vid[v], "labels": [labels[lrow[r]]], "score": srow[r], "rank": r + 1})
             out.append(row)
         return out
 

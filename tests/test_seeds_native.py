@@ -236,3 +236,91 @@ def test_keyed_candidates_match_flat_ones():
             assert np.array_equal(a, c)
     empty = SeedCandidates.combine([], with_flat=False)
     assert empty.n_flat == 0 and len(empty.attach_found_idx(np.zeros(0))[0]) == 0
+
+
+def _attach_both(g, lists, threads):
+    from egraph.seeds import SeedCandidates, attach_native
+    a = attach_native(g, lists, threads)
+    b = SeedCandidates(lists).attach(g)
+    for x, y in zip(a, b):
+        assert x.dtype == y.dtype and len(x) == len(y)
+        if x.dtype == np.float32:
+            assert np.array_equal(x, y, equal_nan=True)
+        else:
+            assert np.array_equal(x, y)
+    return a
+
+
+def _edge_graph():
+    """A graph holding some of EDGE's candidate ids (and ids the workers must format: None,
+    True, non-ASCII) so that first-present-wins is exercised on each candidate position."""
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    ids = ["pod:ns:p", "deployment:ns:d", "node:n1", "node:n", "hpa:ns:h", "configmap:ns:c",
+           "event:ns:e", "pod:other:p", "service:ns:svc", "deployment:ns:svc", "metric:1.5:False",
+           "pod:None:5", "deployment:None:d", "none:ns:None", "7:None:3", "pod:ns:pé-テ",
+           "deployment:ns:sub"]
+    g.merge_nodes(ids, ["X"] * len(ids))
+    g.merge_nodes(["pod:ns:p"], ["Y"])              # a second vertex with the same id: first wins
+    return g
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_attach_native_matches_python_on_collector_evidence(threads):
+    """seeds_for_batch's native pass (csrc/pyhost.c seed_attach over egr_graph_find) attaches
+    exactly like SeedCandidates.attach (str ids + egr_graph_lookup), on the worker pool
+    (>= 4096 rows) and on the calling thread."""
+    from egraph import synth
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    cases = synth.make_incidents(c, 120, seed=10)
+    synth.add_incidents(c, cases)
+    g = synth.build_graph(c)
+    lists = [x.evidence for x in cases]
+    assert sum(map(len, lists)) >= 4096
+    v, col, s = _attach_both(g, lists, threads)
+    assert len(v) > 1000
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_attach_native_matches_python_on_edge_rows(threads):
+    rng = random.Random(5)
+    uni = [{"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "pé-テ"},
+           {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "x",
+            "data": {"involved_object": {"kind": "DÉPLOYMENT", "name": "d"}}},
+           {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "x",
+            "data": {"involved_object": {"kind": "NODE", "name": "n1"}}},
+           {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p" * 600}]
+    rows = EDGE + uni
+    # pad past the parallel threshold so the worker pass runs with edge rows inside it
+    lists = [rows, [], rows[::-1]] + [rng.sample(rows, 12) for _ in range(400)]
+    _attach_both(_edge_graph(), lists, threads)
+
+
+@pytest.mark.parametrize("bad", [
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": "x"},
+    {"evidence_type": "kubernetes_event", "entity_namespace": "ns", "entity_name": "e",
+     "data": {"involved_object": ["x"]}},
+    ["not", "a", "dict"],
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "\ud800"},
+])
+def test_attach_native_raises_like_python(bad):
+    from egraph.seeds import SeedCandidates, attach_native
+    g = _edge_graph()
+    lists = [[dict(EDGE[0])] * 5000, [bad]]
+    with pytest.raises(Exception) as e1:
+        SeedCandidates(lists).attach(g)
+    for th in (1, 4):
+        with pytest.raises(Exception) as e2:
+            attach_native(g, lists, th)
+        assert type(e1.value) is type(e2.value)
+
+
+def test_graph_find_matches_lookup():
+    from egraph import _lib
+    g = _edge_graph()
+    ids = ["pod:ns:p", "node:n1", "absent", "", "pod:ns:pé-テ", "deployment:ns:sub"]
+    want = g.lookup(ids).tolist()
+    got = [_lib.lib.egr_graph_find(g.handle, x.encode(), len(x.encode())) for x in ids]
+    assert got == want and want[0] == 0 and want[2] == -1
