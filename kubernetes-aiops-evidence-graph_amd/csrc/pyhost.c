@@ -1852,8 +1852,113 @@ done:
   return result;
 }
 
+/* ---- fused-rank reuse (egraph/ranker.py FusedRanks.apply) ---------------------------------
+ * fused_apply(hyps, rec) -> the ranked list, False (not the registered list: a miss), or
+ * None (a value this path does not compare without Python: FusedRanks.apply decides).
+ * rec = FusedRanks.register's record (ids, catalog, slots, conf, strength, final, orank, cat)
+ * with cat = (R, rule categories, rule support counts, (confidence, category, support,
+ * strength) of the unknown hypothesis), all plain values.  The checks are FusedRanks.apply's, in its
+ * order: every dict is an exact dict with the registered id at its position and the four
+ * ranker inputs the kernel emitted; then final_score / rank are written as egr_rank would. */
+static PyObject *f_confidence, *f_category, *f_support, *f_final, *f_rank, *f_unknown, *f_half,
+    *f_zero;
+
+/* v (borrowed, NULL = missing -> dflt) == want for plain numbers: 1 / 0, -1 = not plain */
+static inline int f_num_eq(PyObject* v, PyObject* dflt, PyObject* want) {
+  if (v == NULL) v = dflt;
+  if (!(PyFloat_CheckExact(v) || PyLong_CheckExact(v) || PyBool_Check(v))) return -1;
+  return PyObject_RichCompareBool(v, want, Py_EQ);   /* built-in numbers: no user code */
+}
+
+static PyObject* fused_apply(PyObject* self, PyObject* args) {
+  PyObject *hyps, *rec;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &hyps, &PyTuple_Type, &rec)) return NULL;
+  if (PyTuple_GET_SIZE(rec) < 8 || !PyTuple_Check(PyTuple_GET_ITEM(rec, 7))) Py_RETURN_NONE;
+  PyObject *ids = PyTuple_GET_ITEM(rec, 0), *slots = PyTuple_GET_ITEM(rec, 2),
+           *conf = PyTuple_GET_ITEM(rec, 3), *strength = PyTuple_GET_ITEM(rec, 4),
+           *final = PyTuple_GET_ITEM(rec, 5), *orank = PyTuple_GET_ITEM(rec, 6);
+  PyObject *cats, *sups, *unk;
+  Py_ssize_t R;
+  if (!PyArg_ParseTuple(PyTuple_GET_ITEM(rec, 7), "nOOO", &R, &cats, &sups, &unk)) return NULL;
+  const Py_ssize_t n = PyList_GET_SIZE(hyps);
+  if (!PyTuple_Check(ids) || !PyList_Check(slots) || !PyList_Check(orank) || PyTuple_GET_SIZE(ids) != n ||
+      PyList_GET_SIZE(slots) != n || PyList_GET_SIZE(orank) != n || !PyList_Check(conf) ||
+      !PyList_Check(strength) || !PyList_Check(final) || !PyTuple_Check(cats) || !PyTuple_Check(sups) ||
+      !PyTuple_Check(unk) || PyTuple_GET_SIZE(unk) != 4)
+    Py_RETURN_NONE;
+  Py_ssize_t pos[64];
+  if (n > 64 || R >= 64) Py_RETURN_NONE;
+  for (Py_ssize_t q = 0; q < 64; ++q) pos[q] = -1;
+  for (Py_ssize_t p = 0; p < n; ++p) {
+    PyObject* h = PyList_GET_ITEM(hyps, p);
+    if (!PyDict_CheckExact(h)) Py_RETURN_NONE;
+    PyObject *hid, *c, *cg, *sp, *st;
+    if (dget(h, k_id, &hid) || dget(h, f_confidence, &c) || dget(h, f_category, &cg) ||
+        dget(h, f_support, &sp) || dget(h, h_strength, &st))
+      Py_RETURN_NONE;
+    PyObject* want_id = PyTuple_GET_ITEM(ids, p);
+    if (hid == NULL || !PyUnicode_CheckExact(hid) || !PyUnicode_CheckExact(want_id)) Py_RETURN_NONE;
+    if (PyUnicode_Compare(hid, want_id) != 0) Py_RETURN_FALSE;
+    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(slots, p));
+    if (slot < 0 || slot > R) { PyErr_Clear(); Py_RETURN_NONE; }
+    PyObject *wc, *wcat, *wsup, *wst;
+    if (slot == R) {
+      wc = PyTuple_GET_ITEM(unk, 0); wcat = PyTuple_GET_ITEM(unk, 1);
+      wsup = PyTuple_GET_ITEM(unk, 2); wst = PyTuple_GET_ITEM(unk, 3);
+    } else {
+      if (slot >= PyList_GET_SIZE(conf) || slot >= PyList_GET_SIZE(strength) ||
+          slot >= PyTuple_GET_SIZE(cats) || slot >= PyTuple_GET_SIZE(sups))
+        Py_RETURN_NONE;
+      wc = PyList_GET_ITEM(conf, slot); wcat = PyTuple_GET_ITEM(cats, slot);
+      wsup = PyTuple_GET_ITEM(sups, slot); wst = PyList_GET_ITEM(strength, slot);
+    }
+    int eq = f_num_eq(c, f_half, wc);
+    if (eq < 0) { PyErr_Clear(); Py_RETURN_NONE; }
+    if (!eq) Py_RETURN_FALSE;
+    if (cg == NULL) cg = f_unknown;
+    if (!PyUnicode_CheckExact(cg) || !PyUnicode_CheckExact(wcat)) Py_RETURN_NONE;
+    if (PyUnicode_Compare(cg, wcat) != 0) Py_RETURN_FALSE;
+    if ((eq = f_num_eq(sp, f_zero, wsup)) < 0) { PyErr_Clear(); Py_RETURN_NONE; }
+    if (!eq) Py_RETURN_FALSE;
+    if ((eq = f_num_eq(st, f_zero, wst)) < 0) { PyErr_Clear(); Py_RETURN_NONE; }
+    if (!eq) Py_RETURN_FALSE;
+    if (pos[slot] >= 0) Py_RETURN_NONE;          /* (a slot twice: not a kernel list) */
+    pos[slot] = p;
+  }
+  /* verified: final scores, then the kernel's order and ranks */
+  PyObject* out = PyList_New(n);
+  if (!out) return NULL;
+  for (Py_ssize_t q = 0; q < n; ++q) {
+    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(orank, q));
+    if (slot < 0 || slot > R || pos[slot] < 0 || slot >= PyList_GET_SIZE(final)) {
+      PyErr_Clear();
+      Py_DECREF(out);
+      Py_RETURN_NONE;
+    }
+    PyObject* h = PyList_GET_ITEM(hyps, pos[slot]);
+    Py_INCREF(h);
+    PyList_SET_ITEM(out, q, h);
+  }
+  for (Py_ssize_t p = 0; p < n; ++p) {
+    PyObject* h = PyList_GET_ITEM(hyps, p);
+    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(slots, p));
+    if (PyDict_SetItem(h, f_final, PyList_GET_ITEM(final, slot)) < 0) { Py_DECREF(out); return NULL; }
+  }
+  for (Py_ssize_t q = 0; q < n; ++q) {
+    PyObject* r = PyLong_FromSsize_t(q + 1);
+    if (!r || PyDict_SetItem(PyList_GET_ITEM(out, q), f_rank, r) < 0) {
+      Py_XDECREF(r);
+      Py_DECREF(out);
+      return NULL;
+    }
+    Py_DECREF(r);
+  }
+  return out;
+}
+
 static PyMethodDef methods[] = {
     {"seed_candidates", seed_candidates, METH_VARARGS, "evidence rows -> seed attachment candidates"},
+    {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
     {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},
     {"assemble", assemble, METH_VARARGS, "kernel outputs -> hypothesis dicts"},
@@ -1864,5 +1969,10 @@ static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_egr_pyhost", NULL, 
 
 PyMODINIT_FUNC PyInit__egr_pyhost(void) {
   if (intern_all() < 0 || intern_seeds() < 0 || intern_worker_keys() < 0) return NULL;
+#define S(var, text) if (!(var = PyUnicode_InternFromString(text))) return NULL
+  S(f_confidence, "confidence"); S(f_category, "category"); S(f_support, "support_count");
+  S(f_final, "final_score"); S(f_rank, "rank"); S(f_unknown, "unknown");
+#undef S
+  if (!(f_half = PyFloat_FromDouble(0.5)) || !(f_zero = PyLong_FromLong(0))) return NULL;
   return PyModule_Create(&module);
 }

@@ -25,7 +25,6 @@ import asyncio
 import contextlib
 import gc
 import time
-from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -277,12 +276,14 @@ def concat(encs: list[EncodedBatch]) -> EncodedBatch:
                         np.concatenate(seg), [i for e in encs for i in e.evidence_ids])
 
 
-@dataclass
 class _Call:
-    incident_ids: list
-    evidence_lists: list
-    ranked: bool
-    fut: asyncio.Future
+    """One caller's incidents; `single`: submit() of one incident (its future gets the list
+    itself, not a list of one list)."""
+    __slots__ = ("incident_ids", "evidence_lists", "ranked", "fut", "single")
+
+    def __init__(self, incident_ids: list, evidence_lists: list, ranked: bool, fut, single=False):
+        self.incident_ids, self.evidence_lists, self.ranked = incident_ids, evidence_lists, ranked
+        self.fut, self.single = fut, single
 
 
 class RulesBatcher:
@@ -299,14 +300,19 @@ class RulesBatcher:
 
     async def submit(self, incident_id, evidence: list[dict], ranked: bool) -> list[dict]:
         """One incident's hypothesis list (generate_hypotheses, ranked or not)."""
-        return (await self.submit_many([incident_id], [evidence], ranked))[0]
+        loop = asyncio.get_running_loop()
+        return await self._submit(loop, _Call([str(incident_id)], [evidence], ranked,
+                                              loop.create_future(), True))
 
     async def submit_many(self, incident_ids: list, evidence_lists: list, ranked: bool
                           ) -> list[list[dict]]:
         """Several incidents as ONE call (it raises as a whole if any row makes the
         reference raise, as the reference's loop over them would)."""
         loop = asyncio.get_running_loop()
-        call = _Call([str(i) for i in incident_ids], list(evidence_lists), ranked, loop.create_future())
+        return await self._submit(loop, _Call([str(i) for i in incident_ids], list(evidence_lists),
+                                              ranked, loop.create_future()))
+
+    async def _submit(self, loop, call: "_Call"):
         self.calls += 1
         self.queue.append(call)
         if self.busy:
@@ -396,7 +402,7 @@ class RulesBatcher:
                     if not c.ranked:
                         FUSED.register(self.cat, res, lists, range(len(lists)))
                     if not c.fut.done():
-                        c.fut.set_result(lists)
+                        c.fut.set_result(lists[0] if c.single else lists)
                     return
                 # incident rows of every call, then one native assembly per ranking mode
                 starts = np.cumsum([0] + [len(c.incident_ids) for c in ok])
@@ -407,21 +413,28 @@ class RulesBatcher:
                 raise
 
     def _deliver(self, ok: list, starts, enc: EncodedBatch, res: RulesResult) -> None:
+        modes = np.fromiter((c.ranked for c in ok), bool, len(ok))
+        counts = np.diff(starts)
         for ranked in (False, True):
-            cs = [j for j, c in enumerate(ok) if c.ranked == ranked]
-            if not cs:
+            sel = modes == ranked
+            if not sel.any():
                 continue
-            idx = np.concatenate([np.arange(starts[j], starts[j + 1]) for j in cs])
-            sub = res if len(idx) == enc.n_incidents else RulesResult(*(a[idx] for a in (
-                res.mask, res.n_hyp, res.order_conf, res.order_rank, res.confidence,
-                res.final_score, res.strength)))
-            ids = [i for j in cs for i in ok[j].incident_ids]
-            lists = hypothesis_lists(self.cat, sub, ids, [enc.evidence_ids[i] for i in idx], ranked)
+            if sel.all():                  # (the common case: every call in one mode)
+                cs, sub, eids = ok, res, enc.evidence_ids
+            else:
+                cs = [c for c, m in zip(ok, sel) if m]
+                idx = np.flatnonzero(np.repeat(sel, counts))
+                sub = RulesResult(*(a[idx] for a in (
+                    res.mask, res.n_hyp, res.order_conf, res.order_rank, res.confidence,
+                    res.final_score, res.strength)))
+                eids = [enc.evidence_ids[i] for i in idx.tolist()]
+            ids = [i for c in cs for i in c.incident_ids]
+            lists = hypothesis_lists(self.cat, sub, ids, eids, ranked)
             if not ranked:             # the kernel ranked them too: HypothesisRanker.rank reuses it
                 FUSED.register(self.cat, sub, lists, range(len(lists)))
             pos = 0
-            for j in cs:
-                n = len(ok[j].incident_ids)
-                if not ok[j].fut.done():
-                    ok[j].fut.set_result(lists[pos:pos + n])
+            for c in cs:
+                n = len(c.incident_ids)
+                if not c.fut.done():
+                    c.fut.set_result(lists[pos] if n == 1 and c.single else lists[pos:pos + n])
                 pos += n

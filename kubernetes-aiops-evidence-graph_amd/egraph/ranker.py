@@ -145,12 +145,18 @@ class FusedRanks:
         final = res.final_score[sel].tolist()
         oconf = res.order_conf[sel].tolist()
         orank = res.order_rank[sel].tolist()
+        u = cat.unknown
+        # what the native check (pyhost.fused_apply) compares against, read from the catalog
+        # now as apply() would read it
+        ncat = (cat.n_rules, tuple(r["category"] for r in cat.rules),
+                tuple(len(r["conditions"]) for r in cat.rules),
+                (u["confidence"], u["category"], u["support_count"], u["signal_strength"]))
         recs = []
         for j, hyps in enumerate(lists):
             if hyps:
                 n = len(hyps)
                 recs.append((hyps[0]["id"], (tuple(h["id"] for h in hyps), cat, oconf[j][:n],
-                                              conf[j], strength[j], final[j], orank[j][:n])))
+                                              conf[j], strength[j], final[j], orank[j][:n], ncat)))
         with self.lock:
             for key, rec in recs:
                 self.recs[key] = rec
@@ -166,7 +172,17 @@ class FusedRanks:
         if rec is None or len(hyps) != len(rec[0]):
             self.misses += 1
             return None
-        ids, cat, slots, conf, strength, final, orank = rec
+        if type(hyps) is list:
+            # the same checks and writes in native code (csrc/pyhost.c fused_apply); None: a
+            # value it leaves to the Python statement below
+            r = L.pyhost.fused_apply(hyps, rec)
+            if r is not None:
+                if r is False:
+                    self.misses += 1
+                    return None
+                self.hits += 1
+                return r
+        ids, cat, slots, conf, strength, final, orank, _ = rec
         R, rules, u = cat.n_rules, cat.rules, cat.unknown
         for h, hid, slot in zip(hyps, ids, slots):
             if not isinstance(h, dict) or h.get("id") != hid:
