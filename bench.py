@@ -46,6 +46,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "kubernetes-aiops-evidence-graph_amd"))
 
 METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod graph"
+XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -658,24 +659,45 @@ def time_dense(ctx, hops: int, steps: int, B: int, V: int, nnz: int, dev) -> dic
 
 
 class _TimedPlan:
-    """Delegates to a Plan, recording HIP events around the non-seed propagation hops."""
+    """Delegates to a Plan, recording HIP events around the non-seed propagation hops (`ev`)
+    and, per partition (`part`: a list collecting this partition's (start, end) pairs), around
+    every kernel of the partition's own compute (hops, reach hops, candidates, top-k)."""
 
-    def __init__(self, plan, ev):
-        self._p, self._ev, self._h = plan, ev, 0
+    def __init__(self, plan, ev, part=None):
+        self._p, self._ev, self._h, self._part = plan, ev, 0, part
 
     def __getattr__(self, name):
         return getattr(self._p, name)
+
+    def _timed(self, fn, *a):
+        if self._part is None:
+            return fn(*a)
+        x, y = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        x.record()
+        r = fn(*a)
+        y.record()
+        self._part.append((x, y))
+        return r
 
     def hop(self):
         if self._ev is not None and self._h > 0:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            self._p.hop()
+            self._timed(self._p.hop)
             b.record()
             self._ev.append((a, b))
         else:
-            self._p.hop()
+            self._timed(self._p.hop)
         self._h += 1
+
+    def reach_hop(self):
+        return self._timed(self._p.reach_hop)
+
+    def candidates(self, *a):
+        return self._timed(self._p.candidates, *a)
+
+    def topk(self, *a):
+        return self._timed(self._p.topk, *a)
 
 
 def shard_setup(args, world: int, rank: int, dev: torch.device):
@@ -725,13 +747,13 @@ def shard_setup(args, world: int, rank: int, dev: torch.device):
                 enc_full=encode_batch(evidence, catalog.default()), evidence=evidence, V=V)
 
 
-def shard_step(ctx, hops: int, k: int, ev=None):
+def shard_step(ctx, hops: int, k: int, ev=None, parts=None):
     from egraph import shard
     ctx["rules"].launch()
-    for run, (plan, seeds, sources) in zip(ctx["runs"], ctx["plans"]):
+    for i, (run, (plan, seeds, sources)) in enumerate(zip(ctx["runs"], ctx["plans"])):
         plan.set_seeds(*seeds)
         plan.set_sources(sources)
-        run.eng = _TimedPlan(plan, ev)
+        run.eng = _TimedPlan(plan, ev, parts[i] if parts is not None else None)
     return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k,
                                  sparse=not ctx.get("dense_halo", False))
 
@@ -757,6 +779,13 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     elapsed = time.perf_counter() - t0
     if dist:
         elapsed = max_over_ranks(dist, elapsed, dev)
+    # untimed: each partition's own compute (its kernels only, no exchange) per step, from HIP
+    # events -- the per-GPU time of P GPUs running their partitions side by side
+    parts = [[] for _ in ctx["runs"]]
+    for _ in range(3):
+        shard_step(ctx, args.hops, args.k, None, parts)
+    torch.cuda.synchronize(dev)
+    part_ms = [sum(a.elapsed_time(b) for a, b in q) / 3 for q in parts]
     B = args.batch
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -786,6 +815,13 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "halo_exchange": "dense" if args.dense_halo else "sparse (non-zero entries only)",
             "halo_bytes_sent_per_hop_max_rank": sent,
             "halo_reduction_vs_dense": halo / sent if sent else None,
+            "partition_compute_ms": part_ms,
+            "projected_ms_per_gpu": max(part_ms) + (args.hops - 1) * sent / (XGMI_LINK_GBS * 1e6),
+            "projected_note": "max over partitions of their own kernels' time (HIP events, untimed "
+                              "steps) + the score and reach halo entries of the largest sender over "
+                              "one xGMI link per exchange; what P GPUs running one partition each "
+                              "would take per step (the in-process ms_per_step runs them one after "
+                              "another on one GPU)",
         },
         "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -906,6 +942,9 @@ def storm_main(args, world: int, rank: int, dev: torch.device) -> None:
                    "involuntary_switches_per_tick": float(np.mean([s_["invol_cs"] for s_ in stats])),
                    "new_incidents_per_tick": float(np.mean([s_["new_incidents"] for s_ in stats])),
                    "affected_per_tick": float(np.mean([s_["affected"] for s_ in stats])),
+                   "reseed_per_tick": {k_: float(np.mean([s_["reseed"].get(k_, 0) for s_ in stats]))
+                                       for k_ in ("incidents", "new", "candidates_ms", "attach_ms",
+                                                  "pending_ms")},
                    "open_incidents_end": stats[-1]["open_incidents"],
                    "parallelism": (f"fingerprint-sharded dedup x{world}, replicated graph, "
                                    f"incidents re-ranked by owner rank") if world > 1 else "one GPU",

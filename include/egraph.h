@@ -288,7 +288,9 @@ int egr_plan_induced_edges(const egr_plan* p, int32_t col, uint32_t* out_src, ui
  * Per hop the owners' fresh rows of the exported vertices are packed, exchanged (RCCL
  * all-gather, done by the caller) and unpacked into the halo rows.
  *   egr_snapshot_from_csr : host arrays row_ptr [V+1], col/meta/val [row_ptr[V]], vlabel [V].
- *   egr_plan_set_owned    : rows [0, n_owned) are the only top-k candidates.
+ *   egr_plan_set_owned    : rows [0, n_owned) are the only top-k candidates, and the hop /
+ *                           reach sweeps cover only them (halo rows [n_owned, V) hold what
+ *                           the exchange unpacks; their values are not computed here).
  *   egr_plan_pack_*       : out[i] = row rows[i] of the current scores ([n][Bpad] fp32, column
  *                           b at b) / reach ([n][ceil(n_cols/64)] u64).
  *   egr_plan_unpack_*     : row rows[i] = in[src[i]] (same layouts).

@@ -1384,6 +1384,17 @@ int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const ui
 int egr_plan_set_owned(egr_plan* p, int64_t n_owned) {
   if (!p || n_owned <= 0 || n_owned > p->s->V)
     return egr::fail(EGR_EINVAL, "egr_plan_set_owned: need 0 < n_owned <= n_vertices");
+  // a partition's halo rows (vertices past n_owned) have no row data here: their values arrive
+  // through the halo exchange, so the hop and reach sweeps run over the owned rows only
+  // (fewer chunks than the plan's tables hold: they fit the allocations)
+  DeviceGuard guard(p->s->device);
+  const std::vector<uint32_t> chunks = build_chunks(p->s->row_ptr_host, (uint32_t)n_owned, hop_rows(p->TW));
+  const std::vector<uint32_t> rchunks = build_chunks(p->s->row_ptr_host, (uint32_t)n_owned, reach_rows(p->RG));
+  if (hipMemcpy(p->chunk_start, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p->rchunk_start, rchunks.data(), rchunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: chunk table upload failed");
+  p->nchunks = (uint32_t)chunks.size() - 1;
+  p->rnchunks = (uint32_t)rchunks.size() - 1;
   p->owned = (uint32_t)n_owned;
   p->cand_valid = false;
   return EGR_OK;

@@ -1548,9 +1548,45 @@ enum { ST_POD, ST_DEPLOY, ST_DCHANGE, ST_ICHANGE, ST_NODE, ST_HPA, ST_CONFIG, ST
 static PyObject** seed_types[ST_N] = {&t_pod, &t_deploy, &t_dchange, &t_ichange, &t_node, &t_hpa,
                                       &t_config, &t_event, &t_log, &t_metric};
 
-/* resolve prefix + a [+ ":" + b]: 1 = found (*v), 0 = absent, -1 = id too long (hand over) */
-static inline int s_try(FindFn find, const void* g, const char* pre, size_t pn, const char* a,
-                        size_t an, const char* b, Py_ssize_t bn, int32_t* v) {
+/* Where a row's candidate ids go, in order: the attachment (`find` each until one is present)
+ * or the key list (every id appended to a byte buffer).  put: 1 = stop (found), 0 = go on,
+ * -1 = cannot (hand the row over). */
+typedef struct IdSink {
+  int (*put)(struct IdSink*, const char* p, size_t n);
+  FindFn find;                  /* attach */
+  const void* g;
+  int32_t v;
+  char* buf;                    /* keys: malloc'd (worker threads hold no GIL-side allocator) */
+  size_t n, cap;
+  int nid;                      /* ids appended for the current row */
+} IdSink;
+
+static int sink_find(IdSink* k, const char* p, size_t n) {
+  k->v = k->find(k->g, p, (int64_t)n);
+  return k->v >= 0;
+}
+
+static int sink_keys(IdSink* k, const char* p, size_t n) {
+  if (k->n + n + 8 > k->cap) {
+    size_t c = k->cap ? 2 * k->cap : 1 << 16;
+    while (c < k->n + n + 8) c *= 2;
+    char* b = realloc(k->buf, c);
+    if (!b) return -1;
+    k->buf = b;
+    k->cap = c;
+  }
+  const uint32_t len = (uint32_t)n;                 /* u32 length, then the bytes */
+  memcpy(k->buf + k->n, &len, 4);
+  k->n += 4;
+  memcpy(k->buf + k->n, p, n);
+  k->n += n;
+  ++k->nid;
+  return 0;
+}
+
+/* prefix + a [+ ":" + b] into the sink: its put's result, -1 = id too long (hand over) */
+static inline int s_try(IdSink* k, const char* pre, size_t pn, const char* a, size_t an,
+                        const char* b, Py_ssize_t bn) {
   IdBuf B;
   B.n = 0;
   B.ovf = 0;
@@ -1561,13 +1597,14 @@ static inline int s_try(FindFn find, const void* g, const char* pre, size_t pn, 
     ib_put(&B, b, (size_t)bn);
   }
   if (B.ovf) return -1;
-  *v = find(g, B.b, (int64_t)B.n);
-  return *v >= 0;
+  return k->put(k, B.b, B.n);
 }
 
-/* One row on a worker: 0 = done (*vout = the attached vertex or NO_NODE), 1 = hand over */
-static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float* sout) {
-  *vout = NO_NODE;
+/* One row on a worker: 0 = done (*seeds = the row seeds: it has candidate ids, all given to the
+ * sink, and a strength > 0 or NaN in *sv), 1 = hand over.  The ids are given in attach_ids'
+ * order; a sink that returns 1 stops the row there. */
+static int s_row_ids(PyObject* ev, IdSink* k, int* seeds, double* svp) {
+  *seeds = 0;
   if (!PyDict_CheckExact(ev)) return 1;
   PyObject* o[5];
   if (w_get(ev, K_SEED, 5, o)) return 1;
@@ -1583,6 +1620,7 @@ static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float
     if (ovf) return 1;
     sv = (double)x;                 /* round to nearest, as float(int) */
   } else return 1;
+  *svp = sv;
   if (t == NULL || t == Py_None) return 0;                       /* no candidate */
   if (!PyUnicode_CheckExact(t)) return 1;
   if (data != NULL && data != Py_None && !PyDict_CheckExact(data)) return 1;
@@ -1597,12 +1635,37 @@ static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float
   }
   if (ty < 0) return 0;                                          /* any other type: none */
   if (sv <= 0.0) return 0;                                       /* `s <= 0` (NaN seeds) */
-  int32_t v = -1;
+  PyObject *kind = NULL, *oname = NULL, *ons = NULL;
+  if (ty == ST_EVENT) {                   /* (the involved object is read before any id is given) */
+    PyObject* obj = NULL;
+    if (data != NULL && data != Py_None && PyDict_GET_SIZE(data) > 0 && w_get(data, K_INV, 1, &obj))
+      return 1;
+    if (obj != NULL && obj != Py_None && !PyDict_CheckExact(obj)) return 1;
+    if (obj != NULL && (obj == Py_None || PyDict_GET_SIZE(obj) == 0)) obj = NULL;
+    if (obj != NULL) {
+      PyObject* q[3];
+      if (w_get(obj, K_OBJ, 3, q)) return 1;
+      kind = q[0]; oname = q[1]; ons = q[2];
+    }
+  }
+  const char *kp = "", *op = NULL, *sp = NULL;
+  Py_ssize_t kn = 0, on = 0, sn = 0;
+  char kl[64];
+  if (ty == ST_EVENT) {
+    /* kind = str(obj.get("kind", "")).lower() (ASCII here: lower() is per-byte) */
+    if (kind != NULL && w_part(kind, &kp, &kn)) return 1;
+    if (kn >= (Py_ssize_t)sizeof(kl)) return 1;
+    for (Py_ssize_t i = 0; i < kn; ++i) kl[i] = (char)((kp[i] >= 'A' && kp[i] <= 'Z') ? kp[i] + 32 : kp[i]);
+    if (w_part(oname, &op, &on)) return 1;                      /* obj.get('name') */
+    if (ons == NULL) { sp = a; sn = an; }                        /* obj.get('namespace', ns) */
+    else if (w_part(ons, &sp, &sn)) return 1;
+  }
+  *seeds = 1;
   int r = 0;
 #define TRY(pre, x, xn, y, yn) do {                                              \
-    r = s_try(find, g, pre, sizeof(pre) - 1, x, (size_t)(xn), y, yn, &v);      \
+    r = s_try(k, pre, sizeof(pre) - 1, x, (size_t)(xn), y, yn);                \
     if (r < 0) return 1;                                                       \
-    if (r > 0) goto found;                                                     \
+    if (r > 0) return 0;                                                       \
   } while (0)
   switch (ty) {
     case ST_POD: TRY("pod:", a, an, b, bn); break;
@@ -1616,31 +1679,8 @@ static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float
       TRY("deployment:", a, an, b, bn);
       break;
     case ST_METRIC: TRY("metric:", a, an, b, bn); break;
-    case ST_EVENT: {
-      PyObject* obj = NULL;
-      if (data != NULL && data != Py_None && PyDict_GET_SIZE(data) > 0 && w_get(data, K_INV, 1, &obj))
-        return 1;
-      if (obj != NULL && obj != Py_None && !PyDict_CheckExact(obj)) return 1;
-      if (obj != NULL && (obj == Py_None || PyDict_GET_SIZE(obj) == 0)) obj = NULL;
-      PyObject *kind = NULL, *oname = NULL, *ons = NULL;
-      if (obj != NULL) {
-        PyObject* q[3];
-        if (w_get(obj, K_OBJ, 3, q)) return 1;
-        kind = q[0]; oname = q[1]; ons = q[2];
-      }
+    case ST_EVENT:
       TRY("event:", a, an, b, bn);
-      /* kind = str(obj.get("kind", "")).lower() (ASCII here: lower() is per-byte) */
-      const char* kp = "";
-      Py_ssize_t kn = 0;
-      if (kind != NULL && w_part(kind, &kp, &kn)) return 1;
-      char kl[64];
-      if (kn >= (Py_ssize_t)sizeof(kl)) return 1;
-      for (Py_ssize_t i = 0; i < kn; ++i) kl[i] = (char)((kp[i] >= 'A' && kp[i] <= 'Z') ? kp[i] + 32 : kp[i]);
-      const char *op, *sp;
-      Py_ssize_t on, sn;
-      if (w_part(oname, &op, &on)) return 1;                      /* obj.get('name') */
-      if (ons == NULL) { sp = a; sn = an; }                        /* obj.get('namespace', ns) */
-      else if (w_part(ons, &sp, &sn)) return 1;
       if (kn == 4 && memcmp(kl, "node", 4) == 0) {
         TRY("node:", op, on, NULL, -1);
       } else if (kn > 0) {
@@ -1653,17 +1693,32 @@ static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float
         ib_put(&B, ":", 1);
         ib_put(&B, op, (size_t)on);
         if (B.ovf) return 1;
-        v = find(g, B.b, (int64_t)B.n);
-        if (v >= 0) goto found;
+        r = k->put(k, B.b, B.n);
+        if (r < 0) return 1;
       }
       break;
-    }
   }
 #undef TRY
   return 0;
-found:
-  *vout = (uint32_t)v;
-  *sout = (float)sv;
+}
+
+/* One row on a worker for the attachment: 0 = done (*vout = the attached vertex or NO_NODE),
+ * 1 = hand over */
+static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float* sout) {
+  *vout = NO_NODE;
+  IdSink k;
+  memset(&k, 0, sizeof(k));
+  k.put = sink_find;
+  k.find = find;
+  k.g = g;
+  k.v = -1;
+  int seeds = 0;
+  double sv = 0.0;
+  if (s_row_ids(ev, &k, &seeds, &sv)) return 1;
+  if (seeds && k.v >= 0) {
+    *vout = (uint32_t)k.v;
+    *sout = (float)sv;
+  }
   return 0;
 }
 
@@ -1956,8 +2011,339 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
   return out;
 }
 
+/* ---- seed attachment candidates as keys (egraph/seeds.py SeedCandidates.per_column keys=True)
+ * seed_keys(evidence_lists, slow[, threads]) -> (blob, off i64 [n+1], hash i64 [n], count i64
+ * [rows], col u32 [rows], val f32 [rows]): SeedCandidates(evidence_lists) with its candidate ids
+ * as ONE UTF-8 blob + offsets + 64-bit hashes of the bytes (id_hash64, the alert storm's pending
+ * index key; pyhost.hash_ids hashes query ids the same way) instead of a list of Python strs.
+ * Row pass on the worker pool as seed_attach; rows handed over are redone serially in row order. */
+static inline uint64_t id_hash64(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xFF51AFD7ED558CCDull);
+  while (n >= 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    h = (h ^ (w * 0xC4CEB9FE1A85EC53ull)) * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 29;
+    p += 8;
+    n -= 8;
+  }
+  if (n) {
+    uint64_t w = 0;
+    memcpy(&w, p, n);
+    h = (h ^ (w * 0xC4CEB9FE1A85EC53ull)) * 0x9E3779B97F4A7C15ull;
+  }
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
+}
+
+typedef struct {
+  PyObject* const* lists;
+  const int64_t* base;
+  Py_ssize_t i0, i1;
+  IdSink sink;                  /* this job's id records (u32 length + bytes) */
+  int64_t* rowpos;              /* per row: its first record's offset in the job's buffer */
+  uint8_t* nid;                 /* per row: ids given (0: the row does not seed) */
+  float* val;
+  uint8_t* redo;
+} KJob;
+
+static void* k_main(void* arg) {
+  KJob* J = (KJob*)arg;
+  for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
+    PyObject* evs = J->lists[i];
+    const Py_ssize_t n = PyList_GET_SIZE(evs);
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      const Py_ssize_t r = J->base[i] + j;
+      const size_t pos = J->sink.n;
+      J->sink.nid = 0;
+      int seeds = 0;
+      double sv = 0.0;
+      const int redo = s_row_ids(PyList_GET_ITEM(evs, j), &J->sink, &seeds, &sv);
+      J->redo[r] = (uint8_t)redo;
+      J->rowpos[r] = (int64_t)pos;
+      if (redo) J->sink.n = pos;                   /* (drop a partial row) */
+      J->nid[r] = (uint8_t)(redo || !seeds ? 0 : J->sink.nid);
+      J->val[r] = (float)sv;
+    }
+  }
+  return NULL;
+}
+
+typedef struct {
+  char* blob;
+  int64_t *off, *hash, *count;
+  uint32_t* col;
+  float* val;
+  Py_ssize_t nb, capb, nf, capf, nr, capr;
+} KOut;
+
+static int kout_id(KOut* o, const char* p, size_t n) {
+  if ((size_t)(o->capb - o->nb) < n) {
+    Py_ssize_t c = o->capb ? 2 * o->capb : 1 << 16;
+    while ((size_t)(c - o->nb) < n) c *= 2;
+    char* b = PyMem_Realloc(o->blob, (size_t)c);
+    if (!b) { PyErr_NoMemory(); return -1; }
+    o->blob = b;
+    o->capb = c;
+  }
+  if (o->nf + 2 > o->capf) {
+    const Py_ssize_t c = o->capf ? 2 * o->capf : 4096;
+    int64_t* f = PyMem_Realloc(o->off, sizeof(int64_t) * (size_t)c);
+    if (f) o->off = f;
+    int64_t* h = PyMem_Realloc(o->hash, sizeof(int64_t) * (size_t)c);
+    if (h) o->hash = h;
+    if (!f || !h) { PyErr_NoMemory(); return -1; }
+    o->capf = c;
+  }
+  memcpy(o->blob + o->nb, p, n);
+  o->off[o->nf] = o->nb;
+  o->hash[o->nf] = (int64_t)id_hash64(p, n);
+  o->nb += (Py_ssize_t)n;
+  ++o->nf;
+  return 0;
+}
+
+static int kout_row(KOut* o, int64_t k, uint32_t col, float v) {
+  if (o->nr == o->capr) {
+    const Py_ssize_t c = o->capr ? 2 * o->capr : 4096;
+    int64_t* a = PyMem_Realloc(o->count, sizeof(int64_t) * (size_t)c);
+    if (a) o->count = a;
+    uint32_t* b = PyMem_Realloc(o->col, sizeof(uint32_t) * (size_t)c);
+    if (b) o->col = b;
+    float* d = PyMem_Realloc(o->val, sizeof(float) * (size_t)c);
+    if (d) o->val = d;
+    if (!a || !b || !d) { PyErr_NoMemory(); return -1; }
+    o->capr = c;
+  }
+  o->count[o->nr] = k;
+  o->col[o->nr] = col;
+  o->val[o->nr] = v;
+  ++o->nr;
+  return 0;
+}
+
+/* One row on the calling thread: cand_ids or the Python statement, its ids appended */
+static int k_row_serial(PyObject* ev, PyObject* slow, KOut* o, uint32_t col, int* ran_python) {
+  PyObject* ids = PyList_New(0);
+  if (!ids) return -1;
+  double sv = 0.0;
+  int fast = 0;
+  if (PyDict_CheckExact(ev)) {
+    PyObject* st;
+    fast = cand_ids(ev, ids);
+    if (fast == 1) {
+      if (dget(ev, a_strength, &st)) fast = 0;
+      else if (st == NULL) sv = 0.5;
+      else if (PyFloat_CheckExact(st)) sv = PyFloat_AS_DOUBLE(st);
+      else if (PyLong_CheckExact(st) || PyBool_Check(st)) {
+        sv = PyLong_AsDouble(st);
+        if (sv == -1.0 && PyErr_Occurred()) { PyErr_Clear(); fast = 0; }
+      } else fast = 0;
+    }
+  }
+  if (fast < 0) { Py_DECREF(ids); return -1; }
+  if (!fast) {
+    Py_DECREF(ids);
+    *ran_python = 1;
+    PyObject* r = PyObject_CallOneArg(slow, ev);
+    if (!r) return -1;
+    if (!PyArg_ParseTuple(r, "Od", &ids, &sv) || !PyList_Check(ids)) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "seed_keys: bad slow row");
+      Py_DECREF(r);
+      return -1;
+    }
+    Py_INCREF(ids);
+    Py_DECREF(r);
+  }
+  const Py_ssize_t k = PyList_GET_SIZE(ids);
+  int rc = 0;
+  if (k > 0 && !(sv <= 0.0)) {
+    for (Py_ssize_t i = 0; i < k && rc == 0; ++i) {
+      PyObject* x = PyList_GET_ITEM(ids, i);
+      Py_ssize_t n;
+      const char* u = PyUnicode_Check(x) ? PyUnicode_AsUTF8AndSize(x, &n) : NULL;
+      if (!u) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "seed_keys: candidate id is not a str");
+        rc = -1;
+      } else {
+        rc = kout_id(o, u, (size_t)n);
+      }
+    }
+    if (rc == 0) rc = kout_row(o, k, col, (float)sv);
+  }
+  Py_DECREF(ids);
+  return rc;
+}
+
+static PyObject* seed_keys(PyObject* self, PyObject* args) {
+  PyObject *lists, *slow;
+  int threads = 1;
+  if (!PyArg_ParseTuple(args, "OO|i", &lists, &slow, &threads)) return NULL;
+  PyObject* seq = PySequence_Fast(lists, "evidence_lists must be a sequence");
+  if (!seq) return NULL;
+  PyObject* result = NULL;
+  KOut o;
+  memset(&o, 0, sizeof(o));
+  int64_t* base = NULL;
+  int64_t* rowpos = NULL;
+  uint8_t *nid = NULL, *redo = NULL, *jobof = NULL;
+  float* wval = NULL;
+  KJob jobs[PAR_MAX_THREADS];
+  int njobs = 0;
+  const Py_ssize_t B = PySequence_Fast_GET_SIZE(seq);
+  int par = threads > 1;
+  Py_ssize_t total = 0;
+  for (Py_ssize_t i = 0; par && i < B; ++i) {
+    PyObject* evs = PySequence_Fast_GET_ITEM(seq, i);
+    if (!PyList_CheckExact(evs)) par = 0;
+    else total += PyList_GET_SIZE(evs);
+  }
+  if (par && total < PAR_MIN_ROWS) par = 0;
+  if (par) {
+    base = PyMem_Malloc(sizeof(int64_t) * (size_t)(B + 1));
+    rowpos = PyMem_Malloc(sizeof(int64_t) * (size_t)total);
+    nid = PyMem_Malloc((size_t)total);
+    redo = PyMem_Malloc((size_t)total);
+    jobof = PyMem_Malloc((size_t)total);
+    wval = PyMem_Malloc(sizeof(float) * (size_t)total);
+    if (!base || !rowpos || !nid || !redo || !jobof || !wval) { PyErr_NoMemory(); goto done; }
+    base[0] = 0;
+    for (Py_ssize_t i = 0; i < B; ++i) base[i + 1] = base[i] + PyList_GET_SIZE(PySequence_Fast_GET_ITEM(seq, i));
+    if (threads > PAR_MAX_THREADS) threads = PAR_MAX_THREADS;
+    Py_ssize_t i = 0;
+    for (int t = 0; t < threads; ++t) {
+      const int64_t goal = (int64_t)((total * (t + 1)) / threads);
+      const Py_ssize_t i0 = i;
+      while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
+      memset(&jobs[t], 0, sizeof(KJob));
+      jobs[t].lists = PySequence_Fast_ITEMS(seq);
+      jobs[t].base = base;
+      jobs[t].i0 = i0;
+      jobs[t].i1 = i;
+      jobs[t].sink.put = sink_keys;
+      jobs[t].rowpos = rowpos;
+      jobs[t].nid = nid;
+      jobs[t].val = wval;
+      jobs[t].redo = redo;
+      for (int64_t r = base[i0]; r < base[i]; ++r) jobof[r] = (uint8_t)t;
+    }
+    njobs = threads;
+    pool_run_fn(k_main, jobs, sizeof(KJob), threads);   /* (the GIL stays held) */
+  }
+  {
+    int ran_python = 0;
+    Py_ssize_t r = 0;
+    for (Py_ssize_t i = 0; i < B; ++i) {
+      PyObject* evs = PySequence_Fast(PySequence_Fast_GET_ITEM(seq, i), "evidence is not iterable");
+      if (!evs) goto done;
+      const Py_ssize_t n = PySequence_Fast_GET_SIZE(evs);
+      for (Py_ssize_t j = 0; j < n; ++j, ++r) {
+        if (par && !ran_python && !redo[r]) {
+          if (!nid[r]) continue;
+          const IdSink* k = &jobs[jobof[r]].sink;
+          const char* q = k->buf + rowpos[r];
+          for (int x = 0; x < nid[r]; ++x) {
+            uint32_t len;
+            memcpy(&len, q, 4);
+            if (kout_id(&o, q + 4, len) < 0) { Py_DECREF(evs); goto done; }
+            q += 4 + len;
+          }
+          if (kout_row(&o, nid[r], (uint32_t)i, wval[r]) < 0) { Py_DECREF(evs); goto done; }
+        } else {
+          /* (a small batch: the worker's row function on this thread first) */
+          if (!par && !ran_python) {
+            IdSink k;
+            memset(&k, 0, sizeof(k));
+            k.put = sink_keys;
+            int seeds = 0;
+            double sv = 0.0;
+            if (!s_row_ids(PySequence_Fast_GET_ITEM(evs, j), &k, &seeds, &sv)) {
+              int bad = 0;
+              if (seeds && k.nid > 0) {
+                const char* q = k.buf;
+                for (int x = 0; x < k.nid && !bad; ++x) {
+                  uint32_t len;
+                  memcpy(&len, q, 4);
+                  bad = kout_id(&o, q + 4, len) < 0;
+                  q += 4 + len;
+                }
+                if (!bad) bad = kout_row(&o, k.nid, (uint32_t)i, (float)sv) < 0;
+              }
+              free(k.buf);
+              if (bad) { Py_DECREF(evs); goto done; }
+              continue;
+            }
+            free(k.buf);
+          }
+          if (k_row_serial(PySequence_Fast_GET_ITEM(evs, j), slow, &o, (uint32_t)i, &ran_python) < 0) {
+            Py_DECREF(evs);
+            goto done;
+          }
+        }
+      }
+      Py_DECREF(evs);
+    }
+  }
+  if (o.nf + 1 > o.capf || !o.off) {
+    int64_t* f = PyMem_Realloc(o.off, sizeof(int64_t) * (size_t)(o.nf + 1));
+    if (!f) { PyErr_NoMemory(); goto done; }
+    o.off = f;
+  }
+  o.off[o.nf] = o.nb;
+  result = Py_BuildValue("(y#y#y#y#y#y#)", o.blob ? o.blob : "", o.nb,
+                         (const char*)o.off, (o.nf + 1) * (Py_ssize_t)sizeof(int64_t),
+                         o.hash ? (const char*)o.hash : "", o.nf * (Py_ssize_t)sizeof(int64_t),
+                         o.count ? (const char*)o.count : "", o.nr * (Py_ssize_t)sizeof(int64_t),
+                         o.col ? (const char*)o.col : "", o.nr * (Py_ssize_t)sizeof(uint32_t),
+                         o.val ? (const char*)o.val : "", o.nr * (Py_ssize_t)sizeof(float));
+done:
+  for (int t = 0; t < njobs; ++t) free(jobs[t].sink.buf);
+  PyMem_Free(base);
+  PyMem_Free(rowpos);
+  PyMem_Free(nid);
+  PyMem_Free(redo);
+  PyMem_Free(jobof);
+  PyMem_Free(wval);
+  PyMem_Free(o.blob);
+  PyMem_Free(o.off);
+  PyMem_Free(o.hash);
+  PyMem_Free(o.count);
+  PyMem_Free(o.col);
+  PyMem_Free(o.val);
+  Py_DECREF(seq);
+  return result;
+}
+
+/* hash_ids(ids) -> int64 bytes: id_hash64 of each str's UTF-8 bytes (seed_keys' hashes) */
+static PyObject* hash_ids(PyObject* self, PyObject* arg) {
+  PyObject* seq = PySequence_Fast(arg, "ids must be a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  int64_t* h = PyMem_Malloc(sizeof(int64_t) * (size_t)(n + 1));
+  PyObject* out = NULL;
+  if (!h) { PyErr_NoMemory(); goto done; }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* x = PySequence_Fast_GET_ITEM(seq, i);
+    Py_ssize_t len;
+    const char* u = PyUnicode_Check(x) ? PyUnicode_AsUTF8AndSize(x, &len) : NULL;
+    if (!u) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "hash_ids: ids must be strs");
+      goto done;
+    }
+    h[i] = (int64_t)id_hash64(u, (size_t)len);
+  }
+  out = PyBytes_FromStringAndSize((const char*)h, n * (Py_ssize_t)sizeof(int64_t));
+done:
+  PyMem_Free(h);
+  Py_DECREF(seq);
+  return out;
+}
+
 static PyMethodDef methods[] = {
     {"seed_candidates", seed_candidates, METH_VARARGS, "evidence rows -> seed attachment candidates"},
+    {"seed_keys", seed_keys, METH_VARARGS, "evidence rows -> seed candidates as a keyed blob"},
+    {"hash_ids", hash_ids, METH_O, "64-bit hashes of ids' UTF-8 bytes"},
     {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
     {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},

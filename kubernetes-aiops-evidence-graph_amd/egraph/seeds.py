@@ -91,32 +91,41 @@ class SeedCandidates:
         return len(self.flat) if self.flat is not None else len(self.keys[2])
 
     def _flat_keys(self):
-        """(utf-8 blob, int64 offsets [n+1], int64 Python hashes [n]) of the flat ids: what a
-        blob graph lookup and the storm's pending index read, computed once per batch."""
+        """(utf-8 blob, int64 offsets [n+1], int64 hashes of the ids' bytes [n]) of the flat ids:
+        what a blob graph lookup and the storm's pending index read (pyhost.hash_ids)."""
+        from . import _lib
         from .graph import str_blob
         b, o = str_blob(self.flat)
-        return b, o, np.fromiter(map(hash, self.flat), np.int64, len(self.flat))
+        return b, o, np.frombuffer(_lib.pyhost.hash_ids(self.flat), np.int64)
 
     @classmethod
     def per_column(cls, evidence_lists: list[list[dict]], keys: bool = False) -> list["SeedCandidates"]:
         """One SeedCandidates per evidence list, from ONE native pass over all of them.  With
         `keys`, each also carries its ids' blob / offsets / hashes (for combine(with_flat=False))
         and drops the per-id str list."""
-        sc = cls(evidence_lists)
-        n = sc.n_cols
-        rb = np.searchsorted(sc.col, np.arange(n + 1, dtype=np.uint32))       # rows per column
-        fb = np.concatenate([[0], np.cumsum(sc.count)])[rb]                   # flat ids per column
+        n = len(evidence_lists)
         if not keys:
+            sc = cls(evidence_lists)
+            rb = np.searchsorted(sc.col, np.arange(n + 1, dtype=np.uint32))   # rows per column
+            fb = np.concatenate([[0], np.cumsum(sc.count)])[rb]               # flat ids per column
             return [cls._of(1, sc.flat[fb[b]:fb[b + 1]], sc.count[rb[b]:rb[b + 1]],
                             np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]])
                     for b in range(n)]
-        blob, off, hs = sc._flat_keys()
+        # keyed form: one native pass emits the ids as a blob + offsets + hashes directly
+        # (csrc/pyhost.c seed_keys; no Python str per id)
+        from . import _lib
+        from .encode import encode_threads
+        blob, off, hs, count, col, val = _lib.pyhost.seed_keys(evidence_lists, _row, encode_threads())
+        off, hs = np.frombuffer(off, np.int64), np.frombuffer(hs, np.int64)
+        count, col = np.frombuffer(count, np.int64), np.frombuffer(col, np.uint32)
+        val = np.frombuffer(val, np.float32)
+        rb = np.searchsorted(col, np.arange(n + 1, dtype=np.uint32))
+        fb = np.concatenate([[0], np.cumsum(count)])[rb]
         out = []
         for b in range(n):
-            f0, f1 = fb[b], fb[b + 1]
+            f0, f1, r0, r1 = fb[b], fb[b + 1], rb[b], rb[b + 1]
             k = (blob[off[f0]:off[f1]], off[f0:f1 + 1] - off[f0], hs[f0:f1])
-            out.append(cls._of(1, None, sc.count[rb[b]:rb[b + 1]],
-                               np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]], k))
+            out.append(cls._of(1, None, count[r0:r1], np.zeros(r1 - r0, np.uint32), val[r0:r1], k))
         return out
 
     @classmethod

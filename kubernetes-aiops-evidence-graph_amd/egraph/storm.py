@@ -105,6 +105,7 @@ class StormEngine:
         self._gen = np.zeros(0, np.int64)
         self._frontiers: dict[int, object] = {}
         self.ticks = 0
+        self.last_reseed: dict = {}
         # (vertex, incident) pairs the affected test reads: incident vertices and seed vertices
         self._chk_v = torch.zeros(0, dtype=torch.int64, device=self.dev)
         self._chk_o = torch.zeros(0, dtype=torch.int64, device=self.dev)
@@ -126,6 +127,7 @@ class StormEngine:
         """(Re)attach the evidence rows of these incidents to the current graph: their
         candidate ids are extracted once per incident (native, egraph/seeds.py; the incidents
         without them in ONE pass) and all of them are looked up and attached in ONE batch."""
+        t0 = time.perf_counter()
         xs = [self.incidents[h] for h in handles]
         need = [x for x in xs if x.cand is None]
         if need:
@@ -133,6 +135,7 @@ class StormEngine:
                 x.cand = c
                 if not self.keep_evidence:
                     x.evidence = None
+        t1 = time.perf_counter()
         if not xs:
             return
         cand = SeedCandidates.combine([x.cand for x in xs], with_flat=False)
@@ -142,6 +145,7 @@ class StormEngine:
         cut = np.searchsorted(col, np.arange(len(xs) + 1, dtype=np.uint32))
         for j, x in enumerate(xs):
             x.sv, x.ss = sv[cut[j]:cut[j + 1]], ss[cut[j]:cut[j + 1]]
+        t2 = time.perf_counter()
         # the incidents' pending ids: their earlier entries retire (generation bump)
         hs = np.array([x.handle for x in xs], np.int64)
         top = int(hs.max()) + 1
@@ -162,13 +166,16 @@ class StormEngine:
                 if live.sum() * 2 < len(live):
                     self._pend_h, self._pend_o, self._pend_g = (
                         self._pend_h[live], self._pend_o[live], self._pend_g[live])
+        self.last_reseed = {"incidents": len(xs), "new": len(need), "candidates_ms": (t1 - t0) * 1e3,
+                            "attach_ms": (t2 - t1) * 1e3, "pending_ms": (time.perf_counter() - t2) * 1e3}
 
     def _pending_hit(self, ids: list) -> set:
         """Incidents with a live pending entry whose hash matches one of these ids: a binary
         search of the ids' hashes in the hash-sorted index, then the runs of equal hashes."""
         if not ids or not len(self._pend_h):
             return set()
-        q = np.fromiter((hash(v) for v in ids), np.int64, len(ids))
+        from egraph import _lib
+        q = np.frombuffer(_lib.pyhost.hash_ids(ids), np.int64)    # (seed_keys' id hashes)
         lo = np.searchsorted(self._pend_h, q, "left")
         n = np.searchsorted(self._pend_h, q, "right") - lo
         tot = int(n.sum())
@@ -324,7 +331,7 @@ class StormEngine:
                 "open_incidents": len(self.incidents),
                 "ms": dict(zip(("fingerprint_dedup", "merge_host", "csr_update", "affected", "seeds_host",
                                "rerank"), ms)),
-                "collect_ms": t_collect * 1e3}
+                "collect_ms": t_collect * 1e3, "reseed": dict(self.last_reseed)}
 
     def rankings(self) -> list[tuple[np.ndarray, np.ndarray]]:
         """(top ids, top scores) of every incident (None for those another rank owns)."""

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3: the edge-cut path with owned-row sweeps -- the partition tests, then C4 at P = 1, 2,
+# 4, 8 partitions in one process (per-partition compute times + the projected per-GPU step).
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${TAG:-shard_r03}
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_shard_gpu.py tests/test_configs_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "shard or C4 or partition" > $OUT/pytest.log 2>&1
+echo "tests ok"; tail -1 $OUT/pytest.log
+for P in 1 2 4 8; do
+  timeout -k 10 200 python -u bench.py --shard graph --config C4 --partitions $P --steps 5 --warmup 2 --no-cpu-baseline > $OUT/c4_p$P.json 2> $OUT/c4_p$P.err
+  python -c "import json;d=json.load(open('$OUT/c4_p$P.json'));c=d['config'];print('P=$P', round(d['ms_per_step'],2), 'ms in-process; partitions', [round(x,2) for x in c['partition_compute_ms']], 'projected per GPU', round(c['projected_ms_per_gpu'],2), 'sent/hop', c['halo_bytes_sent_per_hop_max_rank'])"
+done

@@ -196,7 +196,8 @@ def test_storm_pending_index_lookup():
     ids = [f"pod/ns/p{i}" for i in range(300)]
     ent = [(ids[int(rng.integers(300))], int(rng.integers(40)), int(rng.integers(3))) for _ in range(2000)]
     gen = rng.integers(0, 3, 40)
-    h = np.array([hash(e[0]) for e in ent], np.int64)
+    from egraph import _lib
+    h = np.frombuffer(_lib.pyhost.hash_ids([e[0] for e in ent]), np.int64)
     o = np.array([e[1] for e in ent], np.int64)
     g = np.array([e[2] for e in ent], np.int64)
     k = np.argsort(h, kind="stable")
@@ -211,7 +212,7 @@ def test_keyed_candidates_match_flat_ones():
     offsets and hashes instead of str lists) name the same ids in the same order, and attach
     identically, as the str-list form -- including non-ASCII names and empty columns."""
     import numpy as np
-    from egraph import synth
+    from egraph import _lib, synth
     from egraph.graph import str_blob
     from egraph.seeds import SeedCandidates
     cl = synth.build_cluster(synth.ClusterConfig(pods=400, namespaces=3, nodes=8,
@@ -228,7 +229,7 @@ def test_keyed_candidates_match_flat_ones():
     for f, k in ((flat, keyed), (part_f, part_k)):
         b, o = str_blob(f.flat)
         assert k.keys[0] == b and np.array_equal(k.keys[1], o)
-        assert np.array_equal(k.keys[2], np.array([hash(x) for x in f.flat], np.int64))
+        assert np.array_equal(k.keys[2], np.frombuffer(_lib.pyhost.hash_ids(f.flat), np.int64))
         assert k.n_flat == f.n_flat and np.array_equal(k.count, f.count)
         assert np.array_equal(k.col, f.col) and np.array_equal(k.val, f.val)
         found = np.random.default_rng(3).integers(-1, 30, f.n_flat)
@@ -324,3 +325,45 @@ def test_graph_find_matches_lookup():
     want = g.lookup(ids).tolist()
     got = [_lib.lib.egr_graph_find(g.handle, x.encode(), len(x.encode())) for x in ids]
     assert got == want and want[0] == 0 and want[2] == -1
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_seed_keys_match_seed_candidates(threads):
+    """pyhost.seed_keys (the keyed per_column form, one native pass) names the same ids, counts,
+    columns and strengths as SeedCandidates (str ids through the Python statement for the rows
+    it hands over), with hash_ids' hashes -- on collector rows and on edge rows, both thread
+    modes (the worker pool runs from 4096 rows)."""
+    from egraph import _lib, synth
+    from egraph.graph import str_blob
+    from egraph.seeds import SeedCandidates, _row
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    lists = [x.evidence for x in synth.make_incidents(c, 120, seed=10)]
+    rng = random.Random(7)
+    lists += [EDGE, [], EDGE[::-1]] + [rng.sample(EDGE, 8) for _ in range(30)]
+    lists[5] = [dict(lists[5][0], entity_name="pé-テ")] + lists[5][1:]
+    sc = SeedCandidates(lists)
+    blob, off, hs, count, col, val = _lib.pyhost.seed_keys(lists, _row, threads)
+    b, o = str_blob(sc.flat)
+    assert blob == b and np.array_equal(np.frombuffer(off, np.int64), o)
+    assert np.array_equal(np.frombuffer(hs, np.int64), np.frombuffer(_lib.pyhost.hash_ids(sc.flat), np.int64))
+    assert np.array_equal(np.frombuffer(count, np.int64), sc.count)
+    assert np.array_equal(np.frombuffer(col, np.uint32), sc.col)
+    assert np.array_equal(np.frombuffer(val, np.float32), sc.val, equal_nan=True)
+
+
+@pytest.mark.parametrize("bad", [
+    {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
+     "signal_strength": "x"},
+    ["not", "a", "dict"],
+])
+def test_seed_keys_raise_like_python(bad):
+    from egraph import _lib
+    from egraph.seeds import _row, candidates_py
+    lists = [[dict(EDGE[0])] * 5000, [bad]]
+    with pytest.raises(Exception) as e1:
+        candidates_py(lists)
+    for th in (1, 4):
+        with pytest.raises(Exception) as e2:
+            _lib.pyhost.seed_keys(lists, _row, th)
+        assert type(e1.value) is type(e2.value)
