@@ -699,6 +699,26 @@ class _TimedPlan:
     def topk(self, *a):
         return self._timed(self._p.topk, *a)
 
+    # the halo exchange's own device work (pack before, unpack after the transfer) runs on the
+    # partition's GPU too: counted in its compute (the pack's host read of the peer sizes included)
+    def pack_sparse(self, *a, **k):
+        return self._timed(lambda: self._p.pack_sparse(*a, **k))
+
+    def unpack_sparse(self, *a, **k):
+        return self._timed(lambda: self._p.unpack_sparse(*a, **k))
+
+    def pack_scores(self, *a):
+        return self._timed(self._p.pack_scores, *a)
+
+    def unpack_scores(self, *a):
+        return self._timed(self._p.unpack_scores, *a)
+
+    def pack_reach(self, *a):
+        return self._timed(self._p.pack_reach, *a)
+
+    def unpack_reach(self, *a):
+        return self._timed(self._p.unpack_reach, *a)
+
 
 def shard_setup(args, world: int, rank: int, dev: torch.device):
     from egraph import catalog, shard, synth
@@ -817,11 +837,12 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "halo_reduction_vs_dense": halo / sent if sent else None,
             "partition_compute_ms": part_ms,
             "projected_ms_per_gpu": max(part_ms) + (args.hops - 1) * sent / (XGMI_LINK_GBS * 1e6),
-            "projected_note": "max over partitions of their own kernels' time (HIP events, untimed "
-                              "steps) + the score and reach halo entries of the largest sender over "
-                              "one xGMI link per exchange; what P GPUs running one partition each "
-                              "would take per step (the in-process ms_per_step runs them one after "
-                              "another on one GPU)",
+            "projected_note": "max over partitions of their own device work per step (hops, reach "
+                              "hops, candidates, top-k and the halo pack / unpack kernels; HIP events, "
+                              "untimed steps) + the largest sender's halo entries over one xGMI link "
+                              "per exchange; what P GPUs running one partition each would take per "
+                              "step (the in-process ms_per_step runs them one after another on one "
+                              "GPU)",
         },
         "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

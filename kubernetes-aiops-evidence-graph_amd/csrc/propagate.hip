@@ -95,6 +95,8 @@ __device__ __forceinline__ void add_seeds(float4& acc, uint32_t v, uint32_t lo,
 // single rounding as the oracle).  Reachability is a separate pass (reach_kernel): folding
 // its words into this walk costs more TA cycles than the reach pass itself (PMC, round 1).
 constexpr uint32_t CSR_CAP = 2048;
+// sparse halo exchange: mask words per send row (32-column groups; EGR_MAX_COLS columns)
+#define EGR_SX_MASK_WORDS ((EGR_MAX_COLS / 32 + 31) / 32)
 constexpr int NB = 4;
 
 template <int G>
@@ -113,6 +115,8 @@ struct HopArgs {
   const uint32_t* seed_tiles;
   const float* xin;
   float* xout;
+  uint8_t* nzout;     // partitioned plans: [V][ntiles] "row v's tile holds a non-zero" of xout
+  uint32_t ntiles;    // (nullptr otherwise: the flags cost nothing on the unpartitioned path)
   uint32_t V;
   uint32_t nchunks;
 };
@@ -261,6 +265,16 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
 #else
     Y[(size_t)v * G + gl] = acc;
 #endif
+    if (A.nzout) {
+      // the row's tile flag for the sparse halo pack: OR over the G lanes of this row (a
+      // group's lanes are contiguous; lanes of a finished group vote nothing)
+      const bool nz = (__float_as_uint(acc.x) | __float_as_uint(acc.y) | __float_as_uint(acc.z) |
+                       __float_as_uint(acc.w)) != 0u;
+      const uint64_t m = __ballot(nz);
+      const uint32_t sh = (tid & 63u) / G * G;
+      const uint64_t gm = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+      if (gl == 0) A.nzout[(size_t)v * A.ntiles + tile] = ((m >> sh) & gm) ? 1 : 0;
+    }
   };
 
   Batch<FROM_SEEDS> ba, bb;
@@ -283,13 +297,15 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
 __global__ void seed_add_kernel(const uint64_t* __restrict__ ukeys,
                                 const float* __restrict__ uval,
                                 const uint32_t* __restrict__ n_unique, uint32_t Bpad,
-                                uint32_t TW, uint32_t V, float* __restrict__ X) {
+                                uint32_t TW, uint32_t V, float* __restrict__ X,
+                                uint8_t* __restrict__ nz, uint32_t ntiles) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= *n_unique) return;
   const uint64_t k = ukeys[i];
   const uint32_t v = (uint32_t)(k / Bpad), b = (uint32_t)(k % Bpad);
   float* p = X + ((size_t)(b / TW) * V + v) * TW + (b % TW);
   *p = *p + uval[i];
+  if (nz) nz[(size_t)v * ntiles + b / TW] = 1;   // (s0 > 0 or NaN: the entry is non-zero)
 }
 
 __global__ void seed_tiles_kernel(const uint64_t* __restrict__ ukeys,
@@ -743,67 +759,146 @@ __device__ __forceinline__ uint32_t sx_value(const float* X, const uint64_t* R, 
   return bits != 0u;     // -0.0 is not +0: sent (bit-exact)
 }
 
-__global__ __launch_bounds__(256) void sx_count_kernel(const float* __restrict__ X,
-    const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
-    const uint32_t* __restrict__ rows, int64_t* __restrict__ cnt) {
-  __shared__ int wsum[4];
-  const uint32_t v = rows[blockIdx.x];
-  int c = 0;
-  for (int b = threadIdx.x; b < width; b += 256) {
-    uint64_t w;
-    c += sx_value(X, R, V, TW, RS, v, b, reach, &w);
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+// off[seg[q]] for q = 0..P: the entry offsets at the peer boundaries, contiguous
+__global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t* __restrict__ seg, int P,
+                                 int64_t* __restrict__ out) {
+  const int q = threadIdx.x;
+  if (q <= P) out[q] = off[seg[q]];
 }
 
+// The exchange kernels run ONE WAVE PER ROW (four rows per 256-thread block): a boundary row
+// is cheap, and a block per row made them bound by workgroup dispatch (~120k blocks per C4
+// exchange at P = 8).
+constexpr int SX_ROWS = 4;
+
+// Sender, pass 1: the row's non-zero count, and a bit per 32-column group that holds any
+// (masks [n_rows][MW] u32) so that pass 2 reads only those groups; score rows of a partitioned
+// plan skip the tiles the hop wrote no non-zero to (nzf).
+__global__ __launch_bounds__(256) void sx_count_kernel(const float* __restrict__ X,
+    const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
+    const uint32_t* __restrict__ rows, int64_t n, int64_t* __restrict__ cnt,
+    uint32_t* __restrict__ masks, int MW, const uint8_t* __restrict__ nzf, uint32_t ntiles) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
+  if (r >= n) return;                                      // (no barrier below)
+  const uint32_t v = rows[r];
+  const uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
+  // the row's tile flags in one wave-wide load (up to 64 tiles; more: read per column)
+  const uint64_t fm = fl && ntiles <= 64u ? __ballot(lane < (int)ntiles && fl[lane]) : ~0ull;
+  auto flagged = [&](int t) { return !fl || (ntiles <= 64u ? ((fm >> t) & 1ull) != 0ull : fl[t] != 0); };
+  uint32_t mk[EGR_SX_MASK_WORDS];
+#pragma unroll
+  for (int i = 0; i < EGR_SX_MASK_WORDS; ++i) mk[i] = 0u;
+  int c = 0;
+  for (int b0 = 0; b0 < width; b0 += 64) {
+    if (fl && TW >= 64 && !flagged(b0 / TW)) continue;    // (uniform: one tile per 64 columns)
+    const int b = b0 + lane;
+    uint64_t w;
+    const bool nz = b < width && flagged(b / TW) && sx_value(X, R, V, TW, RS, v, b, reach, &w);
+    const uint64_t m = __ballot(nz);
+    c += __popcll(m);
+    const int g = b0 >> 5;
+#pragma unroll
+    for (int i = 0; i < EGR_SX_MASK_WORDS; ++i) {
+      if (i == (g >> 5) && (uint32_t)m) mk[i] |= 1u << (g & 31);
+      if (i == ((g + 1) >> 5) && (m >> 32)) mk[i] |= 1u << ((g + 1) & 31);
+    }
+  }
+  if (lane == 0) {
+    cnt[r] = c;
+    for (int i = 0; i < MW; ++i) masks[(size_t)r * MW + i] = mk[i];
+  }
+}
+
+// index of the k-th set bit (k from 0) of the MW-word mask m
+__device__ __forceinline__ int kth_bit(const uint32_t* __restrict__ m, int MW, int k) {
+  for (int i = 0; i < MW; ++i) {
+    uint32_t x = m[i];
+    const int c = __popc(x);
+    if (k < c) {
+      for (int j = 0; j < k; ++j) x &= x - 1u;
+      return 32 * i + (__ffs((int)x) - 1);
+    }
+    k -= c;
+  }
+  return -1;
+}
+
+// Sender, pass 2: the non-zero entries of the row's marked groups, in column order, at the
+// row's offset (the exclusive scan of pass 1's counts).  Each half-wave takes one marked group
+// per round.
 __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ X,
     const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
-    const uint32_t* __restrict__ rows, const int64_t* __restrict__ seg, int P,
-    const int64_t* __restrict__ off, int64_t* __restrict__ out) {
-  __shared__ int wcnt[4];
-  const int64_t r = blockIdx.x;
+    const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
+    const int64_t* __restrict__ off, const uint32_t* __restrict__ masks, int MW,
+    int64_t* __restrict__ out, int64_t cap) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
+  if (r >= n) return;
+  uint32_t mk[EGR_SX_MASK_WORDS];
+  int nset = 0;
+#pragma unroll
+  for (int i = 0; i < EGR_SX_MASK_WORDS; ++i) {
+    mk[i] = i < MW ? masks[(size_t)r * MW + i] : 0u;
+    nset += __popc(mk[i]);
+  }
+  if (nset == 0) return;                                   // (uniform in the wave)
   const uint32_t v = rows[r];
   int q = 0;
   while (q + 1 < P && seg[q + 1] <= r) ++q;
   const int64_t rl = r - seg[q];
   int64_t pos = off[r];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int b0 = 0; b0 < width; b0 += 256) {
-    const int b = b0 + (int)threadIdx.x;
+  for (int base = 0; base < nset; base += 2) {
+    const int g = base + half < nset ? kth_bit(mk, MW, base + half) : -1;
+    const int b = g >= 0 ? 32 * g + hl : width;
     uint64_t w = 0;
     const bool nz = b < width && sx_value(X, R, V, TW, RS, v, b, reach, &w);
     const uint64_t m = __ballot(nz);
-    if (lane == 0) wcnt[wv] = __popcll(m);
-    __syncthreads();
-    int before = __popcll(m & ((1ull << lane) - 1ull));
-    for (int j = 0; j < wv; ++j) before += wcnt[j];
-    const int total = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    const uint32_t mine = half ? hi : lo;
+    const int before = __popc(mine & ((1u << hl) - 1u)) + (half ? __popc(lo) : 0);
+    // (launched before the host has checked the total against the buffer: entries past `cap`
+    // words are dropped here and the call then fails)
     if (nz) {
       const int64_t idx = rl * width + b;
       if (reach) {
-        out[2 * (pos + before)] = idx;
-        out[2 * (pos + before) + 1] = (int64_t)w;
-      } else {
+        if (2 * (pos + before) + 1 < cap) {
+          out[2 * (pos + before)] = idx;
+          out[2 * (pos + before) + 1] = (int64_t)w;
+        }
+      } else if (pos + before < cap) {
         out[pos + before] = (idx << 32) | (int64_t)w;
       }
     }
-    pos += total;
-    __syncthreads();                      // wcnt is reused by the next round
+    pos += __popcll(m);
   }
 }
 
 // Receiver: zero the received halo rows, then scatter the entries (one thread per entry; the
 // sender s of entry e: eseg[s] <= e < eseg[s+1]; its recv rows start at rbase[s]).
-__global__ void sx_zero_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V, int TW,
-                               uint32_t RS, int width, bool reach,
-                               const uint32_t* __restrict__ recv_vertex) {
-  const uint32_t v = recv_vertex[blockIdx.x];
-  for (int b = threadIdx.x; b < width; b += blockDim.x) {
+// With flags (scores of a partitioned plan whose buffer has been zeroed once): only the tiles
+// a scatter (or a seed add) wrote since are cleared, and their flags with them.
+__global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uint64_t* __restrict__ R,
+                               uint32_t V, int TW, uint32_t RS, int width, bool reach,
+                               const uint32_t* __restrict__ recv_vertex, int64_t n,
+                               uint8_t* __restrict__ nzf, uint32_t ntiles, bool flagged) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
+  if (r >= n) return;
+  const uint32_t v = recv_vertex[r];
+  uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
+  const uint64_t fm = flagged && ntiles <= 64u ? __ballot(lane < (int)ntiles && fl[lane]) : ~0ull;
+  auto set = [&](int t) { return !flagged || (ntiles <= 64u ? ((fm >> t) & 1ull) != 0ull : fl[t] != 0); };
+  for (int b0 = 0; b0 < width; b0 += 64) {
+    if (flagged && TW >= 64 && !set(b0 / TW)) continue;    // (uniform: one tile per 64 columns)
+    const int b = b0 + lane;
+    if (b >= width || !set(b / TW)) continue;
     if (reach) R[(size_t)v * RS + b] = 0ull;
     else X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = 0.f;
+  }
+  if (fl) {
+    __builtin_amdgcn_wave_barrier();                       // every lane has read the flags
+    for (uint32_t t = lane; t < ntiles; t += 64) fl[t] = 0;
   }
 }
 
@@ -812,7 +907,8 @@ __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ 
                                   const uint32_t* __restrict__ recv_vertex,
                                   const int64_t* __restrict__ in, int64_t n,
                                   const int64_t* __restrict__ eseg,
-                                  const int64_t* __restrict__ rbase, int P) {
+                                  const int64_t* __restrict__ rbase, int P,
+                                  uint8_t* __restrict__ nzf, uint32_t ntiles) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   int s = 0;
@@ -831,7 +927,10 @@ __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ 
   const int b = (int)(idx % width);
   const uint32_t v = recv_vertex[row];
   if (reach) R[(size_t)v * RS + b] = w;
-  else X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = __uint_as_float((uint32_t)w);
+  else {
+    X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = __uint_as_float((uint32_t)w);
+    if (nzf) nzf[(size_t)v * ntiles + b / TW] = 1;  // (the next unpack clears only these tiles)
+  }
 }
 
 }  // namespace
@@ -849,6 +948,11 @@ struct egr_plan {
   uint32_t* rchunk_start = nullptr;
   float* x[2] = {nullptr, nullptr};
   int xcur = 0;
+  // partitioned plans (egr_plan_set_owned): per x buffer, [V][ntiles] tile flags -- owned rows:
+  // the hop's non-zero tiles (the sparse pack reads only those); halo rows: the tiles written
+  // since the last unpack (it clears only those, once the buffer has been zeroed in full)
+  uint8_t* nzf[2] = {nullptr, nullptr};
+  bool xzeroed[2] = {false, false};
   uint64_t* reach[2] = {nullptr, nullptr};
   int rcur = 0;
   int reach_hops = -1;  // -1: sources not set
@@ -874,7 +978,10 @@ struct egr_plan {
   size_t sx_cap = 0;
   void* sx_tmp = nullptr;
   size_t sx_tmp_bytes = 0;
-  int64_t* sx_tot = nullptr;        // [EGR_SX_MAX_PEERS + 1]
+  int64_t* sx_tot = nullptr;        // [EGR_SX_MAX_PEERS + 1] peer bounds, then the segments
+  int64_t* sx_pin = nullptr;        // pinned host: the segments up, the peer bounds down
+  uint32_t* sx_mask = nullptr;      // [rows][MW] non-zero 32-column groups of each send row
+  size_t sx_mask_cap = 0;
 };
 
 namespace {
@@ -953,6 +1060,8 @@ int plan_hop(egr_plan* p, void* stream) {
   a.seed_tiles = p->seed_tiles;
   a.xin = seeds ? nullptr : p->x[p->xcur];
   a.xout = p->x[seeds ? 0 : 1 - p->xcur];
+  a.nzout = p->nzf[seeds ? 0 : 1 - p->xcur];
+  a.ntiles = (uint32_t)p->ntiles;
   a.V = (uint32_t)s->V;
   a.nchunks = p->nchunks;
   const dim3 grid(p->nchunks * p->ntiles);
@@ -965,7 +1074,7 @@ int plan_hop(egr_plan* p, void* stream) {
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
                      dim3(256), 0, st, p->sp.ukeys, p->sp.uval, p->sp.n_unique, (uint32_t)p->Bpad,
-                     (uint32_t)p->TW, (uint32_t)s->V, a.xout);
+                     (uint32_t)p->TW, (uint32_t)s->V, a.xout, a.nzout, a.ntiles);
   EGR_CHECK_LAUNCH();
   p->xcur = seeds ? 0 : 1 - p->xcur;
   ++p->hops_done;
@@ -1111,6 +1220,8 @@ void egr_plan_free(egr_plan* p) {
   if (!p) return;
   DeviceGuard guard(p->s->device);
   for (auto* q : {&p->x[0], &p->x[1]}) dfree(*q);
+  dfree(p->nzf[0]);
+  dfree(p->nzf[1]);
   dfree(p->reach[0]);
   dfree(p->reach[1]);
   p->sp.free_all();
@@ -1126,6 +1237,8 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->rchunk_start);
   dfree(p->sx_off);
   dfree(p->sx_tot);
+  if (p->sx_pin) (void)hipHostFree(p->sx_pin);
+  dfree(p->sx_mask);
   if (p->sx_tmp) (void)hipFree(p->sx_tmp);
   delete p;
 }
@@ -1395,6 +1508,16 @@ int egr_plan_set_owned(egr_plan* p, int64_t n_owned) {
     return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: chunk table upload failed");
   p->nchunks = (uint32_t)chunks.size() - 1;
   p->rnchunks = (uint32_t)rchunks.size() - 1;
+  for (int b = 0; b < 2; ++b) {
+    if (!p->nzf[b]) {
+      const size_t nb = (size_t)p->s->V * p->ntiles;
+      const int rc = dalloc(&p->nzf[b], nb);
+      if (rc != EGR_OK) return rc;
+      if (hipMemset(p->nzf[b], 0, nb) != hipSuccess)
+        return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: flag init failed");
+    }
+    p->xzeroed[b] = false;
+  }
   p->owned = (uint32_t)n_owned;
   p->cand_valid = false;
   return EGR_OK;
@@ -1419,6 +1542,7 @@ int egr_plan_unpack_scores(egr_plan* p, const uint32_t* rows, const uint32_t* sr
     return egr::fail(EGR_EINVAL, "egr_plan_unpack_scores: bad arguments");
   if (p->hops_done < 1) return egr::fail(EGR_ESTATE, "egr_plan_unpack_scores: run a hop first");
   if (n == 0) return EGR_OK;
+  p->xzeroed[p->xcur] = false;              // full halo rows written: no tile tracking
   DeviceGuard guard(p->s->device);
   hipLaunchKernelGGL(unpack_scores_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
                      p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->Bpad, rows, src, in);
@@ -1493,32 +1617,53 @@ int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_
     const int rc = dalloc(&p->sx_tot, (size_t)EGR_SX_MAX_PEERS + 1 + EGR_SX_MAX_PEERS + 1);
     if (rc != EGR_OK) return rc;
   }
+  if (!p->sx_pin)
+    EGR_HIP(hipHostMalloc(reinterpret_cast<void**>(&p->sx_pin),
+                          sizeof(int64_t) * 2 * ((size_t)EGR_SX_MAX_PEERS + 1), hipHostMallocDefault));
   int64_t* dseg = p->sx_tot + EGR_SX_MAX_PEERS + 1;
-  EGR_HIP(hipMemcpyAsync(dseg, seg, sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, st));
+  int64_t* pseg = p->sx_pin;                                  // (free: the last call synchronised)
+  int64_t* pbound = p->sx_pin + EGR_SX_MAX_PEERS + 1;
+  for (int q = 0; q <= P; ++q) pseg[q] = seg[q];
+  EGR_HIP(hipMemcpyAsync(dseg, pseg, sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, st));
   const float* X = reach ? nullptr : p->x[p->xcur];
   const uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;
+  const int MW = (((width + 31) / 32) + 31) / 32;            // mask words per row
+  if ((size_t)n * MW > p->sx_mask_cap) {
+    dfree(p->sx_mask);
+    p->sx_mask_cap = 0;
+    const int rc = dalloc(&p->sx_mask, (size_t)n * MW);
+    if (rc != EGR_OK) return rc;
+    p->sx_mask_cap = (size_t)n * MW;
+  }
   EGR_HIP(hipMemsetAsync(p->sx_off + n, 0, sizeof(int64_t), st));
-  hipLaunchKernelGGL(sx_count_kernel, dim3((unsigned)n), dim3(256), 0, st, X, R, V, p->TW,
-                     (uint32_t)p->RS, width, reach, rows, p->sx_off);
+  const dim3 sxg((unsigned)((n + SX_ROWS - 1) / SX_ROWS));
+  hipLaunchKernelGGL(sx_count_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
+                     (uint32_t)p->RS, width, reach, rows, (int64_t)n, p->sx_off, p->sx_mask, MW,
+                     reach ? nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles);
   EGR_CHECK_LAUNCH();
   size_t tb = p->sx_tmp_bytes;
   EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sx_tmp, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
-  // the entry offsets at the peer boundaries (P + 1 values) decide the all-to-all split sizes
-  std::vector<int64_t> bound((size_t)P + 1);
-  for (int q = 0; q <= P; ++q)
-    EGR_HIP(hipMemcpyAsync(&bound[q], p->sx_off + seg[q], sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  // the entry offsets at the peer boundaries (P + 1 values) decide the all-to-all split sizes:
+  // gathered on the device and read back in ONE pinned copy (one small pageable copy per peer
+  // cost a staged round trip each: 288 per C4 step at P = 8)
+  hipLaunchKernelGGL(sx_bounds_kernel, dim3(1), dim3(EGR_SX_MAX_PEERS + 1), 0, st, p->sx_off, dseg, P,
+                     p->sx_tot);
+  EGR_CHECK_LAUNCH();
+  EGR_HIP(hipMemcpyAsync(pbound, p->sx_tot, sizeof(int64_t) * (P + 1), hipMemcpyDeviceToHost, st));
+  // the entries go out before the host reads the sizes (the emit needs only the device offsets):
+  // the device works while the copy and the host's synchronisation round trip are in flight
+  hipLaunchKernelGGL(sx_emit_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
+                     (uint32_t)p->RS, width, reach, rows, (int64_t)n, dseg, P, p->sx_off, p->sx_mask,
+                     MW, out, cap);
+  EGR_CHECK_LAUNCH();
   EGR_HIP(hipStreamSynchronize(st));
+  const int64_t* bound = pbound;
   const int64_t total = bound[P];
   const int64_t words = reach ? 2 * total : total;
   if (words > cap) return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse: output too small (" +
                                                     std::to_string(words) + " words)");
   for (int q = 0; q < P; ++q) counts[q] = bound[q + 1] - bound[q];
-  if (total > 0) {
-    hipLaunchKernelGGL(sx_emit_kernel, dim3((unsigned)n), dim3(256), 0, st, X, R, V, p->TW,
-                       (uint32_t)p->RS, width, reach, rows, dseg, P, p->sx_off, out);
-    EGR_CHECK_LAUNCH();
-  }
   return EGR_OK;
 }
 
@@ -1538,13 +1683,17 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
   float* X = reach ? nullptr : p->x[p->xcur];
   uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;
-  hipLaunchKernelGGL(sx_zero_kernel, dim3((unsigned)n_rows), dim3(256), 0, st, X, R, V, p->TW,
-                     (uint32_t)p->RS, width, reach, recv_vertex);
+  uint8_t* nzf = reach ? nullptr : p->nzf[p->xcur];
+  hipLaunchKernelGGL(sx_zero_kernel, dim3((unsigned)((n_rows + SX_ROWS - 1) / SX_ROWS)), dim3(256), 0,
+                     st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, (int64_t)n_rows,
+                     nzf, (uint32_t)p->ntiles,
+                     nzf != nullptr && p->xzeroed[p->xcur]);
   EGR_CHECK_LAUNCH();
+  if (nzf) p->xzeroed[p->xcur] = true;      // its halo rows are now tracked by their tile flags
   if (n_entries > 0) {
     hipLaunchKernelGGL(sx_scatter_kernel, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0,
                        st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, in,
-                       n_entries, eseg, rbase, P);
+                       n_entries, eseg, rbase, P, nzf, (uint32_t)p->ntiles);
     EGR_CHECK_LAUNCH();
   }
   p->cand_valid = false;
