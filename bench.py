@@ -400,6 +400,31 @@ def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
         return min(ts), (b0.launches - l0) // 3
 
     t_conc, conc_launches = asyncio.run(concurrent())
+
+    async def floor():
+        # the event loop's own cost for the same pattern: len(ev) tasks, each awaiting a future
+        # that one batch resolves (no rules, no ranking) -- the bound on `concurrent`
+        loop = asyncio.get_running_loop()
+        futs: list = []
+
+        async def wait_one():
+            f = loop.create_future()
+            futs.append(f)
+            return await f
+
+        async def resolve():
+            await asyncio.sleep(0)
+            for f in futs:
+                f.set_result(None)
+        ts = []
+        for _ in range(3):
+            futs.clear()
+            gc.collect()
+            t0 = time.perf_counter()
+            await asyncio.gather(resolve(), *[wait_one() for _ in range(len(ev))])
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+    t_floor = asyncio.run(floor())
     from egraph.encode import encode_threads
     return {"value": len(ev) / best, "unit": "incidents/s",
             "cores": encode_threads(), "cores_note": "the encoder's parallel row pass; assembly "
@@ -418,6 +443,10 @@ def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
                                                  "restatement), same incidents, 1 core"},
             "concurrent": {"value": len(ev) / t_conc, "unit": "incidents/s",
                            "calls": len(ev), "launches": conc_launches,
+                           "asyncio_floor": len(ev) / t_floor,
+                           "asyncio_floor_what": "the same number of tasks awaiting futures one "
+                                                 "batch resolves, nothing else: CPython's own cost "
+                                                 "for one task per call on this host",
                            "what": "every incident its own generate_hypotheses + rank call, all "
                                    "in flight at once; the batcher coalesces them"}}
 
