@@ -766,10 +766,12 @@ __global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t*
   if (q <= P) out[q] = off[seg[q]];
 }
 
-// The exchange kernels run ONE WAVE PER ROW (four rows per 256-thread block): a boundary row
-// is cheap, and a block per row made them bound by workgroup dispatch (~120k blocks per C4
-// exchange at P = 8).
+// The exchange kernels run ONE WAVE PER ROW, four per 256-thread block, in a grid of at most
+// SX_MAX_BLOCKS blocks that strides over the rows: a boundary row is cheap, and a block (or a
+// wave) per row launched them bound by workgroup dispatch (~120k rows per C4 exchange at P = 8).
 constexpr int SX_ROWS = 4;
+constexpr int64_t SX_MAX_BLOCKS = 2048;      // grid-stride beyond this (8 blocks per CU)
+inline dim3 sx_grid(int64_t n) { return dim3((unsigned)std::min<int64_t>((n + SX_ROWS - 1) / SX_ROWS, SX_MAX_BLOCKS)); }
 
 // Sender, pass 1: the row's non-zero count, and a bit per 32-column group that holds any
 // (masks [n_rows][MW] u32) so that pass 2 reads only those groups; score rows of a partitioned
@@ -779,8 +781,7 @@ __global__ __launch_bounds__(256) void sx_count_kernel(const float* __restrict__
     const uint32_t* __restrict__ rows, int64_t n, int64_t* __restrict__ cnt,
     uint32_t* __restrict__ masks, int MW, const uint8_t* __restrict__ nzf, uint32_t ntiles) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
-  if (r >= n) return;                                      // (no barrier below)
+  for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   const uint32_t v = rows[r];
   const uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
   // the row's tile flags in one wave-wide load (up to 64 tiles; more: read per column)
@@ -808,6 +809,7 @@ __global__ __launch_bounds__(256) void sx_count_kernel(const float* __restrict__
     cnt[r] = c;
     for (int i = 0; i < MW; ++i) masks[(size_t)r * MW + i] = mk[i];
   }
+  }
 }
 
 // index of the k-th set bit (k from 0) of the MW-word mask m
@@ -833,8 +835,7 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     const int64_t* __restrict__ off, const uint32_t* __restrict__ masks, int MW,
     int64_t* __restrict__ out, int64_t cap) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
-  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
-  if (r >= n) return;
+  for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   uint32_t mk[EGR_SX_MASK_WORDS];
   int nset = 0;
 #pragma unroll
@@ -842,7 +843,7 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     mk[i] = i < MW ? masks[(size_t)r * MW + i] : 0u;
     nset += __popc(mk[i]);
   }
-  if (nset == 0) return;                                   // (uniform in the wave)
+  if (nset == 0) continue;                                 // (uniform in the wave)
   const uint32_t v = rows[r];
   int q = 0;
   while (q + 1 < P && seg[q + 1] <= r) ++q;
@@ -872,6 +873,7 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     }
     pos += __popcll(m);
   }
+  }
 }
 
 // Receiver: zero the received halo rows, then scatter the entries (one thread per entry; the
@@ -883,8 +885,7 @@ __global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uin
                                const uint32_t* __restrict__ recv_vertex, int64_t n,
                                uint8_t* __restrict__ nzf, uint32_t ntiles, bool flagged) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv;
-  if (r >= n) return;
+  for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   const uint32_t v = recv_vertex[r];
   uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
   const uint64_t fm = flagged && ntiles <= 64u ? __ballot(lane < (int)ntiles && fl[lane]) : ~0ull;
@@ -899,6 +900,7 @@ __global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uin
   if (fl) {
     __builtin_amdgcn_wave_barrier();                       // every lane has read the flags
     for (uint32_t t = lane; t < ntiles; t += 64) fl[t] = 0;
+  }
   }
 }
 
@@ -1637,7 +1639,7 @@ int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_
     p->sx_mask_cap = (size_t)n * MW;
   }
   EGR_HIP(hipMemsetAsync(p->sx_off + n, 0, sizeof(int64_t), st));
-  const dim3 sxg((unsigned)((n + SX_ROWS - 1) / SX_ROWS));
+  const dim3 sxg = sx_grid(n);
   hipLaunchKernelGGL(sx_count_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
                      (uint32_t)p->RS, width, reach, rows, (int64_t)n, p->sx_off, p->sx_mask, MW,
                      reach ? nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles);
@@ -1684,7 +1686,7 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
   uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;
   uint8_t* nzf = reach ? nullptr : p->nzf[p->xcur];
-  hipLaunchKernelGGL(sx_zero_kernel, dim3((unsigned)((n_rows + SX_ROWS - 1) / SX_ROWS)), dim3(256), 0,
+  hipLaunchKernelGGL(sx_zero_kernel, sx_grid(n_rows), dim3(256), 0,
                      st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, (int64_t)n_rows,
                      nzf, (uint32_t)p->ntiles,
                      nzf != nullptr && p->xzeroed[p->xcur]);

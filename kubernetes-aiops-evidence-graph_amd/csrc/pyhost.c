@@ -2340,8 +2340,87 @@ done:
   return out;
 }
 
+/* ---- ranked root-cause entities (src/database/graph.py GraphService._rank_locked) ----------
+ * entity_rows(ids u32 [B*k], scores f32 [B*k], labels u8 [B*k], k, vertex_ids list, label_names
+ * list) -> B lists of {"id": vertex_ids[v], "labels": [label_names[label]], "score": float,
+ * "rank": r}: each list stops at the first EGR_NO_NODE.  Dicts are copies of one 4-key template
+ * (keys in the Python statement's order); scores are the f32 values as Python floats, as
+ * ndarray.tolist() gives them. */
+static PyObject *e_id, *e_labels, *e_score, *e_rank;
+
+static PyObject* entity_rows(PyObject* self, PyObject* args) {
+  Py_buffer bi = {0}, bs = {0}, bl = {0};
+  PyObject *vids, *names;
+  Py_ssize_t k;
+  if (!PyArg_ParseTuple(args, "y*y*y*nO!O!", &bi, &bs, &bl, &k, &PyList_Type, &vids, &PyList_Type, &names))
+    return NULL;
+  PyObject* out = NULL;
+  PyObject* tmpl = NULL;
+  const Py_ssize_t n = bi.len / 4;
+  if (k <= 0 || n % k || bs.len / 4 != n || bl.len != n) {
+    PyErr_SetString(PyExc_ValueError, "entity_rows: ids / scores / labels differ in size or k");
+    goto done;
+  }
+  const uint32_t* ids = (const uint32_t*)bi.buf;
+  const float* sc = (const float*)bs.buf;
+  const uint8_t* lab = (const uint8_t*)bl.buf;
+  const Py_ssize_t B = n / k, NV = PyList_GET_SIZE(vids), NL = PyList_GET_SIZE(names);
+  if (!(tmpl = PyDict_New())) goto done;
+  if (PyDict_SetItem(tmpl, e_id, Py_None) < 0 || PyDict_SetItem(tmpl, e_labels, Py_None) < 0 ||
+      PyDict_SetItem(tmpl, e_score, Py_None) < 0 || PyDict_SetItem(tmpl, e_rank, Py_None) < 0)
+    goto done;
+  if (!(out = PyList_New(B))) goto done;
+  /* (the cyclic GC deferred while ~3 objects per entity are created, as the hypothesis
+   * assembly does: collections triggered by them traverse the caller's whole heap) */
+  const int gc_was = PyGC_Disable();
+  for (Py_ssize_t b = 0; b < B; ++b) {
+    Py_ssize_t m = 0;
+    while (m < k && ids[b * k + m] != NO_NODE) ++m;
+    PyObject* row = PyList_New(m);
+    if (!row) goto fail;
+    PyList_SET_ITEM(out, b, row);
+    for (Py_ssize_t r = 0; r < m; ++r) {
+      const uint32_t v = ids[b * k + r];
+      const uint8_t l = lab[b * k + r];
+      if ((Py_ssize_t)v >= NV || (Py_ssize_t)l >= NL) {
+        PyErr_SetString(PyExc_IndexError, "entity_rows: vertex or label index out of range");
+        goto fail;
+      }
+      PyObject* d = PyDict_Copy(tmpl);
+      if (!d) goto fail;
+      PyList_SET_ITEM(row, r, d);
+      PyObject* ls = PyList_New(1);
+      PyObject* f = PyFloat_FromDouble((double)sc[b * k + r]);
+      PyObject* rk = PyLong_FromSsize_t(r + 1);
+      if (!ls || !f || !rk) { Py_XDECREF(ls); Py_XDECREF(f); Py_XDECREF(rk); goto fail; }
+      PyObject* nm = PyList_GET_ITEM(names, l);
+      Py_INCREF(nm);
+      PyList_SET_ITEM(ls, 0, nm);
+      const int bad = PyDict_SetItem(d, e_id, PyList_GET_ITEM(vids, v)) < 0 ||
+                      PyDict_SetItem(d, e_labels, ls) < 0 || PyDict_SetItem(d, e_score, f) < 0 ||
+                      PyDict_SetItem(d, e_rank, rk) < 0;
+      Py_DECREF(ls);
+      Py_DECREF(f);
+      Py_DECREF(rk);
+      if (bad) goto fail;
+    }
+  }
+  if (gc_was) PyGC_Enable();
+  goto done;
+fail:
+  if (gc_was) PyGC_Enable();
+  Py_CLEAR(out);
+done:
+  Py_XDECREF(tmpl);
+  PyBuffer_Release(&bi);
+  PyBuffer_Release(&bs);
+  PyBuffer_Release(&bl);
+  return out;
+}
+
 static PyMethodDef methods[] = {
     {"seed_candidates", seed_candidates, METH_VARARGS, "evidence rows -> seed attachment candidates"},
+    {"entity_rows", entity_rows, METH_VARARGS, "frontier top-k -> ranked root-cause entity dicts"},
     {"seed_keys", seed_keys, METH_VARARGS, "evidence rows -> seed candidates as a keyed blob"},
     {"hash_ids", hash_ids, METH_O, "64-bit hashes of ids' UTF-8 bytes"},
     {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
@@ -2358,6 +2437,7 @@ PyMODINIT_FUNC PyInit__egr_pyhost(void) {
 #define S(var, text) if (!(var = PyUnicode_InternFromString(text))) return NULL
   S(f_confidence, "confidence"); S(f_category, "category"); S(f_support, "support_count");
   S(f_final, "final_score"); S(f_rank, "rank"); S(f_unknown, "unknown");
+  S(e_id, "id"); S(e_labels, "labels"); S(e_score, "score"); S(e_rank, "rank");
 #undef S
   if (!(f_half = PyFloat_FromDouble(0.5)) || !(f_zero = PyLong_FromLong(0))) return NULL;
   return PyModule_Create(&module);

@@ -215,11 +215,11 @@ FUSED = FusedRanks()
 def rank_lists(lists: list[list[dict]], device=None) -> list[list[dict]]:
     """Rank every list in one launch; mutates and returns the dicts like the reference.  Lists
     the rules kernel generated and already ranked are served from FUSED."""
-    dev = require_device(device)
     out: list = [FUSED.apply(hyps) for hyps in lists]
     todo = [j for j, r in enumerate(out) if r is None]
     if not todo:
-        return out
+        return out                     # (every list was a kernel-ranked one: no device call)
+    dev = require_device(device)
     cols = ([], [], [], [])
     off = [0]
     for j in todo:

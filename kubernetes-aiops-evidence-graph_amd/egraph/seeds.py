@@ -111,22 +111,32 @@ class SeedCandidates:
             return [cls._of(1, sc.flat[fb[b]:fb[b + 1]], sc.count[rb[b]:rb[b + 1]],
                             np.zeros(rb[b + 1] - rb[b], np.uint32), sc.val[rb[b]:rb[b + 1]])
                     for b in range(n)]
-        # keyed form: one native pass emits the ids as a blob + offsets + hashes directly
-        # (csrc/pyhost.c seed_keys; no Python str per id)
+        batch = cls.keyed_batch(evidence_lists)
+        return [batch.column(b) for b in range(n)]
+
+    @classmethod
+    def keyed_batch(cls, evidence_lists: list[list[dict]]) -> "SeedCandidates":
+        """The keyed candidates of a whole batch (columns = the lists' positions) from one native
+        pass that emits the ids as a blob + offsets + hashes directly (csrc/pyhost.c seed_keys;
+        no Python str per id).  column(b) is list b's own SeedCandidates, sliced on demand."""
         from . import _lib
         from .encode import encode_threads
         blob, off, hs, count, col, val = _lib.pyhost.seed_keys(evidence_lists, _row, encode_threads())
         off, hs = np.frombuffer(off, np.int64), np.frombuffer(hs, np.int64)
-        count, col = np.frombuffer(count, np.int64), np.frombuffer(col, np.uint32)
-        val = np.frombuffer(val, np.float32)
-        rb = np.searchsorted(col, np.arange(n + 1, dtype=np.uint32))
-        fb = np.concatenate([[0], np.cumsum(count)])[rb]
-        out = []
-        for b in range(n):
-            f0, f1, r0, r1 = fb[b], fb[b + 1], rb[b], rb[b + 1]
-            k = (blob[off[f0]:off[f1]], off[f0:f1 + 1] - off[f0], hs[f0:f1])
-            out.append(cls._of(1, None, count[r0:r1], np.zeros(r1 - r0, np.uint32), val[r0:r1], k))
-        return out
+        return cls._of(len(evidence_lists), None, np.frombuffer(count, np.int64),
+                       np.frombuffer(col, np.uint32), np.frombuffer(val, np.float32), (blob, off, hs))
+
+    def column(self, b: int) -> "SeedCandidates":
+        """Column b of a keyed batch as a one-column SeedCandidates (keys re-based)."""
+        cut = getattr(self, "_cut", None)
+        if cut is None:
+            rb = np.searchsorted(self.col, np.arange(self.n_cols + 1, dtype=np.uint32))
+            cut = self._cut = (rb, np.concatenate([[0], np.cumsum(self.count)])[rb])
+        rb, fb = cut
+        blob, off, hs = self.keys
+        f0, f1, r0, r1 = fb[b], fb[b + 1], rb[b], rb[b + 1]
+        k = (blob[off[f0]:off[f1]], off[f0:f1 + 1] - off[f0], hs[f0:f1])
+        return self._of(1, None, self.count[r0:r1], np.zeros(r1 - r0, np.uint32), self.val[r0:r1], k)
 
     @classmethod
     def combine(cls, parts: list["SeedCandidates"], with_flat: bool = True) -> "SeedCandidates":

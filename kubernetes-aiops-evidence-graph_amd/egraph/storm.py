@@ -70,7 +70,8 @@ class OpenIncident:
     vertex: int = -1
     sv: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))    # seed vertices
     ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
-    cand: SeedCandidates | None = None     # its rows' attachment candidates (computed once)
+    cand: object = None                    # its rows' attachment candidates (computed once):
+                                           # SeedCandidates, or (keyed batch, column) until sliced
     top_ids: np.ndarray | None = None      # [k] u32 vertex ids, NO_NODE padded
     top_scores: np.ndarray | None = None   # [k] f32
     ranked_at: int = -1                    # tick of the last re-rank
@@ -130,15 +131,22 @@ class StormEngine:
         t0 = time.perf_counter()
         xs = [self.incidents[h] for h in handles]
         need = [x for x in xs if x.cand is None]
+        batch = None
         if need:
-            for x, c in zip(need, SeedCandidates.per_column([x.evidence for x in need], keys=True)):
-                x.cand = c
+            # one keyed batch for the tick's new incidents; an incident keeps (batch, column) and
+            # is sliced out of it only if it is ever re-attached together with other incidents
+            batch = SeedCandidates.keyed_batch([x.evidence for x in need])
+            for j, x in enumerate(need):
+                x.cand = (batch, j)
                 if not self.keep_evidence:
                     x.evidence = None
         t1 = time.perf_counter()
         if not xs:
             return
-        cand = SeedCandidates.combine([x.cand for x in xs], with_flat=False)
+        if batch is not None and len(need) == len(xs):
+            cand = batch                       # (xs are exactly the new incidents, in order)
+        else:
+            cand = SeedCandidates.combine([self._cand(x) for x in xs], with_flat=False)
         blob, off, hashes = cand.keys
         found = self.g.lookup_blob(blob, off) if cand.n_flat else np.zeros(0, np.int64)
         sv, col, ss, before, bcol = cand.attach_found_idx(found)
@@ -168,6 +176,13 @@ class StormEngine:
                         self._pend_h[live], self._pend_o[live], self._pend_g[live])
         self.last_reseed = {"incidents": len(xs), "new": len(need), "candidates_ms": (t1 - t0) * 1e3,
                             "attach_ms": (t2 - t1) * 1e3, "pending_ms": (time.perf_counter() - t2) * 1e3}
+
+    @staticmethod
+    def _cand(x: "OpenIncident") -> SeedCandidates:
+        """x's own candidates (a column of the keyed batch it arrived in)."""
+        if isinstance(x.cand, tuple):
+            x.cand = x.cand[0].column(x.cand[1])
+        return x.cand
 
     def _pending_hit(self, ids: list) -> set:
         """Incidents with a live pending entry whose hash matches one of these ids: a binary

@@ -33,6 +33,7 @@ import numpy as np
 import torch
 
 from egraph import ops
+from egraph._lib import pyhost
 from egraph.device import to_device
 from egraph.graph import EvidenceGraph
 from egraph.seeds import seeds_for_batch
@@ -167,21 +168,17 @@ class GraphService:
         ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
                                        to_device(ss, dev), src, hops, inc)
         ids = ids.cpu().numpy().view("uint32")
-        scores = scores.cpu().numpy().tolist()
+        scores = scores.cpu().numpy()
         fr.adapt()              # overflowing columns: the wide-table retry from the next call on
-        # the ranked vertices' labels by numpy indexing (no per-vertex list of the whole graph)
+        # the ranked vertices' labels by numpy indexing (no per-vertex list of the whole graph),
+        # then the entity dicts natively (csrc/pyhost.c entity_rows; the loop it replaces:
+        # {"id": vid[v], "labels": [labels[label of v]], "score": score, "rank": r + 1} per
+        # ranked vertex, each list up to its first EGR_NO_NODE)
         lab = np.zeros(ids.shape, np.uint8)
         ok = ids != 0xFFFFFFFF
         lab[ok] = g.vertex_labels()[ids[ok]]
-        vid = g.vertex_ids()
-        out = []
-        for irow, srow, lrow in zip(ids.tolist(), scores, lab.tolist()):
-            row = []
-            for r, v in enumerate(irow):
-                if v == 0xFFFFFFFF:
-                    break
-                row.append({"id": vid[v], "labels": [labels[lrow[r]]], "score": srow[r], "rank": r + 1})
-            out.append(row)
+        out = pyhost.entity_rows(np.ascontiguousarray(ids), np.ascontiguousarray(scores, np.float32),
+                                 lab, ids.shape[1] if ids.ndim == 2 else k, g.vertex_ids(), list(labels))
         return out
 
     @staticmethod

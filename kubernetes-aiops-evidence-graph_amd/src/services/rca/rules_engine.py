@@ -38,15 +38,27 @@ DIAGNOSIS_RULES = [
 _BATCHERS: dict = {}
 
 
+_LAST: list = [None, None, None, None]   # weak catalog, weak loop, device, batcher: the last hit
+
+
 def _batcher(catalog: _catalog.Catalog, device) -> RulesBatcher:
     """The batcher of a (catalog, running event loop, device): concurrent activities of one
     worker loop share it, so calls that overlap in time go out in one launch."""
+    loop = asyncio.get_running_loop()
+    last = _LAST
+    if last[0] is not None and last[0]() is catalog and last[1]() is loop and last[2] == device:
+        return last[3]                 # (one call per incident: the common case is a repeat)
+    b = _batcher_slow(catalog, device, loop)
+    last[:] = [weakref.ref(catalog), weakref.ref(loop), device, b]
+    return b
+
+
+def _batcher_slow(catalog: _catalog.Catalog, device, loop) -> RulesBatcher:
     key = id(catalog)
     ent = _BATCHERS.get(key)
     if ent is None or ent[0]() is not catalog:
         ent = _BATCHERS[key] = (weakref.ref(catalog, lambda _r, k=key: _BATCHERS.pop(k, None)),
                                 weakref.WeakKeyDictionary())
-    loop = asyncio.get_running_loop()
     per_dev = ent[1].get(loop)
     if per_dev is None:
         per_dev = ent[1][loop] = {}

@@ -122,3 +122,41 @@ def test_custom_ops_registered():
     assert "Tensor rule_table" in str(torch.ops.egraph.rules_eval.default._schema)
     with pytest.raises(NotImplementedError):       # device kernels only: no CPU fallback
         torch.ops.egraph.reach(1, torch.zeros(4, dtype=torch.int32), 10, 3)
+
+
+def test_entity_rows_match_python_assembly():
+    """pyhost.entity_rows (GraphService.rank_root_causes' result dicts) equals the Python loop it
+    replaces: per incident, {"id", "labels", "score", "rank"} for each ranked vertex up to the
+    first EGR_NO_NODE, scores as the f32 values' Python floats."""
+    import numpy as np
+    from egraph import _lib
+    rng = np.random.default_rng(3)
+    B, k, V = 37, 10, 500
+    ids = rng.integers(0, V, (B, k)).astype(np.uint32)
+    for b in range(B):                      # ragged lists: EGR_NO_NODE past a random length
+        ids[b, rng.integers(0, k + 1):] = 0xFFFFFFFF
+    ids[3, :] = 0xFFFFFFFF
+    scores = rng.random((B, k), dtype=np.float32) * 3
+    scores[5, 0] = np.float32("inf")
+    vlabel = rng.integers(0, 4, V).astype(np.uint8)
+    names = ["Pod", "Node", "Service", "Deployment"]
+    vids = [f"v:{i}" for i in range(V)]
+    lab = np.zeros(ids.shape, np.uint8)
+    ok = ids != 0xFFFFFFFF
+    lab[ok] = vlabel[ids[ok]]
+    got = _lib.pyhost.entity_rows(ids, scores, lab, k, vids, names)
+    want = []
+    for irow, srow in zip(ids.tolist(), scores.tolist()):
+        row = []
+        for r, (v, sc) in enumerate(zip(irow, srow)):
+            if v == 0xFFFFFFFF:
+                break
+            row.append({"id": vids[v], "labels": [names[vlabel[v]]], "score": sc, "rank": r + 1})
+        want.append(row)
+    assert got == want
+    assert [list(d) for d in got[0]] == [list(d) for d in want[0]]      # key order too
+    import pytest
+    with pytest.raises(ValueError):
+        _lib.pyhost.entity_rows(ids, scores[:-1], lab, k, vids, names)
+    with pytest.raises(IndexError):
+        _lib.pyhost.entity_rows(ids, scores, lab, k, vids[:10], names)
