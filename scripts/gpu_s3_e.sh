@@ -10,3 +10,7 @@ timeout -k 10 300 python -u bench.py --workload storm > $OUT/storm.json 2> $OUT/
 echo "storm ok"
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --dense-steps 0 --steps 200 > $OUT/bench.json 2> $OUT/bench.err
 echo "bench ok"
+for K in 1 2 5 20; do
+  timeout -k 10 120 python -u bench.py --steps $K --warmup 5 --no-cpu-baseline --no-dropin --dense-steps 0 > $OUT/bench_k$K.json 2> $OUT/bench_k$K.err
+  python -c "import json;d=json.load(open('$OUT/bench_k$K.json'));print('K=$K', round(d['ms_per_step']*$K,4), 'ms region')"
+done
