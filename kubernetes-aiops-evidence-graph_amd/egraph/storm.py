@@ -72,9 +72,47 @@ class OpenIncident:
     ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
     cand: object = None                    # its rows' attachment candidates (computed once):
                                            # SeedCandidates, or (keyed batch, column) until sliced
-    top_ids: np.ndarray | None = None      # [k] u32 vertex ids, NO_NODE padded
-    top_scores: np.ndarray | None = None   # [k] f32
-    ranked_at: int = -1                    # tick of the last re-rank
+    store: "RankStore | None" = None       # the engine's rankings (rows by handle)
+
+    # its ranking, read from the engine's arrays (a re-rank writes them in one step per launch)
+    @property
+    def top_ids(self) -> np.ndarray | None:      # [k] u32 vertex ids, NO_NODE padded
+        return self.store.row(self.handle)[0] if self.store is not None else None
+
+    @property
+    def top_scores(self) -> np.ndarray | None:   # [k] f32
+        return self.store.row(self.handle)[1] if self.store is not None else None
+
+    @property
+    def ranked_at(self) -> int:                  # tick of the last re-rank (-1: never)
+        return self.store.row(self.handle)[2] if self.store is not None else -1
+
+
+class RankStore:
+    """Every incident's latest top-k, by handle: [n, k] ids and scores and the tick each was
+    ranked at; a row is None until its incident is first ranked."""
+
+    def __init__(self, k: int):
+        self.k = k
+        self.ids = np.full((0, k), NO_NODE, np.uint32)
+        self.scores = np.zeros((0, k), np.float32)
+        self.tick = np.full(0, -1, np.int64)
+
+    def put(self, handles: np.ndarray, ids: np.ndarray, scores: np.ndarray, tick: int) -> None:
+        top = int(handles.max()) + 1 if len(handles) else 0
+        if top > len(self.tick):
+            n = max(top, 2 * len(self.tick), 1024)
+            self.ids = np.concatenate([self.ids, np.full((n - len(self.tick), self.k), NO_NODE, np.uint32)])
+            self.scores = np.concatenate([self.scores, np.zeros((n - len(self.tick), self.k), np.float32)])
+            self.tick = np.concatenate([self.tick, np.full(n - len(self.tick), -1, np.int64)])
+        self.ids[handles] = ids
+        self.scores[handles] = scores
+        self.tick[handles] = tick
+
+    def row(self, h: int):
+        if h >= len(self.tick) or self.tick[h] < 0:
+            return None, None, -1
+        return self.ids[h].copy(), self.scores[h].copy(), int(self.tick[h])
 
 
 class StormEngine:
@@ -105,6 +143,7 @@ class StormEngine:
         self._pend_g = np.zeros(0, np.int64)
         self._gen = np.zeros(0, np.int64)
         self._frontiers: dict[int, object] = {}
+        self.ranks = RankStore(k)
         self.ticks = 0
         self.last_reseed: dict = {}
         # (vertex, incident) pairs the affected test reads: incident vertices and seed vertices
@@ -238,10 +277,9 @@ class StormEngine:
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
             fr.adapt()              # overflowing columns: the wide-table retry from the next call on
-            # each incident keeps row views of this launch's (fresh) host arrays
-            for x, i_row, s_row in zip(part, ids, scores):
-                x.top_ids, x.top_scores = i_row, s_row
-                x.ranked_at = self.ticks
+            # the launch's rows into the engine's arrays, one step for all of them
+            n = len(part)
+            self.ranks.put(np.asarray(handles[lo:lo + n], np.int64), ids[:n], scores[:n], self.ticks)
 
     def tick(self, keys: list[str], now_ms: int, make_case: Callable[[int, int], StormCase],
              topology: tuple | None = None, seq=None) -> dict:
@@ -276,15 +314,18 @@ class StormEngine:
             t_collect += time.perf_counter() - tc
             assert h == len(self.incidents), "incident handles are dense and ordered"
             self.incidents.append(OpenIncident(h, case.incident_id, case.evidence
-                                               if self.keep_evidence or self.owns(h) else None))
+                                               if self.keep_evidence or self.owns(h) else None,
+                                               store=self.ranks))
             new_handles.append(h)
-            for vid, lab in case.entities:
-                ids.append(vid)
-                labels.append(lab)
-            for s, d, ty in case.relations:
-                es.append(s)
-                ed.append(d)
-                et.append(ty)
+            if case.entities:                      # (column-wise, in C: zip(*) per case)
+                a, b = zip(*case.entities)
+                ids += a
+                labels += b
+            if case.relations:
+                a, b, c = zip(*case.relations)
+                es += a
+                ed += b
+                et += c
         if topology is not None:
             tv, tl, ts, td, tt = topology
             ids += list(tv)
