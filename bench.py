@@ -385,19 +385,20 @@ def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
     ref = np.array(ref) * 1e6
 
     async def concurrent():
-        # one event loop, as in a worker: a warm-up round, then the best of three rounds, each
+        # one event loop, as in a worker: a warm-up round, then the best of five rounds, each
         # from a collected heap
         async def one(i):
             return ranker.rank(await eng.generate_hypotheses(incs[i], ev[i]))
         b0 = RE._batcher(eng.catalog, eng.device)
         await asyncio.gather(*[one(i) for i in range(len(ev))])
         l0, ts = b0.launches, []
-        for _ in range(3):
+        for _ in range(5):
             gc.collect()
             t0 = time.perf_counter()
             await asyncio.gather(*[one(i) for i in range(len(ev))])
             ts.append(time.perf_counter() - t0)
-        return min(ts), (b0.launches - l0) // 3
+        log(f"concurrent drop-in rounds (ms): {[round(t * 1e3, 2) for t in ts]}")
+        return min(ts), (b0.launches - l0) // 5
 
     t_conc, conc_launches = asyncio.run(concurrent())
 

@@ -301,22 +301,26 @@ class RulesBatcher:
     async def submit(self, incident_id, evidence: list[dict], ranked: bool) -> list[dict]:
         """One incident's hypothesis list (generate_hypotheses, ranked or not)."""
         loop = asyncio.get_running_loop()
-        return await self._submit(loop, _Call([str(incident_id)], [evidence], ranked,
-                                              loop.create_future(), True))
+        call = _Call([str(incident_id)], [evidence], ranked, loop.create_future(), True)
+        self.calls += 1
+        self.queue.append(call)
+        if self.busy:                  # (a launch is running: this call joins the next one)
+            return await call.fut
+        return await self._launch_idle(loop, call)
 
     async def submit_many(self, incident_ids: list, evidence_lists: list, ranked: bool
                           ) -> list[list[dict]]:
         """Several incidents as ONE call (it raises as a whole if any row makes the
         reference raise, as the reference's loop over them would)."""
         loop = asyncio.get_running_loop()
-        return await self._submit(loop, _Call([str(i) for i in incident_ids], list(evidence_lists),
-                                              ranked, loop.create_future()))
-
-    async def _submit(self, loop, call: "_Call"):
+        call = _Call([str(i) for i in incident_ids], list(evidence_lists), ranked, loop.create_future())
         self.calls += 1
         self.queue.append(call)
         if self.busy:
             return await call.fut
+        return await self._launch_idle(loop, call)
+
+    async def _launch_idle(self, loop, call: "_Call"):
         # idle: this call launches at once from its own task; calls arriving while it runs
         # (its wait yields one loop turn) go out together from a drain task afterwards
         self.busy = True

@@ -212,10 +212,11 @@ class FusedRanks:
 FUSED = FusedRanks()
 
 
-def rank_lists(lists: list[list[dict]], device=None) -> list[list[dict]]:
+def rank_lists(lists: list[list[dict]], device=None, fused: bool = True) -> list[list[dict]]:
     """Rank every list in one launch; mutates and returns the dicts like the reference.  Lists
-    the rules kernel generated and already ranked are served from FUSED."""
-    out: list = [FUSED.apply(hyps) for hyps in lists]
+    the rules kernel generated and already ranked are served from FUSED (`fused=False`: the
+    caller already asked it)."""
+    out: list = [FUSED.apply(hyps) for hyps in lists] if fused else [None] * len(lists)
     todo = [j for j, r in enumerate(out) if r is None]
     if not todo:
         return out                     # (every list was a kernel-ranked one: no device call)

@@ -6,7 +6,7 @@ returns `[]`.  The score and Python-exact round(score, 4) run in egr_rank (csrc/
 """
 from __future__ import annotations
 
-from egraph.ranker import rank_lists
+from egraph.ranker import FUSED, rank_lists
 
 
 class HypothesisRanker:
@@ -18,7 +18,10 @@ class HypothesisRanker:
     def rank(self, hypotheses: list[dict]) -> list[dict]:
         if not hypotheses:
             return []
-        return rank_lists([hypotheses], self.device)[0]
+        # a list the rules kernel generated and ranked: its fused ranking, verified field by
+        # field (egraph/ranker.py FusedRanks); anything else goes through egr_rank
+        r = FUSED.apply(hypotheses)
+        return r if r is not None else rank_lists([hypotheses], self.device, fused=False)[0]
 
     def rank_many(self, lists: list[list[dict]]) -> list[list[dict]]:
         """Rank many independent hypothesis lists in one launch."""

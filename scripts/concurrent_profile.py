@@ -6,7 +6,7 @@ batcher coalesces them into launches.  Here the launch itself is replaced by the
 orc_rules_eval on the same encoded columns (a test stand-in: only the host path is measured),
 so the host overheads -- per-call bookkeeping, the coalesced encode, dict assembly and the
 ranker's fused reuse -- can be profiled and tuned without a GPU.
-  python scripts/concurrent_profile.py [n_incidents] [--cprofile]"""
+  python scripts/concurrent_profile.py [n_incidents] [--cprofile] [--gpu]"""
 import asyncio
 import cProfile
 import gc
@@ -48,12 +48,18 @@ class CpuRunner:
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1024
-    B.RulesRunner = CpuRunner
-    import egraph.ranker as R
-    R.require_device = lambda device=None: None      # every list is served by the fused ranks
+    if "--gpu" not in sys.argv:                      # (--gpu: the real launches, on a GPU box)
+        B.RulesRunner = CpuRunner
+        import egraph.ranker as R
+        R.require_device = lambda device=None: None  # every list is served by the fused ranks
     from egraph import synth
     from src.services.rca import rules_engine as RE
     from src.services.rca.hypothesis_ranker import HypothesisRanker
+    # --heap: also build the C3 evidence graph, as bench.py's process holds it (229k vertices,
+    # their id tuples and property dicts: a much larger set of GC-tracked objects)
+    keep = None
+    if "--heap" in sys.argv:
+        keep = synth.build_graph(synth.build_cluster(synth.CONFIGS["C3"]))
     cl = synth.build_cluster(synth.CONFIGS["C3"])
     cases = synth.make_incidents(cl, n, seed=1000)
     ev = [x.evidence for x in cases]
