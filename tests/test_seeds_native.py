@@ -367,3 +367,23 @@ def test_seed_keys_raise_like_python(bad):
         with pytest.raises(Exception) as e2:
             _lib.pyhost.seed_keys(lists, _row, th)
         assert type(e1.value) is type(e2.value)
+
+
+def test_storm_rank_store_rows():
+    """StormEngine's RankStore (host logic): rows by handle, grown on demand, None / -1 until an
+    incident is first ranked, later puts overwrite, and OpenIncident reads its row through it."""
+    import numpy as np
+    from egraph.storm import OpenIncident, RankStore
+    st = RankStore(4)
+    x = OpenIncident(7, "i7", None, store=st)
+    assert x.top_ids is None and x.top_scores is None and x.ranked_at == -1
+    ids = np.arange(8, dtype=np.uint32).reshape(2, 4)
+    sc = np.linspace(0, 1, 8, dtype=np.float32).reshape(2, 4)
+    st.put(np.array([7, 2000]), ids, sc, 3)
+    assert np.array_equal(x.top_ids, ids[0]) and x.top_scores.tobytes() == sc[0].tobytes()
+    assert x.ranked_at == 3 and st.row(2000)[2] == 3 and st.row(5)[0] is None
+    st.put(np.array([7]), ids[1:], sc[1:], 4)
+    assert np.array_equal(x.top_ids, ids[1]) and x.ranked_at == 4
+    got = x.top_ids
+    got[0] = 99                                   # a copy: the store is not written through
+    assert st.row(7)[0][0] == ids[1][0]
