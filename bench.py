@@ -10,11 +10,16 @@ resident in HBM (encoded evidence rows, seed triples, incident vertices):
     egr_rules_eval  ->  egr_plan_set_seeds  ->  egr_plan_set_sources
     ->  3 x (egr_plan_hop + egr_plan_reach_hop)  ->  egr_plan_candidates  ->  egr_plan_topk.
 Both engines produce bit-identical scores, reach sets and top-k (tests/test_frontier_gpu.py).
-Frontier batches are pipelined (--pipeline 3, default): three independent frontier + rules
-states on their own streams take batches in turn, so the tail of one batch's frontier launch
-(its last, unevenly long columns) overlaps the start of the next (P = 2 / 3 / 4: 0.103 / 0.080 /
-0.108 ms per step, profiles/r01_ab_pipe.txt).  Every batch is computed in full;
-`value` = batches x B / wall time of the timed region.
+Frontier batches are scheduled explicitly on ONE stream (--merge, default: the largest divisor
+of --steps up to 24): a launch carries M consecutive batches (M x B columns, each batch's seeds
+at its own column offset, rules over the M batches' rows) and the hardware dispatcher hands its
+workgroups out costliest column first across all M batches, so one batch's tail (its last,
+unevenly long columns) runs beside the next batch's columns inside the same launch.  Nothing
+depends on how streams map to HIP's hardware queues (GPU_MAX_HW_QUEUES 1 / 2 / 4 within 1 %;
+round 2's three lanes on four queues was an accident of that mapping: 35-140 % slower on any
+other setting, profiles/r03_ab_merge_schedule.txt).  --pipeline P > 1 still runs P such lanes
+on their own streams.  Every batch is computed in full; `value` = batches x B / wall time of
+the timed region.
 The default run also times a few dense steps after the timed region and reports them under
 "dense_engine" (with the dense hop kernel's HBM roofline) for comparison.
 Workload: BASELINE.json configs[2] (C3: 100k pods / 100 namespaces / 2k nodes / 10k
@@ -48,6 +53,9 @@ sys.path.insert(0, str(REPO / "kubernetes-aiops-evidence-graph_amd"))
 METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod graph"
 XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# --merge default cap: 24 batches per launch is 24,576 C3 columns, ~1.45 ms per launch
+# (0.0626 ms per batch against 0.0653 at 16 and 0.0734 at 8, profiles/r03_ab_merge_schedule.txt)
+MERGE_MAX = 24
 
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
@@ -105,7 +113,7 @@ def launch_ranks(n: int) -> int:
 
 
 def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1,
-          pool_entries: int = 0):
+          pool_entries: int = 0, merge: int = 1):
     from egraph import catalog, synth
     from egraph.device import to_device
     from egraph.encode import encode_batch
@@ -126,19 +134,42 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     with torch.cuda.device(dev):
         snap = g.snapshot(device=dev)
         plan = snap.plan(B, max_seeds=len(sv), k=k)
-        # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
-        # members outside the candidate set); 0 keeps every member's score for inspection
-        fr = snap.frontier(B, max_seeds=len(sv), k=k, pool_entries=pool_entries)
         rules = RulesDeviceBatch(enc, catalog.default(), dev)
         seeds = tuple(to_device(a, dev) for a in (sv, sc, ss))
         sources = to_device(src, dev)
-        lanes = build_lanes(snap, B, len(sv), k, pipeline, pool_entries, dev,
-                            [(fr, rules, seeds, sources)] + [(None, enc, seeds, sources)] * (pipeline - 1))
+        # --merge M: a lane's launch carries M consecutive batches (M x B columns, each batch's
+        # seeds at its own column offset, the rules over the M batches' rows): the hardware
+        # dispatcher hands the columns out costliest-first across all M batches, so batch i's
+        # tail runs beside batch i+1's columns inside one launch on one stream
+        Bm = B * merge
+        if merge > 1:
+            msv, msc, mss, msrc = merge_batches([(sv, sc, ss, src)] * merge, B)
+            lane_seeds = tuple(to_device(a, dev) for a in (msv, msc, mss))
+            lane_src = to_device(msrc, dev)
+            lane_rules = encode_batch(evidence * merge, catalog.default())
+        else:
+            lane_seeds, lane_src, lane_rules = seeds, sources, rules
+        # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
+        # members outside the candidate set); 0 keeps every member's score for inspection
+        fr = snap.frontier(Bm, max_seeds=len(sv) * merge, k=k, pool_entries=pool_entries)
+        lanes = build_lanes(snap, Bm, len(sv) * merge, k, pipeline, pool_entries, dev,
+                            [(fr, lane_rules, lane_seeds, lane_src)]
+                            + [(None, lane_rules if merge > 1 else enc, lane_seeds, lane_src)] * (pipeline - 1))
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
     return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
-                lanes=lanes, tick=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
+                lanes=lanes, tick=0, merge=merge, sub=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence, incident_ids=[str(x.incident["id"]) for x in cases])
+
+
+def merge_batches(batches: list, B: int) -> tuple:
+    """One launch's input from M batches of B incidents, each (seed vertex, seed column, seed
+    strength, source vertex per column): batch i's columns become columns i*B .. i*B + B - 1."""
+    sv = np.concatenate([np.asarray(b[0]) for b in batches])
+    sc = np.concatenate([np.asarray(b[1], np.int64) + i * B for i, b in enumerate(batches)])
+    ss = np.concatenate([np.asarray(b[2]) for b in batches])
+    src = np.concatenate([np.asarray(b[3]) for b in batches])
+    return sv, sc.astype(np.asarray(batches[0][1]).dtype), ss, src
 
 
 def build_lanes(snap, B: int, max_seeds: int, k: int, pipeline: int, pool_entries: int, dev,
@@ -185,6 +216,18 @@ def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) ->
             lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
 
 
+def _launch_due(ctx) -> bool:
+    """--merge M: batch t is launched by the launch of batch t - t % M (the first of its group);
+    the other M - 1 calls enqueue nothing.  A timed region of K steps with K % M != 0 computes
+    the whole last group (more work than it counts)."""
+    m = ctx.get("merge", 1)
+    if m <= 1:
+        return True
+    due = ctx["sub"] == 0
+    ctx["sub"] = (ctx["sub"] + 1) % m
+    return due
+
+
 _GRAPH_NAME = {"C2": "10k-pod", "C3": "100k-pod", "C4": "400k-pod (1M-vertex)"}
 
 
@@ -194,6 +237,8 @@ def step_frontier(ctx, hops: int, ev=None):
     (35 VGPRs, no LDS) co-reside with the frontier kernel's (101 VGPRs x 4 per SIMD) instead of
     running in front of the seed preparation.  The timed region ends with a device-wide
     synchronize, which joins every stream."""
+    if not _launch_due(ctx):
+        return None
     lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
     ctx["tick"] += 1
     if lane["main"] is None:
@@ -264,7 +309,10 @@ def capture_lanes(ctx, hops: int, inline_rules: bool | None = None) -> None:
 
 
 def step_graph(ctx, hops: int, ev=None):
-    """One batch = one replay of the next lane's captured graph on that lane's stream."""
+    """One batch = one replay of the next lane's captured graph on that lane's stream (with
+    --merge M, one replay per M batches: the call that starts a group of M launches them all)."""
+    if not _launch_due(ctx):
+        return None
     lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
     ctx["tick"] += 1
     with torch.cuda.stream(lane["cap_stream"]):
@@ -487,7 +535,8 @@ def dropin_graph(ctx, dev, hops: int, k: int, reps: int = 5) -> dict:
     # the same batch's ids from the bench's own frontier (lane 0 ran the same evidence): the
     # drop-in's entities must be the engine's top-k
     g = ctx["graph"]
-    ids0 = ctx["lanes"][0]["frontier"].out_ids.view(len(data), k).cpu().numpy().view(np.uint32)
+    # (--merge: the lane's first len(data) columns are this batch)
+    ids0 = ctx["lanes"][0]["frontier"].out_ids.view(-1, k)[:len(data)].cpu().numpy().view(np.uint32)
     same = all([e["id"] for e in row] == [g.vertex_id(int(v)) for v in ids0[b] if v != 0xFFFFFFFF]
                for b, row in enumerate(out))
     GraphService.reset()
@@ -568,16 +617,17 @@ def _traffic(name: str):
 
 
 def _frontier_traffic(ctx, B: int):
-    """Bytes past L2 per frontier launch (profiles/pmc_frontier_calibrated.json), when this run
-    is the workload the counters were collected on; else None."""
-    pmc = REPO / "profiles" / "pmc_frontier_calibrated.json"
-    if not pmc.is_file():
-        return None
-    d = json.loads(pmc.read_text())
-    w = d.get("workload", {})
-    if w.get("config") != ctx.get("config") or w.get("batch") != B:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    """Bytes past L2 per frontier launch (profiles/pmc_frontier_calibrated*.json, one per
+    collected workload), when this run is a workload the counters were collected on (config,
+    batch and batches per launch); else None."""
+    M = ctx.get("merge", 1)
+    for pmc in sorted((REPO / "profiles").glob("pmc_frontier_calibrated*.json")):
+        d = json.loads(pmc.read_text())
+        w = d.get("workload", {})
+        if (w.get("config") == ctx.get("config") and w.get("batch") == B // M
+                and w.get("batches_per_launch", 1) == M):
+            return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
@@ -664,13 +714,13 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
              # Infinity-Cache hits count as fetched: an upper bound on HBM bytes.
              "traffic": _frontier_traffic(ctx, B),
              "traffic_note": "TCC_EA0_RDREQ x 128 B (calibrated: profiles/r02_calib_gather.txt) + "
-                             "write requests, profiles/pmc_frontier_calibrated.json; counts "
+                             "write requests, profiles/pmc_frontier_calibrated*.json; counts "
                              "Infinity-Cache hits (C3 CSR resident there): upper bound on HBM bytes",
              "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes,
              # with batches in flight, launches overlap: per batch the GPU delivers nbytes
              # in one step's wall time
              "achieved_per_step": nbytes / (step_ms * 1e-3) / 1e9,
-             "batches_in_flight": len(ctx["lanes"])}, work)
+             "lanes": len(ctx["lanes"]), "batches_per_launch": ctx.get("merge", 1)}, work)
 
 
 def time_dense(ctx, hops: int, steps: int, B: int, V: int, nnz: int, dev) -> dict:
@@ -1020,8 +1070,12 @@ def main():
     ap.add_argument("--hops", type=int, default=3)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="frontier batches in flight (independent states on their own streams)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="frontier lanes in flight (independent states on their own streams)")
+    ap.add_argument("--merge", type=int, default=0,
+                    help="frontier batches per launch: each lane's launch carries this many "
+                         "consecutive batches (one costliest-first column order across them); "
+                         f"0 = the largest divisor of --steps up to {MERGE_MAX}")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the end-to-end drop-in RulesEngine measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -1058,6 +1112,8 @@ def main():
         args.steps = 400 if short else 20
     if args.warmup is None:
         args.warmup = 10 if short else 3
+    if args.merge <= 0:
+        args.merge = max(m for m in range(1, MERGE_MAX + 1) if args.steps % m == 0)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `bench.py --gpus N` outside a launcher: start the N ranks ourselves (one per GPU,
@@ -1099,10 +1155,12 @@ def main():
         return
     ctx = setup(args.config, args.batch, args.k, rank, dev,
                 args.pipeline if args.engine == "frontier" else 1,
-                pool_entries=0 if args.pool else -1)
+                pool_entries=0 if args.pool else -1,
+                merge=max(1, args.merge) if args.engine == "frontier" else 1)
+    M = ctx["merge"]
     run_step = step_frontier if args.engine == "frontier" else step
     # (at least one step per lane: every lane's frontier has run before adapt() reads its stats)
-    for _ in range(max(args.warmup, len(ctx.get("lanes", ())))):
+    for _ in range(max(args.warmup, len(ctx.get("lanes", ())) * M)):
         run_step(ctx, args.hops)
     torch.cuda.synchronize(dev)
     if args.engine == "frontier":
@@ -1123,6 +1181,10 @@ def main():
         torch.cuda.synchronize(dev)
 
     events: list = EventPool(args.steps) if args.engine == "frontier" else []
+    ctx["sub"] = 0                  # the timed region starts a group of M batches
+    if args.steps % M:
+        log(f"[rank {rank}] --steps {args.steps} is not a multiple of --merge {M}: the last "
+            f"launch computes {M - args.steps % M} batches more than the region counts")
     elapsed = timed_steps(lambda: run_step(ctx, args.hops, events), args.steps, dist, rank,
                           lambda: torch.cuda.synchronize(dev), dev)
 
@@ -1136,7 +1198,7 @@ def main():
         # across the lanes, so an event pair there also times the wait for CUs held by the
         # other batches (reported as avg_launch_ms_in_flight when the run was eager)
         launch_ms = roofline_probe(ctx, args.hops, args.roofline_reps)
-        roof, work = frontier_roofline(ctx, launch_ms, B, args.k, ms)
+        roof, work = frontier_roofline(ctx, launch_ms, B * M, args.k, ms * M)
         roof["isolated_launches"] = args.roofline_reps
         rules_iso = rules_probe(ctx)
         if timed:
@@ -1150,8 +1212,9 @@ def main():
                         else "egr_frontier_run span",
                 "span_ms_mean": float(spans.mean()), "span_ms_p50": float(np.median(spans)),
                 "span_ms_sum_per_step": float(spans.sum() / args.steps),
-                "batches_in_flight_mean": float(spans.sum() / (elapsed * 1e3)),
-                "isolated_launch_ms_over_step_ms": launch_ms / ms}
+                "launches_in_flight_mean": float(spans.sum() / (elapsed * 1e3)),
+                "batches_per_launch": M,
+                "isolated_launch_ms_over_launch_group_ms": launch_ms / (ms * M)}
         out_graph = graphs
     else:
         launch_ms = float(np.mean([a.elapsed_time(b) for a, b in timed]))
@@ -1184,7 +1247,8 @@ def main():
             "vertices": V, "csr_entries": nnz, "incidents_per_gpu": B,
             "evidence_rows_per_gpu": ctx["enc"].n_rows, "seeds_per_gpu": int(len(ctx["seed_host"][0])),
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
-            "batches_in_flight": args.pipeline if args.engine == "frontier" else 1,
+            "lanes": args.pipeline if args.engine == "frontier" else 1,
+            "batches_per_launch": M,
             "hip_graph_replay": out_graph,
             "seed_input": ("grouped by incident + column offsets + costliest-first launch order, "
                            "resident (egr_frontier_run_grouped)" if GROUPED and args.engine == "frontier"

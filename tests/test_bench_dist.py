@@ -114,3 +114,19 @@ def test_gpus_flag_launches_ranks(monkeypatch):
     assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "7"] and cmd[-5].endswith("bench.py")
+
+
+def test_merge_batches_offsets_columns_and_launch_groups():
+    """--merge M: batch i's seed columns move to i*B.., sources concatenate in batch order; the
+    step functions enqueue on the first call of every group of M and on no other."""
+    import bench
+    b0 = (np.array([5, 6], np.uint32), np.array([0, 1], np.uint32), np.array([1.0, 2.0], np.float32),
+          np.array([10, 11], np.uint32))
+    b1 = (np.array([7], np.uint32), np.array([1], np.uint32), np.array([3.0], np.float32),
+          np.array([12, 13], np.uint32))
+    sv, sc, ss, src = bench.merge_batches([b0, b1], 2)
+    assert sv.tolist() == [5, 6, 7] and sc.tolist() == [0, 1, 3] and sc.dtype == np.uint32
+    assert ss.tolist() == [1.0, 2.0, 3.0] and src.tolist() == [10, 11, 12, 13]
+    ctx = {"merge": 3, "sub": 0}
+    assert [bench._launch_due(ctx) for _ in range(7)] == [True, False, False, True, False, False, True]
+    assert all(bench._launch_due({"merge": 1, "sub": 0}) for _ in range(3))

@@ -160,6 +160,52 @@ def test_bench_config_c3_graph_replay(inline):
         _check_rules(x["rules"].fetch(), x["enc"])
 
 
+def test_bench_config_c3_merged_launch():
+    """bench.py --merge 3: three different C3 batches in one lane's launch (columns at their
+    batch's offset, one costliest-first order across all 3072), captured and replayed twice:
+    every batch's slice of the outputs equals the oracle's ranking of that batch alone, and the
+    rules over the three batches' rows equal the oracle's."""
+    import bench
+    monkey = bench.GROUPED
+    bench.GROUPED = "order"
+    try:
+        from egraph import catalog
+        from egraph.encode import encode_batch
+        from egraph.rca import RulesDeviceBatch
+        B, k, hops, M = 1024, 10, 3, 3
+        g, batches = _world("C3", [B] * M, seed0=5000)
+        dev = torch.device("cuda", 0)
+        hosts, evs = [], []
+        for cases in batches:
+            ev, sv, sc, ss, src = _batch_inputs(g, cases)
+            hosts.append((sv, sc, ss, src))
+            evs += ev
+        msv, msc, mss, msrc = bench.merge_batches(hosts, B)
+        enc = encode_batch(evs, catalog.default())
+        rules = RulesDeviceBatch(enc, catalog.default(), dev)
+        snap = g.snapshot(device=dev)
+        lanes = bench.build_lanes(snap, B * M, len(msv), k, 1, -1, dev,
+                                  [(None, rules, (_dev(msv), _dev(msc), _dev(mss)), _dev(msrc))])
+        ctx = dict(lanes=lanes, tick=0, inc_label=g.labels().index("Incident"), merge=M, sub=0)
+        bench.capture_lanes(ctx, hops)
+        lanes[0]["frontier"].out_ids.fill_(-7)
+        torch.cuda.synchronize()
+        for _ in range(2 * M):
+            bench.step_graph(ctx, hops)
+        torch.cuda.synchronize()
+        csr = g.csr()
+        vl, _, _, _ = g.export()
+        ids = lanes[0]["frontier"].out_ids.cpu().numpy().view(np.uint32).reshape(M, B, k)
+        sco = lanes[0]["frontier"].out_scores.cpu().numpy().reshape(M, B, k)
+        for i, (sv, sc, ss, src) in enumerate(hosts):
+            e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k, hops)
+            np.testing.assert_array_equal(ids[i], e_ids, err_msg=f"batch {i}")
+            assert sco[i].tobytes() == e_sc.tobytes(), f"batch {i}"
+        _check_rules(rules.fetch(), enc)
+    finally:
+        bench.GROUPED = monkey
+
+
 def test_c2_rules_dropin_and_frontier():
     import asyncio
     from types import SimpleNamespace
