@@ -11,7 +11,7 @@ resident in HBM (encoded evidence rows, seed triples, incident vertices):
     ->  3 x (egr_plan_hop + egr_plan_reach_hop)  ->  egr_plan_candidates  ->  egr_plan_topk.
 Both engines produce bit-identical scores, reach sets and top-k (tests/test_frontier_gpu.py).
 Frontier batches are scheduled explicitly on ONE stream (--merge, default: the largest divisor
-of --steps up to 24): a launch carries M consecutive batches (M x B columns, each batch's seeds
+of --steps up to 50): a launch carries M consecutive batches (M x B columns, each batch's seeds
 at its own column offset, rules over the M batches' rows) and the hardware dispatcher hands its
 workgroups out costliest column first across all M batches, so one batch's tail (its last,
 unevenly long columns) runs beside the next batch's columns inside the same launch.  Nothing
@@ -53,9 +53,10 @@ sys.path.insert(0, str(REPO / "kubernetes-aiops-evidence-graph_amd"))
 METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod graph"
 XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# --merge default cap: 24 batches per launch is 24,576 C3 columns, ~1.45 ms per launch
-# (0.0626 ms per batch against 0.0653 at 16 and 0.0734 at 8, profiles/r03_ab_merge_schedule.txt)
-MERGE_MAX = 24
+# --merge default cap: a launch costs ~0.12 ms of tail + ~0.055 ms per C3 batch (0.0734 / 0.0653 /
+# 0.0626 ms per batch at 8 / 16 / 24 batches, profiles/r03_ab_merge_schedule.txt); 50 batches
+# (51,200 columns, ~2.9 ms per launch) leave the tail ~4 % of the launch
+MERGE_MAX = 50
 
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
