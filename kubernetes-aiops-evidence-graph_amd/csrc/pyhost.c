@@ -1513,7 +1513,11 @@ done:
  * Python statement `slow` = seeds._row, which raises what the reference expression raises), and
  * once Python has run it redoes every later row too.  The graph must not change during the call
  * (GraphService holds its lock). */
-typedef int32_t (*FindFn)(const void* g, const char* id, int64_t len);
+/* egr_graph_find's exact type (include/egraph.h), so the call through the pointer handed over
+ * from ctypes is a call of the function's own type (UBSan -fsanitize=function checks it) */
+struct egr_graph;
+typedef const struct egr_graph* GraphP;
+typedef int32_t (*FindFn)(GraphP g, const char* id, int64_t len);
 
 
 typedef struct {
@@ -1554,7 +1558,7 @@ static PyObject** seed_types[ST_N] = {&t_pod, &t_deploy, &t_dchange, &t_ichange,
 typedef struct IdSink {
   int (*put)(struct IdSink*, const char* p, size_t n);
   FindFn find;                  /* attach */
-  const void* g;
+  GraphP g;
   int32_t v;
   char* buf;                    /* keys: malloc'd (worker threads hold no GIL-side allocator) */
   size_t n, cap;
@@ -1704,7 +1708,7 @@ static int s_row_ids(PyObject* ev, IdSink* k, int* seeds, double* svp) {
 
 /* One row on a worker for the attachment: 0 = done (*vout = the attached vertex or NO_NODE),
  * 1 = hand over */
-static int s_row(PyObject* ev, FindFn find, const void* g, uint32_t* vout, float* sout) {
+static int s_row(PyObject* ev, FindFn find, GraphP g, uint32_t* vout, float* sout) {
   *vout = NO_NODE;
   IdSink k;
   memset(&k, 0, sizeof(k));
@@ -1727,7 +1731,7 @@ typedef struct {
   const int64_t* base;
   Py_ssize_t i0, i1;
   FindFn find;
-  const void* g;
+  GraphP g;
   uint32_t* vert;
   float* val;
   uint8_t* redo;
@@ -1748,7 +1752,7 @@ static void* s_main(void* arg) {
 }
 
 /* One row on the calling thread (GIL held): cand_ids, or the Python statement. */
-static int s_row_serial(PyObject* ev, PyObject* slow, FindFn find, const void* g, uint32_t* vout,
+static int s_row_serial(PyObject* ev, PyObject* slow, FindFn find, GraphP g, uint32_t* vout,
                         float* sout, int* ran_python) {
   *vout = NO_NODE;
   PyObject* ids = PyList_New(0);
@@ -1812,7 +1816,7 @@ static PyObject* seed_attach(PyObject* self, PyObject* args) {
   int threads = 1;
   if (!PyArg_ParseTuple(args, "OOKK|i", &lists, &slow, &find_addr, &g_addr, &threads)) return NULL;
   const FindFn find = (FindFn)(uintptr_t)find_addr;
-  const void* g = (const void*)(uintptr_t)g_addr;
+  GraphP g = (GraphP)(uintptr_t)g_addr;
   if (!find || !g) {
     PyErr_SetString(PyExc_ValueError, "seed_attach: NULL find function or graph");
     return NULL;

@@ -24,11 +24,12 @@ EGRAPH_LIB=$PKG/lib/asan/libegraph.so EGRAPH_PYHOST_DIR=$PKG/lib/asan PYTHONPATH
   python -c "import egraph._lib as L; m = open('/proc/self/maps').read(); \
 assert 'lib/asan/libegraph.so' in m and 'lib/asan/_egr_pyhost' in m and 'clang_rt.asan' in m; \
 print('loaded:', L.LIB_PATH, L.pyhost.__file__)" | tee -a "$OUT/r03_sanitize_asan.txt"
-echo "== TSan: _egr_pyhost (the encoder's worker pool) ==" | tee "$OUT/r03_sanitize_tsan.txt"
+echo "== TSan: _egr_pyhost (the worker pool: encoder, seed attachment, seed keys) ==" | tee "$OUT/r03_sanitize_tsan.txt"
 LD_PRELOAD=$($CLANG -print-file-name=libclang_rt.tsan-x86_64.so) \
 TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 \
 EGRAPH_PYHOST_DIR=$PKG/lib/tsan EGRAPH_ENCODE_THREADS=8 \
-  python -m pytest tests/test_pyhost.py tests/test_encoder.py -q -p no:xdist -p no:cacheprovider 2>&1 | tee -a "$OUT/r03_sanitize_tsan.txt"
+  python -m pytest tests/test_pyhost.py tests/test_encoder.py tests/test_seeds_native.py tests/test_native_host.py \
+    -q -p no:xdist -p no:cacheprovider 2>&1 | tee -a "$OUT/r03_sanitize_tsan.txt"
 LD_PRELOAD=$($CLANG -print-file-name=libclang_rt.tsan-x86_64.so) \
 EGRAPH_PYHOST_DIR=$PKG/lib/tsan PYTHONPATH=$PKG \
   python -c "import egraph._lib as L; m = open('/proc/self/maps').read(); \
