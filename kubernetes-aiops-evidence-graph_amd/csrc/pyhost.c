@@ -1563,29 +1563,56 @@ typedef struct IdSink {
   char* buf;                    /* keys: malloc'd (worker threads hold no GIL-side allocator) */
   size_t n, cap;
   int nid;                      /* ids appended for the current row */
+  int64_t* idoff;               /* keys: per id its first byte in buf, and its id_hash64 */
+  int64_t* idhash;
+  size_t nids, capids;
 } IdSink;
+
+static inline uint64_t id_hash64(const char* p, size_t n);
 
 static int sink_find(IdSink* k, const char* p, size_t n) {
   k->v = k->find(k->g, p, (int64_t)n);
   return k->v >= 0;
 }
 
+/* keys: the id's bytes appended to buf, its start offset and hash to the id arrays (an id ends
+ * where the next one starts, or at n) -- the final blob / offsets / hashes format, so a batch
+ * whose rows all stayed on the workers is assembled by copying each job's arrays */
 static int sink_keys(IdSink* k, const char* p, size_t n) {
-  if (k->n + n + 8 > k->cap) {
+  if (k->n + n > k->cap) {
     size_t c = k->cap ? 2 * k->cap : 1 << 16;
-    while (c < k->n + n + 8) c *= 2;
+    while (c < k->n + n) c *= 2;
     char* b = realloc(k->buf, c);
     if (!b) return -1;
     k->buf = b;
     k->cap = c;
   }
-  const uint32_t len = (uint32_t)n;                 /* u32 length, then the bytes */
-  memcpy(k->buf + k->n, &len, 4);
-  k->n += 4;
+  if (k->nids == k->capids) {
+    const size_t c = k->capids ? 2 * k->capids : 4096;
+    int64_t* f = realloc(k->idoff, sizeof(int64_t) * c);
+    if (f) k->idoff = f;
+    int64_t* h = realloc(k->idhash, sizeof(int64_t) * c);
+    if (h) k->idhash = h;
+    if (!f || !h) return -1;
+    k->capids = c;
+  }
+  k->idoff[k->nids] = (int64_t)k->n;
+  k->idhash[k->nids] = (int64_t)id_hash64(p, n);
+  ++k->nids;
   memcpy(k->buf + k->n, p, n);
   k->n += n;
   ++k->nid;
   return 0;
+}
+
+static inline size_t sink_id_end(const IdSink* k, size_t x) {
+  return x + 1 < k->nids ? (size_t)k->idoff[x + 1] : k->n;
+}
+
+static void sink_free(IdSink* k) {
+  free(k->buf);
+  free(k->idoff);
+  free(k->idhash);
 }
 
 /* prefix + a [+ ":" + b] into the sink: its put's result, -1 = id too long (hand over) */
@@ -1737,6 +1764,35 @@ typedef struct {
   uint8_t* redo;
 } SJob;
 
+/* Software pipelining of the workers' row reads: a row costs a chain of dependent cache misses
+ * (the dict, its keys table, each value object), so a worker touches rows ahead of the one it
+ * works on -- row j + 6's dict, row j + 3's keys table, row j + 1's values -- and the misses of
+ * the next rows overlap the current row's work.  Prefetches only: no value is used. */
+static inline void row_prefetch(PyObject* evs, Py_ssize_t j, Py_ssize_t n) {
+  if (j + 6 < n) __builtin_prefetch(PyList_GET_ITEM(evs, j + 6));
+  if (j + 3 < n) {
+    PyObject* d = PyList_GET_ITEM(evs, j + 3);
+    if (PyDict_CheckExact(d)) {
+      const char* k = (const char*)((PyDictObject*)d)->ma_keys;
+      __builtin_prefetch(k);
+      __builtin_prefetch(k + 64);
+      __builtin_prefetch(k + 128);
+      __builtin_prefetch(k + 192);
+      __builtin_prefetch(k + 256);
+    }
+  }
+  if (j + 1 < n) {
+    PyObject* d = PyList_GET_ITEM(evs, j + 1);
+    if (PyDict_CheckExact(d)) {
+      Py_ssize_t pos = 0;
+      PyObject *key, *v;
+      Py_hash_t h;
+      int c = 0;
+      while (c++ < 16 && _PyDict_Next(d, &pos, &key, &v, &h)) __builtin_prefetch(v);
+    }
+  }
+}
+
 static void* s_main(void* arg) {
   const SJob* J = (const SJob*)arg;
   for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
@@ -1744,6 +1800,7 @@ static void* s_main(void* arg) {
     const Py_ssize_t n = PyList_GET_SIZE(evs);
     for (Py_ssize_t j = 0; j < n; ++j) {
       const Py_ssize_t r = J->base[i] + j;
+      row_prefetch(evs, j, n);
       J->val[r] = 0.f;
       J->redo[r] = (uint8_t)s_row(PyList_GET_ITEM(evs, j), J->find, J->g, &J->vert[r], &J->val[r]);
     }
@@ -2045,11 +2102,15 @@ typedef struct {
   PyObject* const* lists;
   const int64_t* base;
   Py_ssize_t i0, i1;
-  IdSink sink;                  /* this job's id records (u32 length + bytes) */
-  int64_t* rowpos;              /* per row: its first record's offset in the job's buffer */
+  IdSink sink;                  /* this job's ids (bytes, offsets, hashes) */
+  int64_t* rowpos;              /* per row: the index of its first id in the job's sink */
   uint8_t* nid;                 /* per row: ids given (0: the row does not seed) */
   float* val;
   uint8_t* redo;
+  int64_t* rcount;              /* the job's seeding rows in order: id count, column, strength */
+  uint32_t* rcol;
+  float* rval;
+  Py_ssize_t nrows, nredo;
 } KJob;
 
 static void* k_main(void* arg) {
@@ -2059,16 +2120,27 @@ static void* k_main(void* arg) {
     const Py_ssize_t n = PyList_GET_SIZE(evs);
     for (Py_ssize_t j = 0; j < n; ++j) {
       const Py_ssize_t r = J->base[i] + j;
-      const size_t pos = J->sink.n;
+      row_prefetch(evs, j, n);
+      const size_t pos = J->sink.n, ipos = J->sink.nids;
       J->sink.nid = 0;
       int seeds = 0;
       double sv = 0.0;
       const int redo = s_row_ids(PyList_GET_ITEM(evs, j), &J->sink, &seeds, &sv);
       J->redo[r] = (uint8_t)redo;
-      J->rowpos[r] = (int64_t)pos;
-      if (redo) J->sink.n = pos;                   /* (drop a partial row) */
+      J->rowpos[r] = (int64_t)ipos;
+      if (redo) {                                  /* (drop a partial row) */
+        J->sink.n = pos;
+        J->sink.nids = ipos;
+        ++J->nredo;
+      }
       J->nid[r] = (uint8_t)(redo || !seeds ? 0 : J->sink.nid);
       J->val[r] = (float)sv;
+      if (J->nid[r] && !(sv <= 0.0)) {
+        J->rcount[J->nrows] = J->nid[r];
+        J->rcol[J->nrows] = (uint32_t)i;
+        J->rval[J->nrows] = (float)sv;
+        ++J->nrows;
+      }
     }
   }
   return NULL;
@@ -2189,6 +2261,9 @@ static PyObject* seed_keys(PyObject* self, PyObject* args) {
   PyObject* result = NULL;
   KOut o;
   memset(&o, 0, sizeof(o));
+  IdSink one;                   /* the calling thread's row sink (small batches), reused per row */
+  memset(&one, 0, sizeof(one));
+  one.put = sink_keys;
   int64_t* base = NULL;
   int64_t* rowpos = NULL;
   uint8_t *nid = NULL, *redo = NULL, *jobof = NULL;
@@ -2230,12 +2305,53 @@ static PyObject* seed_keys(PyObject* self, PyObject* args) {
       jobs[t].nid = nid;
       jobs[t].val = wval;
       jobs[t].redo = redo;
+      const size_t jr = (size_t)(base[i] - base[i0]) + 1;
+      jobs[t].rcount = malloc(sizeof(int64_t) * jr);
+      jobs[t].rcol = malloc(sizeof(uint32_t) * jr);
+      jobs[t].rval = malloc(sizeof(float) * jr);
+      njobs = t + 1;
+      if (!jobs[t].rcount || !jobs[t].rcol || !jobs[t].rval) { PyErr_NoMemory(); goto done; }
       for (int64_t r = base[i0]; r < base[i]; ++r) jobof[r] = (uint8_t)t;
     }
-    njobs = threads;
     pool_run_fn(k_main, jobs, sizeof(KJob), threads);   /* (the GIL stays held) */
   }
-  {
+  int clean = par;
+  for (int t = 0; t < njobs; ++t) clean = clean && jobs[t].nredo == 0;
+  if (clean) {
+    /* every row stayed on the workers: the output is the jobs' arrays one after another (the jobs
+     * hold consecutive lists), offsets shifted by the bytes before each job */
+    Py_ssize_t nb = 0, nf = 0, nr = 0;
+    for (int t = 0; t < njobs; ++t) {
+      nb += (Py_ssize_t)jobs[t].sink.n;
+      nf += (Py_ssize_t)jobs[t].sink.nids;
+      nr += jobs[t].nrows;
+    }
+    o.blob = PyMem_Malloc((size_t)nb + 1);
+    o.off = PyMem_Malloc(sizeof(int64_t) * (size_t)(nf + 1));
+    o.hash = PyMem_Malloc(sizeof(int64_t) * (size_t)(nf + 1));
+    o.count = PyMem_Malloc(sizeof(int64_t) * (size_t)(nr + 1));
+    o.col = PyMem_Malloc(sizeof(uint32_t) * (size_t)(nr + 1));
+    o.val = PyMem_Malloc(sizeof(float) * (size_t)(nr + 1));
+    if (!o.blob || !o.off || !o.hash || !o.count || !o.col || !o.val) { PyErr_NoMemory(); goto done; }
+    o.capb = nb + 1;
+    o.capf = nf + 1;
+    o.capr = nr + 1;
+    for (int t = 0; t < njobs; ++t) {
+      const IdSink* k = &jobs[t].sink;
+      if (k->n) memcpy(o.blob + o.nb, k->buf, k->n);
+      for (size_t x = 0; x < k->nids; ++x) o.off[o.nf + (Py_ssize_t)x] = o.nb + k->idoff[x];
+      if (k->nids) memcpy(o.hash + o.nf, k->idhash, sizeof(int64_t) * k->nids);
+      const Py_ssize_t m = jobs[t].nrows;
+      if (m) {
+        memcpy(o.count + o.nr, jobs[t].rcount, sizeof(int64_t) * (size_t)m);
+        memcpy(o.col + o.nr, jobs[t].rcol, sizeof(uint32_t) * (size_t)m);
+        memcpy(o.val + o.nr, jobs[t].rval, sizeof(float) * (size_t)m);
+      }
+      o.nb += (Py_ssize_t)k->n;
+      o.nf += (Py_ssize_t)k->nids;
+      o.nr += m;
+    }
+  } else {
     int ran_python = 0;
     Py_ssize_t r = 0;
     for (Py_ssize_t i = 0; i < B; ++i) {
@@ -2246,39 +2362,31 @@ static PyObject* seed_keys(PyObject* self, PyObject* args) {
         if (par && !ran_python && !redo[r]) {
           if (!nid[r]) continue;
           const IdSink* k = &jobs[jobof[r]].sink;
-          const char* q = k->buf + rowpos[r];
-          for (int x = 0; x < nid[r]; ++x) {
-            uint32_t len;
-            memcpy(&len, q, 4);
-            if (kout_id(&o, q + 4, len) < 0) { Py_DECREF(evs); goto done; }
-            q += 4 + len;
+          for (size_t x = (size_t)rowpos[r]; x < (size_t)rowpos[r] + nid[r]; ++x) {
+            const size_t a = (size_t)k->idoff[x];
+            if (kout_id(&o, k->buf + a, sink_id_end(k, x) - a) < 0) { Py_DECREF(evs); goto done; }
           }
           if (kout_row(&o, nid[r], (uint32_t)i, wval[r]) < 0) { Py_DECREF(evs); goto done; }
         } else {
           /* (a small batch: the worker's row function on this thread first) */
           if (!par && !ran_python) {
-            IdSink k;
-            memset(&k, 0, sizeof(k));
-            k.put = sink_keys;
+            IdSink* const kp = &one;
+            kp->n = kp->nids = 0;
+            kp->nid = 0;
             int seeds = 0;
             double sv = 0.0;
-            if (!s_row_ids(PySequence_Fast_GET_ITEM(evs, j), &k, &seeds, &sv)) {
+            if (!s_row_ids(PySequence_Fast_GET_ITEM(evs, j), kp, &seeds, &sv)) {
               int bad = 0;
-              if (seeds && k.nid > 0) {
-                const char* q = k.buf;
-                for (int x = 0; x < k.nid && !bad; ++x) {
-                  uint32_t len;
-                  memcpy(&len, q, 4);
-                  bad = kout_id(&o, q + 4, len) < 0;
-                  q += 4 + len;
+              if (seeds && kp->nid > 0) {
+                for (size_t x = 0; x < kp->nids && !bad; ++x) {
+                  const size_t a = (size_t)kp->idoff[x];
+                  bad = kout_id(&o, kp->buf + a, sink_id_end(kp, x) - a) < 0;
                 }
-                if (!bad) bad = kout_row(&o, k.nid, (uint32_t)i, (float)sv) < 0;
+                if (!bad) bad = kout_row(&o, kp->nid, (uint32_t)i, (float)sv) < 0;
               }
-              free(k.buf);
               if (bad) { Py_DECREF(evs); goto done; }
               continue;
             }
-            free(k.buf);
           }
           if (k_row_serial(PySequence_Fast_GET_ITEM(evs, j), slow, &o, (uint32_t)i, &ran_python) < 0) {
             Py_DECREF(evs);
@@ -2302,7 +2410,13 @@ static PyObject* seed_keys(PyObject* self, PyObject* args) {
                          o.col ? (const char*)o.col : "", o.nr * (Py_ssize_t)sizeof(uint32_t),
                          o.val ? (const char*)o.val : "", o.nr * (Py_ssize_t)sizeof(float));
 done:
-  for (int t = 0; t < njobs; ++t) free(jobs[t].sink.buf);
+  sink_free(&one);
+  for (int t = 0; t < njobs; ++t) {
+    sink_free(&jobs[t].sink);
+    free(jobs[t].rcount);
+    free(jobs[t].rcol);
+    free(jobs[t].rval);
+  }
   PyMem_Free(base);
   PyMem_Free(rowpos);
   PyMem_Free(nid);

@@ -96,6 +96,28 @@ def test_native_matches_python_on_edge_rows():
     _same(a, b)
 
 
+@pytest.mark.parametrize("threads", [2, 4, 7])
+def test_seed_keys_all_rows_on_the_workers(threads):
+    """Collector rows only (none handed over): seed_keys assembles its output by concatenating the
+    workers' arrays -- the same blob, offsets, hashes, counts, columns and strengths as
+    SeedCandidates, for job splits that cut the batch at different lists."""
+    from egraph import _lib, synth
+    from egraph.graph import str_blob
+    from egraph.seeds import SeedCandidates, _row
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    lists = [x.evidence for x in synth.make_incidents(c, 150, seed=11)]
+    lists[3] = []                                   # an empty list inside a job
+    sc = SeedCandidates(lists)
+    blob, off, hs, count, col, val = _lib.pyhost.seed_keys(lists, _row, threads)
+    b, o = str_blob(sc.flat)
+    assert blob == b and np.array_equal(np.frombuffer(off, np.int64), o)
+    assert np.array_equal(np.frombuffer(hs, np.int64), np.frombuffer(_lib.pyhost.hash_ids(sc.flat), np.int64))
+    assert np.array_equal(np.frombuffer(count, np.int64), sc.count)
+    assert np.array_equal(np.frombuffer(col, np.uint32), sc.col)
+    assert np.array_equal(np.frombuffer(val, np.float32), sc.val, equal_nan=True)
+
+
 @pytest.mark.parametrize("bad", [
     {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
      "signal_strength": "x"},                                      # float("x"): ValueError
@@ -298,6 +320,28 @@ def test_attach_native_matches_python_on_edge_rows(threads):
     _attach_both(_edge_graph(), lists, threads)
 
 
+@pytest.mark.parametrize("threads", [2, 4, 7])
+def test_seed_keys_all_rows_on_the_workers(threads):
+    """Collector rows only (none handed over): seed_keys assembles its output by concatenating the
+    workers' arrays -- the same blob, offsets, hashes, counts, columns and strengths as
+    SeedCandidates, for job splits that cut the batch at different lists."""
+    from egraph import _lib, synth
+    from egraph.graph import str_blob
+    from egraph.seeds import SeedCandidates, _row
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    lists = [x.evidence for x in synth.make_incidents(c, 150, seed=11)]
+    lists[3] = []                                   # an empty list inside a job
+    sc = SeedCandidates(lists)
+    blob, off, hs, count, col, val = _lib.pyhost.seed_keys(lists, _row, threads)
+    b, o = str_blob(sc.flat)
+    assert blob == b and np.array_equal(np.frombuffer(off, np.int64), o)
+    assert np.array_equal(np.frombuffer(hs, np.int64), np.frombuffer(_lib.pyhost.hash_ids(sc.flat), np.int64))
+    assert np.array_equal(np.frombuffer(count, np.int64), sc.count)
+    assert np.array_equal(np.frombuffer(col, np.uint32), sc.col)
+    assert np.array_equal(np.frombuffer(val, np.float32), sc.val, equal_nan=True)
+
+
 @pytest.mark.parametrize("bad", [
     {"evidence_type": "kubernetes_pod", "entity_namespace": "ns", "entity_name": "p",
      "signal_strength": "x"},
@@ -342,6 +386,28 @@ def test_seed_keys_match_seed_candidates(threads):
     rng = random.Random(7)
     lists += [EDGE, [], EDGE[::-1]] + [rng.sample(EDGE, 8) for _ in range(30)]
     lists[5] = [dict(lists[5][0], entity_name="pé-テ")] + lists[5][1:]
+    sc = SeedCandidates(lists)
+    blob, off, hs, count, col, val = _lib.pyhost.seed_keys(lists, _row, threads)
+    b, o = str_blob(sc.flat)
+    assert blob == b and np.array_equal(np.frombuffer(off, np.int64), o)
+    assert np.array_equal(np.frombuffer(hs, np.int64), np.frombuffer(_lib.pyhost.hash_ids(sc.flat), np.int64))
+    assert np.array_equal(np.frombuffer(count, np.int64), sc.count)
+    assert np.array_equal(np.frombuffer(col, np.uint32), sc.col)
+    assert np.array_equal(np.frombuffer(val, np.float32), sc.val, equal_nan=True)
+
+
+@pytest.mark.parametrize("threads", [2, 4, 7])
+def test_seed_keys_all_rows_on_the_workers(threads):
+    """Collector rows only (none handed over): seed_keys assembles its output by concatenating the
+    workers' arrays -- the same blob, offsets, hashes, counts, columns and strengths as
+    SeedCandidates, for job splits that cut the batch at different lists."""
+    from egraph import _lib, synth
+    from egraph.graph import str_blob
+    from egraph.seeds import SeedCandidates, _row
+    c = synth.build_cluster(synth.ClusterConfig(pods=1500, namespaces=5, nodes=40,
+                                                deployments=150, services=100, seed=9))
+    lists = [x.evidence for x in synth.make_incidents(c, 150, seed=11)]
+    lists[3] = []                                   # an empty list inside a job
     sc = SeedCandidates(lists)
     blob, off, hs, count, col, val = _lib.pyhost.seed_keys(lists, _row, threads)
     b, o = str_blob(sc.flat)
