@@ -5,7 +5,10 @@ additive batch / root-cause activities.
 They stay drop-in sockets for IncidentWorkflow (incident_workflow.py:96-139): JSON-shaped
 dicts in and out.  When temporalio is installed they are registered with @activity.defn,
 otherwise they are plain coroutines.  The optional LLM enhancement of generate_hypotheses
-(:141-151) is out of scope (network-bound; a no-op without an API key in the reference).
+(:141-151) is not rebuilt (network-bound), but its step is kept: when the deployment provides
+the reference's `src.config.settings` and `src.services.rca.llm_summarizer` (path (a) of
+INTEGRATION.md) and `settings.llm_provider` is set, the rules' hypotheses go through
+`LLMSummarizer.enhance_hypotheses` with the reference's fallback to rules-only on any error.
 """
 from __future__ import annotations
 
@@ -40,12 +43,45 @@ async def build_evidence_graph(data: dict) -> dict:
     return {"node_count": node_count, "edge_count": edge_count}
 
 
+def _llm_enhancer():
+    """The reference's LLM step (activities.py:142-151) when the deployment has it configured:
+    an `async (hypotheses, evidence) -> hypotheses` callable, or None.  HYPOTHESIS_ENHANCER, if
+    set, takes precedence (tests, or a deployment wiring its own summarizer)."""
+    if HYPOTHESIS_ENHANCER is not None:
+        return HYPOTHESIS_ENHANCER
+    try:
+        from src.config import settings  # the reference's settings module, when deployed with it
+    except ImportError:
+        return None
+    if not getattr(settings, "llm_provider", None):
+        return None
+    try:
+        from src.services.rca.llm_summarizer import LLMSummarizer
+    except ImportError:
+        return None
+
+    async def enhance(hypotheses, evidence):
+        return await LLMSummarizer().enhance_hypotheses(hypotheses=hypotheses, evidence=evidence)
+    return enhance
+
+
+HYPOTHESIS_ENHANCER = None
+
+
 @_defn
 async def generate_hypotheses(data: dict) -> list[dict]:
-    """Rules-engine hypotheses for one incident (:124-159)."""
+    """Rules-engine hypotheses for one incident (:124-159), then the optional LLM enhancement
+    (:142-151): skipped without hypotheses, rules-only on any error."""
     incident = Incident(**data["incident"])
-    return await RulesEngine().generate_hypotheses(
-        incident=incident, evidence=data["evidence"].get("evidence", []))
+    evidence = data["evidence"].get("evidence", [])
+    hypotheses = await RulesEngine().generate_hypotheses(incident=incident, evidence=evidence)
+    enhance = _llm_enhancer() if hypotheses else None
+    if enhance is not None:
+        try:
+            hypotheses = await enhance(hypotheses, evidence)
+        except Exception as e:  # noqa: BLE001 -- the reference's fallback (:150-151)
+            logger.warning("LLM enhancement failed, using rules-only: %s", e)
+    return hypotheses
 
 
 @_defn
