@@ -245,6 +245,14 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 // cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
 // the column's frontier work, for longest-first launch order).  Both are wave-aggregated: one
 // atomic per run of equal columns (a segmented sum over an inclusive wave scan).
+// A run's pool / stats counters and overflow-list heads cleared in one launch (one graph node
+// instead of two fill nodes in a captured replay: each node costs its own dispatch gap).
+__global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf) {
+  const int tid = threadIdx.x;
+  if (tid < 7) ctr[tid] = 0;
+  if (tid < 4) ovf[tid] = 0;
+}
+
 __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                   int64_t n, uint32_t V, int B, const uint32_t* __restrict__ row_ptr,
                                   uint32_t* cnt, uint32_t* cost) {
@@ -570,8 +578,8 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                              float* out_scores, hipStream_t st) {
   const egr_snapshot* s = f->s;
   if (!(sorted && f->ctr_clean)) {
-    EGR_HIP(hipMemsetAsync(f->ctr, 0, 7 * 8, st));
-    EGR_HIP(hipMemsetAsync(f->ovf, 0, 4 * 4, st));
+    hipLaunchKernelGGL(clear_counters_kernel, dim3(1), dim3(64), 0, st, f->ctr, f->ovf);
+    EGR_CHECK_LAUNCH();
   }
   FArgs a{};
   a.row_ptr = s->row_ptr;
