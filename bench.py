@@ -54,9 +54,10 @@ METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod gra
 XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # --merge default cap: a launch costs ~0.12 ms of tail + ~0.055 ms per C3 batch (0.0734 / 0.0653 /
-# 0.0626 ms per batch at 8 / 16 / 24 batches, profiles/r03_ab_merge_schedule.txt); 50 batches
-# (51,200 columns, ~2.9 ms per launch) leave the tail ~4 % of the launch
-MERGE_MAX = 50
+# 0.0626 ms per batch at 8 / 16 / 24 batches, profiles/r03_ab_merge_schedule.txt).  The M batches
+# of a launch are M different incident sets, all open in the graph (M x B incidents): 20 sets
+# (20,480 incidents) bring C3 to 254k vertices / 1.13M CSR entries, SURVEY §8d's ~250k vertices
+MERGE_MAX = 20
 
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
@@ -114,24 +115,21 @@ def launch_ranks(n: int) -> int:
 
 
 def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: int = 1,
-          pool_entries: int = 0, merge: int = 1):
-    from egraph import catalog, synth
+          pool_entries: int = 0, merge: int = 1, replicate: bool = False):
+    from egraph import catalog
     from egraph.device import to_device
     from egraph.encode import encode_batch
     from egraph.rca import RulesDeviceBatch
     t0 = time.time()
-    cl = synth.build_cluster(synth.CONFIGS[config])
-    # every rank generates the same incident set for the graph (replicated snapshot) and
-    # ranks the slice of columns it owns; one incident set per rank keeps per-GPU work fixed
-    cases = synth.make_incidents(cl, B, seed=1000 + rank)
-    synth.add_incidents(cl, cases)
-    g = synth.build_graph(cl)                 # C4: with its dense telemetry links (~10M entries)
-    evidence = [x.evidence for x in cases]
+    # --merge M: the M batches of one launch are M DIFFERENT incident sets (distinct_batches);
+    # every one of them is open in the graph, so the graph holds M x B incidents.  Each rank
+    # builds its own graph with its own incident sets (per-GPU work fixed: weak scaling)
+    n_sets = merge if (merge > 1 and not replicate) else 1
+    g, batches = make_world(config, B, n_sets, seed0=1000 + rank * n_sets)
+    evidence, sv, sc, ss, src = batches[0]
     enc = encode_batch(evidence, catalog.default())
-    sv, sc, ss = synth.seeds_for_batch(g, evidence)
-    src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
     log(f"[rank {rank}] built {config}: V={g.num_vertices} E={g.num_edges} rows={enc.n_rows} "
-        f"seeds={len(sv)} in {time.time() - t0:.1f}s")
+        f"seeds={len(sv)} incident sets={n_sets} in {time.time() - t0:.1f}s")
     with torch.cuda.device(dev):
         snap = g.snapshot(device=dev)
         plan = snap.plan(B, max_seeds=len(sv), k=k)
@@ -142,25 +140,51 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
         # seeds at its own column offset, the rules over the M batches' rows): the hardware
         # dispatcher hands the columns out costliest-first across all M batches, so batch i's
         # tail runs beside batch i+1's columns inside one launch on one stream
+        # (batch i = batches[i]; --replicate-batches (A/B only): M copies of batch 0, round 3's
+        # launch, whose adjacent copies share L2 lines)
         Bm = B * merge
         if merge > 1:
-            msv, msc, mss, msrc = merge_batches([(sv, sc, ss, src)] * merge, B)
+            parts = [batches[i % n_sets] for i in range(merge)]
+            msv, msc, mss, msrc = merge_batches([p[1:] for p in parts], B)
             lane_seeds = tuple(to_device(a, dev) for a in (msv, msc, mss))
             lane_src = to_device(msrc, dev)
-            lane_rules = encode_batch(evidence * merge, catalog.default())
+            lane_rules = encode_batch([ev for p in parts for ev in p[0]], catalog.default())
+            n_seeds = len(msv)
         else:
-            lane_seeds, lane_src, lane_rules = seeds, sources, rules
+            lane_seeds, lane_src, lane_rules, n_seeds = seeds, sources, rules, len(sv)
         # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
         # members outside the candidate set); 0 keeps every member's score for inspection
-        fr = snap.frontier(Bm, max_seeds=len(sv) * merge, k=k, pool_entries=pool_entries)
-        lanes = build_lanes(snap, Bm, len(sv) * merge, k, pipeline, pool_entries, dev,
+        fr = snap.frontier(Bm, max_seeds=n_seeds, k=k, pool_entries=pool_entries)
+        lanes = build_lanes(snap, Bm, n_seeds, k, pipeline, pool_entries, dev,
                             [(fr, lane_rules, lane_seeds, lane_src)]
                             + [(None, lane_rules if merge > 1 else enc, lane_seeds, lane_src)] * (pipeline - 1))
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
     return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 lanes=lanes, tick=0, merge=merge, sub=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
-                evidence=evidence, incident_ids=[str(x.incident["id"]) for x in cases])
+                evidence=evidence, incident_ids=[str(e[0]["incident_id"]) for e in evidence],
+                distinct_batches=n_sets, incidents_in_graph=n_sets * B)
+
+
+def make_world(config: str, B: int, n_sets: int, seed0: int = 1000, cfg=None):
+    """The config's cluster with n_sets incident sets of B incidents each (make_incidents seeds
+    seed0, seed0 + 1, ...) all added to ONE graph; per set (evidence lists, seed vertex, seed
+    column, seed strength, incident vertex per column).  `cfg` overrides the cluster config."""
+    from egraph import synth
+    cl = synth.build_cluster(cfg or synth.CONFIGS[config])
+    sets = []
+    for i in range(n_sets):
+        cases = synth.make_incidents(cl, B, seed=seed0 + i)
+        synth.add_incidents(cl, cases)
+        sets.append(cases)
+    g = synth.build_graph(cl)                 # C4: with its dense telemetry links (~10M entries)
+    out = []
+    for cases in sets:
+        evidence = [x.evidence for x in cases]
+        sv, sc, ss = synth.seeds_for_batch(g, evidence)
+        src = g.lookup([f"incident:{x.incident['id']}" for x in cases]).astype(np.uint32)
+        out.append((evidence, sv, sc, ss, src))
+    return g, out
 
 
 def merge_batches(batches: list, B: int) -> tuple:
@@ -626,7 +650,8 @@ def _frontier_traffic(ctx, B: int):
         d = json.loads(pmc.read_text())
         w = d.get("workload", {})
         if (w.get("config") == ctx.get("config") and w.get("batch") == B // M
-                and w.get("batches_per_launch", 1) == M):
+                and w.get("batches_per_launch", 1) == M
+                and w.get("distinct_batches", 1) == ctx.get("distinct_batches", 1)):
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -1077,6 +1102,9 @@ def main():
                     help="frontier batches per launch: each lane's launch carries this many "
                          "consecutive batches (one costliest-first column order across them); "
                          f"0 = the largest divisor of --steps up to {MERGE_MAX}")
+    ap.add_argument("--replicate-batches", action="store_true",
+                    help="A/B only: a launch's M batches are M copies of one incident set (round "
+                         "3's launch) instead of M different incident sets")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the end-to-end drop-in RulesEngine measurement")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -1157,7 +1185,8 @@ def main():
     ctx = setup(args.config, args.batch, args.k, rank, dev,
                 args.pipeline if args.engine == "frontier" else 1,
                 pool_entries=0 if args.pool else -1,
-                merge=max(1, args.merge) if args.engine == "frontier" else 1)
+                merge=max(1, args.merge) if args.engine == "frontier" else 1,
+                replicate=args.replicate_batches)
     M = ctx["merge"]
     run_step = step_frontier if args.engine == "frontier" else step
     # (at least one step per lane: every lane's frontier has run before adapt() reads its stats)
@@ -1250,6 +1279,8 @@ def main():
             "hops": args.hops, "k": args.k, "parallelism": f"incident-sharded x{world}",
             "lanes": args.pipeline if args.engine == "frontier" else 1,
             "batches_per_launch": M,
+            "distinct_batches_per_launch": ctx["distinct_batches"],
+            "incidents_in_graph": ctx["incidents_in_graph"],
             "hip_graph_replay": out_graph,
             "seed_input": ("grouped by incident + column offsets + costliest-first launch order, "
                            "resident (egr_frontier_run_grouped)" if GROUPED and args.engine == "frontier"

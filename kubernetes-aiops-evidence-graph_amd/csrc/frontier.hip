@@ -242,9 +242,6 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
   return r;
 }
 
-// cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
-// the column's frontier work, for longest-first launch order).  Both are wave-aggregated: one
-// atomic per run of equal columns (a segmented sum over an inclusive wave scan).
 // A run's pool / stats counters and overflow-list heads cleared in one launch (one graph node
 // instead of two fill nodes in a captured replay: each node costs its own dispatch gap).
 __global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf) {
@@ -253,6 +250,9 @@ __global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* 
   if (tid < 4) ovf[tid] = 0;
 }
 
+// cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
+// the column's frontier work, for longest-first launch order).  Both are wave-aggregated: one
+// atomic per run of equal columns (a segmented sum over an inclusive wave scan).
 __global__ void seed_count_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                   int64_t n, uint32_t V, int B, const uint32_t* __restrict__ row_ptr,
                                   uint32_t* cnt, uint32_t* cost) {

@@ -191,8 +191,12 @@ class EvidenceGraph:
         return buf.raw[:n].decode()
 
     def vertex_ids(self) -> list[str]:
-        """The id of every vertex, by vertex index (a list kept by merge_nodes; rebuilt from
-        the native graph if it ever disagrees with it)."""
+        """The id of every vertex, by vertex index (a copy: callers may edit it)."""
+        return list(self._vertex_ids())
+
+    def _vertex_ids(self) -> list[str]:
+        """The graph's own id list (kept by merge_nodes; rebuilt from the native graph if it
+        ever disagrees with it).  Read-only for callers inside the package."""
         V = self.num_vertices
         if len(self._ids) != V:
             self._ids = []
@@ -263,6 +267,47 @@ class EvidenceGraph:
 
     def snapshot(self, weights=None, device=None) -> "Snapshot":
         return Snapshot(self, weights, device)
+
+    def within_hops(self, v: int, hops: int) -> np.ndarray:
+        """bool[V]: the vertices within `hops` undirected hops of vertex v, v included (the node
+        set of apoc.path.subgraphAll(maxLevel=hops), host side)."""
+        csr = self.csr()
+        rp, col = csr["row_ptr"].astype(np.int64), csr["col"]
+        seen = np.zeros(self.num_vertices, bool)
+        seen[v] = True
+        fr = np.array([v], np.int64)
+        for _ in range(hops):
+            if not len(fr):
+                break
+            lens = rp[fr + 1] - rp[fr]
+            idx = np.repeat(rp[fr] - np.concatenate(([0], np.cumsum(lens)[:-1])), lens) + np.arange(lens.sum())
+            nb = np.unique(col[idx])
+            fr = nb[~seen[nb]].astype(np.int64)
+            seen[fr] = True
+        return seen
+
+    def subgraph(self, keep: np.ndarray) -> "EvidenceGraph":
+        """A new graph of the vertices with keep[v] (ids, labels, properties, relative order)
+        and the edges between them (creation order, types, properties): what DETACH DELETE of
+        the other vertices leaves."""
+        keep = np.asarray(keep, bool)
+        vl, es, ed, et = self.export()
+        labels, types, ids = self.labels(), self.rel_types(), self._vertex_ids()
+        kept = np.nonzero(keep)[0]
+        out = EvidenceGraph()
+        if len(kept):
+            out.merge_nodes([ids[v] for v in kept], [labels[vl[v]] for v in kept])
+        remap = np.full(len(vl), -1, np.int64)
+        remap[kept] = np.arange(len(kept))
+        ok = keep[es] & keep[ed] if len(es) else np.zeros(0, bool)
+        if ok.any():
+            out.add_edges_indexed(remap[es[ok]], remap[ed[ok]], et[ok].astype(np.int32), types)
+        out.node_props = {k: dict(p) for k, p in self.node_props.items()
+                          if k in self.vertex_of and keep[self.vertex_of[k]]}
+        alive = out.vertex_ids_set()
+        out.edge_props = {k: dict(p) for k, p in self.edge_props.items()
+                          if k[0] in alive and k[2] in alive}
+        return out
 
 
 class Snapshot:

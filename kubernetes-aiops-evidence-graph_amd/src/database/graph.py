@@ -1,239 +1,6 @@
-"""Drop-in GraphService (reference src/database/neo4j.py:68-202) backed by the GPU snapshot.
+"""Mirror: `src.database.graph` is `egraph_dropin.graph_service` (the same module object)."""
+import sys
 
-Write path: create_entity / create_entities_batch / create_relation / create_relations_batch
-keep the reference's MERGE semantics and return values (attempted counts, :112 / :166).
-Read path: get_incident_graph(incident_id, depth=3) reproduces
-`MATCH (i:Incident {id}) CALL apoc.path.subgraphAll(i, {maxLevel: depth})` (:170-202): the
-vertex set within `depth` undirected hops (egr_plan_reach_hop on the device) and every edge
-among those vertices (egr_plan_induced_edges).  As in the reference, the Incident vertex's id
-property is the GraphEntity id ("incident:<uuid>", neo4j.py:101-102), so a bare UUID matches
-nothing unless `resolve_bare_uuid=True`.
+import egraph_dropin.graph_service as _impl
 
-Root-cause ranking (build-defined): rank_root_causes runs
-the frontier engine (egr_frontier_*) -- per incident, 3-hop typed propagation of the evidence
-rows' signal strengths over the graph, ranked over the incident's 3-hop reach set.
-
-The graph is process-wide, like the Neo4j database the reference talks to.  Writes go to the host
-graph (MERGE); the next read brings the device snapshot up to date with ONE incremental update
-(egr_snapshot_update: the appended vertices and edges merged into the CSR on the device) instead
-of a rebuild and re-upload.
-
-Concurrency: Temporal runs activities concurrently, and the ranking runs in a worker thread
-(asyncio.to_thread) while writes arrive on the event loop.  Every access to the shared state --
-the host graph (whose C++ vectors a write reallocates), the snapshot sync, the cached plans and
-frontiers and their output buffers -- holds one process-wide lock, from the write or the
-set_seeds through the read-back of the results.
-"""
-from __future__ import annotations
-
-import asyncio
-import threading
-
-import numpy as np
-import torch
-
-from egraph import ops
-from egraph._lib import pyhost
-from egraph.device import to_device
-from egraph.graph import EvidenceGraph
-from egraph.seeds import seeds_for_batch
-from src.models.evidence import GraphEntity, GraphRelation
-
-
-class GraphService:
-    """Service for Evidence Graph operations (process-wide store)."""
-
-    _graph: EvidenceGraph | None = None
-    _snapshot = None
-    _plans: dict = {}
-    _frontiers: dict = {}
-    _lock = threading.RLock()
-    device = None
-
-    @classmethod
-    def graph(cls) -> EvidenceGraph:
-        if cls._graph is None:
-            cls._graph = EvidenceGraph()
-        return cls._graph
-
-    @classmethod
-    def reset(cls) -> None:
-        with cls._lock:
-            cls._graph, cls._snapshot, cls._plans, cls._frontiers = None, None, {}, {}
-
-    @classmethod
-    def _invalidate(cls) -> None:
-        """After a write: the snapshot is synced lazily by the next read (_snap)."""
-
-    @staticmethod
-    async def create_entity(entity: GraphEntity) -> str:
-        GraphService.create_entities_sync([entity])
-        return entity.id
-
-    @staticmethod
-    async def create_entities_batch(entities: list[GraphEntity]) -> int:
-        return GraphService.create_entities_sync(entities)
-
-    @staticmethod
-    async def create_relation(relation: GraphRelation) -> bool:
-        with GraphService._lock:
-            known = GraphService.graph().lookup([relation.source_id, relation.target_id])
-            GraphService.create_relations_sync([relation])
-        return bool((known >= 0).all())
-
-    @staticmethod
-    async def create_relations_batch(relations: list[GraphRelation]) -> int:
-        return GraphService.create_relations_sync(relations)
-
-    @classmethod
-    def create_entities_sync(cls, entities) -> int:
-        with cls._lock:
-            n = cls.graph().create_entities_batch(entities)
-            cls._invalidate()
-        return n
-
-    @classmethod
-    def create_relations_sync(cls, relations) -> int:
-        with cls._lock:
-            n = cls.graph().create_relations_batch(relations)
-            cls._invalidate()
-        return n
-
-    @classmethod
-    def _plan(cls, n_cols: int):
-        snap = cls._snap()          # syncs first: a write drops the plans
-        if n_cols not in cls._plans:
-            cls._plans[n_cols] = snap.plan(n_cols, max_seeds=0, k=1)
-        return cls._plans[n_cols]
-
-    @classmethod
-    def _snap(cls):
-        g = cls.graph()
-        if cls._snapshot is None:
-            cls._snapshot = g.snapshot(device=cls.device)
-        elif cls._snapshot.sync(g) != (0, 0):
-            cls._plans = {}        # plans are sized for one snapshot version
-            cls._frontiers = {k: f for k, f in cls._frontiers.items()
-                              if f.max_vertices >= cls._snapshot.n_vertices}
-        return cls._snapshot
-
-    @classmethod
-    def _frontier(cls, n_cols: int, n_seeds: int, k: int):
-        """A frontier for n_cols columns, reused while its seed capacity suffices."""
-        snap = cls._snap()
-        fr = cls._frontiers.get((n_cols, k))
-        if fr is None or fr.max_seeds < n_seeds:
-            fr = snap.frontier(n_cols, max_seeds=max(n_seeds, 1024), k=k, pool_entries=-1)
-            cls._frontiers[(n_cols, k)] = fr
-        return fr
-
-    @staticmethod
-    async def rank_root_causes(incident_ids: list[str], evidence_lists: list[list[dict]],
-                               hops: int = 3, k: int = 10) -> list[list[dict]]:
-        # the launch + completion wait run off the event loop (the worker is never blocked)
-        return await asyncio.to_thread(GraphService.rank_root_causes_sync, incident_ids,
-                                       evidence_lists, hops, k)
-
-    @classmethod
-    def rank_root_causes_sync(cls, incident_ids: list[str], evidence_lists: list[list[dict]],
-                              hops: int = 3, k: int = 10) -> list[list[dict]]:
-        """Per incident, the top-k graph entities by propagated evidence score, over the
-        entities within `hops` undirected hops of the incident (Incident entities excluded):
-        [{"id", "labels", "score", "rank"}], score descending, entity order on ties.
-        Incidents are matched like get_incident_graph: by Incident id, or "incident:<id>"."""
-        if len(incident_ids) != len(evidence_lists):
-            raise ValueError("incident_ids and evidence_lists differ in length")
-        if not incident_ids:
-            return []
-        with cls._lock:
-            return cls._rank_locked(incident_ids, evidence_lists, hops, k)
-
-    @classmethod
-    def _rank_locked(cls, incident_ids, evidence_lists, hops, k):
-        g = cls.graph()
-        if g.num_vertices == 0:
-            return [[] for _ in incident_ids]
-        keys = []
-        for iid in incident_ids:
-            iid = str(iid)
-            v = g.vertex_of.get(("Incident", iid), g.vertex_of.get(("Incident", f"incident:{iid}"), -1))
-            keys.append(v)
-        sv, sc, ss = seeds_for_batch(g, evidence_lists)
-        fr = cls._frontier(len(keys), len(sv), k)
-        dev = fr.dev
-        src = torch.tensor(keys, dtype=torch.int32, device=dev)   # -1 = EGR_NO_NODE: no column
-        labels = g.labels()
-        inc = labels.index("Incident") if "Incident" in labels else -1
-        # torch.ops.egraph.frontier_run: the registered custom op (seeds + run of the frontier)
-        ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
-                                       to_device(ss, dev), src, hops, inc)
-        ids = ids.cpu().numpy().view("uint32")
-        scores = scores.cpu().numpy()
-        fr.adapt()              # overflowing columns: the wide-table retry from the next call on
-        # the ranked vertices' labels by numpy indexing (no per-vertex list of the whole graph),
-        # then the entity dicts natively (csrc/pyhost.c entity_rows; the loop it replaces:
-        # {"id": vid[v], "labels": [labels[label of v]], "score": score, "rank": r + 1} per
-        # ranked vertex, each list up to its first EGR_NO_NODE)
-        lab = np.zeros(ids.shape, np.uint8)
-        ok = ids != 0xFFFFFFFF
-        lab[ok] = g.vertex_labels()[ids[ok]]
-        out = pyhost.entity_rows(np.ascontiguousarray(ids), np.ascontiguousarray(scores, np.float32),
-                                 lab, ids.shape[1] if ids.ndim == 2 else k, g.vertex_ids(), list(labels))
-        return out
-
-    @staticmethod
-    async def get_incident_graph(incident_id: str, depth: int = 3,
-                                 resolve_bare_uuid: bool = False) -> dict:
-        return GraphService.get_incident_graphs([incident_id], depth, resolve_bare_uuid)[0]
-
-    @classmethod
-    def get_incident_graphs(cls, incident_ids: list[str], depth: int = 3,
-                            resolve_bare_uuid: bool = False) -> list[dict]:
-        """Batched get_incident_graph: one reach launch per hop for all incidents."""
-        with cls._lock:
-            return cls._graphs_locked(incident_ids, depth, resolve_bare_uuid)
-
-    @classmethod
-    def _graphs_locked(cls, incident_ids, depth, resolve_bare_uuid):
-        g = cls.graph()
-        empty = {"nodes": [], "relationships": []}
-        if g.num_vertices == 0 or not incident_ids:
-            return [dict(empty) for _ in incident_ids]
-        keys = []
-        for iid in incident_ids:
-            iid = str(iid)
-            if ("Incident", iid) not in g.vertex_of and resolve_bare_uuid:
-                iid = f"incident:{iid}"
-            keys.append(g.vertex_of.get(("Incident", iid), -1))
-        plan = cls._plan(len(keys))
-        dev = plan.dev
-        # -1 as int32 is EGR_NO_NODE as u32: an empty column
-        src = torch.tensor([k if k >= 0 else -1 for k in keys], dtype=torch.int32, device=dev)
-        plan.set_sources(src)
-        for _ in range(depth):
-            plan.reach_hop()
-        bits = plan.read_reach().cpu().numpy().view("uint64")
-        labels = g.labels()
-        vlabel = g.vertex_labels()
-        rtypes = g.rel_types()
-        out = []
-        for b, k in enumerate(keys):
-            if k < 0:
-                out.append(dict(empty))
-                continue
-            word = bits[b // 64]
-            members = [int(v) for v in ((word >> (b % 64)) & 1).nonzero()[0]]
-            nodes = []
-            for v in members:
-                lab = labels[vlabel[v]]
-                vid = g.vertex_id(v)
-                props = dict(g.node_props.get((lab, vid), {"id": vid}))
-                nodes.append({"id": props.get("id"), "labels": [lab], "properties": props})
-            rels = []
-            for s, d, t in plan.induced_edges(b):
-                sid, did = g.vertex_id(int(s)), g.vertex_id(int(d))
-                rt = rtypes[int(t)]
-                rels.append({"type": rt, "source": sid, "target": did,
-                             "properties": dict(g.edge_props.get((sid, rt, did), {}))})
-            out.append({"nodes": nodes, "relationships": rels})
-        return out
+sys.modules[__name__] = _impl

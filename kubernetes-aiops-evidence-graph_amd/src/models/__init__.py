@@ -1,29 +1,3 @@
-"""Models on the evidence-graph hot path (reference src/models/__init__.py)."""
-from src.models.evidence import (
-    CollectorResult,
-    Evidence,
-    EvidenceSource,
-    EvidenceType,
-    GraphEntity,
-    GraphRelation,
-)
-from src.models.hypothesis import (
-    DiagnosisRule,
-    Hypothesis,
-    HypothesisCategory,
-    HypothesisSource,
-    RCAResult,
-)
-from src.models.incident import (
-    Incident,
-    IncidentCreate,
-    IncidentSeverity,
-    IncidentSource,
-    IncidentStatus,
-)
-
-__all__ = [
-    "CollectorResult", "DiagnosisRule", "Evidence", "EvidenceSource", "EvidenceType",
-    "GraphEntity", "GraphRelation", "Hypothesis", "HypothesisCategory", "HypothesisSource",
-    "Incident", "IncidentCreate", "IncidentSeverity", "IncidentSource", "IncidentStatus", "RCAResult",
-]
+"""Mirror of the hot path's models (reference src/models/__init__.py): egraph_dropin.models."""
+from egraph_dropin.models import *  # noqa: F401,F403
+from egraph_dropin.models import __all__  # noqa: F401

@@ -1,6 +1,6 @@
-"""Alert ingestion front end (reference src/services/ingestion/__init__.py): normalizer with GPU
-fingerprints, deduplicator backed by the GPU TTL table."""
-from src.services.ingestion.deduplicator import AlertDeduplicator, RateLimiter
-from src.services.ingestion.normalizer import AlertNormalizer
+"""Mirror of the alert ingestion front end (reference src/services/ingestion/__init__.py):
+egraph_dropin.normalizer / egraph_dropin.deduplicator."""
+from egraph_dropin.deduplicator import AlertDeduplicator, RateLimiter
+from egraph_dropin.normalizer import AlertNormalizer
 
 __all__ = ["AlertNormalizer", "AlertDeduplicator", "RateLimiter"]

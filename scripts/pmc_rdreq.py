@@ -4,7 +4,8 @@ RDREQ x 128 B (one request per 128-B line for this kernel's 8-B gathers, calibra
 scripts/calib_gather.hip, profiles/r02_calib_gather.txt) + 32 B per write request (64 B for the
 64-B ones).  Writes profiles/pmc_frontier_calibrated_<tag>.json, which bench.py reads when its
 workload (config, batch, batches per launch) matches.
-Usage: python scripts/pmc_rdreq.py <pmc dir> <tag> <config> <batch> <batches_per_launch>"""
+Usage: python scripts/pmc_rdreq.py <pmc dir> <tag> <config> <batch> <batches_per_launch> [distinct]
+(distinct = how many different incident sets the launch's batches are; 1 = copies of one set)"""
 import csv
 import json
 import sys
@@ -12,6 +13,7 @@ from collections import defaultdict
 from pathlib import Path
 
 root, tag, config, batch, merge = Path(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+distinct = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 REPO = Path(__file__).resolve().parents[1]
 vals = defaultdict(list)
 for f in sorted(root.rglob("*counter_collection.csv")):
@@ -21,8 +23,11 @@ for f in sorted(root.rglob("*counter_collection.csv")):
 mean = {c: sum(x) / len(x) for c, x in vals.items()}
 rd, wr, wr64 = mean["TCC_EA0_RDREQ_sum"], mean["TCC_EA0_WRREQ_sum"], mean.get("TCC_EA0_WRREQ_64B_sum", 0.0)
 rep = {
-    "kernel": "frontier_lds_kernel, %s, %d columns per launch (%d batches of %d), pruned top-10" % (config, batch * merge, merge, batch),
-    "workload": {"config": config, "batch": batch, "batches_per_launch": merge},
+    "kernel": "frontier_lds_kernel, %s, %d columns per launch (%d batches of %d, %d different "
+              "incident sets), pruned top-10" % (config, batch * merge, merge, batch, distinct),
+    "workload": {"config": config, "batch": batch, "batches_per_launch": merge,
+                 "distinct_batches": distinct},
+    "l2_read_requests_per_batch": rd / merge,
     "dispatches": len(vals["TCC_EA0_RDREQ_sum"]),
     "tcc_ea0_rdreq_per_launch": rd, "tcc_ea0_wrreq_per_launch": wr, "tcc_ea0_wrreq_64b_per_launch": wr64,
     "bytes_per_rdreq": 128,
