@@ -1,16 +1,13 @@
 #!/bin/bash
-# One GPU call for the edge-cut partitioned path: its GPU tests, then the C4
-# --shard graph bench with P in-process partitions on the one GPU, and the C4 replicated
-# frontier bench for comparison.  Each GPU step has its own limit; the chain stops on failure.
+# The edge-cut path (C4): the partition tests, then C4 at P = 1, 2,
+# 4, 8 partitions in one process (per-partition compute times + the projected per-GPU step).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-shard}
 mkdir -p $OUT
-timeout -k 10 240 python -u -m pytest tests/test_shard_gpu.py -x -v --timeout 120 --timeout-method thread > $OUT/pytest_shard.log 2>&1
-echo "shard tests ok"; tail -2 $OUT/pytest_shard.log
-for P in ${PARTS:-1 2 4}; do
-  timeout -k 10 300 python -u bench.py --shard graph --config C4 --partitions $P --steps 5 --warmup 2 $([ $P = 1 ] || echo --no-cpu-baseline) ${XARGS:-} > $OUT/bench_c4_p$P.json 2> $OUT/bench_c4_p$P.err
-  echo "P=$P"; cat $OUT/bench_c4_p$P.json
+timeout -k 10 400 python -u -m pytest tests/test_shard_gpu.py tests/test_configs_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k "shard or C4 or partition" > $OUT/pytest.log 2>&1
+echo "tests ok"; tail -1 $OUT/pytest.log
+for P in 1 2 4 8; do
+  timeout -k 10 200 python -u bench.py --shard graph --config C4 --partitions $P --steps 5 --warmup 2 --no-cpu-baseline > $OUT/c4_p$P.json 2> $OUT/c4_p$P.err
+  python -c "import json;d=json.load(open('$OUT/c4_p$P.json'));c=d['config'];print('P=$P', round(d['ms_per_step'],2), 'ms in-process; partitions', [round(x,2) for x in c['partition_compute_ms']], 'projected per GPU', round(c['projected_ms_per_gpu'],2), 'sent/hop', c['halo_bytes_sent_per_hop_max_rank'])"
 done
-timeout -k 10 300 python -u bench.py --config C4 --no-cpu-baseline --dense-steps 0 > $OUT/bench_c4_frontier.json 2> $OUT/bench_c4_frontier.err
-echo "C4 frontier"; cat $OUT/bench_c4_frontier.json
