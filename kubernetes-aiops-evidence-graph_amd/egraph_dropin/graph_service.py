@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import asyncio
 import threading
+import time
 
 import numpy as np
 import torch
@@ -38,6 +39,24 @@ from egraph.device import to_device
 from egraph.graph import EvidenceGraph
 from egraph.seeds import seeds_for_batch
 from egraph_dropin.models.evidence import GraphEntity, GraphRelation
+
+
+class _StageClock:
+    """Seconds per stage into `stages` (None: does nothing); a stage given a device ends with
+    a device synchronise, so its device work is counted in it."""
+
+    def __init__(self, stages: dict | None):
+        self.stages = stages
+        self.t = time.perf_counter() if stages is not None else 0.0
+
+    def lap(self, name: str, dev=None) -> None:
+        if self.stages is None:
+            return
+        if dev is not None:
+            torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        self.stages[name] = self.stages.get(name, 0.0) + t - self.t
+        self.t = t
 
 
 class GraphService:
@@ -136,40 +155,51 @@ class GraphService:
 
     @classmethod
     def rank_root_causes_sync(cls, incident_ids: list[str], evidence_lists: list[list[dict]],
-                              hops: int = 3, k: int = 10) -> list[list[dict]]:
+                              hops: int = 3, k: int = 10, stages: dict | None = None) -> list[list[dict]]:
         """Per incident, the top-k graph entities by propagated evidence score, over the
         entities within `hops` undirected hops of the incident (Incident entities excluded):
         [{"id", "labels", "score", "rank"}], score descending, entity order on ties.
-        Incidents are matched like get_incident_graph: by Incident id, or "incident:<id>"."""
+        Incidents are matched like get_incident_graph: by Incident id, or "incident:<id>".
+        `stages` (a dict, diagnostics): filled with each host / device stage's seconds (the
+        device is synchronised between stages, so the parts add up to the call)."""
         if len(incident_ids) != len(evidence_lists):
             raise ValueError("incident_ids and evidence_lists differ in length")
         if not incident_ids:
             return []
         with cls._lock:
-            return cls._rank_locked(incident_ids, evidence_lists, hops, k)
+            return cls._rank_locked(incident_ids, evidence_lists, hops, k, stages)
 
     @classmethod
-    def _rank_locked(cls, incident_ids, evidence_lists, hops, k):
+    def _rank_locked(cls, incident_ids, evidence_lists, hops, k, stages=None):
         g = cls.graph()
         if g.num_vertices == 0:
             return [[] for _ in incident_ids]
+        clock = _StageClock(stages)
+        vo = g.vertex_of
         keys = []
         for iid in incident_ids:
             iid = str(iid)
-            v = g.vertex_of.get(("Incident", iid), g.vertex_of.get(("Incident", f"incident:{iid}"), -1))
-            keys.append(v)
+            v = vo.get(("Incident", iid))
+            keys.append(v if v is not None else vo.get(("Incident", f"incident:{iid}"), -1))
+        clock.lap("incident_lookup")
         sv, sc, ss = seeds_for_batch(g, evidence_lists)
+        clock.lap("seed_attach")
         fr = cls._frontier(len(keys), len(sv), k)
         dev = fr.dev
+        clock.lap("snapshot_sync", dev)
         src = torch.tensor(keys, dtype=torch.int32, device=dev)   # -1 = EGR_NO_NODE: no column
+        dsv, dsc, dss = to_device(sv, dev), to_device(sc, dev), to_device(ss, dev)
+        clock.lap("upload", dev)
         labels = g.labels()
         inc = labels.index("Incident") if "Incident" in labels else -1
         # torch.ops.egraph.frontier_run: the registered custom op (seeds + run of the frontier)
-        ids, scores = ops.frontier_run(fr, to_device(sv, dev), to_device(sc, dev),
-                                       to_device(ss, dev), src, hops, inc)
+        ids, scores = ops.frontier_run(fr, dsv, dsc, dss, src, hops, inc)
+        clock.lap("device", dev)
         ids = ids.cpu().numpy().view("uint32")
         scores = scores.cpu().numpy()
+        clock.lap("readback")
         fr.adapt()              # overflowing columns: the wide-table retry from the next call on
+        clock.lap("adapt")
         # the ranked vertices' labels by numpy indexing (no per-vertex list of the whole graph),
         # then the entity dicts natively (csrc/pyhost.c entity_rows; the loop it replaces:
         # {"id": vid[v], "labels": [labels[label of v]], "score": score, "rank": r + 1} per
@@ -177,8 +207,10 @@ class GraphService:
         lab = np.zeros(ids.shape, np.uint8)
         ok = ids != 0xFFFFFFFF
         lab[ok] = g.vertex_labels()[ids[ok]]
+        clock.lap("labels")
         out = pyhost.entity_rows(np.ascontiguousarray(ids), np.ascontiguousarray(scores, np.float32),
                                  lab, ids.shape[1] if ids.ndim == 2 else k, g._vertex_ids(), list(labels))
+        clock.lap("entity_rows")
         return out
 
     @classmethod
