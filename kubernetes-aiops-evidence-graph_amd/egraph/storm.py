@@ -38,7 +38,7 @@ The union of the owners' rankings equals the single-GPU engine's (tests/test_sto
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Callable
 
 import numpy as np
@@ -62,17 +62,29 @@ class StormCase:
     evidence: list
 
 
-@dataclass
 class OpenIncident:
-    handle: int
-    incident_id: str
-    evidence: list | None     # released once its candidates are extracted (keep_evidence=False)
-    vertex: int = -1
-    sv: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))    # seed vertices
-    ss: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))   # seed strengths
-    cand: object = None                    # its rows' attachment candidates (computed once):
-                                           # SeedCandidates, or (keyed batch, column) until sliced
-    store: "RankStore | None" = None       # the engine's rankings (rows by handle)
+    """One open incident: its handle and id, its incident vertex, its evidence rows (released
+    once its candidates are extracted unless keep_evidence) and its attachment candidates; its
+    seeds and ranking live in the engine's arrays (SeedStore, RankStore), read by handle."""
+    __slots__ = ("handle", "incident_id", "evidence", "cand", "store", "seeds", "vtx")
+
+    def __init__(self, handle: int, incident_id: str, evidence: list | None, store=None,
+                 seeds: "SeedStore | None" = None, vtx: "np.ndarray | None" = None):
+        self.handle, self.incident_id, self.evidence = handle, incident_id, evidence
+        self.cand = None           # SeedCandidates, or (keyed batch, column) until sliced
+        self.store, self.seeds, self.vtx = store, seeds, vtx
+
+    @property
+    def vertex(self) -> int:                     # incident vertex (-1: not in the graph)
+        return int(self.vtx.a[self.handle]) if self.vtx is not None else -1
+
+    @property
+    def sv(self) -> np.ndarray:                  # seed vertices
+        return self.seeds.get(self.handle)[0] if self.seeds is not None else np.zeros(0, np.uint32)
+
+    @property
+    def ss(self) -> np.ndarray:                  # seed strengths
+        return self.seeds.get(self.handle)[1] if self.seeds is not None else np.zeros(0, np.float32)
 
     # its ranking, read from the engine's arrays (a re-rank writes them in one step per launch)
     @property
@@ -86,6 +98,96 @@ class OpenIncident:
     @property
     def ranked_at(self) -> int:                  # tick of the last re-rank (-1: never)
         return self.store.row(self.handle)[2] if self.store is not None else -1
+
+
+class _Grow:
+    """A numpy array indexed by handle, grown geometrically (fill value for new slots)."""
+
+    def __init__(self, dtype, fill):
+        self.a = np.full(0, fill, dtype)
+        self.fill = fill
+
+    def ensure(self, n: int) -> None:
+        if n > len(self.a):
+            m = max(n, 2 * len(self.a), 1024)
+            self.a = np.concatenate([self.a, np.full(m - len(self.a), self.fill, self.a.dtype)])
+
+
+def ranges(start: np.ndarray, length: np.ndarray) -> np.ndarray:
+    """Concatenated index ranges [start[i], start[i] + length[i]) (int64)."""
+    length = np.asarray(length, np.int64)
+    tot = int(length.sum())
+    if not tot:
+        return np.zeros(0, np.int64)
+    ex = np.cumsum(length) - length
+    return np.repeat(np.asarray(start, np.int64) - ex, length) + np.arange(tot, dtype=np.int64)
+
+
+class SeedStore:
+    """Every incident's seed triples in two pooled arrays (vertex u32, strength f32), a slice
+    per handle: setting an incident's seeds appends a new slice (the old one becomes garbage,
+    compacted away once it dominates), and gathering many incidents' seeds is one vectorised
+    index -- no per-incident Python objects or loops."""
+
+    def __init__(self):
+        self.v = np.zeros(0, np.uint32)
+        self.s = np.zeros(0, np.float32)
+        self.n = 0                                   # used length of the pools
+        self.start = _Grow(np.int64, 0)
+        self.len = _Grow(np.int64, 0)
+        self.live = 0
+
+    def set(self, handles: np.ndarray, sv: np.ndarray, ss: np.ndarray, counts: np.ndarray) -> None:
+        """Incident handles[j] gets the next counts[j] entries of (sv, ss), in order."""
+        handles = np.asarray(handles, np.int64)
+        counts = np.asarray(counts, np.int64)
+        if not len(handles):
+            return
+        top = int(handles.max()) + 1
+        self.start.ensure(top)
+        self.len.ensure(top)
+        self.live -= int(self.len.a[handles].sum())
+        m = len(sv)
+        if self.n + m > len(self.v):
+            cap = max(self.n + m, 2 * len(self.v), 4096)
+            self.v = np.concatenate([self.v[: self.n], np.zeros(cap - self.n, np.uint32)])
+            self.s = np.concatenate([self.s[: self.n], np.zeros(cap - self.n, np.float32)])
+        self.v[self.n:self.n + m] = sv
+        self.s[self.n:self.n + m] = ss
+        self.start.a[handles] = self.n + np.cumsum(counts) - counts
+        self.len.a[handles] = counts
+        self.n += m
+        self.live += m
+        if self.n > 4096 and 2 * self.live < self.n:
+            self._compact()
+
+    def _compact(self) -> None:
+        hs = np.flatnonzero(self.len.a)
+        idx = ranges(self.start.a[hs], self.len.a[hs])
+        self.v, self.s = self.v[idx].copy(), self.s[idx].copy()
+        self.start.a[hs] = np.cumsum(self.len.a[hs]) - self.len.a[hs]
+        self.n = self.live = len(idx)
+
+    def counts(self, handles: np.ndarray) -> np.ndarray:
+        h = np.asarray(handles, np.int64)
+        out = np.zeros(len(h), np.int64)
+        ok = h < len(self.len.a)
+        out[ok] = self.len.a[h[ok]]
+        return out
+
+    def gather(self, handles: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(vertices, strengths, per-handle counts) of these incidents, in handle order."""
+        h = np.asarray(handles, np.int64)
+        cnt = self.counts(h)
+        st = np.zeros(len(h), np.int64)
+        ok = h < len(self.start.a)
+        st[ok] = self.start.a[h[ok]]
+        idx = ranges(st, cnt)
+        return self.v[idx], self.s[idx], cnt
+
+    def get(self, h: int) -> tuple[np.ndarray, np.ndarray]:
+        v, s, _ = self.gather(np.array([h], np.int64))
+        return v, s
 
 
 class RankStore:
@@ -144,6 +246,8 @@ class StormEngine:
         self._gen = np.zeros(0, np.int64)
         self._frontiers: dict[int, object] = {}
         self.ranks = RankStore(k)
+        self.seeds = SeedStore()                  # every incident's seed triples, by handle
+        self.vtx = _Grow(np.int64, -1)           # every incident's vertex, by handle
         self.ticks = 0
         self.last_reseed: dict = {}
         # (vertex, incident) pairs the affected test reads: incident vertices and seed vertices
@@ -189,12 +293,11 @@ class StormEngine:
         blob, off, hashes = cand.keys
         found = self.g.lookup_blob(blob, off) if cand.n_flat else np.zeros(0, np.int64)
         sv, col, ss, before, bcol = cand.attach_found_idx(found)
+        hs = np.asarray(handles, np.int64)
         cut = np.searchsorted(col, np.arange(len(xs) + 1, dtype=np.uint32))
-        for j, x in enumerate(xs):
-            x.sv, x.ss = sv[cut[j]:cut[j + 1]], ss[cut[j]:cut[j + 1]]
+        self.seeds.set(hs, sv, ss, np.diff(cut))          # (rows come in column order)
         t2 = time.perf_counter()
         # the incidents' pending ids: their earlier entries retire (generation bump)
-        hs = np.array([x.handle for x in xs], np.int64)
         top = int(hs.max()) + 1
         if top > len(self._gen):
             self._gen = np.concatenate([self._gen, np.zeros(max(top - len(self._gen), 1024), np.int64)])
@@ -240,11 +343,14 @@ class StormEngine:
         o = o[self._pend_g[ix] == self._gen[o]]
         return set(np.unique(o).tolist())
 
-    def _check_parts(self, xs: list[OpenIncident]) -> tuple[torch.Tensor, torch.Tensor]:
-        v = np.concatenate([np.array([max(x.vertex, 0) for x in xs], np.int64)] +
-                           [x.sv.astype(np.int64) for x in xs])
-        o = np.concatenate([np.array([x.handle for x in xs], np.int64)] +
-                           [np.full(len(x.sv), x.handle, np.int64) for x in xs])
+    def _check_parts(self, handles) -> tuple[torch.Tensor, torch.Tensor]:
+        """(vertex, incident) pairs of these incidents: each incident vertex, then every seed
+        vertex (SeedStore order)."""
+        hs = np.asarray(handles, np.int64)
+        self.vtx.ensure(int(hs.max()) + 1 if len(hs) else 0)
+        sv, _, cnt = self.seeds.gather(hs)
+        v = np.concatenate([np.maximum(self.vtx.a[hs], 0), sv.astype(np.int64)])
+        o = np.concatenate([hs, np.repeat(hs, cnt)])
         return to_device(v, self.dev), to_device(o, self.dev)
 
     def owns(self, handle: int) -> bool:
@@ -252,11 +358,11 @@ class StormEngine:
 
     def _rebuild_check(self) -> None:
         self._chk_v, self._chk_o = self._check_parts(
-            [x for x in self.incidents if self.owns(x.handle)])
+            np.arange(self.rank, len(self.incidents), self.world, dtype=np.int64))
 
     def _append_check(self, handles: list[int]) -> None:
         if handles:
-            v, o = self._check_parts([self.incidents[h] for h in handles])
+            v, o = self._check_parts(handles)
             self._chk_v = torch.cat([self._chk_v, v])
             self._chk_o = torch.cat([self._chk_o, o])
 
@@ -264,22 +370,23 @@ class StormEngine:
         """Re-rank these incidents from their cached seeds (one frontier launch per 4096)."""
         inc_label = self.g.labels().index("Incident") if "Incident" in self.g.labels() else -1
         top = self.COL_BUCKETS[-1]
-        for lo in range(0, len(handles), top):
-            part = [self.incidents[h] for h in handles[lo:lo + top]]
-            sv = np.concatenate([x.sv for x in part]) if part else np.zeros(0, np.uint32)
-            ss = np.concatenate([x.ss for x in part]) if part else np.zeros(0, np.float32)
-            sc = np.repeat(np.arange(len(part), dtype=np.uint32), [len(x.sv) for x in part])
-            fr = self._frontier(len(part), len(sv))
+        hs_all = np.asarray(handles, np.int64)
+        for lo in range(0, len(hs_all), top):
+            hs = hs_all[lo:lo + top]
+            n = len(hs)
+            sv, ss, cnt = self.seeds.gather(hs)
+            sc = np.repeat(np.arange(n, dtype=np.uint32), cnt)
+            fr = self._frontier(n, len(sv))
             src = np.full(fr.B, NO_NODE, np.uint32)
-            src[: len(part)] = [x.vertex if x.vertex >= 0 else NO_NODE for x in part]
+            vx = self.vtx.a[hs]
+            src[:n] = np.where(vx >= 0, vx, NO_NODE).astype(np.uint32)
             fr.set_seeds(to_device(sv, self.dev), to_device(sc, self.dev), to_device(ss, self.dev))
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
             fr.adapt()              # overflowing columns: the wide-table retry from the next call on
             # the launch's rows into the engine's arrays, one step for all of them
-            n = len(part)
-            self.ranks.put(np.asarray(handles[lo:lo + n], np.int64), ids[:n], scores[:n], self.ticks)
+            self.ranks.put(hs, ids[:n], scores[:n], self.ticks)
 
     def tick(self, keys: list[str], now_ms: int, make_case: Callable[[int, int], StormCase],
              topology: tuple | None = None, seq=None) -> dict:
@@ -315,7 +422,7 @@ class StormEngine:
             assert h == len(self.incidents), "incident handles are dense and ordered"
             self.incidents.append(OpenIncident(h, case.incident_id, case.evidence
                                                if self.keep_evidence or self.owns(h) else None,
-                                               store=self.ranks))
+                                               store=self.ranks, seeds=self.seeds, vtx=self.vtx))
             new_handles.append(h)
             if case.entities:                      # (column-wise, in C: zip(*) per case)
                 a, b = zip(*case.entities)
@@ -342,8 +449,8 @@ class StormEngine:
             self.g.merge_edges(es, ed, et)
         if new_handles:
             vs = self.g.lookup([f"incident:{self.incidents[h].incident_id}" for h in new_handles])
-            for h, v in zip(new_handles, vs):
-                self.incidents[h].vertex = int(v)
+            self.vtx.ensure(new_handles[-1] + 1)
+            self.vtx.a[np.asarray(new_handles, np.int64)] = vs
         t.append(time.perf_counter())
         n_v, n_e = self.snap.sync(self.g)                                 # GPU CSR update
         t.append(time.perf_counter())
@@ -371,7 +478,8 @@ class StormEngine:
         # re-attached incidents: append their new seed vertices; the old entries stay (a
         # superset only re-ranks more) until they make up half the arrays
         self._append_check(sorted(set(new_handles) | reseed))
-        self._stale += sum(len(self.incidents[h].sv) + 1 for h in reseed)
+        if reseed:
+            self._stale += int(self.seeds.counts(np.fromiter(reseed, np.int64, len(reseed))).sum()) + len(reseed)
         if self._stale * 2 > self._chk_v.numel():
             self._rebuild_check()
             self._stale = 0

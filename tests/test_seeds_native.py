@@ -453,3 +453,35 @@ def test_storm_rank_store_rows():
     got = x.top_ids
     got[0] = 99                                   # a copy: the store is not written through
     assert st.row(7)[0][0] == ids[1][0]
+
+
+def test_storm_seed_store():
+    """StormEngine's SeedStore (host logic): per-handle slices of pooled arrays; a reset of an
+    incident's seeds replaces its slice, gathers follow the requested handle order, unknown and
+    empty handles gather nothing, and compaction keeps every live slice."""
+    import numpy as np
+    from egraph.storm import OpenIncident, SeedStore, ranges
+    assert ranges(np.array([5, 0, 9]), np.array([2, 0, 3])).tolist() == [5, 6, 9, 10, 11]
+    st = SeedStore()
+    rng = np.random.default_rng(3)
+    want = {}
+    for it in range(300):
+        hs = rng.choice(200, size=int(rng.integers(1, 20)), replace=False)
+        cnt = rng.integers(0, 40, len(hs))
+        sv = rng.integers(0, 1 << 20, int(cnt.sum())).astype(np.uint32)
+        ss = rng.random(int(cnt.sum())).astype(np.float32)
+        st.set(hs, sv, ss, cnt)
+        o = 0
+        for h, c in zip(hs.tolist(), cnt.tolist()):
+            want[h] = (sv[o:o + c].copy(), ss[o:o + c].copy())
+            o += c
+        if it % 50 == 49:
+            q = np.array(sorted(want, key=lambda _: rng.random()) + [5000], np.int64)
+            v, s, c = st.gather(q)
+            assert c[-1] == 0
+            assert v.tolist() == [x for h in q[:-1].tolist() for x in want[h][0].tolist()]
+            assert s.tobytes() == b"".join(want[h][1].tobytes() for h in q[:-1].tolist())
+    assert st.n <= 2 * st.live + 4096                 # garbage was compacted
+    x = OpenIncident(int(next(iter(want))), "i", None, seeds=st)
+    assert x.sv.tolist() == want[x.handle][0].tolist()
+    assert OpenIncident(7, "j", None).sv.size == 0 and OpenIncident(7, "j", None).vertex == -1
