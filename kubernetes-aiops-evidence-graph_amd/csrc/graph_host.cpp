@@ -16,54 +16,82 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
-#include <unordered_set>
 #include <vector>
 
 #include "egr_internal.h"
 
 struct egr_graph {
   std::vector<std::string> labels, rtypes;
-  std::unordered_map<std::string, int> label_idx, rtype_idx;
   std::vector<std::string> vid;          // vertex id strings, creation order
   std::vector<uint8_t> vlabel;
-  std::unordered_map<std::string, std::vector<int32_t>> by_id;  // id -> vertices, creation order
-  // id -> first vertex, open addressing over the id bytes (egr_graph_find): a lookup hashes the
-  // caller's bytes in place (no std::string per query) and compares them with vid[v].  Read-only
-  // between merges, so concurrent finds are safe while no merge runs.
+  // id -> first vertex, open addressing over the id bytes: a lookup hashes the caller's bytes in
+  // place (no std::string per query) and compares them with vid[v].  Read-only between merges,
+  // so concurrent finds (egr_graph_find) are safe while no merge runs.
   struct IdSlot {
     uint32_t tag;   // high hash bits | 1 (0 = empty)
     int32_t v;
   };
   std::vector<IdSlot> idx;
   size_t idx_n = 0;
+  // An id carried by several vertices (one per label: MERGE keys a vertex by (label, id)) keeps
+  // its vertices, creation order, under its first vertex; vmulti[first] marks such ids.  Every
+  // other id has exactly the one vertex idx names.
+  std::unordered_map<int32_t, std::vector<int32_t>> multi;
+  std::vector<uint8_t> vmulti;
   std::vector<int32_t> esrc, edst;
   std::vector<uint8_t> etype;
-  struct EdgeKey {
-    int32_t s, d;
-    uint8_t t;
-    bool operator==(const EdgeKey& o) const { return s == o.s && d == o.d && t == o.t; }
+  // the (source, type, target) edge set, open addressing (load <= 1/2; t = -1: empty slot)
+  struct ESlot {
+    int32_t s, d, t;
   };
-  struct EdgeHash {
-    size_t operator()(const EdgeKey& k) const {
-      uint64_t h = (uint64_t)(uint32_t)k.s * 0x9E3779B97F4A7C15ull;
-      h ^= ((uint64_t)(uint32_t)k.d << 8 | k.t) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
-      return (size_t)h;
-    }
-  };
-  std::unordered_set<EdgeKey, EdgeHash> edges;
+  std::vector<ESlot> eset;
+  size_t eset_n = 0;
 };
 
 namespace {
 
-int intern(std::vector<std::string>& names, std::unordered_map<std::string, int>& idx,
-           std::string_view s, size_t max_names, const char* what) {
-  auto it = idx.find(std::string(s));
-  if (it != idx.end()) return it->second;
+// Index of name s in names, appended if absent.  Label and relationship-type tables are tiny
+// (at most 255 / 127 names), so a scan beats hashing a std::string built per call.
+int intern(std::vector<std::string>& names, std::string_view s, size_t max_names, const char* what) {
+  for (size_t i = 0; i < names.size(); ++i)
+    if (names[i].size() == s.size() && memcmp(names[i].data(), s.data(), s.size()) == 0) return (int)i;
   if (names.size() >= max_names) return egr::fail(EGR_EINVAL, std::string("too many distinct ") + what);
-  int i = (int)names.size();
   names.emplace_back(s);
-  idx.emplace(names.back(), i);
-  return i;
+  return (int)names.size() - 1;
+}
+
+inline uint64_t edge_hash(int32_t s, int32_t d, int32_t t) {
+  uint64_t h = ((uint64_t)(uint32_t)s << 32 | (uint32_t)d) * 0x9E3779B97F4A7C15ull;
+  h ^= (uint64_t)(uint32_t)t * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 31;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
+}
+
+// true if (s, d, t) was not in the edge set (and is now)
+bool eset_insert(egr_graph* g, int32_t s, int32_t d, int32_t t) {
+  if (2 * (g->eset_n + 1) > g->eset.size()) {         // grow to keep the load at most 1/2
+    std::vector<egr_graph::ESlot> old;
+    old.swap(g->eset);
+    g->eset.assign(std::max<size_t>(4096, 2 * old.size()), egr_graph::ESlot{0, 0, -1});
+    const size_t m = g->eset.size() - 1;
+    for (const auto& e : old) {
+      if (e.t < 0) continue;
+      size_t i = (size_t)edge_hash(e.s, e.d, e.t) & m;
+      while (g->eset[i].t >= 0) i = (i + 1) & m;
+      g->eset[i] = e;
+    }
+  }
+  const size_t m = g->eset.size() - 1;
+  for (size_t i = (size_t)edge_hash(s, d, t) & m;; i = (i + 1) & m) {
+    egr_graph::ESlot& e = g->eset[i];
+    if (e.t < 0) {
+      e = egr_graph::ESlot{s, d, t};
+      ++g->eset_n;
+      return true;
+    }
+    if (e.s == s && e.d == d && e.t == t) return false;
+  }
 }
 
 // 64-bit hash of an id's bytes, 8 at a time (a multiply-xorshift mix per word)
@@ -124,6 +152,28 @@ inline int32_t idx_find(const egr_graph* g, const char* p, size_t n) {
   }
 }
 
+// The vertices carrying an id (creation order): none, its one vertex, or its multi list.
+struct IdVerts {
+  const int32_t* p;
+  size_t n;
+  int32_t one;
+};
+
+inline IdVerts id_vertices(const egr_graph* g, const char* p, size_t n) {
+  IdVerts r{nullptr, 0, -1};
+  const int32_t v = idx_find(g, p, n);
+  if (v < 0) return r;
+  if (g->vmulti[v]) {
+    const auto& vs = g->multi.at(v);
+    r.p = vs.data();
+    r.n = vs.size();
+  } else {
+    r.one = v;
+    r.n = 1;
+  }
+  return r;
+}
+
 inline std::string_view str_at(const char* blob, const int64_t* off, int64_t i) {
   return std::string_view(blob + off[i], (size_t)(off[i + 1] - off[i]));
 }
@@ -156,19 +206,33 @@ int egr_graph_merge_nodes(egr_graph* g, const char* id_blob, const int64_t* id_o
     return egr::fail(EGR_EINVAL, "egr_graph_merge_nodes: bad arguments");
   for (int64_t i = 0; i < n; ++i) {
     std::string_view id = str_at(id_blob, id_off, i);
-    int lab = intern(g->labels, g->label_idx, str_at(label_blob, label_off, i), 255, "labels");
+    int lab = intern(g->labels, str_at(label_blob, label_off, i), 255, "labels");
     if (lab < 0) return lab;
-    auto& vs = g->by_id[std::string(id)];
+    const int32_t first = idx_find(g, id.data(), id.size());
     int32_t v = -1;
-    for (int32_t c : vs)
-      if (g->vlabel[c] == lab) { v = c; break; }
+    if (first >= 0) {
+      if (g->vmulti[first]) {
+        for (int32_t c : g->multi.at(first))
+          if (g->vlabel[c] == lab) { v = c; break; }
+      } else if (g->vlabel[first] == lab) {
+        v = first;
+      }
+    }
     if (v < 0) {
       if (g->vid.size() >= 0x7FFFFFF0u) return egr::fail(EGR_EINVAL, "too many vertices");
       v = (int32_t)g->vid.size();
       g->vid.emplace_back(id);
       g->vlabel.push_back((uint8_t)lab);
-      if (vs.empty()) idx_put(g, g->vid.back(), v);   // the id's first vertex
-      vs.push_back(v);
+      g->vmulti.push_back(0);
+      if (first < 0) {
+        idx_put(g, g->vid.back(), v);                 // the id's first vertex
+      } else {                                        // another label of an existing id
+        if (!g->vmulti[first]) {
+          g->multi[first] = {first};
+          g->vmulti[first] = 1;
+        }
+        g->multi[first].push_back(v);
+      }
     }
     if (out_vertex) out_vertex[i] = v;
   }
@@ -181,21 +245,19 @@ int egr_graph_merge_edges(egr_graph* g, const char* src_blob, const int64_t* src
   if (!g || n < 0 || (n > 0 && (!src_blob || !src_off || !dst_blob || !dst_off || !type_blob || !type_off)))
     return egr::fail(EGR_EINVAL, "egr_graph_merge_edges: bad arguments");
   int64_t created = 0;
-  std::string key;
   for (int64_t i = 0; i < n; ++i) {
-    key.assign(str_at(src_blob, src_off, i));
-    auto si = g->by_id.find(key);
-    if (si == g->by_id.end() || si->second.empty()) continue;
-    key.assign(str_at(dst_blob, dst_off, i));
-    auto di = g->by_id.find(key);
-    if (di == g->by_id.end() || di->second.empty()) continue;
-    int t = intern(g->rtypes, g->rtype_idx, str_at(type_blob, type_off, i), 127,
-                   "relationship types");
+    const std::string_view sid = str_at(src_blob, src_off, i);
+    const IdVerts sv = id_vertices(g, sid.data(), sid.size());
+    if (!sv.n) continue;
+    const std::string_view did = str_at(dst_blob, dst_off, i);
+    const IdVerts dv = id_vertices(g, did.data(), did.size());
+    if (!dv.n) continue;
+    int t = intern(g->rtypes, str_at(type_blob, type_off, i), 127, "relationship types");
     if (t < 0) return t;
-    for (int32_t s : si->second)
-      for (int32_t d : di->second) {
-        egr_graph::EdgeKey k{s, d, (uint8_t)t};
-        if (g->edges.insert(k).second) {
+    for (size_t a = 0; a < sv.n; ++a)
+      for (size_t b = 0; b < dv.n; ++b) {
+        const int32_t s = sv.p ? sv.p[a] : sv.one, d = dv.p ? dv.p[b] : dv.one;
+        if (eset_insert(g, s, d, t)) {
           g->esrc.push_back(s);
           g->edst.push_back(d);
           g->etype.push_back((uint8_t)t);
@@ -215,7 +277,7 @@ int egr_graph_add_edges_indexed(egr_graph* g, const int32_t* src, const int32_t*
     return egr::fail(EGR_EINVAL, "egr_graph_add_edges_indexed: bad arguments");
   std::vector<int> tmap((size_t)n_types);
   for (int32_t i = 0; i < n_types; ++i) {
-    tmap[i] = intern(g->rtypes, g->rtype_idx, str_at(type_blob, type_off, i), 127, "relationship types");
+    tmap[i] = intern(g->rtypes, str_at(type_blob, type_off, i), 127, "relationship types");
     if (tmap[i] < 0) return tmap[i];
   }
   const int64_t V = (int64_t)g->vid.size();
@@ -223,11 +285,11 @@ int egr_graph_add_edges_indexed(egr_graph* g, const int32_t* src, const int32_t*
   for (int64_t i = 0; i < n; ++i) {
     if (src[i] < 0 || src[i] >= V || dst[i] < 0 || dst[i] >= V || type_idx[i] < 0 || type_idx[i] >= n_types)
       return egr::fail(EGR_EINVAL, "egr_graph_add_edges_indexed: vertex or type index out of range");
-    egr_graph::EdgeKey k{src[i], dst[i], (uint8_t)tmap[type_idx[i]]};
-    if (g->edges.insert(k).second) {
-      g->esrc.push_back(k.s);
-      g->edst.push_back(k.d);
-      g->etype.push_back(k.t);
+    const int32_t t = tmap[type_idx[i]];
+    if (eset_insert(g, src[i], dst[i], t)) {
+      g->esrc.push_back(src[i]);
+      g->edst.push_back(dst[i]);
+      g->etype.push_back((uint8_t)t);
       ++created;
     }
   }

@@ -2458,6 +2458,45 @@ done:
   return out;
 }
 
+/* str_blob(list of str) -> (UTF-8 blob bytes, int64 offsets [n+1] as bytes), or None when the
+ * argument is not an exact list of exact strs (egraph/graph.py str_blob then builds it in
+ * Python).  The C-ABI's string arrays for MERGE batches and lookups: one pass for the lengths,
+ * one memcpy per id, no per-id bytes object. */
+static PyObject* str_blob(PyObject* self, PyObject* arg) {
+  if (!PyList_CheckExact(arg)) Py_RETURN_NONE;
+  const Py_ssize_t n = PyList_GET_SIZE(arg);
+  int64_t* off = PyMem_Malloc(sizeof(int64_t) * (size_t)(n + 1));
+  if (!off) return PyErr_NoMemory();
+  PyObject* out = NULL;
+  off[0] = 0;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* x = PyList_GET_ITEM(arg, i);
+    Py_ssize_t len;
+    if (!PyUnicode_CheckExact(x) || !PyUnicode_AsUTF8AndSize(x, &len)) {
+      PyErr_Clear();
+      PyMem_Free(off);
+      Py_RETURN_NONE;
+    }
+    off[i + 1] = off[i] + (int64_t)len;
+  }
+  PyObject* blob = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)off[n]);
+  if (!blob) goto done;
+  char* dst = PyBytes_AS_STRING(blob);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    Py_ssize_t len;
+    const char* u = PyUnicode_AsUTF8AndSize(PyList_GET_ITEM(arg, i), &len);  /* cached: no alloc */
+    memcpy(dst + off[i], u, (size_t)len);
+  }
+  PyObject* ob = PyBytes_FromStringAndSize((const char*)off, (n + 1) * (Py_ssize_t)sizeof(int64_t));
+  if (!ob) { Py_DECREF(blob); goto done; }
+  out = PyTuple_Pack(2, blob, ob);
+  Py_DECREF(blob);
+  Py_DECREF(ob);
+done:
+  PyMem_Free(off);
+  return out;
+}
+
 /* ---- ranked root-cause entities (src/database/graph.py GraphService._rank_locked) ----------
  * entity_rows(ids u32 [B*k], scores f32 [B*k], labels u8 [B*k], k, vertex_ids list, label_names
  * list) -> B lists of {"id": vertex_ids[v], "labels": [label_names[label]], "score": float,
@@ -2541,6 +2580,7 @@ static PyMethodDef methods[] = {
     {"entity_rows", entity_rows, METH_VARARGS, "frontier top-k -> ranked root-cause entity dicts"},
     {"seed_keys", seed_keys, METH_VARARGS, "evidence rows -> seed candidates as a keyed blob"},
     {"hash_ids", hash_ids, METH_O, "64-bit hashes of ids' UTF-8 bytes"},
+    {"str_blob", str_blob, METH_O, "list of str -> (UTF-8 blob, int64 offsets)"},
     {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
     {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},

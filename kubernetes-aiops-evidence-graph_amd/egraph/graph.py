@@ -37,7 +37,12 @@ DEFAULT_OTHER_WEIGHT = (0.5, 0.5)
 
 
 def str_blob(strs: Sequence[str]) -> tuple[bytes, np.ndarray]:
-    """UTF-8 blob + int64 offsets [n+1] for the C-ABI string arrays."""
+    """UTF-8 blob + int64 offsets [n+1] for the C-ABI string arrays (native for a list of strs:
+    csrc/pyhost.c str_blob)."""
+    if type(strs) is list:
+        r = L.pyhost.str_blob(strs)
+        if r is not None:
+            return r[0], np.frombuffer(r[1], np.int64)
     if isinstance(strs, list) and strs and all(type(s) is str for s in strs):
         joined = "".join(strs)
         if joined.isascii():                  # one encode; byte lengths = character lengths

@@ -160,3 +160,20 @@ def test_entity_rows_match_python_assembly():
         _lib.pyhost.entity_rows(ids, scores[:-1], lab, k, vids, names)
     with pytest.raises(IndexError):
         _lib.pyhost.entity_rows(ids, scores, lab, k, vids[:10], names)
+
+
+def test_str_blob_native_matches_python():
+    """egraph.graph.str_blob's native path (csrc/pyhost.c str_blob) gives the Python path's blob
+    and offsets, UTF-8 included; non-str items and non-lists fall back to Python."""
+    from egraph import _lib as L
+    from egraph.graph import str_blob
+    for strs in (["pod:ns:a", "node:n1", "", "café:é", "x" * 300], [], ["only"]):
+        r = L.pyhost.str_blob(strs)
+        enc = [s.encode() for s in strs]
+        assert r[0] == b"".join(enc)
+        assert np.frombuffer(r[1], np.int64).tolist() == np.concatenate([[0], np.cumsum([len(b) for b in enc])]).astype(np.int64).tolist()
+        b, o = str_blob(strs)
+        assert b == r[0] and o.tolist() == np.frombuffer(r[1], np.int64).tolist()
+    assert L.pyhost.str_blob(["a", 3]) is None and L.pyhost.str_blob(("a",)) is None
+    b, o = str_blob(("a", "bc"))
+    assert b == b"abc" and o.tolist() == [0, 1, 3]
