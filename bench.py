@@ -178,6 +178,19 @@ def make_world(config: str, B: int, n_sets: int, seed0: int = 1000, cfg=None):
         synth.add_incidents(cl, cases)
         sets.append(cases)
     g = synth.build_graph(cl)                 # C4: with its dense telemetry links (~10M entries)
+    if os.environ.get("EGRAPH_BENCH_HUB_ORDER"):
+        # (experiment: the same graph MERGEd in egraph.graph.locality_order's vertex order)
+        from egraph.graph import EvidenceGraph, locality_order
+        csr = g.csr()
+        o = locality_order(csr["row_ptr"], csr["col"])
+        ids, labels = g.vertex_ids(), g.labels()
+        vl, es, ed, et = g.export()
+        g2 = EvidenceGraph()
+        g2.merge_nodes([ids[v] for v in o], [labels[vl[v]] for v in o])
+        pos = np.empty(len(o), np.int64)
+        pos[o] = np.arange(len(o))
+        g2.add_edges_indexed(pos[es], pos[ed], et.astype(np.int32), g.rel_types())
+        g = g2
     out = []
     for cases in sets:
         evidence = [x.evidence for x in cases]

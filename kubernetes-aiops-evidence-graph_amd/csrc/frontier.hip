@@ -115,12 +115,6 @@ struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr
 // column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
 // one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
 // 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
-// Probe scheme (A/B switch while it is measured): 1 reads a key's filter word and its first
-// bucket in one LDS round trip, 0 reads the filter first and the bucket after it.
-#ifndef EGR_FR_SPECPROBE
-#define EGR_FR_SPECPROBE 0
-#endif
-
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144

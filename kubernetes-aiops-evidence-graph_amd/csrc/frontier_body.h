@@ -138,26 +138,13 @@ __device__ __forceinline__ int tab_insert(const Tab<GT>& t, uint32_t v) {
 // slot of v or -1 (only called while no insertion is in flight)
 template <bool GT>
 __device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
-  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
-  uint32_t bk = hbucket(v, nb);
-  uint32_t n0 = 0;
   if constexpr (!GT) {
     const uint32_t h = bloom_hash(v);
-#if EGR_FR_SPECPROBE
-    // the filter word and the first bucket in one LDS round trip (a present key -- most
-    // probed neighbours -- then needs no second one)
-    const uint32_t bw = t.bloom[h >> 5];
-    const uint4 k0 = t.bucket(bk);
-    if (!((bw >> (h & 31u)) & 1u)) return -1;
-    const int r0 = bucket_match(k0, v, bk);
-    if (r0 != -2) return r0;
-    bk = bk + 1 == nb ? 0 : bk + 1;
-    n0 = 1;
-#else
     if (!((t.bloom[h >> 5] >> (h & 31u)) & 1u)) return -1;
-#endif
   }
-  for (uint32_t n = n0; n < nb; ++n) {
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
+  uint32_t bk = hbucket(v, nb);
+  for (uint32_t n = 0; n < nb; ++n) {
     const int r = bucket_match(t.bucket(bk), v, bk);
     if (r != -2) return r;
     bk = bk + 1 == nb ? 0 : bk + 1;
@@ -205,45 +192,17 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
     q[x] = -1;
     if ((uint32_t)x < nq) pend |= 1u << x;
   }
-  uint32_t n0 = 0;
   if constexpr (!GT) {
     // the filter: a key whose bit is clear is not a member
     uint32_t bw[NQ];
-#if EGR_FR_SPECPROBE
-    // filter words and first buckets read together: one LDS round trip resolves a present key
-    // in its first bucket (the common case) instead of two
-    uint4 k0[NQ];
-#pragma unroll
-    for (int x = 0; x < NQ; ++x) {
-      bw[x] = (pend & (1u << x)) ? t.bloom[bloom_hash(key[x]) >> 5] : ~0u;
-      if (pend & (1u << x)) k0[x] = t.bucket(bk[x]);
-    }
-#pragma unroll
-    for (int x = 0; x < NQ; ++x) {
-      if (!(pend & (1u << x))) continue;
-      if (!((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u)) {
-        pend &= ~(1u << x);
-        continue;
-      }
-      const int r = bucket_match(k0[x], key[x], bk[x]);
-      if (r != -2) {
-        q[x] = r;
-        pend &= ~(1u << x);
-      } else {
-        bk[x] = bk[x] + 1 == nb ? 0 : bk[x] + 1;
-      }
-    }
-    n0 = 1;
-#else
 #pragma unroll
     for (int x = 0; x < NQ; ++x)
       bw[x] = (pend & (1u << x)) ? t.bloom[bloom_hash(key[x]) >> 5] : ~0u;
 #pragma unroll
     for (int x = 0; x < NQ; ++x)
       if (!((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u)) pend &= ~(1u << x);
-#endif
   }
-  for (uint32_t n = n0; n < nb && __any(pend != 0); ++n) {
+  for (uint32_t n = 0; n < nb && __any(pend != 0); ++n) {
     uint4 kk[NQ];
 #pragma unroll
     for (int x = 0; x < NQ; ++x)

@@ -66,6 +66,45 @@ def _field(x, name, default=KeyError):
     return getattr(x, name) if default is KeyError else getattr(x, name, default)
 
 
+def locality_order(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """A vertex order that keeps the rows a 3-hop frontier walks close together: every vertex
+    hangs under its highest-degree neighbour when that one has a higher degree (ties: the lower
+    id), and the resulting forest is laid out root by root, each root followed by its subtrees
+    (children by id).  On a Kubernetes evidence graph the roots are the Node hubs, deployments and
+    services, a Node's pods follow it and each pod's attachments follow the pod -- the pods a
+    Node hub expands to (most of a frontier's last-hop rows) become contiguous.  Returns the new
+    order as a list of old vertex ids (order[i] = the vertex placed at i)."""
+    rp = np.asarray(row_ptr, np.int64)
+    col = np.asarray(col, np.int64)
+    V = len(rp) - 1
+    deg = np.diff(rp)
+    parent = np.full(V, -1, np.int64)
+    if len(col):
+        src = np.repeat(np.arange(V), deg)
+        o = np.lexsort((col, -deg[col], src))          # per row: highest degree, then lowest id
+        first = np.ones(len(o), bool)
+        first[1:] = src[o][1:] != src[o][:-1]
+        sel = o[first]
+        best = np.full(V, -1, np.int64)
+        best[src[sel]] = col[sel]
+        ok = best >= 0
+        parent[ok] = np.where(deg[best[ok]] > deg[ok], best[ok], -1)
+    # depth and root of every vertex (degrees strictly grow towards a root: no cycles)
+    root = np.arange(V)
+    top = np.arange(V)          # the vertex right under the root (itself for roots / children)
+    depth = np.zeros(V, np.int64)
+    cur = parent.copy()
+    while True:
+        m = cur >= 0
+        if not m.any():
+            break
+        top = np.where(m & (parent[np.maximum(cur, 0)] >= 0), cur, top)
+        root = np.where(m, cur, root)
+        depth += m
+        cur = np.where(m, parent[np.maximum(cur, 0)], -1)
+    return np.lexsort((np.arange(V), depth, top, root))
+
+
 class EvidenceGraph:
     """The evidence graph with the reference's MERGE semantics (host side, C++)."""
 
