@@ -427,6 +427,14 @@ int egr_snapshot_update(egr_snapshot* s, const uint8_t* new_vlabel, int64_t n_ne
 int egr_snapshot_download(const egr_snapshot* s, uint32_t* row_ptr, uint32_t* col, uint8_t* meta,
                           float* val, uint8_t* vlabel);
 int64_t egr_snapshot_version(const egr_snapshot* s);
+/* The frontier engine's locality order of a CSR (host only; csrc/layout.hip):
+ * out_order[i] = the vertex the snapshot's frontier layout places at internal position i.  Every
+ * snapshot lays its frontier arrays out in this order at creation ($EGRAPH_FRONTIER_LAYOUT=0:
+ * off); the frontier's inputs and outputs stay in original ids, and every result is unchanged
+ * (rows keep their entry order).  No reference counterpart: a storage layout of the graph the
+ * Cypher reads of neo4j.py:169-202 run against. */
+int egr_locality_order(const uint32_t* row_ptr, const uint32_t* col, int64_t n_vertices,
+                       uint32_t* out_order);
 /* multi-source BFS: out_dist[v] (device, V bytes) = undirected hops from the nearest of the n
  * source vertices (device u32; ids >= V ignored), 0xFF beyond `hops`.  The alert storm marks
  * the incidents an update can affect with it. */

@@ -61,6 +61,10 @@ struct FArgs {
   const uint32_t* row_ptr;
   const uint2* cv;             // (col, val bits) per CSR entry
   const uint8_t* vlabel;
+  // the snapshot's locality layout (layout.hip): row_ptr / cv / vlabel are in its internal ids;
+  // inputs are mapped in through perm, outputs and tie-breaks use iperm (nullptr: identity)
+  const uint32_t* perm;
+  const uint32_t* iperm;
   uint32_t V;
   int B, hops, k, exclude;
   int prune;                   // no member pool: the last hop pulls the candidates only
@@ -582,9 +586,12 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     EGR_CHECK_LAUNCH();
   }
   FArgs a{};
-  a.row_ptr = s->row_ptr;
-  a.cv = s->cv;
-  a.vlabel = s->vlabel;
+  const FrLayoutView lay = layout_view(s);
+  a.row_ptr = lay.row_ptr;
+  a.cv = lay.cv;
+  a.vlabel = lay.vlabel;
+  a.perm = lay.perm;
+  a.iperm = lay.iperm;
   a.V = (uint32_t)s->V;
   a.B = f->B;
   a.hops = hops;

@@ -569,7 +569,8 @@ __device__ __forceinline__ uint64_t cand_key(const FArgs& A, const Tab<GT>& t, u
   const uint32_t v = t.key(p);
   if (v >= A.V) return 0;
   if (A.exclude >= 0 && (t.need[p] & NEED_EXCL)) return 0;   // marked after the last pull
-  return topk_key(t.sc(p), v);
+  // (ties break by the ORIGINAL vertex id, which the key also carries out to the caller)
+  return topk_key(t.sc(p), A.iperm ? A.iperm[v] : v);
 }
 
 // This thread's best candidate key strictly below `bound` (global variant: rescans).
@@ -742,7 +743,7 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
   if (keep) {
     for (uint32_t i = tid; i < n; i += FT) {
       const uint32_t p = t.mlist[i];
-      A.pool_v[base + i] = t.key(p);
+      A.pool_v[base + i] = A.iperm ? A.iperm[t.key(p)] : t.key(p);
       A.pool_s[base + i] = t.sc(p);
       A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
     }
@@ -781,7 +782,9 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   stamp();
   // The incident vertex and its row (reach level 1) are loaded first: their latency hides
   // behind the seed passes.
-  const uint32_t src = A.sources[b];
+  // inputs name original vertex ids: mapped to the layout's (perm; identity without a layout)
+  auto inmap = [&](uint32_t v) { return (A.perm && v < A.V) ? A.perm[v] : v; };
+  const uint32_t src = inmap(A.sources[b]);
   const bool src_ok = A.hops >= 1 && src < A.V;
   const uint32_t ie0 = src_ok ? A.row_ptr[src] : 0u, ie1 = src_ok ? A.row_ptr[src + 1] : 0u;
   const uint32_t ic0 = ie0 + tid < ie1 ? A.cv[ie0 + tid].x : 0u;   // first stripe of the row
@@ -801,10 +804,10 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
   };
   const uint32_t i0 = sb + tid;
-  const uint32_t v0 = i0 < se ? A.seed_vert[i0] : 0u;   // the first stripe stays in registers
+  const uint32_t v0 = i0 < se ? inmap(A.seed_vert[i0]) : 0u;   // the first stripe stays in registers
   const float x0 = i0 < se ? A.seed_val[i0] : 0.f;
   for (uint32_t i = i0; i < se; i += FT) {
-    const uint32_t v = i == i0 ? v0 : A.seed_vert[i];
+    const uint32_t v = i == i0 ? v0 : inmap(A.seed_vert[i]);
     const float x = i == i0 ? x0 : A.seed_val[i];
     if (v >= A.V) continue;          // (grouped seeds: out-of-range vertices are dropped)
     const int q = tab_insert<GT>(t, v);
@@ -816,7 +819,7 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   }
   __syncthreads();
   for (uint32_t i = i0; i < se; i += FT) {
-    const int q = tab_find<GT>(t, i == i0 ? v0 : A.seed_vert[i]);
+    const int q = tab_find<GT>(t, i == i0 ? v0 : inmap(A.seed_vert[i]));
     uint2 r = make_uint2(NO_NODE, 0u);
     if (q >= 0) {
       const uint32_t sh8 = ((uint32_t)q & 3u) * 8u;

@@ -25,10 +25,32 @@ struct egr_snapshot {
   int64_t cap_v = 0, cap_e = 0;
   uint64_t version = 0;
   struct SnapUpdate* upd = nullptr;
+  // The frontier engine's locality layout (layout.hip; nullptr when off): the same CSR with its
+  // vertices renumbered so that the rows a 3-hop frontier walks sit close together.  Rows keep
+  // their entries in the canonical order (so every fmaf chain is unchanged); `perm` maps an
+  // original vertex id to its internal one, `iperm` back.  Frontier inputs are mapped in and its
+  // outputs (top-k ids, tie-break order, member pool) are original ids.
+  struct FrLayout* lay = nullptr;
 };
 
 // update.hip: frees egr_snapshot::upd (called by egr_snapshot_free)
 void snapshot_update_free(egr_snapshot* s);
+
+// layout.hip: the frontier layout of a snapshot.  layout_build computes the vertex order from
+// the snapshot's host CSR and lays the device arrays out (egr_snapshot_create / _from_csr);
+// layout_extend re-lays them after an update, new vertices numbered after the old ones;
+// layout_free releases them.  Off when $EGRAPH_FRONTIER_LAYOUT is "0".
+int layout_build(egr_snapshot* s, const uint32_t* row_ptr_host, const uint32_t* col_host);
+int layout_extend(egr_snapshot* s, hipStream_t st);
+void layout_free(egr_snapshot* s);
+struct FrLayoutView {
+  const uint32_t* row_ptr;
+  const uint2* cv;
+  const uint8_t* vlabel;
+  const uint32_t* perm;    // nullptr: identity
+  const uint32_t* iperm;
+};
+FrLayoutView layout_view(const egr_snapshot* s);
 
 namespace egr {
 

@@ -1132,9 +1132,13 @@ int egr_snapshot_create(const egr_graph* g, const float* weights, int32_t n_type
     egr_snapshot_free(s);
     return egr::fail(EGR_EDEVICE, std::string("snapshot upload: ") + hipGetErrorString(e));
   }
-  s->row_ptr_host = std::move(row_ptr);
   s->cap_v = V;
   s->cap_e = 2 * E;
+  if ((rc = layout_build(s, row_ptr.data(), col.data())) != EGR_OK) {
+    egr_snapshot_free(s);
+    return rc;
+  }
+  s->row_ptr_host = std::move(row_ptr);
   *out = s;
   return EGR_OK;
 }
@@ -1149,6 +1153,7 @@ void egr_snapshot_free(egr_snapshot* s) {
   dfree(s->cv);
   dfree(s->vlabel);
   snapshot_update_free(s);
+  layout_free(s);
   delete s;
 }
 
@@ -1492,6 +1497,10 @@ int egr_snapshot_from_csr(const uint32_t* row_ptr, const uint32_t* col, const ui
   s->row_ptr_host.assign(row_ptr, row_ptr + V + 1);
   s->cap_v = V;
   s->cap_e = NE;
+  if ((rc = layout_build(s, row_ptr, col)) != EGR_OK) {
+    egr_snapshot_free(s);
+    return rc;
+  }
   *out = s;
   return EGR_OK;
 }

@@ -332,6 +332,9 @@ int egr_snapshot_update(egr_snapshot* s, const uint8_t* new_vlabel, int64_t n_ne
   s->NE = NEn;
   s->row_ptr_host = std::move(rp_host);
   ++s->version;
+  // the frontier's locality layout follows the update (new vertices after the old ones); if it
+  // cannot be rebuilt it is dropped and the frontier reads the canonical arrays (same results)
+  (void)layout_extend(s, st);
   return EGR_OK;
 }
 

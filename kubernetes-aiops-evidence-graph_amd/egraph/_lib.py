@@ -137,6 +137,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_snapshot_update": (C.c_int, [P, P, I64, P, P, P, I64, P, I32, P]),
     "egr_snapshot_download": (C.c_int, [P, P, P, P, P, P]),
     "egr_snapshot_version": (I64, [P]),
+    "egr_locality_order": (C.c_int, [P, P, I64, P]),
     "egr_snapshot_within": (C.c_int, [P, P, I64, I32, P, P]),
     "egr_frontier_max_vertices": (I64, [P]),
     "egr_graph_export_edges": (C.c_int, [P, I64, I64, P, P, P]),

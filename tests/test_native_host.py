@@ -177,3 +177,32 @@ def test_str_blob_native_matches_python():
     assert L.pyhost.str_blob(["a", 3]) is None and L.pyhost.str_blob(("a",)) is None
     b, o = str_blob(("a", "bc"))
     assert b == b"abc" and o.tolist() == [0, 1, 3]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_locality_order_native_matches_python(seed):
+    """egr_locality_order (csrc/layout.hip, the frontier layout's vertex order) equals the
+    Python statement egraph.graph.locality_order, and is a permutation."""
+    from egraph import _lib as L
+    from egraph import synth
+    from egraph.graph import locality_order
+    cfg = synth.ClusterConfig(pods=800 + 300 * seed, namespaces=5, nodes=20 + seed, deployments=80,
+                              services=40, attach_fraction=0.3, seed=100 + seed)
+    c = synth.build_cluster(cfg)
+    synth.add_incidents(c, synth.make_incidents(c, 30, seed=seed))
+    g = synth.build_graph(c)
+    csr = g.csr()
+    V = g.num_vertices
+    out = np.empty(V, np.uint32)
+    L.check(L.lib.egr_locality_order(csr["row_ptr"].ctypes.data, csr["col"].ctypes.data, V,
+                                     out.ctypes.data), "egr_locality_order")
+    want = locality_order(csr["row_ptr"], csr["col"])
+    assert np.array_equal(out.astype(np.int64), want)
+    assert np.array_equal(np.sort(out), np.arange(V))
+    # a Node hub is followed by vertices hanging under it (its pods)
+    labels = g.labels()
+    vl, _, _, _ = g.export()
+    pos = np.empty(V, np.int64)
+    pos[out] = np.arange(V)
+    first_node = out[np.flatnonzero(vl[out] == labels.index("Node"))[0]]
+    assert vl[out[pos[first_node] + 1]] == labels.index("Pod")
