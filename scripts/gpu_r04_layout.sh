@@ -7,6 +7,7 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-r04lay}
 mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_rccl_gpu.py -m gpu -x -v --timeout 280 --timeout-method thread > $OUT/pytest_rccl.log 2>&1 && echo "rccl test ok" || { echo "rccl test FAILED"; tail -30 $OUT/pytest_rccl.log; }
 timeout -k 10 400 python -u -m pytest tests/test_layout_gpu.py tests/test_frontier_gpu.py tests/test_configs_gpu.py tests/test_storm_gpu.py tests/test_frontier_scale_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
 echo "tests ok"; tail -1 $OUT/pytest.log
 for i in 1 2 3; do
