@@ -62,10 +62,12 @@ MERGE_MAX = 20
 
 BACKEND = os.environ.get("EGRAPH_BENCH_BACKEND", "nccl")
 # --seed-input (main sets it): "grouped" = the seed triples arrive grouped by incident with
-# their column offsets and a costliest-first launch order (the host's seed attachment emits
-# them incident by incident; egr_frontier_run_grouped); "sort" = unordered triples, sorted by
-# column on the device in every step (egr_frontier_set_seeds: count, scan, scatter)
-GROUPED = "order"
+# their column offsets (the host's seed attachment emits them incident by incident;
+# egr_frontier_run_grouped) and the costliest-first launch order is computed on the device in
+# every step (two small kernels in the captured step); "grouped-host-order" (A/B) = the same with
+# the order computed once on the host outside the timed region; "sort" = unordered triples,
+# sorted by column on the device in every step (egr_frontier_set_seeds: count, scan, scatter)
+GROUPED = "device"
 
 
 def max_over_ranks(dist, x: float, dev) -> float:
@@ -249,7 +251,7 @@ def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) ->
         gp, gv, gs = group_seeds(*(a.cpu().numpy() for a in seeds), B)
         lane["grouped"] = tuple(torch.from_numpy(x).to(dev) for x in
                                 (gp.view(np.int32), gv.view(np.int32), gs))
-        if GROUPED == "order":
+        if GROUPED == "order":          # (A/B: --seed-input grouped-host-order)
             rp = row_ptr if row_ptr is not None else snap.download()["row_ptr"]
             lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
 
@@ -1148,9 +1150,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="frontier: enqueue each batch eagerly instead of replaying the lane's "
                          "captured HIP graph")
-    ap.add_argument("--seed-input", default="grouped", choices=["grouped", "sort"],
-                    help="grouped: seeds grouped by incident + launch order as resident input "
-                         "(egr_frontier_run_grouped); sort: device counting sort per step")
+    ap.add_argument("--seed-input", default="grouped", choices=["grouped", "grouped-host-order", "sort"],
+                    help="grouped: seeds grouped by incident as resident input, launch order on "
+                         "the device per step (egr_frontier_run_grouped); grouped-host-order: the "
+                         "order computed once on the host (A/B); sort: device counting sort per step")
     ap.add_argument("--roofline-reps", type=int, default=20,
                     help="isolated frontier launches timed after the run for the roofline")
     args = ap.parse_args()
@@ -1175,7 +1178,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     global GROUPED
-    GROUPED = "order" if args.seed_input == "grouped" else None
+    GROUPED = {"grouped": "device", "grouped-host-order": "order"}.get(args.seed_input)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a ROCm GPU")
     # EGRAPH_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device); the
@@ -1300,8 +1303,11 @@ def main():
             "distinct_batches_per_launch": ctx["distinct_batches"],
             "incidents_in_graph": ctx["incidents_in_graph"],
             "hip_graph_replay": out_graph,
-            "seed_input": ("grouped by incident + column offsets + costliest-first launch order, "
-                           "resident (egr_frontier_run_grouped)" if GROUPED and args.engine == "frontier"
+            "seed_input": ("grouped by incident + column offsets, resident; costliest-first launch "
+                           "order computed on the device in every step (egr_frontier_run_grouped)"
+                           if GROUPED == "device" and args.engine == "frontier" else
+                           "grouped by incident + column offsets + a launch order computed once on "
+                           "the host (A/B)" if GROUPED == "order" and args.engine == "frontier"
                            else "unordered triples, device counting sort per step"),
         },
         "roofline": roof,

@@ -376,10 +376,11 @@ int egr_frontier_run(egr_frontier* f, const uint32_t* source_vertex, int32_t hop
  * entries [seed_ptr[b], seed_ptr[b+1]) of seed_vertex / seed_val (device; seed_ptr [n_cols+1]
  * u32, clamped to n_seeds; n_seeds <= the frontier's max_seeds; duplicates max-combined,
  * out-of-range vertices dropped).  Same results as egr_frontier_set_seeds + egr_frontier_run
- * with the same triples.  order [n_cols] (device, or NULL = column order): the order the
- * columns start in, a permutation of 0..n_cols-1 (entries >= n_cols are skipped) --
- * set_seeds orders them costly-first itself, longest-processing-time first; the pointers are
- * read by this call's kernels only (stream order). */
+ * with the same triples.  order [n_cols] (device): the order the columns start in, a
+ * permutation of 0..n_cols-1 (entries >= n_cols are skipped); NULL = costliest first, computed
+ * on the device in the same stream (cost = the column's seeds' 1 + degree, bucketed on a log
+ * scale, as set_seeds orders them) -- longest-processing-time first; the pointers are read by
+ * this call's kernels only (stream order). */
 int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const uint32_t* seed_vertex,
                              const float* seed_val, int64_t n_seeds, const uint32_t* order,
                              const uint32_t* source_vertex,

@@ -342,6 +342,50 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
   for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
 }
 
+// Grouped runs without a caller order (egr_frontier_run_grouped with order = NULL): the cost of
+// column c -- the sum over its seeds of 1 + the seed vertex's degree, the predictor set_seeds
+// sorts by (original ids, canonical row_ptr) -- one wave per column ...
+__global__ __launch_bounds__(256) void grouped_cost_kernel(const uint32_t* __restrict__ seed_ptr,
+                                                          const uint32_t* __restrict__ seed_v,
+                                                          uint32_t n_seeds, int B,
+                                                          const uint32_t* __restrict__ row_ptr,
+                                                          uint32_t V, uint32_t* __restrict__ cost) {
+  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  if (c >= B) return;
+  const uint32_t s0 = min(seed_ptr[c], n_seeds), s1 = max(s0, min(seed_ptr[c + 1], n_seeds));
+  uint32_t sum = 0;
+  for (uint32_t i = s0 + lane; i < s1; i += 64) {
+    const uint32_t v = seed_v[i];
+    if (v < V) sum += 1u + row_ptr[v + 1] - row_ptr[v];
+  }
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) cost[c] = sum;
+}
+
+// ... and the columns by descending cost bucket (the log-scale counting sort of seed_scan_kernel:
+// one block; order within a bucket is arbitrary -- results do not depend on the order)
+__global__ __launch_bounds__(SCAN_T) void cost_order_kernel(const uint32_t* __restrict__ cost, int B,
+                                                            uint32_t* __restrict__ order) {
+  __shared__ uint32_t hist[COST_BUCKETS];
+  const int tid = threadIdx.x;
+  const int per = (B + SCAN_T - 1) / SCAN_T;
+  const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
+  if (tid < COST_BUCKETS) hist[tid] = 0;
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int j = 0; j < COST_BUCKETS; ++j) {
+      const uint32_t x = hist[j];
+      hist[j] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
+}
+
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
                                     const float* __restrict__ sval, int64_t n, uint32_t V, int B,
                                     uint32_t* cursor, uint32_t* out_v, float* out_s) {
@@ -375,6 +419,7 @@ struct egr_frontier {
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
   uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; costs
   uint32_t* order = nullptr;      // [B] launch order of the columns (set_seeds: costly first)
+  uint32_t* gcost = nullptr;      // [B] grouped runs' column costs (device launch order)
   uint32_t* ident = nullptr;      // [B] 0..B-1 (grouped runs: column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
@@ -452,6 +497,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
   if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
       (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
+      (rc = dalloc(&f->gcost, (size_t)n_cols)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
@@ -501,6 +547,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->seed_ptr);
   dfree(f->seed_cnt);
   dfree(f->order);
+  dfree(f->gcost);
   dfree(f->ident);
   dfree(f->seed_v);
   dfree(f->seed_s);
@@ -605,7 +652,15 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.n_seeds = (uint32_t)n_seeds;
   a.seed_rep = f->seed_rep;
   a.sources = source_vertex;
-  a.order = sorted ? f->order : order ? order : f->ident;
+  if (!sorted && !order) {
+    // grouped seeds without a caller order: costliest-first on the device (two small kernels
+    // ahead of the frontier launch, in the same stream -- and in a captured replay)
+    hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 3) / 4)), dim3(256), 0, st,
+                       seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, f->gcost);
+    hipLaunchKernelGGL(cost_order_kernel, dim3(1), dim3(SCAN_T), 0, st, f->gcost, f->B, f->order);
+    EGR_CHECK_LAUNCH();
+  }
+  a.order = (sorted || !order) ? f->order : order;
   a.seed_cnt = sorted ? f->seed_cnt : nullptr;
   a.out_ids = out_ids;
   a.out_scores = out_scores;

@@ -680,7 +680,8 @@ class Frontier:
                     order: torch.Tensor | None = None):
         """One pass over seeds grouped by column (egr_frontier_run_grouped): column b's seeds are
         entries [seed_ptr[b], seed_ptr[b+1]) of vertex / val (device tensors; group_seeds()
-        builds them from triples).  No set_seeds, no sort on the device."""
+        builds them from triples).  No set_seeds, no sort on the device.  `order`: the columns'
+        launch order (device u32); None = costliest first, computed on the device."""
         if sources.numel() != self.B or seed_ptr.numel() != self.B + 1:
             raise ValueError(f"need one source vertex per column ({self.B}) and {self.B + 1} seed offsets")
         if vertex.numel() != val.numel():

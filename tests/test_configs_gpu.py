@@ -68,10 +68,11 @@ def _check_rules(res, enc):
     assert res.confidence.tobytes() == exp["confidence"].tobytes()
 
 
-@pytest.mark.parametrize("seed_input", ["order", None])
+@pytest.mark.parametrize("seed_input", ["device", "order", None])
 def test_bench_config_c3_pipelined_lanes(seed_input, monkeypatch):
     """bench.py's C3 step exactly: three lanes, six different batches, seeds as grouped input
-    with a launch order (the default) or sorted on the device (--seed-input sort)."""
+    with the launch order computed on the device (the default) or on the host, or sorted on the
+    device (--seed-input sort)."""
     import bench
     monkeypatch.setattr(bench, "GROUPED", seed_input)
     from egraph import catalog
@@ -167,7 +168,7 @@ def test_bench_config_c3_merged_launch():
     rules over the three batches' rows equal the oracle's."""
     import bench
     monkey = bench.GROUPED
-    bench.GROUPED = "order"
+    bench.GROUPED = "device"
     try:
         from egraph import catalog
         from egraph.encode import encode_batch
