@@ -363,16 +363,36 @@ __global__ __launch_bounds__(256) void grouped_cost_kernel(const uint32_t* __res
 }
 
 // ... and the columns by descending cost bucket (the log-scale counting sort of seed_scan_kernel:
-// one block; order within a bucket is arbitrary -- results do not depend on the order)
+// one block; order within a bucket is arbitrary -- results do not depend on the order).  Tens
+// of thousands of columns fall into a handful of buckets, so the LDS histogram atomics are
+// aggregated per wave: one atomic per distinct bucket of a wave's 64 columns, each lane's slot
+// its rank among the wave's lanes of its bucket.
+__device__ __forceinline__ void wave_bucket_add(uint32_t* hist, int bk, bool ok, uint32_t* slot) {
+  const int lane = threadIdx.x & 63;
+  uint64_t todo = __ballot(ok);
+  while (todo) {
+    const int lead = __ffsll((long long)todo) - 1;
+    const int b = __shfl(bk, lead, 64);
+    const uint64_t m = __ballot(ok && bk == b);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&hist[b], (uint32_t)__popcll(m));
+    base = __shfl(base, lead, 64);
+    if (ok && bk == b && slot) *slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    todo &= ~m;
+  }
+}
+
 __global__ __launch_bounds__(SCAN_T) void cost_order_kernel(const uint32_t* __restrict__ cost, int B,
                                                             uint32_t* __restrict__ order) {
   __shared__ uint32_t hist[COST_BUCKETS];
   const int tid = threadIdx.x;
-  const int per = (B + SCAN_T - 1) / SCAN_T;
-  const int c0 = min(B, tid * per), c1 = min(B, c0 + per);
   if (tid < COST_BUCKETS) hist[tid] = 0;
   __syncthreads();
-  for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
+  for (int c0 = 0; c0 < B; c0 += SCAN_T) {       // (the block's 256 threads: 4 waves per round)
+    const int c = c0 + tid;
+    const bool ok = c < B;
+    wave_bucket_add(hist, ok ? cost_bucket(cost[c]) : 0, ok, nullptr);
+  }
   __syncthreads();
   if (tid == 0) {
     uint32_t acc = 0;
@@ -383,7 +403,13 @@ __global__ __launch_bounds__(SCAN_T) void cost_order_kernel(const uint32_t* __re
     }
   }
   __syncthreads();
-  for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
+  for (int c0 = 0; c0 < B; c0 += SCAN_T) {
+    const int c = c0 + tid;
+    const bool ok = c < B;
+    uint32_t slot = 0;
+    wave_bucket_add(hist, ok ? cost_bucket(cost[c]) : 0, ok, &slot);
+    if (ok) order[slot] = (uint32_t)c;
+  }
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,

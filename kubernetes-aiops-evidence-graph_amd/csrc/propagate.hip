@@ -766,6 +766,16 @@ __global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t*
   if (q <= P) out[q] = off[seg[q]];
 }
 
+// fixed capacity: words per peer (capped at its slot) and the overflow flag
+__global__ void sx_capcount_kernel(const int64_t* __restrict__ bound, int P, int per, int64_t peer_cap,
+                                   int64_t* __restrict__ counts, uint32_t* __restrict__ overflow) {
+  const int q = threadIdx.x;
+  if (q >= P) return;
+  const int64_t c = bound[q + 1] - bound[q];
+  if (c > peer_cap) atomicOr(overflow, 1u);
+  counts[q] = per * (c < peer_cap ? c : peer_cap);
+}
+
 // The exchange kernels run ONE WAVE PER ROW, four per 256-thread block, in a grid of at most
 // SX_MAX_BLOCKS blocks that strides over the rows: a boundary row is cheap, and a block (or a
 // wave) per row launched them bound by workgroup dispatch (~120k rows per C4 exchange at P = 8).
@@ -829,11 +839,15 @@ __device__ __forceinline__ int kth_bit(const uint32_t* __restrict__ m, int MW, i
 // Sender, pass 2: the non-zero entries of the row's marked groups, in column order, at the
 // row's offset (the exclusive scan of pass 1's counts).  Each half-wave takes one marked group
 // per round.
+// Fixed-capacity mode (bound != nullptr, egr_plan_pack_sparse_cap): peer q's entries start at
+// out[q * peer_cap * per] instead of its offset in one contiguous list (bound[q] = the offset of
+// q's first entry in that list); entries past peer_cap are dropped (the pack flags the overflow).
 __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ X,
     const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
     const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
     const int64_t* __restrict__ off, const uint32_t* __restrict__ masks, int MW,
-    int64_t* __restrict__ out, int64_t cap) {
+    int64_t* __restrict__ out, int64_t cap, const int64_t* __restrict__ bound = nullptr,
+    int64_t peer_cap = 0) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
   for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   uint32_t mk[EGR_SX_MASK_WORDS];
@@ -849,6 +863,13 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
   while (q + 1 < P && seg[q + 1] <= r) ++q;
   const int64_t rl = r - seg[q];
   int64_t pos = off[r];
+  int64_t lim = cap;                     // entries (scores) / words (reach) the target holds
+  int64_t* dst = out;
+  if (bound) {                           // fixed capacity: q's own slot, positions within q
+    pos -= bound[q];
+    dst = out + (size_t)q * peer_cap * (reach ? 2 : 1);
+    lim = reach ? 2 * peer_cap : peer_cap;
+  }
   for (int base = 0; base < nset; base += 2) {
     const int g = base + half < nset ? kth_bit(mk, MW, base + half) : -1;
     const int b = g >= 0 ? 32 * g + hl : width;
@@ -863,12 +884,12 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     if (nz) {
       const int64_t idx = rl * width + b;
       if (reach) {
-        if (2 * (pos + before) + 1 < cap) {
-          out[2 * (pos + before)] = idx;
-          out[2 * (pos + before) + 1] = (int64_t)w;
+        if (2 * (pos + before) + 1 < lim) {
+          dst[2 * (pos + before)] = idx;
+          dst[2 * (pos + before) + 1] = (int64_t)w;
         }
-      } else if (pos + before < cap) {
-        out[pos + before] = (idx << 32) | (int64_t)w;
+      } else if (pos + before < lim) {
+        dst[pos + before] = (idx << 32) | (int64_t)w;
       }
     }
     pos += __popcll(m);
@@ -904,17 +925,25 @@ __global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uin
   }
 }
 
+// Fixed-capacity mode (peer_cap > 0, egr_plan_unpack_sparse_cap): sender s's entries are slots
+// [s * peer_cap, s * peer_cap + cnt[s] / per) of `in`; n = P * peer_cap slots are scanned.
 __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V,
                                   int TW, uint32_t RS, int width, bool reach,
                                   const uint32_t* __restrict__ recv_vertex,
                                   const int64_t* __restrict__ in, int64_t n,
                                   const int64_t* __restrict__ eseg,
                                   const int64_t* __restrict__ rbase, int P,
-                                  uint8_t* __restrict__ nzf, uint32_t ntiles) {
+                                  uint8_t* __restrict__ nzf, uint32_t ntiles,
+                                  int64_t peer_cap = 0, const int64_t* __restrict__ cnt = nullptr) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   int s = 0;
-  while (s + 1 < P && eseg[s + 1] <= e) ++s;
+  if (peer_cap > 0) {
+    s = (int)(e / peer_cap);
+    if (e - (int64_t)s * peer_cap >= cnt[s] / (reach ? 2 : 1)) return;
+  } else {
+    while (s + 1 < P && eseg[s + 1] <= e) ++s;
+  }
   int64_t idx;
   uint64_t w;
   if (reach) {
@@ -925,7 +954,7 @@ __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ 
     idx = (int64_t)(x >> 32);
     w = x & 0xFFFFFFFFull;
   }
-  const int64_t row = rbase[s] + idx / width;
+  const int64_t row = rbase[s] + idx / width;     // (idx is relative to sender s's rows)
   const int b = (int)(idx % width);
   const uint32_t v = recv_vertex[row];
   if (reach) R[(size_t)v * RS + b] = w;
@@ -1707,6 +1736,105 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
                        n_entries, eseg, rbase, P, nzf, (uint32_t)p->ntiles);
     EGR_CHECK_LAUNCH();
   }
+  p->cand_valid = false;
+  return EGR_OK;
+}
+
+int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, int64_t n,
+                             const int64_t* seg_dev, int32_t P, int64_t* out, int64_t peer_cap,
+                             int64_t* counts_dev, uint32_t* overflow_dev, void* stream) {
+  if (!p || (what != 0 && what != 1) || n < 0 || P < 1 || P > EGR_SX_MAX_PEERS || !seg_dev ||
+      !counts_dev || !overflow_dev || peer_cap < 1 || (n > 0 && (!rows || !out)))
+    return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: bad arguments");
+  const bool reach = what == 1;
+  if (reach ? !p->sources_set : p->hops_done < 1)
+    return egr::fail(EGR_ESTATE, "egr_plan_pack_sparse_cap: nothing computed yet");
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int width = reach ? p->W : p->Bpad;
+  if (!reach && (uint64_t)n * (uint64_t)width >= (1ull << 32))
+    return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: send rows x columns exceed the 2^32 "
+                                 "entry index of the score format");
+  if ((size_t)n + 1 > p->sx_cap) {
+    dfree(p->sx_off);
+    p->sx_cap = 0;
+    int rc = dalloc(&p->sx_off, (size_t)n + 1);
+    if (rc != EGR_OK) return rc;
+    p->sx_cap = (size_t)n + 1;
+    if (p->sx_tmp) (void)hipFree(p->sx_tmp);
+    p->sx_tmp = nullptr;
+    size_t tb = 0;
+    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
+    EGR_HIP(hipMalloc(&p->sx_tmp, tb));
+    p->sx_tmp_bytes = tb;
+  }
+  if (!p->sx_tot) {
+    const int rc = dalloc(&p->sx_tot, (size_t)EGR_SX_MAX_PEERS + 1 + EGR_SX_MAX_PEERS + 1);
+    if (rc != EGR_OK) return rc;
+  }
+  const float* X = reach ? nullptr : p->x[p->xcur];
+  const uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
+  const uint32_t V = (uint32_t)p->s->V;
+  const int MW = (((width + 31) / 32) + 31) / 32;
+  if ((size_t)std::max<int64_t>(n, 1) * MW > p->sx_mask_cap) {
+    dfree(p->sx_mask);
+    p->sx_mask_cap = 0;
+    const int rc = dalloc(&p->sx_mask, (size_t)std::max<int64_t>(n, 1) * MW);
+    if (rc != EGR_OK) return rc;
+    p->sx_mask_cap = (size_t)std::max<int64_t>(n, 1) * MW;
+  }
+  EGR_HIP(hipMemsetAsync(p->sx_off, 0, sizeof(int64_t) * ((size_t)n + 1), st));
+  if (n > 0) {
+    const dim3 sxg = sx_grid(n);
+    hipLaunchKernelGGL(sx_count_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
+                       (uint32_t)p->RS, width, reach, rows, (int64_t)n, p->sx_off, p->sx_mask, MW,
+                       reach ? nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles);
+    EGR_CHECK_LAUNCH();
+    size_t tb = p->sx_tmp_bytes;
+    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sx_tmp, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
+  }
+  hipLaunchKernelGGL(sx_bounds_kernel, dim3(1), dim3(EGR_SX_MAX_PEERS + 1), 0, st, p->sx_off, seg_dev,
+                     P, p->sx_tot);
+  hipLaunchKernelGGL(sx_capcount_kernel, dim3(1), dim3(EGR_SX_MAX_PEERS), 0, st, p->sx_tot, P,
+                     reach ? 2 : 1, peer_cap, counts_dev, overflow_dev);
+  EGR_CHECK_LAUNCH();
+  if (n > 0) {
+    hipLaunchKernelGGL(sx_emit_kernel, sx_grid(n), dim3(256), 0, st, X, R, V, p->TW,
+                       (uint32_t)p->RS, width, reach, rows, (int64_t)n, seg_dev, P, p->sx_off,
+                       p->sx_mask, MW, out, (int64_t)0, (const int64_t*)p->sx_tot, peer_cap);
+    EGR_CHECK_LAUNCH();
+  }
+  return EGR_OK;
+}
+
+int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
+                               const int64_t* in, int64_t peer_cap, const int64_t* counts_dev,
+                               const int64_t* rbase, int32_t P, void* stream) {
+  if (!p || (what != 0 && what != 1) || n_rows < 0 || P < 1 || peer_cap < 1 || !counts_dev ||
+      (n_rows > 0 && (!recv_vertex || !in || !rbase)))
+    return egr::fail(EGR_EINVAL, "egr_plan_unpack_sparse_cap: bad arguments");
+  const bool reach = what == 1;
+  if (reach ? !p->sources_set : p->hops_done < 1)
+    return egr::fail(EGR_ESTATE, "egr_plan_unpack_sparse_cap: nothing computed yet");
+  if (n_rows == 0) return EGR_OK;
+  DeviceGuard guard(p->s->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int width = reach ? p->W : p->Bpad;
+  float* X = reach ? nullptr : p->x[p->xcur];
+  uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
+  const uint32_t V = (uint32_t)p->s->V;
+  uint8_t* nzf = reach ? nullptr : p->nzf[p->xcur];
+  hipLaunchKernelGGL(sx_zero_kernel, sx_grid(n_rows), dim3(256), 0,
+                     st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, (int64_t)n_rows,
+                     nzf, (uint32_t)p->ntiles, nzf != nullptr && p->xzeroed[p->xcur]);
+  EGR_CHECK_LAUNCH();
+  if (nzf) p->xzeroed[p->xcur] = true;
+  const int64_t slots = (int64_t)P * peer_cap;
+  hipLaunchKernelGGL(sx_scatter_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0,
+                     st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, in,
+                     slots, (const int64_t*)nullptr, rbase, P, nzf, (uint32_t)p->ntiles, peer_cap,
+                     counts_dev);
+  EGR_CHECK_LAUNCH();
   p->cand_valid = false;
   return EGR_OK;
 }

@@ -533,6 +533,27 @@ class Plan:
                                              n, L.ptr(eseg), L.ptr(rbase), rbase.numel(),
                                              self._st(stream)), "egr_plan_unpack_sparse")
 
+    def pack_sparse_cap(self, what: str, rows: torch.Tensor, seg_dev: torch.Tensor, out: torch.Tensor,
+                        peer_cap: int, counts: torch.Tensor, overflow: torch.Tensor, stream=None) -> None:
+        """egr_plan_pack_sparse_cap: the non-zero entries into fixed slots of peer_cap entries
+        per peer (out: int64 [P * peer_cap * words per entry]), the word counts into `counts`
+        (device int64 [P]), overflow into `overflow` (device int32 [1]); no synchronisation."""
+        P = seg_dev.numel() - 1
+        if out.numel() < P * peer_cap * (2 if what == "reach" else 1) or counts.numel() < P:
+            raise ValueError("pack_sparse_cap: output slots or counts too small")
+        L.check(L.lib.egr_plan_pack_sparse_cap(self._h, 1 if what == "reach" else 0, L.ptr(rows),
+                                               rows.numel(), L.ptr(seg_dev), P, L.ptr(out), int(peer_cap),
+                                               L.ptr(counts), L.ptr(overflow), self._st(stream)),
+                "egr_plan_pack_sparse_cap")
+
+    def unpack_sparse_cap(self, what: str, recv_vertex: torch.Tensor, entries: torch.Tensor,
+                          peer_cap: int, counts: torch.Tensor, rbase: torch.Tensor, stream=None) -> None:
+        L.check(L.lib.egr_plan_unpack_sparse_cap(self._h, 1 if what == "reach" else 0,
+                                                 L.ptr(recv_vertex), recv_vertex.numel(), L.ptr(entries),
+                                                 int(peer_cap), L.ptr(counts), L.ptr(rbase),
+                                                 rbase.numel(), self._st(stream)),
+                "egr_plan_unpack_sparse_cap")
+
     def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
         n = vertex.numel()
         if not (col.numel() == n == val.numel()):

@@ -31,11 +31,15 @@ def main():
     ap.add_argument("--hops", type=int, default=3)
     ap.add_argument("--out", default="")
     ap.add_argument("--pool", action="store_true", help="keep the member pool (no last-pull pruning)")
+    ap.add_argument("--merge", type=int, default=1,
+                    help="batches per launch, as bench.py --merge (20 = the headline's launch of "
+                         "20 different incident sets)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    ctx = bench.setup(args.config, args.batch, 10, 0, dev, pool_entries=0 if args.pool else -1)
-    for _ in range(3):
+    ctx = bench.setup(args.config, args.batch, 10, 0, dev, pool_entries=0 if args.pool else -1,
+                      merge=args.merge)
+    for _ in range(3 * args.merge):
         bench.step_frontier(ctx, args.hops)
     torch.cuda.synchronize()
     raw = ctx["frontier"].phase_times()
