@@ -661,6 +661,12 @@ def _traffic(name: str):
     return None
 
 
+def frontier_layout_on() -> bool:
+    """The snapshot lays the frontier's CSR out in locality order (csrc/layout.hip) unless
+    $EGRAPH_FRONTIER_LAYOUT is "0"."""
+    return not os.environ.get("EGRAPH_FRONTIER_LAYOUT", "1").startswith("0")
+
+
 def _frontier_traffic(ctx, B: int):
     """Bytes past L2 per frontier launch (profiles/pmc_frontier_calibrated*.json, one per
     collected workload), when this run is a workload the counters were collected on (config,
@@ -671,7 +677,8 @@ def _frontier_traffic(ctx, B: int):
         w = d.get("workload", {})
         if (w.get("config") == ctx.get("config") and w.get("batch") == B // M
                 and w.get("batches_per_launch", 1) == M
-                and w.get("distinct_batches", 1) == ctx.get("distinct_batches", 1)):
+                and w.get("distinct_batches", 1) == ctx.get("distinct_batches", 1)
+                and w.get("layout", False) == frontier_layout_on()):
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -1301,6 +1308,7 @@ def main():
             "lanes": args.pipeline if args.engine == "frontier" else 1,
             "batches_per_launch": M,
             "distinct_batches_per_launch": ctx["distinct_batches"],
+            "frontier_layout": "locality order (csrc/layout.hip)" if frontier_layout_on() else "canonical",
             "incidents_in_graph": ctx["incidents_in_graph"],
             "hip_graph_replay": out_graph,
             "seed_input": ("grouped by incident + column offsets, resident; costliest-first launch "
