@@ -840,6 +840,12 @@ class _TimedPlan:
     def unpack_sparse(self, *a, **k):
         return self._timed(lambda: self._p.unpack_sparse(*a, **k))
 
+    def pack_sparse_cap(self, *a, **k):
+        return self._timed(lambda: self._p.pack_sparse_cap(*a, **k))
+
+    def unpack_sparse_cap(self, *a, **k):
+        return self._timed(lambda: self._p.unpack_sparse_cap(*a, **k))
+
     def pack_scores(self, *a):
         return self._timed(self._p.pack_scores, *a)
 
@@ -907,13 +913,21 @@ def shard_step(ctx, hops: int, k: int, ev=None, parts=None):
         plan.set_seeds(*seeds)
         plan.set_sources(sources)
         run.eng = _TimedPlan(plan, ev, parts[i] if parts is not None else None)
-    return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k,
-                                 sparse=not ctx.get("dense_halo", False))
+    if ctx.get("dense_halo") or ctx.get("host_counts"):
+        return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k,
+                                     sparse=not ctx.get("dense_halo", False))
+
+    def reset():                   # a pass that overflowed its slots re-runs (recalibrating)
+        for run, (plan, seeds, sources) in zip(ctx["runs"], ctx["plans"]):
+            plan.set_seeds(*seeds)
+            plan.set_sources(sources)
+    return shard.run_partitioned_retry(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k, reset)
 
 
 def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     ctx = shard_setup(args, world, rank, dev)
     ctx["dense_halo"] = args.dense_halo
+    ctx["host_counts"] = args.halo_host_counts
     for _ in range(args.warmup):
         shard_step(ctx, args.hops, args.k)
     torch.cuda.synchronize(dev)
@@ -965,7 +979,12 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "parallelism": f"edge-cut x{ctx['P']}" + (" (one process)" if world == 1 else ""),
             "local_vertices": [len(r.lg.gid) for r in ctx["runs"]],
             "halo_bytes_per_hop_max_rank": halo,
-            "halo_exchange": "dense" if args.dense_halo else "sparse (non-zero entries only)",
+            "halo_exchange": "dense" if args.dense_halo else
+                             "sparse, host-read peer counts" if args.halo_host_counts else
+                             "sparse, fixed-capacity device slots (no host read per exchange)",
+            "halo_slot_entries": None if args.dense_halo or args.halo_host_counts else
+                                 {w: ctx["runs"][0].cap.get(w) for w in ("scores", "reach")},
+            "halo_overflow_reruns": ctx["runs"][0].overflows,
             "halo_bytes_sent_per_hop_max_rank": sent,
             "halo_reduction_vs_dense": halo / sent if sent else None,
             "partition_compute_ms": part_ms,
@@ -1145,6 +1164,9 @@ def main():
                          "edge-cut partitioned graph with halo exchange (C4)")
     ap.add_argument("--dense-halo", action="store_true",
                     help="--shard graph: exchange whole boundary rows instead of their non-zero entries")
+    ap.add_argument("--halo-host-counts", action="store_true",
+                    help="--shard graph: sparse exchange with a host read of the peer counts per "
+                         "exchange (the round-3 path) instead of fixed-capacity device slots")
     ap.add_argument("--partitions", type=int, default=1,
                     help="--shard graph on one process: partitions run on this GPU")
     ap.add_argument("--workload", default="rank", choices=["rank", "storm"],

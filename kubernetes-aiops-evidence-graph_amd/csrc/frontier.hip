@@ -248,10 +248,12 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 
 // A run's pool / stats counters and overflow-list heads cleared in one launch (one graph node
 // instead of two fill nodes in a captured replay: each node costs its own dispatch gap).
-__global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf) {
+__global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf,
+                                                          uint32_t* ghist) {
   const int tid = threadIdx.x;
   if (tid < 7) ctr[tid] = 0;
   if (tid < 4) ovf[tid] = 0;
+  if (ghist) ghist[tid] = 0;      // (64 threads = COST_BUCKETS)
 }
 
 // cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
@@ -342,74 +344,68 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
   for (int c = c0; c < c1; ++c) order[atomicAdd(&hist[cost_bucket(cost[c])], 1u)] = (uint32_t)c;
 }
 
-// Grouped runs without a caller order (egr_frontier_run_grouped with order = NULL): the cost of
-// column c -- the sum over its seeds of 1 + the seed vertex's degree, the predictor set_seeds
-// sorts by (original ids, canonical row_ptr) -- one wave per column ...
+// Grouped runs without a caller order (egr_frontier_run_grouped with order = NULL): the columns
+// costliest-first by the log-scale cost bucket of seed_scan_kernel, where the cost of column c is
+// the sum over its seeds of 1 + the seed vertex's degree (the predictor set_seeds sorts by;
+// original ids, canonical row_ptr).  Order within a bucket is arbitrary -- results do not depend
+// on the order.  Two many-block kernels (one block with a serial histogram was 128 us at 40k
+// columns): the first computes 64 columns per block (4 lanes per column), ranks them inside the
+// block with LDS atomics and claims each bucket's block total with ONE global atomic on the
+// histogram `ghist` (zeroed by clear_counters_kernel ahead of it); the second scans the 64-bucket
+// histogram in one wave per block and scatters each column to its slot.
 __global__ __launch_bounds__(256) void grouped_cost_kernel(const uint32_t* __restrict__ seed_ptr,
                                                           const uint32_t* __restrict__ seed_v,
                                                           uint32_t n_seeds, int B,
                                                           const uint32_t* __restrict__ row_ptr,
-                                                          uint32_t V, uint32_t* __restrict__ cost) {
-  const int c = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  if (c >= B) return;
-  const uint32_t s0 = min(seed_ptr[c], n_seeds), s1 = max(s0, min(seed_ptr[c + 1], n_seeds));
-  uint32_t sum = 0;
-  for (uint32_t i = s0 + lane; i < s1; i += 64) {
-    const uint32_t v = seed_v[i];
-    if (v < V) sum += 1u + row_ptr[v + 1] - row_ptr[v];
-  }
-  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-  if (lane == 0) cost[c] = sum;
-}
-
-// ... and the columns by descending cost bucket (the log-scale counting sort of seed_scan_kernel:
-// one block; order within a bucket is arbitrary -- results do not depend on the order).  Tens
-// of thousands of columns fall into a handful of buckets, so the LDS histogram atomics are
-// aggregated per wave: one atomic per distinct bucket of a wave's 64 columns, each lane's slot
-// its rank among the wave's lanes of its bucket.
-__device__ __forceinline__ void wave_bucket_add(uint32_t* hist, int bk, bool ok, uint32_t* slot) {
-  const int lane = threadIdx.x & 63;
-  uint64_t todo = __ballot(ok);
-  while (todo) {
-    const int lead = __ffsll((long long)todo) - 1;
-    const int b = __shfl(bk, lead, 64);
-    const uint64_t m = __ballot(ok && bk == b);
-    uint32_t base = 0;
-    if (lane == lead) base = atomicAdd(&hist[b], (uint32_t)__popcll(m));
-    base = __shfl(base, lead, 64);
-    if (ok && bk == b && slot) *slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    todo &= ~m;
-  }
-}
-
-__global__ __launch_bounds__(SCAN_T) void cost_order_kernel(const uint32_t* __restrict__ cost, int B,
-                                                            uint32_t* __restrict__ order) {
+                                                          uint32_t V, uint32_t* __restrict__ gbk,
+                                                          uint32_t* __restrict__ gpos,
+                                                          uint32_t* __restrict__ ghist) {
   __shared__ uint32_t hist[COST_BUCKETS];
-  const int tid = threadIdx.x;
+  __shared__ uint32_t base[COST_BUCKETS];
+  const int tid = threadIdx.x, q = tid & 3;
+  const int c = (int)(blockIdx.x * 64 + (tid >> 2));
   if (tid < COST_BUCKETS) hist[tid] = 0;
-  __syncthreads();
-  for (int c0 = 0; c0 < B; c0 += SCAN_T) {       // (the block's 256 threads: 4 waves per round)
-    const int c = c0 + tid;
-    const bool ok = c < B;
-    wave_bucket_add(hist, ok ? cost_bucket(cost[c]) : 0, ok, nullptr);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int j = 0; j < COST_BUCKETS; ++j) {
-      const uint32_t x = hist[j];
-      hist[j] = acc;
-      acc += x;
+  uint32_t sum = 0;
+  if (c < B) {
+    const uint32_t s0 = min(seed_ptr[c], n_seeds), s1 = max(s0, min(seed_ptr[c + 1], n_seeds));
+    for (uint32_t i = s0 + q; i < s1; i += 4) {
+      const uint32_t v = seed_v[i];
+      if (v < V) sum += 1u + row_ptr[v + 1] - row_ptr[v];
     }
   }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
   __syncthreads();
-  for (int c0 = 0; c0 < B; c0 += SCAN_T) {
-    const int c = c0 + tid;
-    const bool ok = c < B;
-    uint32_t slot = 0;
-    wave_bucket_add(hist, ok ? cost_bucket(cost[c]) : 0, ok, &slot);
-    if (ok) order[slot] = (uint32_t)c;
+  const int bk = cost_bucket(sum);
+  uint32_t lpos = 0;
+  if (c < B && q == 0) lpos = atomicAdd(&hist[bk], 1u);
+  __syncthreads();
+  if (tid < COST_BUCKETS) base[tid] = hist[tid] ? atomicAdd(&ghist[tid], hist[tid]) : 0u;
+  __syncthreads();
+  if (c < B && q == 0) {
+    gbk[c] = (uint32_t)bk;
+    gpos[c] = base[bk] + lpos;
   }
+}
+
+__global__ __launch_bounds__(256) void cost_order_kernel(const uint32_t* __restrict__ gbk,
+                                                        const uint32_t* __restrict__ gpos,
+                                                        const uint32_t* __restrict__ ghist, int B,
+                                                        uint32_t* __restrict__ order) {
+  __shared__ uint32_t pre[COST_BUCKETS];
+  const int tid = threadIdx.x;
+  if (tid < COST_BUCKETS) {                      // exclusive scan of the histogram, one wave
+    const uint32_t x = ghist[tid];
+    uint32_t inc = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (tid >= o) inc += y;
+    }
+    pre[tid] = inc - x;
+  }
+  __syncthreads();
+  const int c = (int)(blockIdx.x * 256 + tid);
+  if (c < B) order[pre[gbk[c]] + gpos[c]] = (uint32_t)c;
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
@@ -445,7 +441,8 @@ struct egr_frontier {
   uint32_t* seed_ptr = nullptr;   // [B+1] exclusive scan of seed_cnt
   uint32_t* seed_cnt = nullptr;   // [2B]: per-column counts, then scatter cursors; costs
   uint32_t* order = nullptr;      // [B] launch order of the columns (set_seeds: costly first)
-  uint32_t* gcost = nullptr;      // [B] grouped runs' column costs (device launch order)
+  uint32_t* gcost = nullptr;      // [2B + 64] grouped runs' device launch order: column cost
+                                  // buckets [B], ranks within the bucket [B], bucket histogram
   uint32_t* ident = nullptr;      // [B] 0..B-1 (grouped runs: column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
@@ -523,7 +520,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
   if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
       (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
-      (rc = dalloc(&f->gcost, (size_t)n_cols)) ||
+      (rc = dalloc(&f->gcost, 2 * (size_t)n_cols + 64)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
@@ -655,7 +652,8 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                              float* out_scores, hipStream_t st) {
   const egr_snapshot* s = f->s;
   if (!(sorted && f->ctr_clean)) {
-    hipLaunchKernelGGL(clear_counters_kernel, dim3(1), dim3(64), 0, st, f->ctr, f->ovf);
+    hipLaunchKernelGGL(clear_counters_kernel, dim3(1), dim3(64), 0, st, f->ctr, f->ovf,
+                       (!sorted && !order) ? f->gcost + 2 * (size_t)f->B : (uint32_t*)nullptr);
     EGR_CHECK_LAUNCH();
   }
   FArgs a{};
@@ -681,9 +679,14 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   if (!sorted && !order) {
     // grouped seeds without a caller order: costliest-first on the device (two small kernels
     // ahead of the frontier launch, in the same stream -- and in a captured replay)
-    hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 3) / 4)), dim3(256), 0, st,
-                       seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, f->gcost);
-    hipLaunchKernelGGL(cost_order_kernel, dim3(1), dim3(SCAN_T), 0, st, f->gcost, f->B, f->order);
+    uint32_t* gbk = f->gcost;
+    uint32_t* gpos = f->gcost + f->B;
+    uint32_t* ghist = f->gcost + 2 * (size_t)f->B;
+    hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 63) / 64)), dim3(256), 0, st,
+                       seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, gbk,
+                       gpos, ghist);
+    hipLaunchKernelGGL(cost_order_kernel, dim3((unsigned)((f->B + 255) / 256)), dim3(256), 0, st,
+                       gbk, gpos, ghist, f->B, f->order);
     EGR_CHECK_LAUNCH();
   }
   a.order = (sorted || !order) ? f->order : order;

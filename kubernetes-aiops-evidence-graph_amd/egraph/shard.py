@@ -201,6 +201,26 @@ class TorchComm:
         return [(recv, rc)]
 
 
+    def all_to_all_fixed(self, items: list) -> None:
+        """items = [(send, recv)]: equal splits -- block q of send (numel / P) goes to rank q and
+        block r of recv comes from rank r.  No split sizes, so nothing is read on the host."""
+        ((send, recv),) = items
+        if self.gloo:
+            hr = torch.empty(recv.shape, dtype=recv.dtype)
+            self.dist.all_to_all_single(hr, send.cpu(), group=self.group)
+            recv.copy_(hr)
+            return
+        self.dist.all_to_all_single(recv, send, group=self.group)
+
+    def any_flag(self, flags: list) -> bool:
+        """True if any rank's flag tensor (device int32 [1]) is non-zero (one all-reduce and one
+        host read per call)."""
+        (f,) = flags
+        t = f.to(torch.int64).clone() if not self.gloo else f.to(torch.int64).cpu()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return bool(t.item())
+
+
 class LocalComm:
     """All ranks in one process (tests, and a multi-partition single-GPU run): gathers are
     concatenations, the all-to-all copies each sender's segment into its reader's buffer."""
@@ -221,6 +241,20 @@ class LocalComm:
                     items[q][2][r_off[q][r]: r_off[q][r] + n] = \
                         items[r][0][s_off[r][q]: s_off[r][q] + n].to(items[q][2].device)
 
+
+    def all_to_all_fixed(self, items: list) -> None:
+        P = len(items)
+        for q in range(P):                       # reader
+            recv = items[q][1]
+            bq = recv.numel() // P
+            for r in range(P):                   # sender
+                send = items[r][0]
+                bs = send.numel() // P
+                assert bs == bq
+                recv[r * bq:(r + 1) * bq] = send[q * bs:(q + 1) * bs].to(recv.device)
+
+    def any_flag(self, flags: list) -> bool:
+        return any(bool(f.item()) for f in flags)
 
     def all_to_all_v(self, items: list) -> list:
         P = len(items)
@@ -258,6 +292,14 @@ class RankRun:
         self.recv_base = torch.from_numpy(_seg_starts(lg.recv_counts)[:-1]).to(device)
         self.send_seg = _seg_starts(lg.send_counts)
         self._sx = {}              # sparse send buffers (int64 words), grown on demand
+        # fixed-capacity exchange (run_partitioned(fixed=True)): entries per peer slot per kind,
+        # sized from a calibrating pass over the host-count path; slot buffers; overflow flag
+        self.seg_dev = torch.from_numpy(self.send_seg).to(device)
+        self.cap: dict = {}
+        self.max_seen: dict = {}
+        self._fx: dict = {}
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        self.overflows = 0         # passes that overflowed a slot (and were re-run)
         engine.set_owned(lg.n_owned)
 
     def _dense_bufs(self):
@@ -286,6 +328,46 @@ def _seg_starts(counts) -> np.ndarray:
     return np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
 
 
+class HaloOverflow(RuntimeError):
+    """A fixed-capacity halo exchange had more non-zero entries for a peer than its slot holds:
+    the pass's results are incomplete and it must be run again (the slots have been grown)."""
+
+
+def _fixed_bufs(r: "RankRun", what: str):
+    per = 2 if what == "reach" else 1
+    P = r.lg.P
+    cap = r.cap[what]
+    b = r._fx.get(what)
+    if b is None or b[0] != cap:
+        dev = r.send.device
+        b = r._fx[what] = (cap,
+                           torch.empty(P * cap * per, dtype=torch.int64, device=dev),   # send slots
+                           torch.empty(P * cap * per, dtype=torch.int64, device=dev),   # recv slots
+                           torch.zeros(P, dtype=torch.int64, device=dev),               # words sent
+                           torch.zeros(P, dtype=torch.int64, device=dev))               # words received
+    return b
+
+
+def _exchange_fixed(runs: list[RankRun], comm, what: str) -> None:
+    """The sparse halo exchange with fixed-capacity peer slots: device pack (counts and overflow
+    stay on the device), one equal-split all-to-all of the slots and one of the counts, device
+    unpack -- no host synchronisation per exchange (egr_plan_pack_sparse_cap)."""
+    items_d, items_c = [], []
+    for r in runs:
+        cap, sbuf, rbuf, scnt, rcnt = _fixed_bufs(r, what)
+        r.eng.pack_sparse_cap(what, r.send, r.seg_dev, sbuf, cap, scnt, r.overflow)
+        per = 2 if what == "reach" else 1
+        r.sent_bytes += 8 * len(r.lg.send_counts) * cap * per + 8 * len(r.lg.send_counts)
+        r.exchanges += 1
+        items_d.append((sbuf, rbuf))
+        items_c.append((scnt, rcnt))
+    comm.all_to_all_fixed(items_d)
+    comm.all_to_all_fixed(items_c)
+    for r in runs:
+        cap, _, rbuf, _, rcnt = _fixed_bufs(r, what)
+        r.eng.unpack_sparse_cap(what, r.recv_vertex, rbuf, cap, rcnt, r.recv_base)
+
+
 def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
     """The halo exchange with only the NON-ZERO entries on the wire (module doc).  Engines
     with native sparse packing (the HIP plan: egr_plan_pack_sparse / unpack_sparse) pack and
@@ -303,6 +385,7 @@ def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
         if buf is None or buf.numel() < max(cap, 1):
             buf = r._sx[what] = torch.empty(max(cap, 1), dtype=torch.int64, device=r.send.device)
         counts = r.eng.pack_sparse(what, r.send, r.send_seg, buf)
+        r.max_seen[what] = max(r.max_seen.get(what, 0), max(counts, default=0))
         n_words = [per * c for c in counts]
         r.sent_bytes += 8 * sum(n_words) + 8 * len(counts)
         r.exchanges += 1
@@ -390,20 +473,45 @@ def _exchange(runs: list[RankRun], comm, what: str) -> None:
 
 
 def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int,
-                    sparse: bool = True):
+                    sparse: bool = True, fixed: bool = False):
     """`hops` hops of propagation and reach on every local rank in `runs` (seeds and sources
     already set on their engines), halo exchanges between hops, then the merged global top-k.
-    Returns (ids int64 [B, k] global vertex ids (NO_NODE = none), scores f32 [B, k])."""
+    Returns (ids int64 [B, k] global vertex ids (NO_NODE = none), scores f32 [B, k]).
+    fixed=True: the exchanges use fixed-capacity peer slots with no host synchronisation; the
+    first such pass calibrates the slots over the host-count path (1.5x the largest per-peer
+    count seen), and a pass that overflows a slot raises HaloOverflow after growing it (the
+    caller sets seeds / sources again and re-runs -- run_partitioned_retry does that -- and the
+    re-run recalibrates)."""
+    use_fixed = fixed and sparse and all(r.cap for r in runs) and \
+        all(hasattr(r.eng, "pack_sparse_cap") for r in runs)
+    for r in runs:
+        r.overflow.zero_()
+        if fixed and sparse and not use_fixed:
+            r.max_seen = {}
     for h in range(hops):
         for r in runs:
             r.eng.hop()
-        xch = _exchange_sparse if sparse else _exchange
+        xch = _exchange_fixed if use_fixed else _exchange_sparse if sparse else _exchange
         if h + 1 < hops:
             xch(runs, comm, "scores")
         for r in runs:
             r.eng.reach_hop()
         if h + 1 < hops:
             xch(runs, comm, "reach")
+    if use_fixed:
+        if comm.any_flag([r.overflow for r in runs]):
+            for r in runs:
+                r.cap = {}                # the re-run calibrates again over the host counts
+                r.overflows += 1
+            raise HaloOverflow("a halo exchange overflowed its fixed peer slots (run again)")
+    elif fixed and sparse:
+        # calibration: the slots hold 1.5x the largest per-peer entry count of this pass (the
+        # same on every rank: the all-to-all needs equal block sizes)
+        for what in ("scores", "reach"):
+            m = max((r.max_seen.get(what, 0) for r in runs), default=0)
+            m = _max_over_ranks(comm, m)
+            for r in runs:
+                r.cap[what] = max(1024, (3 * m) // 2 + 1)
     cands = []
     for r in runs:
         r.eng.candidates(exclude_label)
@@ -425,3 +533,28 @@ def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k:
         ids, scs = torch.gather(ids, 1, o2)[:, :k], torch.gather(scs, 1, o2)[:, :k]
         out.append((ids.to(torch.int64), scs.to(torch.float32)))
     return out
+
+
+def _max_over_ranks(comm, x: int) -> int:
+    """max of an int over the process group (LocalComm: the value itself -- every local rank
+    is already in `runs`)."""
+    if not hasattr(comm, "dist"):
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64)
+    if not comm.gloo:
+        import torch as _t
+        t = t.to(_t.device("cuda", _t.cuda.current_device()))
+    comm.dist.all_reduce(t, op=comm.dist.ReduceOp.MAX, group=comm.group)
+    return int(t.item())
+
+
+def run_partitioned_retry(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int,
+                          reset, fixed: bool = True):
+    """run_partitioned with fixed-capacity slots, re-running once (after `reset()`, which sets
+    every engine's seeds and sources again) when a slot overflowed: the re-run goes over the
+    host-count path, which cannot overflow, and recalibrates the slots."""
+    try:
+        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed)
+    except HaloOverflow:
+        reset()
+        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed)

@@ -99,3 +99,59 @@ class CpuEngine:
 
     def scores_owned(self):
         return self.x[: self.owned]
+
+    # ---- the fixed-capacity sparse exchange (egr_plan_pack_sparse_cap / _unpack_sparse_cap) ----
+    def _row_words(self, what, r):
+        if what == "reach":
+            return self._words(r).view(np.int64)                         # [n][W] words
+        return self.x[r].view(np.int32).astype(np.int64) & 0xFFFFFFFF    # [n][B] value bits
+
+    def pack_sparse_cap(self, what, rows, seg_dev, out, peer_cap, counts, overflow):
+        r = rows.numpy().view(np.uint32)
+        seg = seg_dev.numpy()
+        vals = self._row_words(what, r)
+        width = vals.shape[1] if vals.ndim == 2 else 0
+        per = 2 if what == "reach" else 1
+        o = out.numpy()
+        for q in range(len(seg) - 1):
+            ent = []
+            for i in range(seg[q], seg[q + 1]):
+                for b in np.flatnonzero(vals[i]).tolist():
+                    ent.append(((i - seg[q]) * width + b, int(vals[i, b])))
+            if len(ent) > peer_cap:
+                overflow[0] = 1
+            ent = ent[:peer_cap]
+            base = q * peer_cap * per
+            for j, (idx, w) in enumerate(ent):
+                if per == 2:
+                    o[base + 2 * j], o[base + 2 * j + 1] = idx, w          # w: the signed word
+                else:
+                    o[base + j] = (idx << 32) | w
+            counts[q] = per * len(ent)
+
+    def unpack_sparse_cap(self, what, recv_vertex, entries, peer_cap, counts, rbase):
+        rv = recv_vertex.numpy().view(np.uint32)
+        e = entries.numpy()
+        rb = rbase.numpy()
+        per = 2 if what == "reach" else 1
+        width = self.W if what == "reach" else self.padded_cols
+        if what == "reach":
+            self.R[rv] = False
+        else:
+            self.x[rv] = 0.0
+        for s in range(len(rb)):
+            for j in range(int(counts[s]) // per):
+                if per == 2:
+                    idx = int(e[(s * peer_cap + j) * 2])
+                    w = int(e[(s * peer_cap + j) * 2 + 1]) & 0xFFFFFFFFFFFFFFFF
+                else:
+                    x = int(e[s * peer_cap + j])
+                    idx, w = x >> 32, x & 0xFFFFFFFF
+                row = rv[rb[s] + idx // width]
+                b = idx % width
+                if what == "reach":
+                    for t in range(64):
+                        if b * 64 + t < self.B:
+                            self.R[row, b * 64 + t] = bool((w >> t) & 1)
+                else:
+                    self.x[row, b] = np.array([w], np.uint32).view(np.float32)[0]

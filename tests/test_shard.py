@@ -77,7 +77,7 @@ def test_local_graphs_cover_the_global_csr(P):
             assert len(np.unique(sent[(r, lg.rank)])) == len(sent[(r, lg.rank)])
 
 
-def _rank_main(rank, P, port, q, sparse=True):
+def _rank_main(rank, P, port, q, sparse=True, fixed=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=P)
@@ -95,7 +95,24 @@ def _rank_main(rank, P, port, q, sparse=True):
         eng.set_sources(shard.local_sources(lg, V, src))
         run = shard.RankRun(lg, eng, torch.device("cpu"))
         inc = g.labels().index("Incident")
-        (ids, scores), = shard.run_partitioned([run], shard.TorchComm(), 3, inc, 6, sparse=sparse)
+        if fixed:
+            # calibrating pass, a pass on the fixed slots, then one whose slots are forced too
+            # small: it overflows, grows them and re-runs (run_partitioned_retry)
+            def reset():
+                eng.set_seeds(*shard.local_seeds(lg, V, sv, sc, ss))
+                eng.set_sources(shard.local_sources(lg, V, src))
+            comm = shard.TorchComm()
+            shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
+            assert run.cap["scores"] >= 1024
+            reset()
+            shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
+            run.cap = {"scores": 2, "reach": 2}
+            reset()
+            (ids, scores), = shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
+            assert run.cap["scores"] >= 1024           # recalibrated by the re-run
+        else:
+            (ids, scores), = shard.run_partitioned([run], shard.TorchComm(), 3, inc, 6,
+                                                   sparse=sparse)
         q.put((rank, lg.gid[: lg.n_owned], eng.scores_owned(), ids.numpy(), scores.numpy(),
                run.sent_bytes, 2 * run.halo_bytes_per_hop))
     finally:
@@ -108,14 +125,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("P,sparse", [(2, True), (2, False), (8, True)])
-def test_partitioned_protocol_gloo_world_size_2(P, sparse):
-    """(P = 8: the 8-GPU layout of the edge-cut path, every peer pair exchanging.)"""
+@pytest.mark.parametrize("P,sparse,fixed", [(2, True, False), (2, False, False), (8, True, False),
+                                            (2, True, True), (4, True, True)])
+def test_partitioned_protocol_gloo_world_size_2(P, sparse, fixed):
+    """(P = 8: the 8-GPU layout of the edge-cut path, every peer pair exchanging.  fixed: the
+    fixed-capacity slot exchange, calibrated, then overflowed and re-run.)"""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, P, port, q, sparse)) for r in range(P)]
+    procs = [ctx.Process(target=_rank_main, args=(r, P, port, q, sparse, fixed)) for r in range(P)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(P)]
@@ -132,7 +151,8 @@ def test_partitioned_protocol_gloo_world_size_2(P, sparse):
     covered = 0
     for rank, gids, owned_scores, ids, scores, sent, dense in res:
         # 2 exchanges (scores + reach) x 2 hops; the sparse one sends only non-zero entries
-        assert sent == dense if not sparse else 0 < sent < dense
+        if not fixed:
+            assert sent == dense if not sparse else 0 < sent < dense
         assert owned_scores.tobytes() == exp[gids].tobytes()          # bit-identical rows
         covered += len(gids)
         got = ids.astype(np.int64)

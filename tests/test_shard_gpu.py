@@ -221,3 +221,55 @@ def test_partitioned_plan_reruns_with_new_seeds(P, B):
             np.testing.assert_array_equal(reach, er[:, lg.gid[: lg.n_owned]])
             np.testing.assert_array_equal(ids.cpu().numpy(), e_ids.astype(np.int64), err_msg=f"run {t}")
             np.testing.assert_array_equal(scores.cpu().numpy(), e_sc, err_msg=f"run {t}")
+
+
+@pytest.mark.parametrize("P,B", [(2, 40), (3, 130), (4, 70)])
+def test_partitioned_fixed_slots_equal_oracle(P, B):
+    """The fixed-capacity halo exchange (egr_plan_pack_sparse_cap / unpack_sparse_cap: device
+    counts and overflow flag, equal-split all-to-all, no host read per exchange): a calibrating
+    pass over the host-count path, passes on the fixed slots with other seed sets, and a pass
+    whose slots are forced too small -- it overflows, recalibrates and re-runs
+    (run_partitioned_retry).  Every pass: owned scores, reach and merged top-k equal the oracle."""
+    from egraph import shard
+    from egraph.graph import Snapshot
+    g, sv, sc, ss, src = _graph(B, seed=120 + P, pods=2500)
+    rng = np.random.default_rng(P)
+    perm = rng.permutation(B).astype(np.uint32)
+    sets = [(sv, sc, ss), (sv, perm[sc], (ss * 1.5).astype(np.float32)), (sv, sc, ss), (sv, sc, ss)]
+    csr = g.csr()
+    vl, _, _, _ = g.export()
+    V, k = g.num_vertices, 8
+    inc = g.labels().index("Incident")
+    owner = shard.partition_vertices(csr["row_ptr"], vl, g.labels(), P)
+    runs = []
+    for r in range(P):
+        lg = shard.build_local(csr, vl, owner, r, P)
+        snap = Snapshot.from_csr(lg.row_ptr, lg.col, lg.meta, lg.val, lg.vlabel, g.labels())
+        plan = snap.plan(B, max_seeds=max(len(sv), 1), k=k)
+        runs.append(shard.RankRun(lg, plan, torch.device("cuda", 0)))
+        runs[-1].snap = snap
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    for t, (a, b, c) in enumerate(sets):
+        def reset():
+            for run in runs:
+                lv, lc, ls = shard.local_seeds(run.lg, V, a, b, c)
+                run.eng.set_seeds(_dev(lv), _dev(lc), _dev(ls))
+                run.eng.set_sources(_dev(shard.local_sources(run.lg, V, src)))
+        reset()
+        if t == 3:
+            for run in runs:
+                run.cap = {"scores": 1, "reach": 1}
+        fixed_before = all(run.cap for run in runs)
+        out = shard.run_partitioned_retry(runs, shard.LocalComm(), 3, inc, k, reset)
+        assert fixed_before == (t > 0)
+        assert all(run.cap["scores"] >= 1024 for run in runs)       # (re)calibrated
+        exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], a, b, c, B, 3)
+        e_ids, e_sc = oracle.topk(exp, er, vl, inc, k)
+        for run, (ids, scores) in zip(runs, out):
+            lg = run.lg
+            got = run.eng.read_scores().cpu().numpy()[: lg.n_owned]
+            assert got.tobytes() == exp[lg.gid[: lg.n_owned]].tobytes(), f"run {t}"
+            reach = run.eng.read_reach().cpu().numpy().view(np.uint64)[:, : lg.n_owned]
+            np.testing.assert_array_equal(reach, er[:, lg.gid[: lg.n_owned]])
+            np.testing.assert_array_equal(ids.cpu().numpy(), e_ids.astype(np.int64), err_msg=f"run {t}")
+            np.testing.assert_array_equal(scores.cpu().numpy(), e_sc, err_msg=f"run {t}")
