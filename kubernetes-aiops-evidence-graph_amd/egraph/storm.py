@@ -217,6 +217,49 @@ class RankStore:
         return self.ids[h].copy(), self.scores[h].copy(), int(self.tick[h])
 
 
+class PendingIndex:
+    """The storm's pending-id index: (hash of a candidate id ranked before a row's attached one,
+    incident handle, generation) entries, searchable by hash.  Entries arrive as hash-sorted
+    runs, one per tick; a query binary-searches every run.  Runs are merged (and retired
+    generations dropped) once there are more than MAX_RUNS of them, so an insert costs the size
+    of the tick's own entries, not of the whole index (np.insert into one sorted array copied
+    every resident entry on every tick)."""
+    MAX_RUNS = 8
+
+    def __init__(self):
+        self.runs: list[tuple[np.ndarray, np.ndarray, np.ndarray]] = []
+
+    def __len__(self) -> int:
+        return sum(len(r[0]) for r in self.runs)
+
+    def insert(self, h: np.ndarray, o: np.ndarray, g: np.ndarray, gen: np.ndarray) -> None:
+        order = np.argsort(h, kind="stable")
+        self.runs.append((h[order], o[order], g[order]))
+        if len(self.runs) > self.MAX_RUNS:
+            hh = np.concatenate([r[0] for r in self.runs])
+            oo = np.concatenate([r[1] for r in self.runs])
+            gg = np.concatenate([r[2] for r in self.runs])
+            live = gg == gen[oo]
+            hh, oo, gg = hh[live], oo[live], gg[live]
+            order = np.argsort(hh, kind="stable")
+            self.runs = [(hh[order], oo[order], gg[order])]
+
+    def hits(self, q: np.ndarray, gen: np.ndarray) -> set:
+        """Handles with a live entry whose hash is one of q's: per run, the runs of equal hashes
+        found by binary search."""
+        out = []
+        for rh, ro, rg in self.runs:
+            lo = np.searchsorted(rh, q, "left")
+            n = np.searchsorted(rh, q, "right") - lo
+            tot = int(n.sum())
+            if not tot:
+                continue
+            ix = np.repeat(lo - (np.cumsum(n) - n), n) + np.arange(tot)
+            o = ro[ix]
+            out.append(o[rg[ix] == gen[o]])
+        return set(np.unique(np.concatenate(out)).tolist()) if out else set()
+
+
 class StormEngine:
     COL_BUCKETS = (64, 256, 1024, 4096)
 
@@ -240,9 +283,7 @@ class StormEngine:
         # handle, generation); an entry is live while its generation is the incident's current
         # one.  A hash match only ever adds an incident to the re-attached set (a spurious
         # match re-attaches and re-ranks it exactly: harmless).
-        self._pend_h = np.zeros(0, np.int64)
-        self._pend_o = np.zeros(0, np.int64)
-        self._pend_g = np.zeros(0, np.int64)
+        self._pending = PendingIndex()
         self._gen = np.zeros(0, np.int64)
         self._frontiers: dict[int, object] = {}
         self.ranks = RankStore(k)
@@ -254,6 +295,10 @@ class StormEngine:
         self._chk_v = torch.zeros(0, dtype=torch.int64, device=self.dev)
         self._chk_o = torch.zeros(0, dtype=torch.int64, device=self.dev)
         self._stale = 0
+        # objects the tick is done with (evidence rows, incident cases): dropped while the GPU
+        # runs the re-rank, so their deallocation overlaps the device work instead of adding to
+        # the host stages
+        self._drop: list = []
 
     # ---- frontier per column bucket, grown / recreated as needed ---------------------------
     def _frontier(self, n_cols: int, n_seeds: int):
@@ -282,6 +327,8 @@ class StormEngine:
             for j, x in enumerate(need):
                 x.cand = (batch, j)
                 if not self.keep_evidence:
+                    # (the rows are freed in _rank, while the tick's frontier launch runs)
+                    self._drop.append(x.evidence)
                     x.evidence = None
         t1 = time.perf_counter()
         if not xs:
@@ -303,19 +350,8 @@ class StormEngine:
             self._gen = np.concatenate([self._gen, np.zeros(max(top - len(self._gen), 1024), np.int64)])
         self._gen[hs] += 1
         if len(before):
-            h = hashes[before]
-            order = np.argsort(h, kind="stable")
-            h, oh = h[order], hs[bcol.astype(np.int64)[order]]
-            # merge into the hash-sorted index (O(entries), no re-sort of the resident part)
-            at = np.searchsorted(self._pend_h, h)
-            self._pend_h = np.insert(self._pend_h, at, h)
-            self._pend_o = np.insert(self._pend_o, at, oh)
-            self._pend_g = np.insert(self._pend_g, at, self._gen[oh])
-            if len(self._pend_h) > 4096:              # drop retired entries once they dominate
-                live = self._pend_g == self._gen[self._pend_o]
-                if live.sum() * 2 < len(live):
-                    self._pend_h, self._pend_o, self._pend_g = (
-                        self._pend_h[live], self._pend_o[live], self._pend_g[live])
+            oh = hs[bcol.astype(np.int64)]
+            self._pending.insert(hashes[before], oh, self._gen[oh], self._gen)
         self.last_reseed = {"incidents": len(xs), "new": len(need), "candidates_ms": (t1 - t0) * 1e3,
                             "attach_ms": (t2 - t1) * 1e3, "pending_ms": (time.perf_counter() - t2) * 1e3}
 
@@ -327,21 +363,12 @@ class StormEngine:
         return x.cand
 
     def _pending_hit(self, ids: list) -> set:
-        """Incidents with a live pending entry whose hash matches one of these ids: a binary
-        search of the ids' hashes in the hash-sorted index, then the runs of equal hashes."""
-        if not ids or not len(self._pend_h):
+        """Incidents with a live pending entry whose hash matches one of these ids."""
+        if not ids or not len(self._pending):
             return set()
         from egraph import _lib
         q = np.frombuffer(_lib.pyhost.hash_ids(ids), np.int64)    # (seed_keys' id hashes)
-        lo = np.searchsorted(self._pend_h, q, "left")
-        n = np.searchsorted(self._pend_h, q, "right") - lo
-        tot = int(n.sum())
-        if not tot:
-            return set()
-        ix = np.repeat(lo - (np.cumsum(n) - n), n) + np.arange(tot)
-        o = self._pend_o[ix]
-        o = o[self._pend_g[ix] == self._gen[o]]
-        return set(np.unique(o).tolist())
+        return self._pending.hits(q, self._gen)
 
     def _check_parts(self, handles) -> tuple[torch.Tensor, torch.Tensor]:
         """(vertex, incident) pairs of these incidents: each incident vertex, then every seed
@@ -382,6 +409,8 @@ class StormEngine:
             src[:n] = np.where(vx >= 0, vx, NO_NODE).astype(np.uint32)
             fr.set_seeds(to_device(sv, self.dev), to_device(sc, self.dev), to_device(ss, self.dev))
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
+            if lo + top >= len(hs_all):
+                self._drop.clear()           # host deallocation overlapping the last launch
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
             fr.adapt()              # overflowing columns: the wide-table retry from the next call on
@@ -420,6 +449,7 @@ class StormEngine:
             case = make_case(h, int(i))
             t_collect += time.perf_counter() - tc
             assert h == len(self.incidents), "incident handles are dense and ordered"
+            self._drop.append(case)
             self.incidents.append(OpenIncident(h, case.incident_id, case.evidence
                                                if self.keep_evidence or self.owns(h) else None,
                                                store=self.ranks, seeds=self.seeds, vtx=self.vtx))
@@ -485,6 +515,7 @@ class StormEngine:
             self._stale = 0
         t.append(time.perf_counter())
         self._rank(sorted(affected))
+        self._drop.clear()                   # (a tick with nothing to re-rank)
         torch.cuda.synchronize(self.dev)
         t.append(time.perf_counter())
         self.ticks += 1

@@ -209,8 +209,8 @@ def test_attach_found_idx_matches_pending_sets():
 
 
 def test_storm_pending_index_lookup():
-    """StormEngine._pending_hit over a hash-sorted index with duplicate hashes and retired
-    generations (host logic only; no device)."""
+    """StormEngine._pending_hit over the pending index (PendingIndex: hash-sorted runs, merged
+    past MAX_RUNS) with duplicate hashes and retired generations (host logic only; no device)."""
     import types
     import numpy as np
     from egraph.storm import StormEngine
@@ -222,11 +222,16 @@ def test_storm_pending_index_lookup():
     h = np.frombuffer(_lib.pyhost.hash_ids([e[0] for e in ent]), np.int64)
     o = np.array([e[1] for e in ent], np.int64)
     g = np.array([e[2] for e in ent], np.int64)
-    k = np.argsort(h, kind="stable")
-    eng = types.SimpleNamespace(_pend_h=h[k], _pend_o=o[k], _pend_g=g[k], _gen=gen)
-    for q in ([], ids[:1], ids[::7], ["absent"], ids):
-        want = {e[1] for e in ent if e[0] in set(q) and e[2] == gen[e[1]]}
-        assert StormEngine._pending_hit(eng, q) == want
+    from egraph.storm import PendingIndex
+    for runs in (1, 5, 12):                   # one run; several; merged past MAX_RUNS
+        idx = PendingIndex()
+        for part in np.array_split(np.arange(len(ent)), runs):
+            idx.insert(h[part], o[part], g[part], gen)
+        assert len(idx.runs) <= PendingIndex.MAX_RUNS
+        eng = types.SimpleNamespace(_pending=idx, _gen=gen)
+        for q in ([], ids[:1], ids[::7], ["absent"], ids):
+            want = {e[1] for e in ent if e[0] in set(q) and e[2] == gen[e[1]]}
+            assert StormEngine._pending_hit(eng, q) == want
 
 
 def test_keyed_candidates_match_flat_ones():
