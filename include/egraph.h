@@ -187,6 +187,11 @@ int64_t egr_graph_vertex_id(const egr_graph* g, int64_t v, char* buf, int64_t ca
 /* first vertex (lowest index) whose id equals each query id, -1 if none */
 int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
                      int32_t* out_vertex);
+/* MATCH (n:label {id: $id}) for n ids: the vertex carrying each id under its label (labels as a
+ * blob + offsets, one per id), -1 if none (neo4j.py:169-202's incident MATCH, the GraphService
+ * incident lookups; replaces a host dict mirror of every (label, id) pair). */
+int egr_graph_lookup_labeled(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
+                             const char* label_blob, const int64_t* label_off, int32_t* out_vertex);
 /* egr_graph_lookup of ONE id given as bytes (len bytes, not NUL-terminated): the first vertex
  * carrying it, -1 if none (or bad arguments).  Read-only: safe from several threads at once
  * while no merge runs (the native seed attachment calls it from its worker threads; the

@@ -137,9 +137,7 @@ void idx_put(egr_graph* g, const std::string& id, int32_t v) {
   ++g->idx_n;
 }
 
-inline int32_t idx_find(const egr_graph* g, const char* p, size_t n) {
-  if (g->idx.empty()) return -1;
-  const uint64_t h = id_hash(p, n);
+inline int32_t idx_find_h(const egr_graph* g, const char* p, size_t n, uint64_t h) {
   const uint32_t tag = (uint32_t)(h >> 32) | 1u;
   const size_t m = g->idx.size() - 1;
   for (size_t i = (size_t)h & m;; i = (i + 1) & m) {
@@ -152,6 +150,46 @@ inline int32_t idx_find(const egr_graph* g, const char* p, size_t n) {
   }
 }
 
+inline int32_t idx_find(const egr_graph* g, const char* p, size_t n) {
+  if (g->idx.empty()) return -1;
+  return idx_find_h(g, p, n, id_hash(p, n));
+}
+
+// idx_find of n ids (blob + offsets) into out.  A lookup is three dependent cache misses (its
+// index slot, the vertex's std::string, the string's bytes) into tables far larger than the
+// caches; they are software-pipelined over groups of LB ids -- every id's slot prefetched, then
+// every hit's string object, then its bytes -- so the misses of a group overlap instead of
+// queueing one after another.
+void batch_find(const egr_graph* g, const char* blob, const int64_t* off, int64_t n, int32_t* out) {
+  if (g->idx.empty()) {
+    for (int64_t i = 0; i < n; ++i) out[i] = -1;
+    return;
+  }
+  constexpr int LB = 32;
+  const size_t m = g->idx.size() - 1;
+  uint64_t h[LB];
+  for (int64_t i0 = 0; i0 < n; i0 += LB) {
+    const int c = (int)std::min<int64_t>(LB, n - i0);
+    for (int j = 0; j < c; ++j) {
+      const int64_t i = i0 + j;
+      h[j] = id_hash(blob + off[i], (size_t)(off[i + 1] - off[i]));
+      __builtin_prefetch(&g->idx[(size_t)h[j] & m]);
+    }
+    for (int j = 0; j < c; ++j) {
+      const egr_graph::IdSlot e = g->idx[(size_t)h[j] & m];
+      if (e.tag == ((uint32_t)(h[j] >> 32) | 1u)) __builtin_prefetch(&g->vid[e.v]);
+    }
+    for (int j = 0; j < c; ++j) {
+      const egr_graph::IdSlot e = g->idx[(size_t)h[j] & m];
+      if (e.tag == ((uint32_t)(h[j] >> 32) | 1u)) __builtin_prefetch(g->vid[e.v].data());
+    }
+    for (int j = 0; j < c; ++j) {
+      const int64_t i = i0 + j;
+      out[i] = idx_find_h(g, blob + off[i], (size_t)(off[i + 1] - off[i]), h[j]);
+    }
+  }
+}
+
 // The vertices carrying an id (creation order): none, its one vertex, or its multi list.
 struct IdVerts {
   const int32_t* p;
@@ -159,9 +197,8 @@ struct IdVerts {
   int32_t one;
 };
 
-inline IdVerts id_vertices(const egr_graph* g, const char* p, size_t n) {
+inline IdVerts verts_of(const egr_graph* g, int32_t v) {
   IdVerts r{nullptr, 0, -1};
-  const int32_t v = idx_find(g, p, n);
   if (v < 0) return r;
   if (g->vmulti[v]) {
     const auto& vs = g->multi.at(v);
@@ -245,15 +282,30 @@ int egr_graph_merge_edges(egr_graph* g, const char* src_blob, const int64_t* src
   if (!g || n < 0 || (n > 0 && (!src_blob || !src_off || !dst_blob || !dst_off || !type_blob || !type_off)))
     return egr::fail(EGR_EINVAL, "egr_graph_merge_edges: bad arguments");
   int64_t created = 0;
+  // MATCH never creates vertices: every endpoint id resolves up front, in pipelined batches
+  std::vector<int32_t> fs((size_t)n), fd((size_t)n);
+  batch_find(g, src_blob, src_off, n, fs.data());
+  batch_find(g, dst_blob, dst_off, n, fd.data());
+  // the types of the edges whose endpoints both exist (a MATCH that fails names no type), then
+  // the MERGE loop with each edge's set slot prefetched PF edges ahead
+  std::vector<int8_t> ty((size_t)n, -1);
   for (int64_t i = 0; i < n; ++i) {
-    const std::string_view sid = str_at(src_blob, src_off, i);
-    const IdVerts sv = id_vertices(g, sid.data(), sid.size());
-    if (!sv.n) continue;
-    const std::string_view did = str_at(dst_blob, dst_off, i);
-    const IdVerts dv = id_vertices(g, did.data(), did.size());
-    if (!dv.n) continue;
-    int t = intern(g->rtypes, str_at(type_blob, type_off, i), 127, "relationship types");
+    if (fs[(size_t)i] < 0 || fd[(size_t)i] < 0) continue;
+    const int t = intern(g->rtypes, str_at(type_blob, type_off, i), 127, "relationship types");
     if (t < 0) return t;
+    ty[(size_t)i] = (int8_t)t;
+  }
+  constexpr int64_t PF = 16;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i + PF < n) {
+      const size_t j = (size_t)(i + PF);
+      if (ty[j] >= 0 && !g->vmulti[fs[j]] && !g->vmulti[fd[j]] && !g->eset.empty())
+        __builtin_prefetch(&g->eset[(size_t)edge_hash(fs[j], fd[j], ty[j]) & (g->eset.size() - 1)]);
+    }
+    const int t = ty[(size_t)i];
+    if (t < 0) continue;
+    const IdVerts sv = verts_of(g, fs[(size_t)i]);
+    const IdVerts dv = verts_of(g, fd[(size_t)i]);
     for (size_t a = 0; a < sv.n; ++a)
       for (size_t b = 0; b < dv.n; ++b) {
         const int32_t s = sv.p ? sv.p[a] : sv.one, d = dv.p ? dv.p[b] : dv.one;
@@ -321,8 +373,32 @@ int egr_graph_lookup(const egr_graph* g, const char* blob, const int64_t* off, i
                      int32_t* out_vertex) {
   if (!g || n < 0 || (n > 0 && (!blob || !off || !out_vertex)))
     return egr::fail(EGR_EINVAL, "egr_graph_lookup: bad arguments");
-  for (int64_t i = 0; i < n; ++i)
-    out_vertex[i] = idx_find(g, blob + off[i], (size_t)(off[i + 1] - off[i]));
+  batch_find(g, blob, off, n, out_vertex);
+  return EGR_OK;
+}
+
+int egr_graph_lookup_labeled(const egr_graph* g, const char* blob, const int64_t* off, int64_t n,
+                             const char* label_blob, const int64_t* label_off, int32_t* out_vertex) {
+  if (!g || n < 0 || (n > 0 && (!blob || !off || !label_blob || !label_off || !out_vertex)))
+    return egr::fail(EGR_EINVAL, "egr_graph_lookup_labeled: bad arguments");
+  batch_find(g, blob, off, n, out_vertex);
+  for (int64_t i = 0; i < n; ++i) {
+    const IdVerts vs = verts_of(g, out_vertex[i]);
+    out_vertex[i] = -1;
+    if (!vs.n) continue;
+    const std::string_view lab = str_at(label_blob, label_off, i);
+    int li = -1;
+    for (size_t j = 0; j < g->labels.size() && li < 0; ++j)
+      if (g->labels[j] == lab) li = (int)j;
+    if (li < 0) continue;
+    for (size_t a = 0; a < vs.n; ++a) {
+      const int32_t v = vs.p ? vs.p[a] : vs.one;
+      if (g->vlabel[(size_t)v] == li) {
+        out_vertex[i] = v;
+        break;
+      }
+    }
+  }
   return EGR_OK;
 }
 

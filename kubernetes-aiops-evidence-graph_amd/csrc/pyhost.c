@@ -2458,6 +2458,57 @@ done:
   return out;
 }
 
+/* attach_idx(found, count) -> (vertex u32 [attached rows], ok u8 [rows], before i64 [m],
+ * before_row i64 [m]): SeedCandidates.attach_found_idx's index work in one pass.  found: int64
+ * bytes, the graph vertex of each flat candidate id (-1 absent); count: int64 bytes, the ids per
+ * row.  A row attaches to its first present id (ok[r] = 1, its vertex appended in row order);
+ * `before` lists the flat indices of the ids ranked ahead of it (every id of an unattached row)
+ * with their rows. */
+static PyObject* attach_idx(PyObject* self, PyObject* args) {
+  Py_buffer fb, cb;
+  if (!PyArg_ParseTuple(args, "y*y*", &fb, &cb)) return NULL;
+  PyObject* out = NULL;
+  const int64_t* found = (const int64_t*)fb.buf;
+  const int64_t* count = (const int64_t*)cb.buf;
+  const Py_ssize_t n = fb.len / (Py_ssize_t)sizeof(int64_t);
+  const Py_ssize_t rows = cb.len / (Py_ssize_t)sizeof(int64_t);
+  uint32_t* sv = PyMem_Malloc(sizeof(uint32_t) * (size_t)(rows + 1));
+  uint8_t* ok = PyMem_Malloc((size_t)rows + 1);
+  int64_t* bef = PyMem_Malloc(sizeof(int64_t) * (size_t)(n + 1));
+  int64_t* brow = PyMem_Malloc(sizeof(int64_t) * (size_t)(n + 1));
+  Py_ssize_t k = 0, m = 0, i = 0;
+  if (!sv || !ok || !bef || !brow) { PyErr_NoMemory(); goto done; }
+  for (Py_ssize_t r = 0; r < rows; ++r) {
+    const int64_t c = count[r];
+    if (c < 0 || i + c > n) {
+      PyErr_SetString(PyExc_ValueError, "attach_idx: counts exceed the candidate ids");
+      goto done;
+    }
+    ok[r] = 0;
+    for (int64_t j = 0; j < c; ++j, ++i) {
+      if (ok[r]) continue;
+      if (found[i] >= 0) {
+        ok[r] = 1;
+        sv[k++] = (uint32_t)found[i];
+      } else {
+        bef[m] = (int64_t)i;
+        brow[m++] = (int64_t)r;
+      }
+    }
+  }
+  out = Py_BuildValue("(y#y#y#y#)", (const char*)sv, k * (Py_ssize_t)sizeof(uint32_t),
+                      (const char*)ok, rows, (const char*)bef, m * (Py_ssize_t)sizeof(int64_t),
+                      (const char*)brow, m * (Py_ssize_t)sizeof(int64_t));
+done:
+  PyMem_Free(sv);
+  PyMem_Free(ok);
+  PyMem_Free(bef);
+  PyMem_Free(brow);
+  PyBuffer_Release(&fb);
+  PyBuffer_Release(&cb);
+  return out;
+}
+
 /* str_blob(list of str) -> (UTF-8 blob bytes, int64 offsets [n+1] as bytes), or None when the
  * argument is not an exact list of exact strs (egraph/graph.py str_blob then builds it in
  * Python).  The C-ABI's string arrays for MERGE batches and lookups: one pass for the lengths,
@@ -2580,6 +2631,7 @@ static PyMethodDef methods[] = {
     {"entity_rows", entity_rows, METH_VARARGS, "frontier top-k -> ranked root-cause entity dicts"},
     {"seed_keys", seed_keys, METH_VARARGS, "evidence rows -> seed candidates as a keyed blob"},
     {"hash_ids", hash_ids, METH_O, "64-bit hashes of ids' UTF-8 bytes"},
+    {"attach_idx", attach_idx, METH_VARARGS, "first present candidate per row + the ids before it"},
     {"str_blob", str_blob, METH_O, "list of str -> (UTF-8 blob, int64 offsets)"},
     {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
     {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},

@@ -91,6 +91,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_graph_rel_type_name": (I64, [P, I32, C.c_char_p, I64]),
     "egr_graph_vertex_id": (I64, [P, I64, C.c_char_p, I64]),
     "egr_graph_lookup": (C.c_int, [P, C.c_char_p, P, I64, P]),
+    "egr_graph_lookup_labeled": (C.c_int, [P, C.c_char_p, P, I64, C.c_char_p, P, P]),
     "egr_graph_find": (I32, [P, C.c_char_p, I64]),
     "egr_graph_export": (C.c_int, [P, P, P, P, P]),
     "egr_graph_csr": (C.c_int, [P, P, I32, P, P, P, P]),

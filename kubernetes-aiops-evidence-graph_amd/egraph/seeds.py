@@ -176,16 +176,13 @@ class SeedCandidates:
             z = np.zeros(0, np.int64)
             return (np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.float32), z,
                     np.zeros(0, np.uint32))
-        found = np.asarray(found).astype(np.int64)
-        n = self.n_flat
-        starts = np.concatenate([[0], np.cumsum(self.count)[:-1]])
-        pos = np.where(found >= 0, np.arange(n), n)
-        first = np.minimum.reduceat(pos, starts)
-        ok = first < n
-        before = np.flatnonzero(np.arange(n) < np.repeat(np.where(ok, first, n), self.count))
-        row_of = np.repeat(np.arange(len(self.count)), self.count)
-        return (found[first[ok]].astype(np.uint32), self.col[ok], self.val[ok], before,
-                self.col[row_of[before]])
+        from . import _lib
+        found = np.ascontiguousarray(found, np.int64)
+        sv, ok, before, brow = _lib.pyhost.attach_idx(found, np.ascontiguousarray(self.count, np.int64))
+        ok = np.frombuffer(ok, np.bool_)
+        before = np.frombuffer(before, np.int64)
+        return (np.frombuffer(sv, np.uint32), self.col[ok], self.val[ok], before,
+                self.col[np.frombuffer(brow, np.int64)])
 
     def attach_found(self, found: np.ndarray, pending: list | None = None):
         """attach() with the graph lookup of self.flat already done (callers batch it)."""

@@ -295,9 +295,9 @@ class StormEngine:
         self._chk_v = torch.zeros(0, dtype=torch.int64, device=self.dev)
         self._chk_o = torch.zeros(0, dtype=torch.int64, device=self.dev)
         self._stale = 0
-        # objects the tick is done with (evidence rows, incident cases): dropped while the GPU
-        # runs the re-rank, so their deallocation overlaps the device work instead of adding to
-        # the host stages
+        # objects the tick is done with (the new incidents' evidence rows once their candidates
+        # are extracted, the incident cases once MERGEd): freed at the end of the tick, in a
+        # stage of their own (release_host: ~0.4 us per evidence row on the GPU box)
         self._drop: list = []
 
     # ---- frontier per column bucket, grown / recreated as needed ---------------------------
@@ -327,8 +327,7 @@ class StormEngine:
             for j, x in enumerate(need):
                 x.cand = (batch, j)
                 if not self.keep_evidence:
-                    # (the rows are freed in _rank, while the tick's frontier launch runs)
-                    self._drop.append(x.evidence)
+                    self._drop.append(x.evidence)     # (freed at the end of the tick)
                     x.evidence = None
         t1 = time.perf_counter()
         if not xs:
@@ -409,8 +408,6 @@ class StormEngine:
             src[:n] = np.where(vx >= 0, vx, NO_NODE).astype(np.uint32)
             fr.set_seeds(to_device(sv, self.dev), to_device(sc, self.dev), to_device(ss, self.dev))
             ids, scores = fr.run(to_device(src, self.dev), hops=self.hops, exclude_label=inc_label)
-            if lo + top >= len(hs_all):
-                self._drop.clear()           # host deallocation overlapping the last launch
             ids = ids.cpu().numpy().view(np.uint32)
             scores = scores.cpu().numpy()
             fr.adapt()              # overflowing columns: the wide-table retry from the next call on
@@ -515,8 +512,9 @@ class StormEngine:
             self._stale = 0
         t.append(time.perf_counter())
         self._rank(sorted(affected))
-        self._drop.clear()                   # (a tick with nothing to re-rank)
         torch.cuda.synchronize(self.dev)
+        t.append(time.perf_counter())
+        self._drop.clear()
         t.append(time.perf_counter())
         self.ticks += 1
         ms = [(b - a) * 1e3 for a, b in zip(t, t[1:])]
@@ -525,7 +523,7 @@ class StormEngine:
                 "new_vertices": n_v, "new_edges": n_e, "affected": len(affected),
                 "open_incidents": len(self.incidents),
                 "ms": dict(zip(("fingerprint_dedup", "merge_host", "csr_update", "affected", "seeds_host",
-                               "rerank"), ms)),
+                               "rerank", "release_host"), ms)),
                 "collect_ms": t_collect * 1e3, "reseed": dict(self.last_reseed)}
 
     def rankings(self) -> list[tuple[np.ndarray, np.ndarray]]:

@@ -175,12 +175,12 @@ class GraphService:
         if g.num_vertices == 0:
             return [[] for _ in incident_ids]
         clock = _StageClock(stages)
-        vo = g.vertex_of
-        keys = []
-        for iid in incident_ids:
-            iid = str(iid)
-            v = vo.get(("Incident", iid))
-            keys.append(v if v is not None else vo.get(("Incident", f"incident:{iid}"), -1))
+        ids = [str(i) for i in incident_ids]
+        keys = g.lookup_labeled(ids, "Incident")
+        miss = np.flatnonzero(keys < 0)
+        if len(miss):                        # the collectors' prefixed form of a bare id
+            keys[miss] = g.lookup_labeled([f"incident:{ids[j]}" for j in miss.tolist()], "Incident")
+        keys = keys.tolist()
         clock.lap("incident_lookup")
         sv, sc, ss = seeds_for_batch(g, evidence_lists)
         clock.lap("seed_attach")
@@ -281,12 +281,12 @@ class GraphService:
         empty = {"nodes": [], "relationships": []}
         if g.num_vertices == 0 or not incident_ids:
             return [dict(empty) for _ in incident_ids]
-        keys = []
-        for iid in incident_ids:
-            iid = str(iid)
-            if ("Incident", iid) not in g.vertex_of and resolve_bare_uuid:
-                iid = f"incident:{iid}"
-            keys.append(g.vertex_of.get(("Incident", iid), -1))
+        ids = [str(i) for i in incident_ids]
+        keys = g.lookup_labeled(ids, "Incident")
+        miss = np.flatnonzero(keys < 0)
+        if resolve_bare_uuid and len(miss):
+            keys[miss] = g.lookup_labeled([f"incident:{ids[j]}" for j in miss.tolist()], "Incident")
+        keys = keys.tolist()
         plan = cls._plan(len(keys))
         dev = plan.dev
         # -1 as int32 is EGR_NO_NODE as u32: an empty column
