@@ -766,22 +766,16 @@ __global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t*
   if (q <= P) out[q] = off[seg[q]];
 }
 
-// fixed capacity: words per peer (capped at its slot) and the overflow flag
-__global__ void sx_capcount_kernel(const int64_t* __restrict__ bound, int P, int per, int64_t peer_cap,
-                                   int64_t* __restrict__ counts, uint32_t* __restrict__ overflow) {
-  const int q = threadIdx.x;
-  if (q >= P) return;
-  const int64_t c = bound[q + 1] - bound[q];
-  if (c > peer_cap) atomicOr(overflow, 1u);
-  counts[q] = per * (c < peer_cap ? c : peer_cap);
-}
-
 // The exchange kernels run ONE WAVE PER ROW, four per 256-thread block, in a grid of at most
 // SX_MAX_BLOCKS blocks that strides over the rows: a boundary row is cheap, and a block (or a
 // wave) per row launched them bound by workgroup dispatch (~120k rows per C4 exchange at P = 8).
 constexpr int SX_ROWS = 4;
 constexpr int64_t SX_MAX_BLOCKS = 2048;      // grid-stride beyond this (8 blocks per CU)
 inline dim3 sx_grid(int64_t n) { return dim3((unsigned)std::min<int64_t>((n + SX_ROWS - 1) / SX_ROWS, SX_MAX_BLOCKS)); }
+// the lane-per-row work map kernels: 64 rows per wave, four waves per block
+inline dim3 sx_lane_grid(int64_t n) {
+  return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, SX_MAX_BLOCKS)));
+}
 
 // Sender, pass 1: the row's non-zero count, and a bit per 32-column group that holds any
 // (masks [n_rows][MW] u32) so that pass 2 reads only those groups; score rows of a partitioned
@@ -839,15 +833,11 @@ __device__ __forceinline__ int kth_bit(const uint32_t* __restrict__ m, int MW, i
 // Sender, pass 2: the non-zero entries of the row's marked groups, in column order, at the
 // row's offset (the exclusive scan of pass 1's counts).  Each half-wave takes one marked group
 // per round.
-// Fixed-capacity mode (bound != nullptr, egr_plan_pack_sparse_cap): peer q's entries start at
-// out[q * peer_cap * per] instead of its offset in one contiguous list (bound[q] = the offset of
-// q's first entry in that list); entries past peer_cap are dropped (the pack flags the overflow).
 __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ X,
     const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
     const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
     const int64_t* __restrict__ off, const uint32_t* __restrict__ masks, int MW,
-    int64_t* __restrict__ out, int64_t cap, const int64_t* __restrict__ bound = nullptr,
-    int64_t peer_cap = 0) {
+    int64_t* __restrict__ out, int64_t cap) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
   for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   uint32_t mk[EGR_SX_MASK_WORDS];
@@ -863,13 +853,8 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
   while (q + 1 < P && seg[q + 1] <= r) ++q;
   const int64_t rl = r - seg[q];
   int64_t pos = off[r];
-  int64_t lim = cap;                     // entries (scores) / words (reach) the target holds
+  const int64_t lim = cap;               // entries (scores) / words (reach) the target holds
   int64_t* dst = out;
-  if (bound) {                           // fixed capacity: q's own slot, positions within q
-    pos -= bound[q];
-    dst = out + (size_t)q * peer_cap * (reach ? 2 : 1);
-    lim = reach ? 2 * peer_cap : peer_cap;
-  }
   for (int base = 0; base < nset; base += 2) {
     const int g = base + half < nset ? kth_bit(mk, MW, base + half) : -1;
     const int b = g >= 0 ? 32 * g + hl : width;
@@ -894,6 +879,143 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     }
     pos += __popcll(m);
   }
+  }
+}
+
+// The work map of 64 exchange rows, one lane per row (the fixed-capacity pack and unpack): a
+// bit per 64-column chunk of the row that may hold a non-zero -- for a score row, the chunks
+// over the tiles its flags mark (every chunk without flags); for a reach row, the chunks holding
+// a non-zero word (the row's W <= 64 words... read by the lane: RS-word rows, 16-B loads).
+// One lane per row puts 64 rows' dependent loads (row id, then its flags) in flight at once;
+// the wave then walks only the rows with work (a row a wave at a time had ~15 rows of round
+// trips per wave queued one after another: ~100 us per C4 exchange for rows that were nearly
+// all empty).
+__device__ __forceinline__ uint64_t sx_chunk_mask(const uint64_t* __restrict__ R, uint32_t RS,
+                                                  int width, bool reach, uint32_t v,
+                                                  const uint8_t* __restrict__ fl, uint32_t ntiles,
+                                                  int TW) {
+  const int nchunks = (width + 63) / 64;
+  const uint64_t all = nchunks >= 64 ? ~0ull : ((1ull << nchunks) - 1ull);
+  if (reach) {                                  // width = W words (one chunk while W <= 64)
+    const uint64_t* row = R + (size_t)v * RS;
+    uint64_t any = 0;
+    for (int w = 0; w < width; ++w) any |= row[w];
+    return any ? all : 0ull;
+  }
+  if (!fl || ntiles > 64u) return all;
+  uint64_t m = 0;
+  for (uint32_t t = 0; t < ntiles; ++t)
+    if (fl[t]) {
+      const int c0 = (int)(t * TW) / 64, c1 = (int)(t * TW + TW - 1) / 64;
+      for (int c = c0; c <= c1; ++c) m |= 1ull << c;
+    }
+  return m;
+}
+
+// Fixed-capacity send in one launch (egr_plan_pack_sparse_cap): for each row with work, per
+// 64-column chunk holding non-zeros, one atomic on the peer's cursor (zeroed before the launch)
+// reserves that many entries of its slot and the wave writes them there.  The order inside a
+// slot is the order the reservations happened to run in; the receiver's scatter is order-free
+// (every (row, column) appears once), so the exchanged values are bit-identical to the ordered
+// two-pass pack, with no count pass, scan or per-peer bound kernels.  cursor[q] ends as q's entry
+// count (it may exceed peer_cap: the entries past the slot are dropped and `overflow` is set).
+__global__ __launch_bounds__(256) void sx_emit_slots_kernel(const float* __restrict__ X,
+    const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
+    const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
+    const uint8_t* __restrict__ nzf, uint32_t ntiles, int64_t* __restrict__ out,
+    int64_t peer_cap, unsigned long long* __restrict__ cursor, uint32_t* __restrict__ overflow) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
+    const int64_t rmine = r0 + lane;
+    uint32_t vm = 0;
+    uint64_t cm = 0;
+    if (rmine < n) {
+      vm = rows[rmine];
+      cm = sx_chunk_mask(R, RS, width, reach, vm, nzf ? nzf + (size_t)vm * ntiles : nullptr,
+                         ntiles, TW);
+    }
+    for (uint64_t todo = __ballot(cm != 0ull); todo; todo &= todo - 1ull) {
+      const int l = __ffsll((long long)todo) - 1;
+      const int64_t r = r0 + l;
+      const uint32_t v = (uint32_t)__shfl((int)vm, l, 64);
+      const uint64_t m = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cm >> 32), l, 64) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)cm, l, 64);
+      int q = 0;
+      while (q + 1 < P && seg[q + 1] <= r) ++q;
+      const int64_t rl = r - seg[q];
+      const uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
+      int64_t* dst = out + (size_t)q * peer_cap * (reach ? 2 : 1);
+      for (uint64_t cs = m; cs; cs &= cs - 1ull) {
+        const int b = 64 * (__ffsll((long long)cs) - 1) + lane;
+        uint64_t w = 0;
+        const bool nz = b < width && (!fl || fl[b / TW]) && sx_value(X, R, V, TW, RS, v, b, reach, &w);
+        const uint64_t bm = __ballot(nz);
+        if (!bm) continue;
+        const int c = __popcll(bm);
+        unsigned long long base = 0;
+        if (lane == 0) {
+          base = atomicAdd(&cursor[q], (unsigned long long)c);
+          if ((int64_t)base + c > peer_cap) atomicOr(overflow, 1u);
+        }
+        const int64_t pos = (int64_t)__shfl((long long)base, 0, 64) + __popcll(bm & lt);
+        if (nz && pos < peer_cap) {
+          const int64_t idx = rl * width + b;
+          if (reach) {
+            dst[2 * pos] = idx;
+            dst[2 * pos + 1] = (int64_t)w;
+          } else {
+            dst[pos] = (idx << 32) | (int64_t)w;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Receiver of the fixed-capacity exchange: zero the received halo rows (score rows: only the
+// tiles written since the last unpack, once the buffer has been zeroed in full; their flags with
+// them), the work map taken one lane per row as in the send.
+__global__ __launch_bounds__(256) void sx_zero_rows_kernel(float* __restrict__ X,
+    uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
+    const uint32_t* __restrict__ recv_vertex, int64_t n, uint8_t* __restrict__ nzf,
+    uint32_t ntiles, bool flagged) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
+    const int64_t rmine = r0 + lane;
+    uint32_t vm = 0;
+    uint64_t cm = 0;
+    if (rmine < n) {
+      vm = recv_vertex[rmine];
+      if (reach) {                                   // a lane clears its own row's W words
+        uint64_t* row = R + (size_t)vm * RS;
+        for (int w = 0; w < width; ++w) row[w] = 0ull;
+      } else {
+        const int nchunks = (width + 63) / 64;
+        cm = nchunks >= 64 ? ~0ull : ((1ull << nchunks) - 1ull);
+        if (flagged) cm = sx_chunk_mask(R, RS, width, false, vm, nzf + (size_t)vm * ntiles, ntiles, TW);
+      }
+    }
+    if (reach) continue;
+    for (uint64_t todo = __ballot(cm != 0ull); todo; todo &= todo - 1ull) {
+      const int l = __ffsll((long long)todo) - 1;
+      const uint32_t v = (uint32_t)__shfl((int)vm, l, 64);
+      const uint64_t m = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cm >> 32), l, 64) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)cm, l, 64);
+      const uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
+      for (uint64_t cs = m; cs; cs &= cs - 1ull) {
+        const int b = 64 * (__ffsll((long long)cs) - 1) + lane;
+        if (b < width && (!flagged || fl[b / TW])) X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = 0.f;
+      }
+    }
+    if (nzf) {
+      // every lane of the wave has read the flags of the wave's rows: clear them
+      __builtin_amdgcn_wave_barrier();
+      if (rmine < n)
+        for (uint32_t t = 0; t < ntiles; ++t) nzf[(size_t)vm * ntiles + t] = 0;
+    }
   }
 }
 
@@ -926,7 +1048,8 @@ __global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uin
 }
 
 // Fixed-capacity mode (peer_cap > 0, egr_plan_unpack_sparse_cap): sender s's entries are slots
-// [s * peer_cap, s * peer_cap + cnt[s] / per) of `in`; n = P * peer_cap slots are scanned.
+// [s * peer_cap, s * peer_cap + min(cnt[s], peer_cap)) of `in` (cnt: sender s's entry count);
+// n = P * peer_cap slots are scanned.
 __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V,
                                   int TW, uint32_t RS, int width, bool reach,
                                   const uint32_t* __restrict__ recv_vertex,
@@ -940,7 +1063,7 @@ __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ 
   int s = 0;
   if (peer_cap > 0) {
     s = (int)(e / peer_cap);
-    if (e - (int64_t)s * peer_cap >= cnt[s] / (reach ? 2 : 1)) return;
+    if (e - (int64_t)s * peer_cap >= cnt[s]) return;      // (cnt: entries; past the slot: dropped)
   } else {
     while (s + 1 < P && eseg[s + 1] <= e) ++s;
   }
@@ -1755,53 +1878,14 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
   if (!reach && (uint64_t)n * (uint64_t)width >= (1ull << 32))
     return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: send rows x columns exceed the 2^32 "
                                  "entry index of the score format");
-  if ((size_t)n + 1 > p->sx_cap) {
-    dfree(p->sx_off);
-    p->sx_cap = 0;
-    int rc = dalloc(&p->sx_off, (size_t)n + 1);
-    if (rc != EGR_OK) return rc;
-    p->sx_cap = (size_t)n + 1;
-    if (p->sx_tmp) (void)hipFree(p->sx_tmp);
-    p->sx_tmp = nullptr;
-    size_t tb = 0;
-    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
-    EGR_HIP(hipMalloc(&p->sx_tmp, tb));
-    p->sx_tmp_bytes = tb;
-  }
-  if (!p->sx_tot) {
-    const int rc = dalloc(&p->sx_tot, (size_t)EGR_SX_MAX_PEERS + 1 + EGR_SX_MAX_PEERS + 1);
-    if (rc != EGR_OK) return rc;
-  }
   const float* X = reach ? nullptr : p->x[p->xcur];
   const uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
-  const uint32_t V = (uint32_t)p->s->V;
-  const int MW = (((width + 31) / 32) + 31) / 32;
-  if ((size_t)std::max<int64_t>(n, 1) * MW > p->sx_mask_cap) {
-    dfree(p->sx_mask);
-    p->sx_mask_cap = 0;
-    const int rc = dalloc(&p->sx_mask, (size_t)std::max<int64_t>(n, 1) * MW);
-    if (rc != EGR_OK) return rc;
-    p->sx_mask_cap = (size_t)std::max<int64_t>(n, 1) * MW;
-  }
-  EGR_HIP(hipMemsetAsync(p->sx_off, 0, sizeof(int64_t) * ((size_t)n + 1), st));
+  EGR_HIP(hipMemsetAsync(counts_dev, 0, sizeof(int64_t) * (size_t)P, st));
   if (n > 0) {
-    const dim3 sxg = sx_grid(n);
-    hipLaunchKernelGGL(sx_count_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
-                       (uint32_t)p->RS, width, reach, rows, (int64_t)n, p->sx_off, p->sx_mask, MW,
-                       reach ? nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles);
-    EGR_CHECK_LAUNCH();
-    size_t tb = p->sx_tmp_bytes;
-    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sx_tmp, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
-  }
-  hipLaunchKernelGGL(sx_bounds_kernel, dim3(1), dim3(EGR_SX_MAX_PEERS + 1), 0, st, p->sx_off, seg_dev,
-                     P, p->sx_tot);
-  hipLaunchKernelGGL(sx_capcount_kernel, dim3(1), dim3(EGR_SX_MAX_PEERS), 0, st, p->sx_tot, P,
-                     reach ? 2 : 1, peer_cap, counts_dev, overflow_dev);
-  EGR_CHECK_LAUNCH();
-  if (n > 0) {
-    hipLaunchKernelGGL(sx_emit_kernel, sx_grid(n), dim3(256), 0, st, X, R, V, p->TW,
-                       (uint32_t)p->RS, width, reach, rows, (int64_t)n, seg_dev, P, p->sx_off,
-                       p->sx_mask, MW, out, (int64_t)0, (const int64_t*)p->sx_tot, peer_cap);
+    hipLaunchKernelGGL(sx_emit_slots_kernel, sx_lane_grid(n), dim3(256), 0, st, X, R, (uint32_t)p->s->V,
+                       p->TW, (uint32_t)p->RS, width, reach, rows, n, seg_dev, P,
+                       reach ? (const uint8_t*)nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles, out,
+                       peer_cap, reinterpret_cast<unsigned long long*>(counts_dev), overflow_dev);
     EGR_CHECK_LAUNCH();
   }
   return EGR_OK;
@@ -1824,7 +1908,7 @@ int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_v
   uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;
   uint8_t* nzf = reach ? nullptr : p->nzf[p->xcur];
-  hipLaunchKernelGGL(sx_zero_kernel, sx_grid(n_rows), dim3(256), 0,
+  hipLaunchKernelGGL(sx_zero_rows_kernel, sx_lane_grid(n_rows), dim3(256), 0,
                      st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, (int64_t)n_rows,
                      nzf, (uint32_t)p->ntiles, nzf != nullptr && p->xzeroed[p->xcur]);
   EGR_CHECK_LAUNCH();

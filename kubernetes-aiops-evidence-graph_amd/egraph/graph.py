@@ -593,8 +593,10 @@ class Plan:
     def pack_sparse_cap(self, what: str, rows: torch.Tensor, seg_dev: torch.Tensor, out: torch.Tensor,
                         peer_cap: int, counts: torch.Tensor, overflow: torch.Tensor, stream=None) -> None:
         """egr_plan_pack_sparse_cap: the non-zero entries into fixed slots of peer_cap entries
-        per peer (out: int64 [P * peer_cap * words per entry]), the word counts into `counts`
-        (device int64 [P]), overflow into `overflow` (device int32 [1]); no synchronisation."""
+        per peer (out: int64 [P * peer_cap * words per entry]; an entry is one word for scores,
+        two for reach), each peer's entry count into `counts` (device int64 [P]; past peer_cap
+        the entries are dropped and `overflow`, device int32 [1], is set); one launch, no
+        synchronisation."""
         P = seg_dev.numel() - 1
         if out.numel() < P * peer_cap * (2 if what == "reach" else 1) or counts.numel() < P:
             raise ValueError("pack_sparse_cap: output slots or counts too small")

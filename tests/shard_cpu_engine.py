@@ -120,6 +120,7 @@ class CpuEngine:
                     ent.append(((i - seg[q]) * width + b, int(vals[i, b])))
             if len(ent) > peer_cap:
                 overflow[0] = 1
+            counts[q] = len(ent)                  # entries, uncapped (the receiver clamps)
             ent = ent[:peer_cap]
             base = q * peer_cap * per
             for j, (idx, w) in enumerate(ent):
@@ -127,7 +128,6 @@ class CpuEngine:
                     o[base + 2 * j], o[base + 2 * j + 1] = idx, w          # w: the signed word
                 else:
                     o[base + j] = (idx << 32) | w
-            counts[q] = per * len(ent)
 
     def unpack_sparse_cap(self, what, recv_vertex, entries, peer_cap, counts, rbase):
         rv = recv_vertex.numpy().view(np.uint32)
@@ -140,7 +140,7 @@ class CpuEngine:
         else:
             self.x[rv] = 0.0
         for s in range(len(rb)):
-            for j in range(int(counts[s]) // per):
+            for j in range(min(int(counts[s]), peer_cap)):
                 if per == 2:
                     idx = int(e[(s * peer_cap + j) * 2])
                     w = int(e[(s * peer_cap + j) * 2 + 1]) & 0xFFFFFFFFFFFFFFFF
