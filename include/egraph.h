@@ -331,10 +331,9 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
                            const int64_t* rbase, int32_t P, void* stream);
 /* The same exchange with FIXED-CAPACITY peer slots and no host synchronisation (a halo exchange
  * per hop then never waits for the host: the all-to-all runs with equal splits of peer_cap
- * entries).  pack_cap: seg_dev[P + 1] on the device; ONE kernel (after zeroing counts_dev)
- * writes peer q's entries to out[q * peer_cap * words_per_entry ...) in no particular order
- * (the scatter is order-free, so the result is bit-identical), its entry count to counts_dev[q]
- * (device int64), and *overflow_dev (device u32) gets 1 when a peer has more than peer_cap
+ * entries).  pack_cap: seg_dev[P + 1] on the device; a count pass, a scan and an emit pass
+ * write peer q's entries to out[q * peer_cap * words_per_entry ...) in (row, column) order, its
+ * entry count to counts_dev[q] (device int64), and *overflow_dev (device u32) gets 1 when a peer has more than peer_cap
  * entries (the excess is dropped: the caller re-runs the pass with larger slots).  unpack_cap:
  * sender s's entries are the first min(counts_dev[s], peer_cap) of its slot of `in` (the peers'
  * counts, exchanged beside the data); zero + scatter as egr_plan_unpack_sparse.  Both are
