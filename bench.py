@@ -802,14 +802,20 @@ class _TimedPlan:
     def __getattr__(self, name):
         return getattr(self._p, name)
 
-    def _timed(self, fn, *a):
+    def _timed(self, fn, *a, tail: bool = False):
         if self._part is None:
             return fn(*a)
         x, y = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         x.record()
         r = fn(*a)
         y.record()
-        self._part.append((x, y))
+        # which chain the call belongs to: the side stream's (reach), the main stream's
+        # (propagation), or the tail after both joined (candidates, top-k)
+        from egraph import shard
+        side = shard._SIDE.get(torch.cuda.current_device())
+        chain = "tail" if tail else ("side" if side is not None and torch.cuda.current_stream() == side
+                                     else "main")
+        self._part.append((x, y, chain))
         return r
 
     def hop(self):
@@ -827,10 +833,10 @@ class _TimedPlan:
         return self._timed(self._p.reach_hop)
 
     def candidates(self, *a):
-        return self._timed(self._p.candidates, *a)
+        return self._timed(self._p.candidates, *a, tail=True)
 
     def topk(self, *a):
-        return self._timed(self._p.topk, *a)
+        return self._timed(self._p.topk, *a, tail=True)
 
     # the halo exchange's own device work (pack before, unpack after the transfer) runs on the
     # partition's GPU too: counted in its compute (the pack's host read of the peer sizes included)
@@ -915,25 +921,28 @@ def shard_step(ctx, hops: int, k: int, ev=None, parts=None):
         run.eng = _TimedPlan(plan, ev, parts[i] if parts is not None else None)
     if ctx.get("dense_halo") or ctx.get("host_counts"):
         return shard.run_partitioned(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k,
-                                     sparse=not ctx.get("dense_halo", False))
+                                     sparse=not ctx.get("dense_halo", False),
+                                     overlap=not ctx.get("no_overlap", False))
 
     def reset():                   # a pass that overflowed its slots re-runs (recalibrating)
         for run, (plan, seeds, sources) in zip(ctx["runs"], ctx["plans"]):
             plan.set_seeds(*seeds)
             plan.set_sources(sources)
-    return shard.run_partitioned_retry(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k, reset)
+    return shard.run_partitioned_retry(ctx["runs"], ctx["comm"], hops, ctx["inc_label"], k, reset,
+                                       overlap=not ctx.get("no_overlap", False))
 
 
 def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     ctx = shard_setup(args, world, rank, dev)
     ctx["dense_halo"] = args.dense_halo
     ctx["host_counts"] = args.halo_host_counts
+    ctx["no_overlap"] = args.no_overlap
     for _ in range(args.warmup):
         shard_step(ctx, args.hops, args.k)
     torch.cuda.synchronize(dev)
     events: list = []
     for r in ctx["runs"]:
-        r.sent_bytes, r.exchanges = 0, 0
+        r.sent_bytes, r.exchanges, r.link_bytes = 0, 0, 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -948,11 +957,21 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
         elapsed = max_over_ranks(dist, elapsed, dev)
     # untimed: each partition's own compute (its kernels only, no exchange) per step, from HIP
     # events -- the per-GPU time of P GPUs running their partitions side by side
+    # the timed steps' wire bytes (the untimed steps below exchange too)
+    sent_t = max(r.sent_bytes for r in ctx["runs"])
+    link_t = max(r.link_bytes for r in ctx["runs"])
     parts = [[] for _ in ctx["runs"]]
     for _ in range(3):
         shard_step(ctx, args.hops, args.k, None, parts)
     torch.cuda.synchronize(dev)
-    part_ms = [sum(a.elapsed_time(b) for a, b in q) / 3 for q in parts]
+    part_ms = [sum(a.elapsed_time(b) for a, b, _ in q) / 3 for q in parts]
+    # the critical path of a partition with the reach chain on its own stream: the longer of the
+    # two chains, then the tail (what one GPU running the partition waits for, if the chains
+    # overlap; the in-process ms_per_step with and without --no-overlap measures that they do)
+    def chain_ms(q, c):
+        return sum(a.elapsed_time(b) for a, b, t in q if t == c) / 3
+    crit_ms = [max(chain_ms(q, "main"), chain_ms(q, "side")) + chain_ms(q, "tail") for q in parts]
+    overlap_on = not args.no_overlap
     B = args.batch
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -964,7 +983,8 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     nnz = len(ctx["csr"]["col"])
     halo = max(r.halo_bytes_per_hop for r in ctx["runs"])
     per_hop = max(1, args.steps * max(args.hops - 1, 1))
-    sent = max(r.sent_bytes for r in ctx["runs"]) / per_hop
+    sent = sent_t / per_hop
+    link = link_t / max(args.steps, 1)
     out = {
         "metric": METRIC, "value": B / (ms * 1e-3), "unit": "incidents/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
@@ -988,13 +1008,20 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "halo_bytes_sent_per_hop_max_rank": sent,
             "halo_reduction_vs_dense": halo / sent if sent else None,
             "partition_compute_ms": part_ms,
-            "projected_ms_per_gpu": max(part_ms) + (args.hops - 1) * sent / (XGMI_LINK_GBS * 1e6),
+            "link_bytes_per_step_max_rank": link,
+            "reach_chain_overlap": overlap_on,
+            "partition_critical_ms": crit_ms if overlap_on else part_ms,
+            "projected_ms_per_gpu": max(crit_ms if overlap_on else part_ms) + link / (XGMI_LINK_GBS * 1e6),
+            "projected_serial_ms_per_gpu": max(part_ms) + link / (XGMI_LINK_GBS * 1e6),
             "projected_note": "max over partitions of their own device work per step (hops, reach "
                               "hops, candidates, top-k and the halo pack / unpack kernels; HIP events, "
-                              "untimed steps) + the largest sender's halo entries over one xGMI link "
-                              "per exchange; what P GPUs running one partition each would take per "
-                              "step (the in-process ms_per_step runs them one after another on one "
-                              "GPU)",
+                              "untimed steps) -- with the reach chain on its own stream, the longer "
+                              "chain plus the top-k tail (partition_critical_ms; the serial sum is "
+                              "projected_serial_ms_per_gpu) -- + per exchange the largest transfer "
+                              "from one rank to ONE peer over its xGMI link (point to point: the "
+                              "peers' transfers run on separate links at once); what P GPUs running "
+                              "one partition each would take per step (the in-process ms_per_step "
+                              "runs them one after another on one GPU)",
         },
         "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1167,6 +1194,8 @@ def main():
     ap.add_argument("--halo-host-counts", action="store_true",
                     help="--shard graph: sparse exchange with a host read of the peer counts per "
                          "exchange (the round-3 path) instead of fixed-capacity device slots")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="--shard graph: run the reach chain on the main stream too (A/B)")
     ap.add_argument("--partitions", type=int, default=1,
                     help="--shard graph on one process: partitions run on this GPU")
     ap.add_argument("--workload", default="rank", choices=["rank", "storm"],

@@ -784,9 +784,11 @@ __global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t*
 constexpr int SX_ROWS = 4;
 constexpr int64_t SX_MAX_BLOCKS = 2048;      // grid-stride beyond this (8 blocks per CU)
 inline dim3 sx_grid(int64_t n) { return dim3((unsigned)std::min<int64_t>((n + SX_ROWS - 1) / SX_ROWS, SX_MAX_BLOCKS)); }
-// the lane-per-row work map kernels: 64 rows per wave, four waves per block
+// the work-map kernels: the same waves as sx_grid, each wave's rows strided by the wave count
+// and mapped one lane each up front (a wave-per-row walk paid its row id, flags and data loads
+// one after another for each of its ~15 rows)
 inline dim3 sx_lane_grid(int64_t n) {
-  return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, SX_MAX_BLOCKS)));
+  return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + SX_ROWS - 1) / SX_ROWS, SX_MAX_BLOCKS)));
 }
 
 // Sender, pass 1: the row's non-zero count, and a bit per 32-column group that holds any
@@ -894,14 +896,12 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
   }
 }
 
-// The work map of 64 exchange rows, one lane per row (the fixed-capacity pack and unpack): a
+// The work map of a wave's exchange rows, one lane per row (the fixed-capacity pack and unpack): a
 // bit per 64-column chunk of the row that may hold a non-zero -- for a score row, the chunks
 // over the tiles its flags mark (every chunk without flags); for a reach row, the chunks holding
 // a non-zero word (the row's W <= 64 words... read by the lane: RS-word rows, 16-B loads).
-// One lane per row puts 64 rows' dependent loads (row id, then its flags) in flight at once;
-// the wave then walks only the rows with work (a row a wave at a time had ~15 rows of round
-// trips per wave queued one after another: ~100 us per C4 exchange for rows that were nearly
-// all empty).
+// One lane per row puts the wave's rows' dependent loads (row id, then its flags) in flight at
+// once; the wave then walks the rows with work, chunk by chunk.
 __device__ __forceinline__ uint64_t sx_chunk_mask(const uint64_t* __restrict__ R, uint32_t RS,
                                                   int width, bool reach, uint32_t v,
                                                   const uint8_t* __restrict__ fl, uint32_t ntiles,
@@ -936,8 +936,8 @@ __global__ __launch_bounds__(256) void sx_count_rows_kernel(const float* __restr
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
   if (wave == 0 && lane == 0) cnt[n] = 0;
-  for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
-    const int64_t rmine = r0 + lane;
+  for (int64_t g0 = wave; g0 < n; g0 += nw * 64) {   // rows g0 + j * nw, j = lane
+    const int64_t rmine = g0 + (int64_t)lane * nw;
     uint32_t vm = 0;
     uint64_t cm = 0;
     if (rmine < n) {
@@ -985,8 +985,8 @@ __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restri
       if (c > peer_cap) atomicOr(overflow, 1u);
     }
   }
-  for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
-    const int64_t rmine = r0 + lane;
+  for (int64_t g0 = wave; g0 < n; g0 += nw * 64) {   // rows g0 + j * nw, j = lane
+    const int64_t rmine = g0 + (int64_t)lane * nw;
     uint32_t vm = 0;
     uint64_t cm = 0;
     if (rmine < n && off[rmine + 1] > off[rmine]) {     // (the scan says which rows have entries)
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restri
     }
     for (uint64_t todo = __ballot(cm != 0ull); todo; todo &= todo - 1ull) {
       const int l = __ffsll((long long)todo) - 1;
-      const int64_t r = r0 + l;
+      const int64_t r = g0 + (int64_t)l * nw;
       const uint32_t v = (uint32_t)__shfl((int)vm, l, 64);
       const uint64_t m = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cm >> 32), l, 64) << 32) |
                          (uint32_t)__shfl((int)(uint32_t)cm, l, 64);
@@ -1036,8 +1036,8 @@ __global__ __launch_bounds__(256) void sx_zero_rows_kernel(float* __restrict__ X
     uint32_t ntiles, bool flagged) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
-  for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
-    const int64_t rmine = r0 + lane;
+  for (int64_t g0 = wave; g0 < n; g0 += nw * 64) {   // rows g0 + j * nw, j = lane
+    const int64_t rmine = g0 + (int64_t)lane * nw;
     uint32_t vm = 0;
     uint64_t cm = 0;
     if (rmine < n) {
@@ -1185,6 +1185,12 @@ struct egr_plan {
   size_t sx_cap = 0;
   void* sx_tmp = nullptr;
   size_t sx_tmp_bytes = 0;
+  // the fixed-capacity pack's row offsets and scan scratch, one set per kind (scores, reach):
+  // the two kinds' exchanges may run at once on two streams
+  int64_t* sxc_off[2] = {nullptr, nullptr};
+  size_t sxc_cap[2] = {0, 0};
+  void* sxc_tmp[2] = {nullptr, nullptr};
+  size_t sxc_tmp_bytes[2] = {0, 0};
   int64_t* sx_tot = nullptr;        // [EGR_SX_MAX_PEERS + 1] peer bounds, then the segments
   int64_t* sx_pin = nullptr;        // pinned host: the segments up, the peer bounds down
   uint32_t* sx_mask = nullptr;      // [rows][MW] non-zero 32-column groups of each send row
@@ -1448,6 +1454,10 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->chunk_start);
   dfree(p->rchunk_start);
   dfree(p->sx_off);
+  for (int k = 0; k < 2; ++k) {
+    dfree(p->sxc_off[k]);
+    if (p->sxc_tmp[k]) (void)hipFree(p->sxc_tmp[k]);
+  }
   dfree(p->sx_tot);
   if (p->sx_pin) (void)hipHostFree(p->sx_pin);
   dfree(p->sx_mask);
@@ -1931,32 +1941,34 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
   if (!reach && (uint64_t)n * (uint64_t)width >= (1ull << 32))
     return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: send rows x columns exceed the 2^32 "
                                  "entry index of the score format");
-  if ((size_t)n + 1 > p->sx_cap) {
-    dfree(p->sx_off);
-    p->sx_cap = 0;
-    int rc = dalloc(&p->sx_off, (size_t)n + 1);
+  const int kk = reach ? 1 : 0;
+  if ((size_t)n + 1 > p->sxc_cap[kk]) {
+    dfree(p->sxc_off[kk]);
+    p->sxc_cap[kk] = 0;
+    int rc = dalloc(&p->sxc_off[kk], (size_t)n + 1);
     if (rc != EGR_OK) return rc;
-    p->sx_cap = (size_t)n + 1;
-    if (p->sx_tmp) (void)hipFree(p->sx_tmp);
-    p->sx_tmp = nullptr;
+    p->sxc_cap[kk] = (size_t)n + 1;
+    if (p->sxc_tmp[kk]) (void)hipFree(p->sxc_tmp[kk]);
+    p->sxc_tmp[kk] = nullptr;
     size_t tb = 0;
-    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
-    EGR_HIP(hipMalloc(&p->sx_tmp, tb));
-    p->sx_tmp_bytes = tb;
+    EGR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, p->sxc_off[kk], p->sxc_off[kk], (int)(n + 1), st));
+    EGR_HIP(hipMalloc(&p->sxc_tmp[kk], tb));
+    p->sxc_tmp_bytes[kk] = tb;
   }
+  int64_t* const off = p->sxc_off[kk];
   const float* X = reach ? nullptr : p->x[p->xcur];
   const uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;
   const uint8_t* nzf = reach ? (const uint8_t*)nullptr : p->nzf[p->xcur];
   const dim3 grid = sx_lane_grid(n);
   hipLaunchKernelGGL(sx_count_rows_kernel, grid, dim3(256), 0, st, X, R, V, p->TW, (uint32_t)p->RS,
-                     width, reach, rows, n, nzf, (uint32_t)p->ntiles, p->sx_off);
+                     width, reach, rows, n, nzf, (uint32_t)p->ntiles, off);
   EGR_CHECK_LAUNCH();
-  size_t tb = p->sx_tmp_bytes;
-  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sx_tmp, tb, p->sx_off, p->sx_off, (int)(n + 1), st));
+  size_t tb = p->sxc_tmp_bytes[kk];
+  EGR_HIP(hipcub::DeviceScan::ExclusiveSum(p->sxc_tmp[kk], tb, off, off, (int)(n + 1), st));
   hipLaunchKernelGGL(sx_emit_rows_kernel, grid, dim3(256), 0, st, X, R, V, p->TW, (uint32_t)p->RS,
                      width, reach, rows, n, seg_dev, P, nzf, (uint32_t)p->ntiles,
-                     (const int64_t*)p->sx_off, out, peer_cap, counts_dev, overflow_dev);
+                     (const int64_t*)off, out, peer_cap, counts_dev, overflow_dev);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
 }

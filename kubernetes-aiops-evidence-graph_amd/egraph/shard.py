@@ -24,6 +24,8 @@ Scores, reach sets and top-k are bit-identical to the single-GPU plan (tests/tes
 """
 from __future__ import annotations
 
+import contextlib
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -283,6 +285,9 @@ class RankRun:
         ns, nr = len(lg.send_rows), len(lg.halo_rows)
         self._dense = None         # dense exchange buffers, allocated on first use
         self.sent_bytes = 0        # bytes this rank put on the wire (every exchange so far)
+        # per exchange, the largest transfer to ONE peer (xGMI is point to point: the peers'
+        # transfers run on separate links at once, so this is what an exchange waits for)
+        self.link_bytes = 0
         self.exchanges = 0
         # sparse exchange: the local vertex of each received row (rows grouped by sender) and
         # each sender's first received row
@@ -324,6 +329,11 @@ class RankRun:
 
 
 
+def _max_peer(r: "RankRun", per_peer: list) -> int:
+    """The largest of the bytes a rank sends to each OTHER rank in one exchange."""
+    return max((b for q, b in enumerate(per_peer) if q != r.lg.rank), default=0)
+
+
 def _seg_starts(counts) -> np.ndarray:
     return np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
 
@@ -358,6 +368,7 @@ def _exchange_fixed(runs: list[RankRun], comm, what: str) -> None:
         r.eng.pack_sparse_cap(what, r.send, r.seg_dev, sbuf, cap, scnt, r.overflow)
         per = 2 if what == "reach" else 1
         r.sent_bytes += 8 * len(r.lg.send_counts) * cap * per + 8 * len(r.lg.send_counts)
+        r.link_bytes += (8 * cap * per + 8) if r.lg.P > 1 else 0
         r.exchanges += 1
         items_d.append((sbuf, rbuf))
         items_c.append((scnt, rcnt))
@@ -388,6 +399,7 @@ def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
         r.max_seen[what] = max(r.max_seen.get(what, 0), max(counts, default=0))
         n_words = [per * c for c in counts]
         r.sent_bytes += 8 * sum(n_words) + 8 * len(counts)
+        r.link_bytes += _max_peer(r, [8 * w + 8 for w in n_words])
         r.exchanges += 1
         items.append((buf[: sum(n_words)], n_words))
     out = comm.all_to_all_v(items)
@@ -431,6 +443,7 @@ def _exchange_sparse_py(runs: list[RankRun], comm, what: str) -> None:
             payload = torch.stack([local, flat[nz]], dim=1).reshape(-1)
             n_per = [2 * c for c in counts]
         r.sent_bytes += int(payload.numel()) * 8 + 8 * len(counts)
+        r.link_bytes += _max_peer(r, [8 * w + 8 for w in n_per])
         r.exchanges += 1
         items.append((payload.contiguous(), n_per))
         meta.append(width)
@@ -464,7 +477,9 @@ def _exchange(runs: list[RankRun], comm, what: str) -> None:
             items.append((r.send_r, r.lg.send_counts, r.recv_r, r.lg.recv_counts))
     comm.all_to_all(items)
     for r in runs:
-        r.sent_bytes += len(r.lg.send_rows) * (r.Bpad * 4 if what == "scores" else r.W * 8)
+        row_b = r.Bpad * 4 if what == "scores" else r.W * 8
+        r.sent_bytes += len(r.lg.send_rows) * row_b
+        r.link_bytes += _max_peer(r, [int(c) * row_b for c in r.lg.send_counts])
         r.exchanges += 1
         if what == "scores":
             r.eng.unpack_scores(r.halo, r.src, r.recv_s)
@@ -472,8 +487,19 @@ def _exchange(runs: list[RankRun], comm, what: str) -> None:
             r.eng.unpack_reach(r.halo, r.src, r.recv_r)
 
 
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device):
+    """The second stream the reach chain runs on (one per device, created once)."""
+    st = _SIDE.get(dev.index)
+    if st is None:
+        st = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return st
+
+
 def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int,
-                    sparse: bool = True, fixed: bool = False):
+                    sparse: bool = True, fixed: bool = False, overlap: bool | None = None):
     """`hops` hops of propagation and reach on every local rank in `runs` (seeds and sources
     already set on their engines), halo exchanges between hops, then the merged global top-k.
     Returns (ids int64 [B, k] global vertex ids (NO_NODE = none), scores f32 [B, k]).
@@ -481,23 +507,37 @@ def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k:
     first such pass calibrates the slots over the host-count path (1.5x the largest per-peer
     count seen), and a pass that overflows a slot raises HaloOverflow after growing it (the
     caller sets seeds / sources again and re-runs -- run_partitioned_retry does that -- and the
-    re-run recalibrates)."""
+    re-run recalibrates).
+    overlap (default: on for device engines): the propagation chain (hop, score exchange, hop,
+    ...) and the reach chain (reach hop, reach exchange, ...) share no buffer until the top-k, so
+    the reach chain runs on a second stream beside it and its hops and exchanges hide under the
+    score chain's."""
     use_fixed = fixed and sparse and all(r.cap for r in runs) and \
         all(hasattr(r.eng, "pack_sparse_cap") for r in runs)
     for r in runs:
         r.overflow.zero_()
         if fixed and sparse and not use_fixed:
             r.max_seen = {}
+    if overlap is None:
+        overlap = all(getattr(r.send, "is_cuda", False) for r in runs)
+    dev = runs[0].send.device if runs else None
+    main = torch.cuda.current_stream(dev) if overlap else None
+    side = _side_stream(dev) if overlap else None
+    if overlap:
+        side.wait_stream(main)                   # seeds and sources were set on the main stream
+    xch = _exchange_fixed if use_fixed else _exchange_sparse if sparse else _exchange
     for h in range(hops):
         for r in runs:
             r.eng.hop()
-        xch = _exchange_fixed if use_fixed else _exchange_sparse if sparse else _exchange
         if h + 1 < hops:
             xch(runs, comm, "scores")
-        for r in runs:
-            r.eng.reach_hop()
-        if h + 1 < hops:
-            xch(runs, comm, "reach")
+        with (torch.cuda.stream(side) if overlap else contextlib.nullcontext()):
+            for r in runs:
+                r.eng.reach_hop()
+            if h + 1 < hops:
+                xch(runs, comm, "reach")
+    if overlap:
+        main.wait_stream(side)
     if use_fixed:
         if comm.any_flag([r.overflow for r in runs]):
             for r in runs:
@@ -549,12 +589,14 @@ def _max_over_ranks(comm, x: int) -> int:
 
 
 def run_partitioned_retry(runs: list[RankRun], comm, hops: int, exclude_label: int, k: int,
-                          reset, fixed: bool = True):
+                          reset, fixed: bool = True, overlap: bool | None = None):
     """run_partitioned with fixed-capacity slots, re-running once (after `reset()`, which sets
     every engine's seeds and sources again) when a slot overflowed: the re-run goes over the
     host-count path, which cannot overflow, and recalibrates the slots."""
     try:
-        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed)
+        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed,
+                               overlap=overlap)
     except HaloOverflow:
         reset()
-        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed)
+        return run_partitioned(runs, comm, hops, exclude_label, k, sparse=True, fixed=fixed,
+                               overlap=overlap)

@@ -36,9 +36,12 @@ def _dev(a):
     return to_device(np.ascontiguousarray(a), torch.device("cuda", 0))
 
 
-@pytest.mark.parametrize("P,B,sparse", [(2, 40, True), (3, 130, True), (4, 70, True),
-                                        (2, 40, False), (4, 70, False)])
-def test_partitioned_plan_equals_unpartitioned(P, B, sparse):
+@pytest.mark.parametrize("P,B,sparse,overlap", [(2, 40, True, None), (3, 130, True, None),
+                                                (4, 70, True, None), (2, 40, False, None),
+                                                (4, 70, False, None), (3, 130, True, False)])
+def test_partitioned_plan_equals_unpartitioned(P, B, sparse, overlap):
+    """(overlap None: the reach chain on its own stream, the default for device engines;
+    False: every kernel on one stream.)"""
     from egraph import shard
     from egraph.graph import Snapshot
     g, sv, sc, ss, src = _graph(B, seed=80 + P, pods=2500)
@@ -57,7 +60,7 @@ def test_partitioned_plan_equals_unpartitioned(P, B, sparse):
         plan.set_sources(_dev(shard.local_sources(lg, V, src)))
         runs.append(shard.RankRun(lg, plan, torch.device("cuda", 0)))
         runs[-1].snap = snap
-    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k, sparse=sparse)
+    out = shard.run_partitioned(runs, shard.LocalComm(), 3, inc, k, sparse=sparse, overlap=overlap)
     for run in runs:                 # 2 hops x (scores + reach) exchanged
         dense = 2 * run.halo_bytes_per_hop
         assert run.sent_bytes == dense if not sparse else run.sent_bytes < dense
