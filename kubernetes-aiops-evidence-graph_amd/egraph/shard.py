@@ -36,7 +36,9 @@ NO_NODE = 0xFFFFFFFF
 
 def partition_vertices(row_ptr: np.ndarray, vlabel: np.ndarray, label_names: list[str], P: int,
                        hash_labels: tuple[str, ...] = ("Node",)) -> np.ndarray:
-    """owner[v] in [0, P): hashed for `hash_labels`, entry-balanced contiguous ranges otherwise."""
+    """owner[v] in [0, P): hashed for `hash_labels`, contiguous ranges otherwise, balanced so
+    that every rank's total row weight (degree + 1: a dense hop writes a row and gathers its
+    entries) -- its hashed vertices' included -- is as equal as the ranges allow."""
     V = len(row_ptr) - 1
     if P < 1:
         raise ValueError("P must be >= 1")
@@ -45,12 +47,20 @@ def partition_vertices(row_ptr: np.ndarray, vlabel: np.ndarray, label_names: lis
         return owner
     hashed = np.isin(vlabel, [label_names.index(n) for n in hash_labels if n in label_names])
     deg = np.diff(row_ptr.astype(np.int64))
+    ids = np.flatnonzero(hashed).astype(np.uint64)
+    hown = (((ids * np.uint64(0x9E3779B1)) >> np.uint64(7)) % np.uint64(P)).astype(np.int64)
+    # the hashed vertices' weight per rank, then each rank's share of the contiguous weight:
+    # what brings it to the common target (never negative)
+    hw = np.bincount(hown, weights=deg[hashed] + 1, minlength=P) if len(ids) else np.zeros(P)
     w = np.where(hashed, 0, deg + 1)            # +1: isolated vertices still weigh something
     cum = np.cumsum(w)
-    total = int(cum[-1]) if V else 0
-    owner[:] = np.minimum((cum - 1) * P // max(total, 1), P - 1).astype(np.int32)
-    ids = np.flatnonzero(hashed).astype(np.uint64)
-    owner[hashed] = ((ids * np.uint64(0x9E3779B1)) >> np.uint64(7)) % np.uint64(P)
+    total = float(cum[-1]) if V else 0.0
+    target = (total + hw.sum()) / P
+    cap = np.maximum(target - hw, 0.0)
+    cap *= total / max(cap.sum(), 1e-9)         # (the contiguous weight, all of it, is assigned)
+    bounds = np.cumsum(cap)[:-1]
+    owner[:] = np.minimum(np.searchsorted(bounds, cum - 0.5, side="right"), P - 1).astype(np.int32)
+    owner[hashed] = hown.astype(np.int32)
     return owner
 
 

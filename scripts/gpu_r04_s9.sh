@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 session 9: edge-cut with the strided work-map exchange kernels and the reach chain on
 # its own stream: partition tests, C4 at P = 1/2/4/8 (scripts/gpu_shard.sh), P = 8 without the
-# overlap (A/B of the in-process step), kernel stats at P = 8.
+# overlap (A/B of the in-process step), kernel stats at P = 8, C4 through the replicated frontier.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/r04s9
@@ -19,3 +19,6 @@ rows = list(csv.DictReader(open("gpurun_out/r04s9/shard_p8/run_kernel_stats.csv"
 for r in rows[:12]:
     print(f"  {r['Name'][:60]:60s} calls {r['Calls']:>5s} avg {float(r['AverageNs'])/1e3:8.1f} us")
 PY
+# C4 through the replicated frontier (distinct batches, merged launch, wide-first after adapt)
+timeout -k 10 300 python -u bench.py --config C4 --steps 20 --warmup 5 --no-cpu-baseline --no-dropin --dense-steps 0 > $OUT/c4_frontier.json 2> $OUT/c4_frontier.err
+python -c "import json;d=json.load(open('$OUT/c4_frontier.json'));print('C4 frontier', round(d['value']), round(d['ms_per_step'],4), d.get('frontier_work'))"
