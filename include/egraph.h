@@ -380,10 +380,6 @@ typedef struct egr_frontier egr_frontier;
  * overflow and skip the launch).  Takes effect from the next run (capture it into a graph
  * after setting it).                                                                       */
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
-/* Grouped runs with the retry on: the first n_cols columns of the launch order (the costliest
- * predicted) run on the wide grid from the start, on a second stream beside the narrow kernel
- * over the rest (0 = off, the default).  Takes effect from the next run.                    */
-int egr_frontier_set_heavy(egr_frontier* f, int32_t n_cols);
 /* Top-k-only frontiers with the retry on: `on` != 0 sends EVERY column straight to the wide grid
  * (for graphs where most columns overflow the narrow table, e.g. the dense C4: the narrow
  * attempt would be wasted work).  Same results; takes effect from the next egr_frontier_run. */

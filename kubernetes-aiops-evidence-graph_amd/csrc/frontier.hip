@@ -96,7 +96,6 @@ struct FArgs {
   uint32_t* spill_n;
   const uint32_t* retry_list;   // the retry kernel's input list and count (block i takes
   const uint32_t* retry_n;      // entries i, i + gridDim.x, ...)
-  uint32_t retry_imm;           // != 0: the retry list's length (instead of *retry_n)
   float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
                                 // narrow (FR_DBUF): the seeds' values by slot
   // global tables (one per resident workgroup of the fallback kernel)
@@ -430,11 +429,6 @@ struct egr_frontier {
   bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
                                   // wide retry grid over every column (egr_frontier_set_wide_first)
   uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
-  int32_t heavy = 0;              // grouped runs with the retry on: the first `heavy` columns of
-                                  // the launch order (the costliest predicted) go to the wide
-                                  // grid on a second stream from the start (egr_frontier_set_heavy)
-  hipStream_t side = nullptr;     // ... that stream, and its fork / join events
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
                                   // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
   int64_t vmax = 0;               // vertex count the V-sized buffers were sized for (headroom
@@ -589,9 +583,6 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->mem_cnt);
   dfree(f->ovf);
   dfree(f->all_n);
-  if (f->ev_fork) (void)hipEventDestroy(f->ev_fork);
-  if (f->ev_join) (void)hipEventDestroy(f->ev_join);
-  if (f->side) (void)hipStreamDestroy(f->side);
   dfree(f->gkeys);
   dfree(f->gs);
   dfree(f->gsnew);
@@ -761,39 +752,13 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
       EGR_CHECK_LAUNCH();
       skipped_lds = true;
     } else {
-      // heavy split (grouped runs, retry on): the launch order's first H columns -- the
-      // costliest predicted, where nearly every narrow overflow is -- start at once on the wide
-      // grid on a second stream, beside the narrow kernel over the rest, instead of failing the
-      // narrow table first and waiting for it to drain (the retry tail)
-      const int H = (!sorted && rb > 0) ? std::min(f->heavy, f->B) : 0;
-      if (H > 0) {
-        if (!f->side) {
-          EGR_HIP(hipStreamCreateWithFlags(&f->side, hipStreamNonBlocking));
-          EGR_HIP(hipEventCreateWithFlags(&f->ev_fork, hipEventDisableTiming));
-          EGR_HIP(hipEventCreateWithFlags(&f->ev_join, hipEventDisableTiming));
-        }
-        EGR_HIP(hipEventRecord(f->ev_fork, st));
-        EGR_HIP(hipStreamWaitEvent(f->side, f->ev_fork, 0));
-        FArgs ah = a;
-        ah.retry_list = a.order;
-        ah.retry_imm = (uint32_t)H;
-        hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, H)),
-                           dim3(fr_wide::FT), 0, f->side, ah);
-        EGR_CHECK_LAUNCH();
-        EGR_HIP(hipEventRecord(f->ev_join, f->side));
-      }
-      if (H < f->B) {
-        FArgs a2 = an;
-        a2.order = a.order + H;
-        hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B - H), dim3(fr_narrow::FT), 0, st, a2);
-        EGR_CHECK_LAUNCH();
-      }
+      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
+      EGR_CHECK_LAUNCH();
       if (rb > 0) {
         hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
                            dim3(fr_wide::FT), 0, st, a);
         EGR_CHECK_LAUNCH();
       }
-      if (H > 0) EGR_HIP(hipStreamWaitEvent(st, f->ev_join, 0));
     }
   } else {
     hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
@@ -848,12 +813,6 @@ int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const ui
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on) {
   if (!f) return egr::fail(EGR_EINVAL, "egr_frontier_set_wide_first: NULL frontier");
   f->wide_first = on != 0;
-  return EGR_OK;
-}
-
-int egr_frontier_set_heavy(egr_frontier* f, int32_t n_cols) {
-  if (!f || n_cols < 0) return egr::fail(EGR_EINVAL, "egr_frontier_set_heavy: bad arguments");
-  f->heavy = n_cols;
   return EGR_OK;
 }
 

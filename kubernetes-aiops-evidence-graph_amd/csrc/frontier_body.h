@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER
 void frontier_lds_retry_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
-  const uint32_t n = A.retry_imm ? A.retry_imm : *A.retry_n;
+  const uint32_t n = *A.retry_n;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     lds_column(A, (int)A.retry_list[i], L, sh);
     __syncthreads();              // the next column clears the table this one used

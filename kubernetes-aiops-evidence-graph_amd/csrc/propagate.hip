@@ -278,14 +278,14 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
     Y[(size_t)v * G + gl] = acc;
 #endif
     if (A.nzout) {
-      // the row's tile flag for the sparse halo pack: OR over the G lanes of this row (a
-      // group's lanes are contiguous; lanes of a finished group vote nothing)
-      const bool nz = (__float_as_uint(acc.x) | __float_as_uint(acc.y) | __float_as_uint(acc.z) |
-                       __float_as_uint(acc.w)) != 0u;
-      const uint64_t m = __ballot(nz);
-      const uint32_t sh = (tid & 63u) / G * G;
-      const uint64_t gm = G == 64 ? ~0ull : ((1ull << G) - 1ull);
-      if (gl == 0) A.nzout[(size_t)v * A.ntiles + tile] = ((m >> sh) & gm) ? 1 : 0;
+      // the row's non-zero count in this tile for the sparse halo pack (TW = 4G <= 128 columns:
+      // a byte): summed over the G lanes of the row's group (contiguous lanes, all active for
+      // the same row); -0.0 counts as non-zero, as the pack sends it
+      int c = (__float_as_uint(acc.x) != 0u) + (__float_as_uint(acc.y) != 0u) +
+              (__float_as_uint(acc.z) != 0u) + (__float_as_uint(acc.w) != 0u);
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) c += __shfl_xor(c, o, 64);
+      if (gl == 0) A.nzout[(size_t)v * A.ntiles + tile] = (uint8_t)c;
     }
   };
 
@@ -306,6 +306,10 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
 }
 
 // out[v, b] = acc + s0[v, b] for every unique seed (after the hop wrote acc)
+// partitioned plans' per-(row, tile) byte: the hop's non-zero count of the tile (0..TW <= 128),
+// or NZ_UNKNOWN once a seed was added into it (non-zero, count not kept)
+constexpr uint8_t NZ_UNKNOWN = 0xFF;
+
 __global__ void seed_add_kernel(const uint64_t* __restrict__ ukeys,
                                 const float* __restrict__ uval,
                                 const uint32_t* __restrict__ n_unique, uint32_t Bpad,
@@ -317,7 +321,9 @@ __global__ void seed_add_kernel(const uint64_t* __restrict__ ukeys,
   const uint32_t v = (uint32_t)(k / Bpad), b = (uint32_t)(k % Bpad);
   float* p = X + ((size_t)(b / TW) * V + v) * TW + (b % TW);
   *p = *p + uval[i];
-  if (nz) nz[(size_t)v * ntiles + b / TW] = 1;   // (s0 > 0 or NaN: the entry is non-zero)
+  // (s0 > 0 or NaN: the entry is non-zero.)  The tile's count is no longer known without reading
+  // it: NZ_UNKNOWN makes the pack count that tile from the scores
+  if (nz) nz[(size_t)v * ntiles + b / TW] = NZ_UNKNOWN;
 }
 
 __global__ void seed_tiles_kernel(const uint64_t* __restrict__ ukeys,
@@ -936,16 +942,32 @@ __global__ __launch_bounds__(256) void sx_count_rows_kernel(const float* __restr
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
   if (wave == 0 && lane == 0) cnt[n] = 0;
+  // score rows of a partitioned plan: the hop's per-tile counts add up on the lane; only the
+  // tiles a seed add marked unknown are counted from the scores by the wave below
+  const bool counted = !reach && nzf && ntiles <= 64u;
   for (int64_t g0 = wave; g0 < n; g0 += nw * 64) {   // rows g0 + j * nw, j = lane
     const int64_t rmine = g0 + (int64_t)lane * nw;
     uint32_t vm = 0;
     uint64_t cm = 0;
     if (rmine < n) {
       vm = rows[rmine];
-      cm = sx_chunk_mask(R, RS, width, reach, vm, nzf ? nzf + (size_t)vm * ntiles : nullptr,
-                         ntiles, TW);
+      if (!counted)
+        cm = sx_chunk_mask(R, RS, width, reach, vm, nzf ? nzf + (size_t)vm * ntiles : nullptr,
+                           ntiles, TW);
     }
     int64_t mine = 0;
+    if (counted && rmine < n) {
+      const uint8_t* fl = nzf + (size_t)vm * ntiles;
+      for (uint32_t t = 0; t < ntiles; ++t) {
+        const uint8_t x = fl[t];
+        if (x != NZ_UNKNOWN) {
+          mine += x;
+        } else {
+          const int c0 = (int)(t * TW) / 64, c1 = (int)(t * TW + TW - 1) / 64;
+          for (int c = c0; c <= c1; ++c) cm |= 1ull << c;
+        }
+      }
+    }
     for (uint64_t todo = __ballot(cm != 0ull); todo; todo &= todo - 1ull) {
       const int l = __ffsll((long long)todo) - 1;
       const uint32_t v = (uint32_t)__shfl((int)vm, l, 64);
@@ -956,10 +978,10 @@ __global__ __launch_bounds__(256) void sx_count_rows_kernel(const float* __restr
       for (uint64_t cs = m; cs; cs &= cs - 1ull) {
         const int b = 64 * (__ffsll((long long)cs) - 1) + lane;
         uint64_t w = 0;
-        c += __popcll(__ballot(b < width && (!fl || fl[b / TW]) &&
+        c += __popcll(__ballot(b < width && (!fl || (counted ? fl[b / TW] == NZ_UNKNOWN : fl[b / TW] != 0)) &&
                                sx_value(X, R, V, TW, RS, v, b, reach, &w)));
       }
-      if (lane == l) mine = c;
+      if (lane == l) mine += c;
     }
     if (rmine < n) cnt[rmine] = mine;
   }

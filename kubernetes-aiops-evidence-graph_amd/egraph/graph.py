@@ -9,8 +9,6 @@
 """
 from __future__ import annotations
 
-import os
-
 import ctypes as C
 from collections.abc import Iterable, Sequence
 
@@ -731,7 +729,6 @@ class Frontier:
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
         self.retry_blocks = 0
         self.wide_first = False
-        self.heavy = 0
         self._adapt_calls = 0
 
     def __del__(self):
@@ -790,12 +787,6 @@ class Frontier:
         L.check(L.lib.egr_frontier_set_retry(self._h, int(blocks)), "egr_frontier_set_retry")
         self.retry_blocks = int(blocks)
 
-    def set_heavy(self, n_cols: int) -> None:
-        """Grouped runs with the retry on: the first n_cols columns of the launch order start on
-        the wide grid beside the narrow kernel (egr_frontier_set_heavy); 0 turns it off."""
-        L.check(L.lib.egr_frontier_set_heavy(self._h, int(n_cols)), "egr_frontier_set_heavy")
-        self.heavy = int(n_cols)
-
     def set_wide_first(self, on: bool) -> None:
         """With the retry on: every column straight to the wide table (egr_frontier_set_wide_first)."""
         L.check(L.lib.egr_frontier_set_wide_first(self._h, int(bool(on))), "egr_frontier_set_wide_first")
@@ -819,12 +810,6 @@ class Frontier:
             self.set_retry(min(self.RETRY_BLOCKS, self.B))
             if st["overflowed"] > self.WIDE_FIRST_FRACTION * self.B:
                 self.set_wide_first(True)
-            elif os.environ.get("EGRAPH_FRONTIER_HEAVY", "1") != "0":
-                # the costliest-predicted columns, with room (x 1.5, whole waves of 64), start
-                # on the wide grid at once instead of overflowing the narrow table first
-                # ($EGRAPH_FRONTIER_HEAVY=0: off, for A/B)
-                h = -(-int(st["overflowed"]) * 3 // 2 // 64) * 64
-                self.set_heavy(min(self.B, max(64, h)))
             return True
         return False
 

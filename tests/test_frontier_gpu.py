@@ -360,31 +360,3 @@ def test_graph_service_concurrent_calls():
             assert [g_[0] for g_ in got] == alone
     finally:
         GraphService.reset()
-
-
-@pytest.mark.parametrize("heavy", [0, 3, 32, 48])
-def test_frontier_heavy_split_grouped(heavy):
-    """Grouped runs with the wide retry on and the launch order's first `heavy` columns started on
-    the wide grid on a second stream (egr_frontier_set_heavy), beside the narrow kernel over the
-    rest: top-k bit-identical to the oracle with the device launch order and a caller's order, on
-    a graph whose dense Node hubs overflow the narrow table (heavy = 48: every column wide)."""
-    from egraph.graph import group_seeds, launch_order
-    B = 48
-    g, sv, sc, ss, src = _world(B, seed=83, pods=16000, nodes=24)
-    inc = g.labels().index("Incident")
-    csr = g.csr()
-    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 3)
-    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
-    vl, _, _, _ = g.export()
-    e_ids, e_sc = oracle.topk(exp, er, vl, inc, 10)
-    gp, gv, gs = group_seeds(sv, sc, ss, B)
-    fr = g.snapshot().frontier(B, max_seeds=max(len(gv), 1), k=10, pool_entries=-1)
-    fr.set_retry(fr.RETRY_BLOCKS)
-    fr.set_heavy(heavy)
-    for order in (None, _dev(launch_order(gp, gv, csr["row_ptr"]))):
-        ids, sco = fr.run_grouped(_dev(gp), _dev(gv), _dev(gs), _dev(src), hops=3, exclude_label=inc,
-                                  order=order)
-        np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids)
-        assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
-    if heavy == 0:
-        assert fr.stats()["overflowed"] >= 1          # the narrow table does overflow here
