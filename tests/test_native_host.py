@@ -206,3 +206,63 @@ def test_locality_order_native_matches_python(seed):
     pos[out] = np.arange(V)
     first_node = out[np.flatnonzero(vl[out] == labels.index("Node"))[0]]
     assert vl[out[pos[first_node] + 1]] == labels.index("Pod")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_labelled_lookup_vertex_of_and_id_list(seed):
+    """egr_graph_lookup_labeled (MATCH (n:label {id})) and the VertexOf view against a Python
+    model of MERGE, with ids carried by several labels, duplicates inside one batch and more
+    ids than one pipelined lookup group (32); the id list merge_nodes keeps equals the native
+    graph's; lookup() of present and absent ids equals egr_graph_find one at a time."""
+    from egraph import _lib as L
+    from egraph.graph import EvidenceGraph
+    rng = random.Random(seed)
+    g = EvidenceGraph()
+    model: dict = {}
+    order: list = []
+    for _ in range(5):
+        ids = [f"v{rng.randrange(150)}" for _ in range(rng.randrange(1, 90))]
+        labels = [rng.choice(["Pod", "Node", "Incident"]) for _ in ids]
+        out = g.merge_nodes(ids, labels)
+        for i, lab, v in zip(ids, labels, out.tolist()):
+            if (lab, i) not in model:
+                model[(lab, i)] = len(order)
+                order.append(i)
+            assert model[(lab, i)] == v
+    assert g._ids == order and g.vertex_ids() == [g.vertex_id(v) for v in range(g.num_vertices)]
+    probe = [f"v{k}" for k in range(160)]
+    for lab in ("Pod", "Node", "Incident", "Service"):
+        got = g.lookup_labeled(probe, lab).tolist()
+        assert got == [model.get((lab, i), -1) for i in probe]
+    mixed = [rng.choice(["Pod", "Node", "Incident"]) for _ in probe]
+    assert g.lookup_labeled(probe, mixed).tolist() == [model.get(k, -1) for k in zip(mixed, probe)]
+    vo = g.vertex_of
+    assert len(vo) == len(order) and dict(vo.items()) == model
+    assert all(vo[k] == v for k, v in model.items()) and ("Service", "v1") not in vo
+    with pytest.raises(KeyError):
+        vo[("Service", "v1")]
+    first = g.lookup(probe).tolist()
+    assert first == [int(L.lib.egr_graph_find(g._h, i.encode(), len(i))) for i in probe]
+
+
+def test_attach_idx_matches_numpy():
+    """pyhost.attach_idx (first present candidate per row, the ids ranked before it) against the
+    numpy statement it replaced."""
+    from egraph import _lib
+    rng = np.random.default_rng(3)
+    count = rng.integers(1, 5, 400).astype(np.int64)
+    n = int(count.sum())
+    found = np.where(rng.random(n) < 0.4, rng.integers(0, 1000, n), -1).astype(np.int64)
+    sv, ok, before, brow = _lib.pyhost.attach_idx(found, count)
+    starts = np.concatenate([[0], np.cumsum(count)[:-1]])
+    pos = np.where(found >= 0, np.arange(n), n)
+    first = np.minimum.reduceat(pos, starts)
+    e_ok = first < n
+    e_before = np.flatnonzero(np.arange(n) < np.repeat(np.where(e_ok, first, n), count))
+    e_row = np.repeat(np.arange(len(count)), count)[e_before]
+    np.testing.assert_array_equal(np.frombuffer(ok, np.bool_), e_ok)
+    np.testing.assert_array_equal(np.frombuffer(sv, np.uint32), found[first[e_ok]].astype(np.uint32))
+    np.testing.assert_array_equal(np.frombuffer(before, np.int64), e_before)
+    np.testing.assert_array_equal(np.frombuffer(brow, np.int64), e_row)
+    with pytest.raises(ValueError):
+        _lib.pyhost.attach_idx(found[:3], count)
