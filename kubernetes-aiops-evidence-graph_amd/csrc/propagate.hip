@@ -790,6 +790,8 @@ __global__ void sx_bounds_kernel(const int64_t* __restrict__ off, const int64_t*
 constexpr int SX_ROWS = 4;
 constexpr int64_t SX_MAX_BLOCKS = 2048;      // grid-stride beyond this (8 blocks per CU)
 inline dim3 sx_grid(int64_t n) { return dim3((unsigned)std::min<int64_t>((n + SX_ROWS - 1) / SX_ROWS, SX_MAX_BLOCKS)); }
+// the work map is one 64-bit mask of 64-column chunks per row: rows up to 4096 columns (words)
+constexpr int SX_MAP_MAX = 64 * 64;
 // the work-map kernels: the same waves as sx_grid, each wave's rows strided by the wave count
 // and mapped one lane each up front (a wave-per-row walk paid its row id, flags and data loads
 // one after another for each of its ~15 rows)
@@ -1963,6 +1965,9 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
   if (!reach && (uint64_t)n * (uint64_t)width >= (1ull << 32))
     return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: send rows x columns exceed the 2^32 "
                                  "entry index of the score format");
+  if (width > SX_MAP_MAX)
+    return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: more than 4096 columns (the work map "
+                                 "holds 64 chunks of 64): use egr_plan_pack_sparse");
   const int kk = reach ? 1 : 0;
   if ((size_t)n + 1 > p->sxc_cap[kk]) {
     dfree(p->sxc_off[kk]);
@@ -2008,6 +2013,9 @@ int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_v
   DeviceGuard guard(p->s->device);
   hipStream_t st = (hipStream_t)stream;
   const int width = reach ? p->W : p->Bpad;
+  if (width > SX_MAP_MAX)
+    return egr::fail(EGR_EINVAL, "egr_plan_unpack_sparse_cap: more than 4096 columns: use "
+                                 "egr_plan_unpack_sparse");
   float* X = reach ? nullptr : p->x[p->xcur];
   uint64_t* R = reach ? p->reach[p->rcur] : nullptr;
   const uint32_t V = (uint32_t)p->s->V;

@@ -522,8 +522,9 @@ def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k:
     ...) and the reach chain (reach hop, reach exchange, ...) share no buffer until the top-k, so
     the reach chain runs on a second stream beside it and its hops and exchanges hide under the
     score chain's."""
+    # (the fixed-slot kernels map rows of up to 4096 columns; wider plans keep the host counts)
     use_fixed = fixed and sparse and all(r.cap for r in runs) and \
-        all(hasattr(r.eng, "pack_sparse_cap") for r in runs)
+        all(hasattr(r.eng, "pack_sparse_cap") and r.Bpad <= 4096 for r in runs)
     for r in runs:
         r.overflow.zero_()
         if fixed and sparse and not use_fixed:
