@@ -661,6 +661,10 @@ def _traffic(name: str):
     return None
 
 
+# the table a frontier column tries first (egraph.graph.Frontier.FIRST_*)
+FIRST_TABLE = ("narrow", "wide", "mid")
+
+
 def frontier_layout_on() -> bool:
     """The snapshot lays the frontier's CSR out in locality order (csrc/layout.hip) unless
     $EGRAPH_FRONTIER_LAYOUT is "0"."""
@@ -1275,12 +1279,17 @@ def main():
     if args.engine == "frontier":
         # graphs with large 3-hop neighbourhoods (the dense C4): columns that overflow the
         # narrow table get the wide-table retry from here on (egraph.graph.Frontier.adapt)
-        for lane in ctx["lanes"]:
-            if lane["frontier"].adapt():
-                log(f"[rank {rank}] wide-table retry on ({lane['frontier'].retry_blocks} blocks)")
-        for _ in range(args.warmup):
-            run_step(ctx, args.hops)
-        torch.cuda.synchronize(dev)
+        # most columns overflowing the narrow table: the mid table first; a second look after the
+        # next warm-up steps moves to wide-first if most columns overflow that one too
+        for check in range(2):
+            for lane in ctx["lanes"]:
+                fr = lane["frontier"]
+                if fr.adapt(fr.stats()):
+                    log(f"[rank {rank}] wide-table retry on ({fr.retry_blocks} blocks), first "
+                        f"table {FIRST_TABLE[fr.wide_first]}")
+            for _ in range(max(args.warmup, 1)):
+                run_step(ctx, args.hops)
+            torch.cuda.synchronize(dev)
     graphs = args.engine == "frontier" and not args.no_graph
     if graphs:
         capture_lanes(ctx, args.hops)
@@ -1360,6 +1369,8 @@ def main():
             "batches_per_launch": M,
             "distinct_batches_per_launch": ctx["distinct_batches"],
             "frontier_layout": "locality order (csrc/layout.hip)" if frontier_layout_on() else "canonical",
+            "first_table": (FIRST_TABLE[ctx["lanes"][0]["frontier"].wide_first]
+                            if args.engine == "frontier" else None),
             "incidents_in_graph": ctx["incidents_in_graph"],
             "hip_graph_replay": out_graph,
             "seed_input": ("grouped by incident + column offsets, resident; costliest-first launch "

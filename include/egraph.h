@@ -380,9 +380,11 @@ typedef struct egr_frontier egr_frontier;
  * overflow and skip the launch).  Takes effect from the next run (capture it into a graph
  * after setting it).                                                                       */
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
-/* Top-k-only frontiers with the retry on: `on` != 0 sends EVERY column straight to the wide grid
- * (for graphs where most columns overflow the narrow table, e.g. the dense C4: the narrow
- * attempt would be wasted work).  Same results; takes effect from the next egr_frontier_run. */
+/* Top-k-only frontiers with the retry on: the first table every column tries, for graphs where
+ * most columns overflow the narrow one (the narrow attempt would be wasted work).  `on` = 0: the
+ * narrow table; 1: EVERY column straight to the wide grid; 2: a 2.8k-slot mid table first (three
+ * workgroups per CU), its overflowing columns through the wide grid (the dense C4).  Same
+ * results in every mode; EGR_EINVAL outside 0..2; takes effect from the next egr_frontier_run. */
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on);
 
 int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, int32_t k,

@@ -119,6 +119,16 @@ struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr
 // column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
 // one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
 // 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
+// buckets per lockstep probe round of each geometry (A/B: -DFR_PROBE_W_*=N)
+#ifndef FR_PROBE_W_WIDE
+#define FR_PROBE_W_WIDE 1
+#endif
+#ifndef FR_PROBE_W_NARROW
+#define FR_PROBE_W_NARROW 1
+#endif
+#ifndef FR_PROBE_W_MID
+#define FR_PROBE_W_MID 1
+#endif
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144
@@ -128,6 +138,7 @@ namespace fr_wide {
 #define FR_HUBCHAIN 1
 #define FR_DBUF 0
 #define FR_KERNELS 7
+#define FR_PROBE_W FR_PROBE_W_WIDE
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -136,6 +147,7 @@ namespace fr_wide {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_wide
 
@@ -151,6 +163,7 @@ namespace fr_narrow {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 1
 #define FR_KERNELS 1
+#define FR_PROBE_W FR_PROBE_W_NARROW
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -159,8 +172,36 @@ namespace fr_narrow {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_narrow
+
+// A 2.8k-slot table at 256 threads (three workgroups per CU by LDS) for graphs whose columns
+// mostly overflow the narrow table but fit 2.1k members (the dense C4: ~1.5k, 92 % of its
+// columns): the first attempt of a mid-first frontier (egr_frontier_set_wide_first(f, 2)), whose
+// overflowing columns take the wide retry.  C4: -2.4 % per step against wide-first
+// (profiles/r04_ab_mid_first.txt).
+namespace fr_mid {
+#define FR_FT 256
+#define FR_LCAP 2816
+#define FR_LLIMIT 2112
+#define FR_BLOOM_LOG 15
+#define FR_WAVES_PER_EU 3
+#define FR_HUBCHAIN 2
+#define FR_DBUF 1
+#define FR_KERNELS 1
+#define FR_PROBE_W FR_PROBE_W_MID
+#include "frontier_body.h"
+#undef FR_FT
+#undef FR_LCAP
+#undef FR_LLIMIT
+#undef FR_BLOOM_LOG
+#undef FR_WAVES_PER_EU
+#undef FR_HUBCHAIN
+#undef FR_DBUF
+#undef FR_PROBE_W
+#undef FR_KERNELS
+}  // namespace fr_mid
 
 // The overflow fallback's launch geometry: one wave per workgroup.  Its grid is launched after
 // every narrow run and nearly always finds no overflowing column; a one-wave workgroup is
@@ -176,6 +217,7 @@ namespace fr_fallback {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 0
 #define FR_KERNELS 4
+#define FR_PROBE_W 1
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -184,6 +226,7 @@ namespace fr_fallback {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_fallback
 
@@ -426,8 +469,9 @@ __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint3
 struct egr_frontier {
   const egr_snapshot* s = nullptr;
   bool big_geom = false;          // global variant in 512-thread workgroups (egr_frontier_set_retry)
-  bool wide_first = false;        // narrow frontier whose columns mostly overflow: straight to the
-                                  // wide retry grid over every column (egr_frontier_set_wide_first)
+  int first = 0;                  // narrow frontier whose columns mostly overflow: 1 = straight to
+                                  // the wide retry grid over every column, 2 = the mid table first
+                                  // (egr_frontier_set_wide_first)
   uint32_t* all_n = nullptr;      // device word = B (the wide-first grid's list length)
   int32_t retry_blocks = -1;      // wide-table second chance for narrow overflows: grid size
                                   // (0 = off; -1 = unset: $EGRAPH_FRONTIER_WIDE_RETRY decides)
@@ -741,7 +785,15 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                        : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
     an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
-    if (f->wide_first && rb > 0) {
+    if (f->first == 2 && rb > 0) {
+      // mid-first: every column in the 2.8k-slot table; what overflows it takes the wide retry
+      FArgs am = an;
+      hipLaunchKernelGGL(fr_mid::frontier_lds_kernel, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
+      EGR_CHECK_LAUNCH();
+      hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
+                         dim3(fr_wide::FT), 0, st, a);
+      EGR_CHECK_LAUNCH();
+    } else if (f->first == 1 && rb > 0) {
       // most columns overflow the narrow table: every column goes straight to the wide grid,
       // in launch order (the narrow kernel, which also zeroes the seed counters, is skipped)
       FArgs aw = a;
@@ -811,8 +863,8 @@ int egr_frontier_run_grouped(egr_frontier* f, const uint32_t* seed_ptr, const ui
 }
 
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on) {
-  if (!f) return egr::fail(EGR_EINVAL, "egr_frontier_set_wide_first: NULL frontier");
-  f->wide_first = on != 0;
+  if (!f || on < 0 || on > 2) return egr::fail(EGR_EINVAL, "egr_frontier_set_wide_first: bad arguments");
+  f->first = on;
   return EGR_OK;
 }
 

@@ -308,32 +308,41 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
 
-// The in-order fmaf chain of one hub-row segment: lane j holds entry j's (w, x) (x of an
-// absent neighbour is +0: fmaf(w, +0, acc) == acc for finite w and acc != -0, so running the
-// chain over every entry equals running it over the present ones).  `rem` = entries left in
-// the row (>= 1, wave-uniform); the result is in every lane (FR_HUBCHAIN 1) or in lane m (2).
-//   FR_HUBCHAIN 1: every entry, unrolled by 8 with immediate lane indices
-//   FR_HUBCHAIN 2: the pairs go through the wave's LDS scratch and lane m runs the chain from
-//                  16-B LDS reads (one lane, 4-cycle dependent fmas)
+// The in-order fmaf chain of one hub-row segment: lane j holds entry j's (w, x).  Only the
+// non-zero terms run: an absent neighbour (x = +0) or a member whose score is +0 gives
+// fmaf(w, +0, acc) == acc for finite w and acc != -0 (acc starts at +0 and no fmaf of finite
+// operands turns it into -0), so the chain over the non-zero entries, in lane (= CSR) order,
+// equals the chain over every entry.  Hub rows are mostly non-members: the chain shrinks to the
+// few members' terms.  `rem` = entries left in the row (>= 1, wave-uniform); the result is in
+// every lane (FR_HUBCHAIN 1) or in lane m (2).
+//   FR_HUBCHAIN 1: v_readlane operands of each set ballot bit, in every lane
+//   FR_HUBCHAIN 2: the non-zero pairs compacted into the wave's LDS scratch (mbcnt rank) and
+//                  lane m runs the chain from 16-B LDS reads (one lane, 4-cycle dependent fmas)
 __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32_t rem, int m,
                                           float& hacc, float2* chain) {
-  const int lane = threadIdx.x & 63;
+  (void)rem;
+  const bool nz = present && x != 0.f;
+  uint64_t mk = __ballot(nz);
+  if (mk == 0) return;                      // (wave-uniform)
 #if FR_HUBCHAIN == 1
-  (void)present; (void)m; (void)chain; (void)lane;
-  const float xw = present ? w : 0.f;
-  const int n = (int)min(rem, 64u);
-  for (int y0 = 0; y0 < n; y0 += 8) {
-#pragma unroll
-    for (int y = 0; y < 8; ++y) hacc = fmaf(readlane_f(xw, y0 + y), readlane_f(x, y0 + y), hacc);
+  (void)m; (void)chain;
+  while (mk) {
+    const int j = __ffsll((long long)mk) - 1;
+    mk &= mk - 1;
+    hacc = fmaf(readlane_f(w, j), readlane_f(x, j), hacc);
   }
 #else
-  (void)present;
-  chain[lane] = make_float2(present ? w : 0.f, x);
+  const int lane = threadIdx.x & 63;
+  const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+  const int n = __popcll(mk);
+  if (nz) chain[r] = make_float2(w, x);
+  if (lane == 0 && (n & 1)) chain[n] = make_float2(0.f, 0.f);   // pads the last 16-B read
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (lane == m) {
     const float4* c4 = reinterpret_cast<const float4*>(chain);
-    const int n2 = (int)((min(rem, 64u) + 1) / 2);
+    const int n2 = (n + 1) / 2;
     float a = hacc;
     for (int y0 = 0; y0 < n2; y0 += 4) {
       float4 p[4];

@@ -728,7 +728,8 @@ class Frontier:
         self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
         self.retry_blocks = 0
-        self.wide_first = False
+        self.wide_first = self.FIRST_NARROW
+        self._mid_checked = False
         self._adapt_calls = 0
 
     def __del__(self):
@@ -787,29 +788,46 @@ class Frontier:
         L.check(L.lib.egr_frontier_set_retry(self._h, int(blocks)), "egr_frontier_set_retry")
         self.retry_blocks = int(blocks)
 
-    def set_wide_first(self, on: bool) -> None:
-        """With the retry on: every column straight to the wide table (egr_frontier_set_wide_first)."""
-        L.check(L.lib.egr_frontier_set_wide_first(self._h, int(bool(on))), "egr_frontier_set_wide_first")
-        self.wide_first = bool(on)
+    # the first table a column tries (egr_frontier_set_wide_first): narrow, the wide grid, or the
+    # 2.8k-slot mid table (then the wide grid for what overflows it)
+    FIRST_NARROW, FIRST_WIDE, FIRST_MID = 0, 1, 2
 
-    # a run in which more than this fraction of the columns overflowed the narrow table switches
-    # to wide-first (the narrow attempt of such columns is wasted work)
+    def set_wide_first(self, mode: int) -> None:
+        """With the retry on: the table every column tries first -- FIRST_NARROW (0 / False),
+        FIRST_WIDE (1 / True: every column straight to the wide table) or FIRST_MID (2)."""
+        mode = int(mode)
+        L.check(L.lib.egr_frontier_set_wide_first(self._h, mode), "egr_frontier_set_wide_first")
+        self.wide_first = mode
+
+    # a run in which more than this fraction of the columns overflowed the narrow table starts
+    # every column in the mid table (the narrow attempt of such columns is wasted work); if the
+    # first checked mid-first run overflows that table for as many, wide-first
     WIDE_FIRST_FRACTION = 0.5
 
     def adapt(self, stats: dict | None = None) -> bool:
         """After a run: turn the wide retry on if that run had overflowing columns (graphs with
-        large 3-hop neighbourhoods, e.g. the dense C4), and send every column straight to the
-        wide table if most of them overflowed.  Returns True if it changed."""
-        if self.retry_blocks != 0 or self.pool_entries >= 0:
+        large 3-hop neighbourhoods, e.g. the dense C4), and start every column in the mid table
+        if most of them overflowed (then in the wide table if most overflow the mid one too).
+        Returns True if it changed."""
+        if self.pool_entries >= 0:
+            return False
+        if self.retry_blocks != 0 and (self.wide_first != self.FIRST_MID or self._mid_checked):
             return False
         self._adapt_calls += 1
         if stats is None and self._adapt_calls % 16 != 1:      # a stats read synchronises
             return False
         st = self.stats() if stats is None else stats
-        if st["overflowed"] > 0:
-            self.set_retry(min(self.RETRY_BLOCKS, self.B))
-            if st["overflowed"] > self.WIDE_FIRST_FRACTION * self.B:
-                self.set_wide_first(True)
+        over = st["overflowed"] > self.WIDE_FIRST_FRACTION * self.B
+        if self.retry_blocks == 0:
+            if st["overflowed"] > 0:
+                self.set_retry(min(self.RETRY_BLOCKS, self.B))
+                if over:
+                    self.set_wide_first(self.FIRST_MID)
+                return True
+            return False
+        self._mid_checked = True        # (one check of a mid-first run)
+        if over:
+            self.set_wide_first(self.FIRST_WIDE)
             return True
         return False
 

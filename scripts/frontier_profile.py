@@ -39,6 +39,9 @@ def main():
     torch.cuda.set_device(dev)
     ctx = bench.setup(args.config, args.batch, 10, 0, dev, pool_entries=0 if args.pool else -1,
                       merge=args.merge)
+    bench.step_frontier(ctx, args.hops)
+    torch.cuda.synchronize()
+    ctx["frontier"].adapt(ctx["frontier"].stats())   # as bench.py's warm-up (C4: mid-first)
     for _ in range(3 * args.merge):
         bench.step_frontier(ctx, args.hops)
     torch.cuda.synchronize()

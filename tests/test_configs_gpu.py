@@ -260,8 +260,10 @@ def c4():
 
 def test_c4_frontier_b256(c4):
     """C4's larger neighbourhoods overflow the narrow table: the first run sends those columns
-    to the global-memory variant, adapt() turns the wide-table retry on, and the rerun takes
-    them through the persistent wide grid -- the same top-k both times (bench.py's C4 path)."""
+    to the global-memory variant, adapt() turns the wide-table retry on with the mid table first,
+    and the rerun takes the columns through the mid table (its overflows through the persistent
+    wide grid) -- the same top-k every time, and in the wide-first and narrow-first modes too
+    (bench.py's C4 path)."""
     g, csr, vl, sv, sc, ss, src = c4
     B = len(src)
     fr = g.snapshot().frontier(B, max_seeds=len(sv), k=10, pool_entries=-1)
@@ -273,14 +275,19 @@ def test_c4_frontier_b256(c4):
         assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
         if run == 0:
             assert fr.stats()["overflowed"] > 0 and fr.adapt() and fr.retry_blocks > 0
-    # most C4 columns overflow the narrow table: adapt() chose wide-first (every column straight
-    # to the wide grid); the narrow-then-retry path and wide-first give the same top-k
-    assert fr.wide_first
-    fr.set_wide_first(False)
-    fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
-    ids, sco = fr.run(_dev(src), hops=3, exclude_label=g.labels().index("Incident"))
-    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids, err_msg="narrow + retry")
-    assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
+    # most C4 columns overflow the narrow table: adapt() chose mid-first (the 2.8k-slot table,
+    # then the wide grid for what overflows it), and most fit that table, so its second look
+    # keeps it; wide-first and narrow-then-retry give the same top-k
+    assert fr.wide_first == fr.FIRST_MID
+    st = fr.stats()
+    assert st["overflowed"] <= B // 2 and st["global_columns"] == 0
+    assert not fr.adapt(st) and fr.wide_first == fr.FIRST_MID
+    for mode, name in ((fr.FIRST_WIDE, "wide-first"), (fr.FIRST_NARROW, "narrow + retry")):
+        fr.set_wide_first(mode)
+        fr.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+        ids, sco = fr.run(_dev(src), hops=3, exclude_label=g.labels().index("Incident"))
+        np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), e_ids, err_msg=name)
+        assert sco.cpu().numpy().tobytes() == e_sc.tobytes()
 
 
 @pytest.mark.parametrize("P", [2, 4])
