@@ -119,16 +119,6 @@ struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr
 // column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
 // one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
 // 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
-// buckets per lockstep probe round of each geometry (A/B: -DFR_PROBE_W_*=N)
-#ifndef FR_PROBE_W_WIDE
-#define FR_PROBE_W_WIDE 1
-#endif
-#ifndef FR_PROBE_W_NARROW
-#define FR_PROBE_W_NARROW 1
-#endif
-#ifndef FR_PROBE_W_MID
-#define FR_PROBE_W_MID 1
-#endif
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144
@@ -138,7 +128,6 @@ namespace fr_wide {
 #define FR_HUBCHAIN 1
 #define FR_DBUF 0
 #define FR_KERNELS 7
-#define FR_PROBE_W FR_PROBE_W_WIDE
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -147,7 +136,6 @@ namespace fr_wide {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
-#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_wide
 
@@ -163,7 +151,6 @@ namespace fr_narrow {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 1
 #define FR_KERNELS 1
-#define FR_PROBE_W FR_PROBE_W_NARROW
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -172,7 +159,6 @@ namespace fr_narrow {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
-#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_narrow
 
@@ -190,7 +176,6 @@ namespace fr_mid {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 1
 #define FR_KERNELS 1
-#define FR_PROBE_W FR_PROBE_W_MID
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -199,7 +184,6 @@ namespace fr_mid {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
-#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_mid
 
@@ -217,7 +201,6 @@ namespace fr_fallback {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 0
 #define FR_KERNELS 4
-#define FR_PROBE_W 1
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -226,7 +209,6 @@ namespace fr_fallback {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
-#undef FR_PROBE_W
 #undef FR_KERNELS
 }  // namespace fr_fallback
 
