@@ -128,6 +128,7 @@ namespace fr_wide {
 #define FR_HUBCHAIN 1
 #define FR_DBUF 0
 #define FR_KERNELS 7
+#define FR_LMAX 12
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -136,6 +137,7 @@ namespace fr_wide {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_LMAX
 #undef FR_KERNELS
 }  // namespace fr_wide
 
@@ -151,6 +153,7 @@ namespace fr_narrow {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 1
 #define FR_KERNELS 1
+#define FR_LMAX 12
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -159,6 +162,7 @@ namespace fr_narrow {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_LMAX
 #undef FR_KERNELS
 }  // namespace fr_narrow
 
@@ -176,6 +180,7 @@ namespace fr_mid {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 1
 #define FR_KERNELS 1
+#define FR_LMAX 16
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -184,6 +189,7 @@ namespace fr_mid {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_LMAX
 #undef FR_KERNELS
 }  // namespace fr_mid
 
@@ -201,6 +207,7 @@ namespace fr_fallback {
 #define FR_HUBCHAIN 2
 #define FR_DBUF 0
 #define FR_KERNELS 4
+#define FR_LMAX 12
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -209,6 +216,7 @@ namespace fr_fallback {
 #undef FR_WAVES_PER_EU
 #undef FR_HUBCHAIN
 #undef FR_DBUF
+#undef FR_LMAX
 #undef FR_KERNELS
 }  // namespace fr_fallback
 

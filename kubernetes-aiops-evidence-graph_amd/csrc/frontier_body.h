@@ -15,10 +15,12 @@ constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
 constexpr uint32_t LLIMIT = FR_LLIMIT;      // members before a column overflows (load 0.75)
 constexpr int LPPT = LCAP / FT;             // slots cleared per thread
-// rows of up to LMAX entries run one lane per row (longer ones across the wave); 12 measured
-// best against 8 and 16 (profiles/r02_ab_frontier_session3.txt)
-constexpr int LMAX = 12;
-static_assert(LMAX % 4 == 0 && LMAX <= 16, "light rows: whole probe batches of LB = 4");
+// rows of up to LMAX = FR_LMAX entries run one lane per row (longer ones across the wave, one
+// 64-entry segment per round); per geometry: C3's rows are <= 12 but for its Node hubs (12
+// measured best against 8 and 16 there, profiles/r02_ab_frontier_session3.txt), C4's telemetry
+// links put 29 % of its entries in rows of 13..16 (profiles/r04_ab_lmax.txt)
+constexpr int LMAX = FR_LMAX;
+static_assert(LMAX % 4 == 0 && LMAX <= 32, "light rows: whole probe batches of LB = 4");
 constexpr int LB = 4;                       // keys probed together per lane
 constexpr int BLOOM_LOG = FR_BLOOM_LOG;
 constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys in one read
@@ -466,18 +468,38 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     float acc = 0.f;
     light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
     tk.tick(1);
+    // hub rows, one 64-entry segment at a time across the wave; the next segment's entries (of
+    // this hub, or the first of the next one) are loaded before the current one is probed
     uint64_t heavy = __ballot(!light);
-    while (heavy) {
-      const int m = __ffsll((long long)heavy) - 1;
+    if (heavy) {
+      int m = __ffsll((long long)heavy) - 1;
       heavy &= heavy - 1;
-      const uint32_t he0 = __builtin_amdgcn_readlane(e0, m);
-      const uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
-      const uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
+      uint32_t he0 = __builtin_amdgcn_readlane(e0, m);
+      uint32_t hdeg = __builtin_amdgcn_readlane(deg, m);
+      uint32_t hkind = __builtin_amdgcn_readlane(kind, m);
+      uint32_t base = 0;
+      uint2 ce = lane < (int)hdeg ? A.cv[he0 + lane] : make_uint2(0u, 0u);
       float hacc = 0.f;
-      for (uint32_t base = 0; base < hdeg; base += 64) {
+      for (;;) {
+        int m2 = m;
+        uint32_t he02 = he0, hdeg2 = hdeg, hkind2 = hkind, base2 = base + 64;
+        bool more = true;
+        if (base2 >= hdeg) {
+          if (heavy) {
+            m2 = __ffsll((long long)heavy) - 1;
+            heavy &= heavy - 1;
+            he02 = __builtin_amdgcn_readlane(e0, m2);
+            hdeg2 = __builtin_amdgcn_readlane(deg, m2);
+            hkind2 = __builtin_amdgcn_readlane(kind, m2);
+            base2 = 0;
+          } else {
+            more = false;
+          }
+        }
+        const uint32_t j2 = base2 + lane;
+        const uint2 cn = (more && j2 < hdeg2) ? A.cv[he02 + j2] : make_uint2(0u, 0u);
         const uint32_t j = base + lane;
         const bool act = j < hdeg;
-        const uint2 ce = act ? A.cv[he0 + j] : make_uint2(0u, 0u);
         const uint32_t u = ce.x;
         tk.tick(8);
         const int q = act ? tab_find<GT>(t, u) : -1;
@@ -490,8 +512,18 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         tk.tick(10);
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
         tk.tick(11);
+        if (base2 == 0 || !more) {          // the hub's last segment
+          if (lane == m) acc = hacc;
+          hacc = 0.f;
+        }
+        if (!more) break;
+        ce = cn;
+        m = m2;
+        he0 = he02;
+        hdeg = hdeg2;
+        hkind = hkind2;
+        base = base2;
       }
-      if (lane == m) acc = hacc;
     }
     tk.tick(2);
     if constexpr (DW) {
