@@ -129,6 +129,7 @@ namespace fr_wide {
 #define FR_DBUF 0
 #define FR_KERNELS 7
 #define FR_LMAX 12
+#define FR_FIND_SELECT 1
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -138,6 +139,7 @@ namespace fr_wide {
 #undef FR_HUBCHAIN
 #undef FR_DBUF
 #undef FR_LMAX
+#undef FR_FIND_SELECT
 #undef FR_KERNELS
 }  // namespace fr_wide
 
@@ -154,6 +156,7 @@ namespace fr_narrow {
 #define FR_DBUF 1
 #define FR_KERNELS 1
 #define FR_LMAX 12
+#define FR_FIND_SELECT 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -163,6 +166,7 @@ namespace fr_narrow {
 #undef FR_HUBCHAIN
 #undef FR_DBUF
 #undef FR_LMAX
+#undef FR_FIND_SELECT
 #undef FR_KERNELS
 }  // namespace fr_narrow
 
@@ -181,6 +185,7 @@ namespace fr_mid {
 #define FR_DBUF 1
 #define FR_KERNELS 1
 #define FR_LMAX 16
+#define FR_FIND_SELECT 1
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -190,6 +195,7 @@ namespace fr_mid {
 #undef FR_HUBCHAIN
 #undef FR_DBUF
 #undef FR_LMAX
+#undef FR_FIND_SELECT
 #undef FR_KERNELS
 }  // namespace fr_mid
 
@@ -208,6 +214,7 @@ namespace fr_fallback {
 #define FR_DBUF 0
 #define FR_KERNELS 4
 #define FR_LMAX 12
+#define FR_FIND_SELECT 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -217,6 +224,7 @@ namespace fr_fallback {
 #undef FR_HUBCHAIN
 #undef FR_DBUF
 #undef FR_LMAX
+#undef FR_FIND_SELECT
 #undef FR_KERNELS
 }  // namespace fr_fallback
 

@@ -9,7 +9,8 @@
 //   through the wave's LDS scratch, one lane), FR_DBUF (1: two slot-indexed score buffers; a
 //   pull reads hop h's and writes hop h + 1's directly, seed add and need-bit clearing
 //   included, so no copy phase follows the walk; 0: pull results by member index in HBM and a
-//   copy phase).  Every combination instantiated by frontier.hip is a shipped path.
+//   copy phase), FR_LMAX (light-row limit), FR_FIND_SELECT (1: branch-free probe rounds, see
+//   find_batch).  Every combination instantiated by frontier.hip is a shipped path.
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -182,6 +183,58 @@ struct Ticker {
 
 // Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
 // still unresolved, so a lane's NQ probe sequences share round trips.
+#if FR_FIND_SELECT
+template <bool GT, int NQ>
+__device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
+                                           int (&q)[NQ]) {
+  // Branch-free per key: every key reads its filter word and, while any lane still probes, its
+  // bucket (a resolved or unused key re-reads one in range, its result unused); the matches,
+  // slots and the next bucket are selects, not branches -- a wave no longer steps through the
+  // exec-mask bookkeeping of NQ divergent ifs per round
+  const uint32_t nb = GT ? t.cap / 4 : LCAP / 4;   // LDS: a compile-time bucket count
+  uint32_t bk[NQ];
+  bool pend[NQ];
+#pragma unroll
+  for (int x = 0; x < NQ; ++x) {
+    bk[x] = hbucket(key[x], nb);
+    q[x] = -1;
+    pend[x] = (uint32_t)x < nq;
+  }
+  if constexpr (!GT) {
+    // the filter: a key whose bit is clear is not a member
+    uint32_t bw[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) bw[x] = t.bloom[bloom_hash(key[x]) >> 5];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) pend[x] = pend[x] && ((bw[x] >> (bloom_hash(key[x]) & 31u)) & 1u);
+  }
+  for (uint32_t n = 0; n < nb; ++n) {
+    bool anyp = false;
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) anyp = anyp || pend[x];
+    if (!__any(anyp)) break;
+    uint4 kk[NQ];
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) kk[x] = t.bucket(bk[x]);
+#pragma unroll
+    for (int x = 0; x < NQ; ++x) {
+      const uint32_t v = key[x];
+      const bool m0 = kk[x].x == v, m1 = kk[x].y == v, m2 = kk[x].z == v, m3 = kk[x].w == v;
+      const bool hit = m0 || m1 || m2 || m3;
+      const uint32_t sl = m0 ? 0u : m1 ? 1u : m2 ? 2u : 3u;
+      // slots fill in order: an empty last slot ends the probe sequence
+      const bool stop = hit || kk[x].w == EMPTY;
+      q[x] = (pend[x] && hit) ? (int)(4 * bk[x] + sl) : q[x];
+      const bool go = pend[x] && !stop;
+      const uint32_t nx = bk[x] + 1 == nb ? 0u : bk[x] + 1;
+      bk[x] = go ? nx : bk[x];
+      pend[x] = go;
+    }
+  }
+}
+#else
+// (branchy: only the keys still probing read -- C3's short rows leave most of a lane's keys
+// unused, and the select form measured +0.4 % there, profiles/r04_ab_branch_free_probe.txt)
 template <bool GT, int NQ>
 __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
                                            int (&q)[NQ]) {
@@ -223,6 +276,7 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
     }
   }
 }
+#endif
 
 // Row kinds of a phase: K_REACH = reach frontier (insert neighbours, give new ones the next
 // depth), K_PULL = recompute the row's score, K_PROP = expansion for the next hop (insert
@@ -291,10 +345,17 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     if (kind & K_PULL) {
       float xs[LB];
 #pragma unroll
+#if FR_FIND_SELECT
+      for (int x = 0; x < LB; ++x) xs[x] = t.s[q[x] >= 0 ? q[x] : 0];   // (slot 0: unused)
+#pragma unroll
+      for (int x = 0; x < LB; ++x)   // absent: skipped (exact)
+        acc = q[x] >= 0 ? fmaf(w[sb * LB + x], xs[x], acc) : acc;
+#else
       for (int x = 0; x < LB; ++x) xs[x] = q[x] >= 0 ? t.s[q[x]] : 0.f;
 #pragma unroll
       for (int x = 0; x < LB; ++x)
         if (q[x] >= 0) acc = fmaf(w[sb * LB + x], xs[x], acc);   // absent: skipped (exact)
+#endif
     }
     tk.tick(6);
     if (kind & (K_REACH | K_PROP)) {
