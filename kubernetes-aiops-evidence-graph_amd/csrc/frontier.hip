@@ -91,11 +91,12 @@ struct FArgs {
   uint32_t* ovf_list;           // where an LDS kernel hands on its overflowing columns
   uint32_t* ovf_n;
   uint32_t* ovf_next;           // the global-memory variant's work counter (over ovf_list)
+  uint32_t* retry_next;         // the wide retry's work counter (over retry_list)
   uint32_t ovf_cap;             // ovf_list entries; further overflowing columns go to spill_*
   uint32_t* spill_list;
   uint32_t* spill_n;
-  const uint32_t* retry_list;   // the retry kernel's input list and count (block i takes
-  const uint32_t* retry_n;      // entries i, i + gridDim.x, ...)
+  const uint32_t* retry_list;   // the retry kernel's input list and count (drained through
+  const uint32_t* retry_n;      // the retry_next work counter)
   float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
                                 // narrow (FR_DBUF): the seeds' values by slot
   // global tables (one per resident workgroup of the fallback kernel)
@@ -130,6 +131,7 @@ namespace fr_wide {
 #define FR_KERNELS 7
 #define FR_LMAX 12
 #define FR_FIND_SELECT 1
+#define FR_HEAD 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -140,6 +142,7 @@ namespace fr_wide {
 #undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
+#undef FR_HEAD
 #undef FR_KERNELS
 }  // namespace fr_wide
 
@@ -157,6 +160,7 @@ namespace fr_narrow {
 #define FR_KERNELS 1
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
+#define FR_HEAD 4
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -167,6 +171,7 @@ namespace fr_narrow {
 #undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
+#undef FR_HEAD
 #undef FR_KERNELS
 }  // namespace fr_narrow
 
@@ -186,6 +191,7 @@ namespace fr_mid {
 #define FR_KERNELS 1
 #define FR_LMAX 16
 #define FR_FIND_SELECT 1
+#define FR_HEAD 8
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -196,6 +202,7 @@ namespace fr_mid {
 #undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
+#undef FR_HEAD
 #undef FR_KERNELS
 }  // namespace fr_mid
 
@@ -215,6 +222,7 @@ namespace fr_fallback {
 #define FR_KERNELS 4
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
+#define FR_HEAD 0
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -225,6 +233,7 @@ namespace fr_fallback {
 #undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
+#undef FR_HEAD
 #undef FR_KERNELS
 }  // namespace fr_fallback
 
@@ -744,6 +753,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.mem_cnt = f->mem_cnt;
   a.ovf_n = f->ovf;
   a.ovf_next = f->ovf + 1;
+  a.retry_next = f->ovf + 3;
   a.ovf_list = f->ovf + 4;
   a.ovf_cap = (uint32_t)f->B;
   a.spill_list = a.ovf_list;

@@ -10,7 +10,9 @@
 //   pull reads hop h's and writes hop h + 1's directly, seed add and need-bit clearing
 //   included, so no copy phase follows the walk; 0: pull results by member index in HBM and a
 //   copy phase), FR_LMAX (light-row limit), FR_FIND_SELECT (1: branch-free probe rounds, see
-//   find_batch).  Every combination instantiated by frontier.hip is a shipped path.
+//   find_batch), FR_HEAD (light-row entries probed in the row's lane; the rest of the row is
+//   spread over the wave, see light_row; 0: all in-lane).  Every combination instantiated by
+//   frontier.hip is a shipped path.
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -311,21 +313,48 @@ __device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q
   if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
 }
 
-// One row of dl <= LMAX entries, one lane per row: every entry is loaded in one round trip,
-// probed LB keys at a time (lockstep), then the in-order fmaf chain runs in registers (K_PULL)
-// and the absent neighbours are inserted (K_REACH / K_PROP).
+// Inclusive sum over the wave's 64 lanes (every lane active): DPP row shifts inside each row of
+// 16 lanes, then the row broadcasts of lanes 15 and 31.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);    // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);    // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);    // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);    // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return x;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// One row of dl <= LMAX entries, one lane per row.  Its first NH entries (FR_HEAD; all LMAX
+// when FR_HEAD is 0) are loaded in one round trip, probed LB keys at a time (lockstep), then
+// the in-order fmaf chain runs in registers (K_PULL) and the absent neighbours are inserted
+// (K_REACH / K_PROP).  With FR_HEAD, the rest of every row (its tail, entries NH..dl-1) is
+// spread over the wave's lanes 64 entries a round, one entry per lane -- a wave's rows are
+// mostly short (C3: 78 % of <= 4 entries), so probing LMAX keys per lane left most lanes idle
+// in the later probe batches: each tail lane loads its entry, probes it, inserts it, and writes
+// (w, x) (w = 0 if absent or not pulled) to the wave's pair scratch, from which the row's lane
+// continues its chain in CSR order.
 template <bool GT>
 __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
                                           uint32_t kind, int h, float& acc, Ticker& tk) {
-  uint32_t c[LMAX];
-  float w[LMAX];
+  constexpr int NH = FR_HEAD ? FR_HEAD : LMAX;
+  static_assert(NH % LB == 0 && NH <= LMAX && LMAX - NH <= 16, "light-row head");
+  static_assert(FR_HEAD == 0 || FR_HUBCHAIN == 2, "light-row tails use the hub-chain scratch");
+  const uint32_t dh = min(dl, (uint32_t)NH);
+  uint32_t c[NH];
+  float w[NH];
   // two entries per 16-B load (8-B aligned: gfx950 global loads need only dword alignment);
   // the second entry of an odd row's last pair lies past the row -- read (the CSR arrays carry
   // two entries of padding) but never used: the probes and the chain stop at dl
 #pragma unroll
-  for (int x = 0; x < LMAX; x += 2) {
+  for (int x = 0; x < NH; x += 2) {
     Pair2 ce = {0u, 0u, 0u, 0u};
-    if ((uint32_t)x < dl) ce = *reinterpret_cast<const Pair2*>(A.cv + e0 + x);
+    if ((uint32_t)x < dh) ce = *reinterpret_cast<const Pair2*>(A.cv + e0 + x);
     c[x] = ce.c0;
     w[x] = __uint_as_float(ce.v0);
     c[x + 1] = ce.c1;
@@ -333,9 +362,9 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
   }
   tk.tick(4);
 #pragma unroll
-  for (int sb = 0; sb < LMAX / LB; ++sb) {
-    if (!__any(dl > (uint32_t)(sb * LB))) continue;   // (continue, not break: keeps it unrolled)
-    const uint32_t nq = dl > (uint32_t)(sb * LB) ? min(dl - sb * LB, (uint32_t)LB) : 0u;
+  for (int sb = 0; sb < NH / LB; ++sb) {
+    if (!__any(dh > (uint32_t)(sb * LB))) continue;   // (continue, not break: keeps it unrolled)
+    const uint32_t nq = dh > (uint32_t)(sb * LB) ? min(dh - sb * LB, (uint32_t)LB) : 0u;
     uint32_t key[LB];
 #pragma unroll
     for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
@@ -365,6 +394,55 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     }
     tk.tick(7);
   }
+#if FR_HEAD
+  const uint32_t tl = dl - dh;                    // this row's tail
+  if (!__any(tl != 0u)) return;                   // (wave-uniform)
+  const int lane = threadIdx.x & 63;
+  const uint32_t incl = wave_incl_sum(tl);
+  const uint32_t off = incl - tl;                 // the tail's first position
+  const uint32_t R = __builtin_amdgcn_readlane(incl, 63);
+  float2* const pr = t.chain + (threadIdx.x >> 6) * CHAIN_W;   // the wave's pair scratch
+  uint8_t* const mk = reinterpret_cast<uint8_t*>(pr);          // (owner marks, read first)
+  for (uint32_t r0 = 0; r0 < R; r0 += 64) {
+    // the owner lane of every position of this round's window [r0, r0 + 64)
+    for (uint32_t y = 0; y < (uint32_t)(LMAX - NH) && __any(y < tl); ++y) {
+      const int p = (int)(off + y) - (int)r0;
+      if (y < tl && p >= 0 && p < 64) mk[p] = (uint8_t)lane;
+    }
+    wave_sync_lds();
+    const uint32_t pos = r0 + lane;
+    const bool valid = pos < R;
+    const int o = valid ? (int)mk[lane] : lane;
+    wave_sync_lds();                              // (the marks are read before the pairs land)
+    const uint32_t oe0 = (uint32_t)__shfl((int)e0, o, 64);
+    const uint32_t ooff = (uint32_t)__shfl((int)off, o, 64);
+    const uint32_t okind = (uint32_t)__shfl((int)kind, o, 64);
+    const uint2 ce = valid ? A.cv[oe0 + NH + (pos - ooff)] : make_uint2(0u, 0u);
+    const uint32_t key1[1] = {ce.x};
+    int q1[1];
+    find_batch<GT, 1>(t, key1, valid ? 1u : 0u, q1);
+    tk.tick(5);
+    const bool term = q1[0] >= 0 && (okind & K_PULL);
+    const float x = term ? t.sc((uint32_t)q1[0]) : 0.f;
+    pr[lane] = make_float2(term ? __uint_as_float(ce.y) : 0.f, x);
+    if (valid && (okind & (K_REACH | K_PROP))) grow_entry<GT>(t, ce.x, q1[0], okind, h);
+    tk.tick(7);
+    wave_sync_lds();
+    // each row's lane continues its chain over its positions in this window, in CSR order
+    // (an absent or unpulled term is (+0, +0): fmaf leaves acc unchanged, acc != -0)
+    const int a0 = max((int)off - (int)r0, 0);
+    const int a1 = min((int)(off + tl) - (int)r0, 64);
+    if ((kind & K_PULL) && a0 < a1) {
+      float2 pw[LMAX - NH];
+#pragma unroll
+      for (int y = 0; y < LMAX - NH; ++y) pw[y] = pr[min(a0 + y, 63)];
+#pragma unroll
+      for (int y = 0; y < LMAX - NH; ++y) acc = a0 + y < a1 ? fmaf(pw[y].x, pw[y].y, acc) : acc;
+    }
+    tk.tick(6);
+    wave_sync_lds();                              // (read before the next round's marks)
+  }
+#endif
 }
 
 __device__ __forceinline__ float readlane_f(float x, int l) {
@@ -1100,15 +1178,22 @@ void frontier_lds_kernel(const FArgs A) {
 
 #if FR_KERNELS & 2
 // Second chance: a persistent grid over the columns another geometry's LDS kernel handed on
-// (A.retry_list, *A.retry_n entries): block i takes entries i, i + gridDim.x, ...; those that
-// overflow this table too go on to the global-memory variant.  Every block leaves once the
-// list is drained (an empty list: at once).
+// (A.retry_list, *A.retry_n entries), drained through a work queue; those that overflow this
+// table too go on to the global-memory variant.  Every block leaves once the list is drained
+// (an empty list: at once).
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
 void frontier_lds_retry_kernel(const FArgs A) {
   __shared__ LdsTab L;
   __shared__ Shared sh;
   const uint32_t n = *A.retry_n;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+  // a work queue (*A.retry_next, zeroed with the run's counters): a block takes the next entry
+  // when it is free, so ~3 columns per block of uneven cost do not leave a fourth static round
+  // to a few blocks
+  for (;;) {
+    if (threadIdx.x == 0) sh.item = atomicAdd(A.retry_next, 1u);
+    __syncthreads();
+    const uint32_t i = sh.item;
+    if (i >= n) break;
     lds_column(A, (int)A.retry_list[i], L, sh);
     __syncthreads();              // the next column clears the table this one used
   }
