@@ -8,6 +8,7 @@ Usage: python scripts/pmc_rdreq.py <pmc dir> <tag> <config> <batch> <batches_per
 (distinct = how many different incident sets the launch's batches are; 1 = copies of one set)"""
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -26,7 +27,9 @@ rep = {
     "kernel": "frontier_lds_kernel, %s, %d columns per launch (%d batches of %d, %d different "
               "incident sets), pruned top-10" % (config, batch * merge, merge, batch, distinct),
     "workload": {"config": config, "batch": batch, "batches_per_launch": merge,
-                 "distinct_batches": distinct},
+                 "distinct_batches": distinct,
+                 # the snapshot's locality layout, as bench.frontier_layout_on() reads it
+                 "layout": not os.environ.get("EGRAPH_FRONTIER_LAYOUT", "1").startswith("0")},
     "l2_read_requests_per_batch": rd / merge,
     "dispatches": len(vals["TCC_EA0_RDREQ_sum"]),
     "tcc_ea0_rdreq_per_launch": rd, "tcc_ea0_wrreq_per_launch": wr, "tcc_ea0_wrreq_64b_per_launch": wr64,
