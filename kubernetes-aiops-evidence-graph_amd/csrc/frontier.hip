@@ -17,19 +17,22 @@
 //
 // Work layout: a hop is two phases over the member list, GROW (the reach level and the
 // expansion of the non-zero members insert their neighbours) and PULL (the members an
-// expansion touched recompute their score).  A wave takes 64 members at a time: a row of <= 12
-// entries is one lane's, which loads and probes all its entries at once and runs the in-order
-// fmaf chain in registers; a longer (hub) row is taken by the whole wave, 64 entries per round,
-// with the chain run over v_readlane operands.  Top-k packs (score, vertex) into one u64 key:
-// each wave extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
+// expansion touched recompute their score).  A wave takes 64 members at a time: a row of up to
+// the geometry's light limit (12 / 16 entries) is one lane's, which loads and probes its first
+// entries at once and runs the in-order fmaf chain in registers, the rest of every row (its
+// tail) spread over the wave one entry per lane with the chain continued from the wave's LDS
+// pair scratch; a longer (hub) row is taken by the whole wave, 64 entries per round, its chain
+// run over its non-zero terms only.  Top-k packs (score, vertex) into one u64 key: each wave
+// extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
 //
-// Capacity: two instantiations of the kernels (frontier_body.h).  The wide one (member-pool
-// runs, every member's score exact) holds 6144 slots in ~78 KB of LDS, 8-wave workgroups, two
-// per CU; the narrow one (pruned top-k runs: ~0.6k members per column on C3) holds 1536 slots
-// and two score buffers in 30 KB, 4-wave workgroups, five per CU.  A column with more members
-// than the table's limit is flagged and redone by the global-memory variant of the same code (a
-// table of >= 2V slots per resident workgroup, never overflows), launched unconditionally right
-// after (it drains an empty work list at once).
+// Capacity: three LDS geometries of the kernels (frontier_body.h).  The narrow one (pruned
+// top-k runs: ~0.6k members per column on C3) holds 1536 slots and two score buffers in 30 KB,
+// 4-wave workgroups, five per CU; the mid one (C4-sized columns, ~1.4k members) 2816 slots in
+// 50 KB, three per CU; the wide one (member-pool runs, every member's score exact, and the
+// retry of what overflows the others) 6144 slots in 80 KB, 8-wave workgroups, two per CU.  A
+// column with more members than the table's limit is flagged and redone by the next table, and
+// last by the global-memory variant of the same code (a table of >= 2V slots per resident
+// workgroup, never overflows), launched unconditionally (it drains an empty work list at once).
 //
 // (Round 3 measured a two-phase alternative for top-k runs -- discover the column's member set
 // and its member-restricted local CSR first, then propagate in LDS only -- at 0.14-0.16 ms per
@@ -116,22 +119,25 @@ struct FArgs {
 struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
 struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr[v + 1]
 
-// Two instantiations of the kernels (frontier_body.h): the wide table keeps every member of a
-// column (member-pool runs: exact scores for every member, ~1.9k per column on C3); the narrow
-// one serves the pruned top-k runs (~0.6k members per column on C3), whose 30 KB of LDS and
-// 96 VGPRs fit five 4-wave workgroups per CU instead of two 8-wave ones.
+// The kernels' table geometries (frontier_body.h): the wide table keeps every member of a
+// column (member-pool runs: exact scores for every member, ~1.9k per column on C3; the retry of
+// what overflows a smaller table), 80 KB with a 2^15-bit filter so two fit a CU, and since
+// round 4 the narrow / mid tables' light-row treatment (LDS hub chains, tails after 8 entries,
+// limit 16: C4 -1.6 %, profiles/r04_ab_wide_tails.txt); the narrow one serves the pruned top-k
+// runs (~0.6k members per column on C3), whose 30 KB of LDS and 83 VGPRs fit five 4-wave
+// workgroups per CU instead of two 8-wave ones.
 namespace fr_wide {
 #define FR_FT 512
 #define FR_LCAP 6144
 #define FR_LLIMIT 4608
-#define FR_BLOOM_LOG 16
+#define FR_BLOOM_LOG 15
 #define FR_WAVES_PER_EU 4
-#define FR_HUBCHAIN 1
+#define FR_HUBCHAIN 2
 #define FR_DBUF 0
 #define FR_KERNELS 7
-#define FR_LMAX 12
+#define FR_LMAX 16
 #define FR_FIND_SELECT 1
-#define FR_HEAD 0
+#define FR_HEAD 8
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
