@@ -100,8 +100,8 @@ struct FArgs {
   uint32_t* spill_n;
   const uint32_t* retry_list;   // the retry kernel's input list and count (drained through
   const uint32_t* retry_n;      // the retry_next work counter)
-  float* lsnew;                 // [B][LLIMIT] wide LDS table: pull results by member index;
-                                // narrow (FR_DBUF): the seeds' values by slot
+  float* lsnew;                 // [B][LLIMIT] pull results by member index (a geometry with
+                                // FR_DBUF keeps the seeds' values by slot there instead)
   // global tables (one per resident workgroup of the fallback kernel)
   uint32_t* gkeys;              // [nbig][gcap]
   float* gs;                    // [nbig][gcap]
@@ -154,15 +154,18 @@ namespace fr_wide {
 
 namespace fr_narrow {
 // hub-row chains through LDS, one lane (+4 % at three batches in flight,
-// profiles/r02_ab_hubchain.txt); two slot-indexed score buffers, no copy phase (+2.5 %,
-// profiles/r02_ab_frontier_session3.txt)
+// profiles/r02_ab_hubchain.txt); one LDS score buffer (pull results by member index in HBM and
+// a copy phase): 24 KB and 80 VGPRs, six workgroups per CU.  Round 2's two slot-indexed buffers
+// (no copy phase, +2.5 % at five per CU, profiles/r02_ab_frontier_session3.txt) lost to the
+// sixth workgroup once the light-row tails cut the registers: C3 -4.5 %
+// (profiles/r04_ab_one_buffer.txt; round 3 measured six per CU neutral at 94 VGPRs).
 #define FR_FT 256
 #define FR_LCAP 1536
 #define FR_LLIMIT 1152
 #define FR_BLOOM_LOG 15
-#define FR_WAVES_PER_EU 5
+#define FR_WAVES_PER_EU 6
 #define FR_HUBCHAIN 2
-#define FR_DBUF 1
+#define FR_DBUF 0
 #define FR_KERNELS 1
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
@@ -181,19 +184,21 @@ namespace fr_narrow {
 #undef FR_KERNELS
 }  // namespace fr_narrow
 
-// A 2.8k-slot table at 256 threads (three workgroups per CU by LDS) for graphs whose columns
-// mostly overflow the narrow table but fit 2.1k members (the dense C4: ~1.5k, 92 % of its
-// columns): the first attempt of a mid-first frontier (egr_frontier_set_wide_first(f, 2)), whose
-// overflowing columns take the wide retry.  C4: -2.4 % per step against wide-first
-// (profiles/r04_ab_mid_first.txt).
+// A 2.8k-slot table at 256 threads for graphs whose columns mostly overflow the narrow table
+// but fit 2.1k members (the dense C4: ~1.4k, 92 % of its columns): the first attempt of a
+// mid-first frontier (egr_frontier_set_wide_first(f, 2)), whose overflowing columns take the
+// wide retry.  One LDS score buffer (pull results by member index in HBM and a copy phase, like
+// the wide table): 39 KB, four workgroups per CU -- with the second buffer it was 50 KB and three,
+// 16 % slower on C4 (profiles/r04_ab_mid_one_buffer.txt); C4 -2.4 % per step against
+// wide-first at its start (profiles/r04_ab_mid_first.txt).
 namespace fr_mid {
 #define FR_FT 256
 #define FR_LCAP 2816
 #define FR_LLIMIT 2112
 #define FR_BLOOM_LOG 15
-#define FR_WAVES_PER_EU 3
+#define FR_WAVES_PER_EU 4
 #define FR_HUBCHAIN 2
-#define FR_DBUF 1
+#define FR_DBUF 0
 #define FR_KERNELS 1
 #define FR_LMAX 16
 #define FR_FIND_SELECT 1
@@ -563,8 +568,10 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const uint32_t lcap = f->narrow ? fr_narrow::LCAP : fr_wide::LCAP;
   // pull results by member index: the narrow kernel and the wide retry index the same buffer
   const uint32_t llimit = std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT);
-  static_assert(fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
+  static_assert(!fr_narrow::DBUF || fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
                 "FR_DBUF: the narrow kernel keeps its seed values by slot in lsnew's column stride");
+  static_assert(fr_mid::LLIMIT <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
+                "the mid kernel's pull results by member index fit lsnew's column stride");
   // fallback table: 2 x nextpow2(V) slots, never more than half full
   size_t gcap = 2 * lcap;
   while (gcap < 2ull * V) gcap *= 2;

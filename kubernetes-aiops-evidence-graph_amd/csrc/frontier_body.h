@@ -12,7 +12,9 @@
 //   copy phase), FR_LMAX (light-row limit), FR_FIND_SELECT (1: branch-free probe rounds, see
 //   find_batch), FR_HEAD (light-row entries probed in the row's lane; the rest of the row is
 //   spread over the wave, see light_row; 0: all in-lane).  Every combination instantiated by
-//   frontier.hip is a shipped path.
+//   frontier.hip is a shipped path; FR_DBUF 1 is instantiated by none since late round 4 (the
+//   narrow and mid tables trade the second score buffer for one more workgroup per CU,
+//   profiles/r04_ab_one_buffer.txt) and stays for the measured A/B history.
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
