@@ -155,15 +155,16 @@ namespace fr_wide {
 namespace fr_narrow {
 // hub-row chains through LDS, one lane (+4 % at three batches in flight,
 // profiles/r02_ab_hubchain.txt); one LDS score buffer (pull results by member index in HBM and
-// a copy phase): 24 KB and 80 VGPRs, six workgroups per CU.  Round 2's two slot-indexed buffers
+// a copy phase) and a 2^14-bit filter: 22 KB and 72 VGPRs (14 spilled), seven workgroups per
+// CU (-1.7 % against six at 24 KB with a 2^15-bit filter, profiles/r04_ab_one_buffer.txt).  Round 2's two slot-indexed buffers
 // (no copy phase, +2.5 % at five per CU, profiles/r02_ab_frontier_session3.txt) lost to the
 // sixth workgroup once the light-row tails cut the registers: C3 -4.5 %
 // (profiles/r04_ab_one_buffer.txt; round 3 measured six per CU neutral at 94 VGPRs).
 #define FR_FT 256
 #define FR_LCAP 1536
 #define FR_LLIMIT 1152
-#define FR_BLOOM_LOG 15
-#define FR_WAVES_PER_EU 6
+#define FR_BLOOM_LOG 14
+#define FR_WAVES_PER_EU 7
 #define FR_HUBCHAIN 2
 #define FR_DBUF 0
 #define FR_KERNELS 1
