@@ -151,9 +151,11 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
             lane_seeds = tuple(to_device(a, dev) for a in (msv, msc, mss))
             lane_src = to_device(msrc, dev)
             lane_rules = encode_batch([ev for p in parts for ev in p[0]], catalog.default())
+            lane_enc, lane_host = lane_rules, (msv, msc, mss, msrc)
             n_seeds = len(msv)
         else:
             lane_seeds, lane_src, lane_rules, n_seeds = seeds, sources, rules, len(sv)
+            lane_enc, lane_host = enc, (sv, sc, ss, src)
         # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
         # members outside the candidate set); 0 keeps every member's score for inspection
         fr = snap.frontier(Bm, max_seeds=n_seeds, k=k, pool_entries=pool_entries)
@@ -165,7 +167,10 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 lanes=lanes, tick=0, merge=merge, sub=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence, incident_ids=[str(e[0]["incident_id"]) for e in evidence],
-                distinct_batches=n_sets, incidents_in_graph=n_sets * B)
+                distinct_batches=n_sets, incidents_in_graph=n_sets * B,
+                # lane 0's launch input on the host (all M batches: seeds, incident vertices,
+                # encoded rows): what the parity test of the headline launch checks against
+                lane_host=lane_host, lane_enc=lane_enc)
 
 
 def make_world(config: str, B: int, n_sets: int, seed0: int = 1000, cfg=None):
@@ -254,6 +259,42 @@ def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) ->
         if GROUPED == "order":          # (A/B: --seed-input grouped-host-order)
             rp = row_ptr if row_ptr is not None else snap.download()["row_ptr"]
             lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
+
+
+def warm_up(ctx, hops: int, warmup: int, dev, rank: int = 0, engine: str = "frontier",
+            graphs: bool = True):
+    """The untimed part of a run, as main() does it: `warmup` eager steps (at least one per lane
+    and launch group), then -- frontier -- two looks of Frontier.adapt() at the stats (the
+    wide-table retry for graphs whose columns overflow the narrow table; mid- or wide-first when
+    most do) with warm-up steps after each, then the lanes captured as HIP graphs and replayed
+    `warmup` times.  Returns the step function of the timed region."""
+    M = ctx.get("merge", 1)
+    run_step = step_frontier if engine == "frontier" else step
+    # (at least one step per lane: every lane's frontier has run before adapt() reads its stats)
+    for _ in range(max(warmup, len(ctx.get("lanes", ())) * M)):
+        run_step(ctx, hops)
+    torch.cuda.synchronize(dev)
+    if engine == "frontier":
+        # graphs with large 3-hop neighbourhoods (the dense C4): columns that overflow the
+        # narrow table get the wide-table retry from here on (egraph.graph.Frontier.adapt)
+        # most columns overflowing the narrow table: the mid table first; a second look after the
+        # next warm-up steps moves to wide-first if most columns overflow that one too
+        for check in range(2):
+            for lane in ctx["lanes"]:
+                fr = lane["frontier"]
+                if fr.adapt(fr.stats()):
+                    log(f"[rank {rank}] wide-table retry on ({fr.retry_blocks} blocks), first "
+                        f"table {FIRST_TABLE[fr.wide_first]}")
+            for _ in range(max(warmup, 1)):
+                run_step(ctx, hops)
+            torch.cuda.synchronize(dev)
+    if graphs and engine == "frontier":
+        capture_lanes(ctx, hops)
+        run_step = step_graph
+        for _ in range(warmup):
+            run_step(ctx, hops)
+        torch.cuda.synchronize(dev)
+    return run_step
 
 
 def _launch_due(ctx) -> bool:
@@ -653,12 +694,29 @@ def cpu_baseline(ctx, hops: int, k: int, threads: int, seconds: float = 8.0) -> 
                                      "(dense V x B sweep per hop; context only)"}}
 
 
+def _lib_hash() -> str:
+    from egraph import _lib
+    return _lib.build_hash()
+
+
+def _stamped(pmc: Path, d: dict):
+    """(bytes, source note) of a counter summary if it was taken on the loaded libegraph.so
+    (its `lib_hash` stamp, scripts/pmc_rdreq.py / pmc_traffic.py), else (None, why not): a
+    figure from another build is never reported as this one's."""
+    h = _lib_hash()
+    if d.get("lib_hash") != h:
+        return None, (f"{pmc.name} was taken on build {d.get('lib_hash')}, this run loads {h}: "
+                      "no current counter pass, traffic not reported")
+    return d.get("hbm_bytes_per_launch"), f"{pmc.name} (build {h})"
+
+
 def _traffic(name: str):
-    """HBM bytes per launch from a committed PMC summary (scripts/pmc_passes.sh), if any."""
+    """HBM bytes per launch from a committed PMC summary (scripts/gpu_pmc.sh) of this build,
+    else None; returns (bytes, note)."""
     pmc = REPO / "profiles" / f"pmc_{name}.json"
     if pmc.is_file():
-        return json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
-    return None
+        return _stamped(pmc, json.loads(pmc.read_text()))
+    return None, f"no {pmc.name}"
 
 
 # the table a frontier column tries first (egraph.graph.Frontier.FIRST_*)
@@ -674,8 +732,9 @@ def frontier_layout_on() -> bool:
 def _frontier_traffic(ctx, B: int):
     """Bytes past L2 per frontier launch (profiles/pmc_frontier_calibrated*.json, one per
     collected workload), when this run is a workload the counters were collected on (config,
-    batch and batches per launch); else None."""
+    batch, batches per launch, layout) AND on this build (lib_hash); returns (bytes or None, note)."""
     M = ctx.get("merge", 1)
+    note = "no counter pass of this workload in profiles/"
     for pmc in sorted((REPO / "profiles").glob("pmc_frontier_calibrated*.json")):
         d = json.loads(pmc.read_text())
         w = d.get("workload", {})
@@ -683,8 +742,10 @@ def _frontier_traffic(ctx, B: int):
                 and w.get("batches_per_launch", 1) == M
                 and w.get("distinct_batches", 1) == ctx.get("distinct_batches", 1)
                 and w.get("layout", False) == frontier_layout_on()):
-            return d.get("hbm_bytes_per_launch")
-    return None
+            v, note = _stamped(pmc, d)
+            if v is not None:
+                return v, note
+    return None, note
 
 
 def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
@@ -692,10 +753,11 @@ def dense_roofline(ctx, hop_ms: float, B: int, V: int, nnz: int) -> dict:
     # scores read once and written once; gathers beyond the one compulsory read are not counted
     hop_bytes = nnz * 5 + (V + 1) * 4 + 2 * V * B * 4
     achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
+    traffic, src = _traffic("hop")
     return {"bound": "hbm", "kernel": f"hop_kernel<{ctx['plan'].tile_width // 4},false> "
                                       "(dense propagation hop + seed_add)",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic("hop"),
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
             "avg_launch_ms": hop_ms, "algorithmic_bytes_per_launch": hop_bytes}
 
 
@@ -761,6 +823,7 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
     nbytes = (8 * work["pull_entries"] + 4 * work["expand_entries"] + 8 * work["rows"]
               + 8 * n_seeds + (9 * work["members"] if ctx["frontier"].pool_entries >= 0 else 0) + 8 * B * k)
     achieved = nbytes / (run_ms * 1e-3) / 1e9
+    traffic, traffic_src = _frontier_traffic(ctx, B)
     return ({"bound": "hbm", "kernel": "frontier_lds_kernel + frontier_global_kernel "
                                        "(egr_frontier_run: reach + propagation + top-k)",
              "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -769,7 +832,7 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
              # workload (C3, B = 1024): TCC_EA0_RDREQ x 128 B, the request size calibrated for
              # this kernel's 8-B gathers by scripts/calib_gather.hip, + the write requests.
              # Infinity-Cache hits count as fetched: an upper bound on HBM bytes.
-             "traffic": _frontier_traffic(ctx, B),
+             "traffic": traffic, "traffic_source": traffic_src,
              "traffic_note": "TCC_EA0_RDREQ x 128 B (calibrated: profiles/r02_calib_gather.txt) + "
                              "write requests, profiles/pmc_frontier_calibrated*.json; counts "
                              "Infinity-Cache hits (C3 CSR resident there): upper bound on HBM bytes",
@@ -1271,32 +1334,9 @@ def main():
                 merge=max(1, args.merge) if args.engine == "frontier" else 1,
                 replicate=args.replicate_batches)
     M = ctx["merge"]
-    run_step = step_frontier if args.engine == "frontier" else step
-    # (at least one step per lane: every lane's frontier has run before adapt() reads its stats)
-    for _ in range(max(args.warmup, len(ctx.get("lanes", ())) * M)):
-        run_step(ctx, args.hops)
-    torch.cuda.synchronize(dev)
-    if args.engine == "frontier":
-        # graphs with large 3-hop neighbourhoods (the dense C4): columns that overflow the
-        # narrow table get the wide-table retry from here on (egraph.graph.Frontier.adapt)
-        # most columns overflowing the narrow table: the mid table first; a second look after the
-        # next warm-up steps moves to wide-first if most columns overflow that one too
-        for check in range(2):
-            for lane in ctx["lanes"]:
-                fr = lane["frontier"]
-                if fr.adapt(fr.stats()):
-                    log(f"[rank {rank}] wide-table retry on ({fr.retry_blocks} blocks), first "
-                        f"table {FIRST_TABLE[fr.wide_first]}")
-            for _ in range(max(args.warmup, 1)):
-                run_step(ctx, args.hops)
-            torch.cuda.synchronize(dev)
     graphs = args.engine == "frontier" and not args.no_graph
-    if graphs:
-        capture_lanes(ctx, args.hops)
-        run_step = step_graph
-        for _ in range(args.warmup):
-            run_step(ctx, args.hops)
-        torch.cuda.synchronize(dev)
+    run_step = warm_up(ctx, args.hops, args.warmup, dev, rank,
+                       engine=args.engine, graphs=graphs)
 
     events: list = EventPool(args.steps) if args.engine == "frontier" else []
     ctx["sub"] = 0                  # the timed region starts a group of M batches

@@ -382,7 +382,7 @@ typedef struct egr_frontier egr_frontier;
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
 /* Top-k-only frontiers with the retry on: the first table every column tries, for graphs where
  * most columns overflow the narrow one (the narrow attempt would be wasted work).  `on` = 0: the
- * narrow table; 1: EVERY column straight to the wide grid; 2: a 2.8k-slot mid table first (three
+ * narrow table; 1: EVERY column straight to the wide grid; 2: a 2.8k-slot mid table first (four
  * workgroups per CU), its overflowing columns through the wide grid (the dense C4).  Same
  * results in every mode; EGR_EINVAL outside 0..2; takes effect from the next egr_frontier_run. */
 int egr_frontier_set_wide_first(egr_frontier* f, int32_t on);
@@ -463,6 +463,18 @@ int egr_locality_order(const uint32_t* row_ptr, const uint32_t* col, int64_t n_v
  * the incidents an update can affect with it. */
 int egr_snapshot_within(const egr_snapshot* s, const uint32_t* sources, int64_t n, int32_t hops,
                         uint8_t* out_dist, void* stream);
+/* One typed hop of a Cypher path pattern over the device snapshot: for query vertex i
+ * (device u32 vertices[i]; ids >= V give 0), its neighbours u over the relationships of type
+ * `rel_type` in direction `dir` -- 1: (vertices[i])-[:type]->(u), 0: (vertices[i])<-[:type]-(u)
+ * -- whose label is `label` (-1: any), in CSR order, written to out_vertices[out_off[i] ..]
+ * (device) with their count in out_counts[i].  out_vertices = NULL: counts only (out_off
+ * unused), so a caller sizes the segments with one call and emits with a second.  Replaces the typed MATCH steps of GraphService.find_related_changes,
+ * find_affected_by_node and get_service_dependencies (src/database/neo4j.py:205-279), which
+ * egraph_dropin.graph_service chains from it. */
+int egr_snapshot_typed_neighbors(const egr_snapshot* s, const uint32_t* vertices, int64_t n,
+                                 int32_t rel_type, int32_t dir, int32_t label,
+                                 const int64_t* out_off, uint32_t* out_vertices,
+                                 uint32_t* out_counts, void* stream);
 /* vertex count a frontier was sized for (it runs while the snapshot stays within it) */
 int64_t egr_frontier_max_vertices(const egr_frontier* f);
 int egr_graph_export_edges(const egr_graph* g, int64_t first, int64_t n, int32_t* edge_src,

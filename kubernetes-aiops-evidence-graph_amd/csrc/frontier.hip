@@ -26,9 +26,9 @@
 // extracts its k best with DPP wave-max rounds, wave 0 merges the lists.
 //
 // Capacity: three LDS geometries of the kernels (frontier_body.h).  The narrow one (pruned
-// top-k runs: ~0.6k members per column on C3) holds 1536 slots and two score buffers in 30 KB,
-// 4-wave workgroups, five per CU; the mid one (C4-sized columns, ~1.4k members) 2816 slots in
-// 50 KB, three per CU; the wide one (member-pool runs, every member's score exact, and the
+// top-k runs: ~0.6k members per column on C3) holds 1536 slots and one score buffer in 22 KB,
+// 4-wave workgroups, seven per CU; the mid one (C4-sized columns, ~1.4k members) 2816 slots in
+// 39 KB, four per CU; the wide one (member-pool runs, every member's score exact, and the
 // retry of what overflows the others) 6144 slots in 80 KB, 8-wave workgroups, two per CU.  A
 // column with more members than the table's limit is flagged and redone by the next table, and
 // last by the global-memory variant of the same code (a table of >= 2V slots per resident
@@ -43,6 +43,14 @@
 #include <vector>
 
 #include "graph_dev.h"
+
+// Per-phase wall-clock stamps ($EGRAPH_FRONTIER_PROFILE, scripts/frontier_profile.py) exist only
+// in a profiling build (-DEGR_FR_PROFILE=1, scripts/build_variant.sh): the shipped kernels carry
+// no timing state in their registers.
+#ifndef EGR_FR_PROFILE
+#define EGR_FR_PROFILE 0
+#endif
+#define FR_PROF_ON(A) (EGR_FR_PROFILE && (A).prof != nullptr)
 
 using egr::DeviceGuard;
 using egr::dalloc;
@@ -124,7 +132,7 @@ struct alignas(4) RowPair { uint32_t e0, e1; };           // row_ptr[v], row_ptr
 // what overflows a smaller table), 80 KB with a 2^15-bit filter so two fit a CU, and since
 // round 4 the narrow / mid tables' light-row treatment (LDS hub chains, tails after 8 entries,
 // limit 16: C4 -1.6 %, profiles/r04_ab_wide_tails.txt); the narrow one serves the pruned top-k
-// runs (~0.6k members per column on C3), whose 30 KB of LDS and 83 VGPRs fit five 4-wave
+// runs (~0.6k members per column on C3), whose 22 KB of LDS and 72 VGPRs fit seven 4-wave
 // workgroups per CU instead of two 8-wave ones.
 namespace fr_wide {
 #define FR_FT 512
@@ -506,6 +514,8 @@ struct egr_frontier {
   uint32_t* order = nullptr;      // [B] launch order of the columns (set_seeds: costly first)
   uint32_t* gcost = nullptr;      // [2B + 64] grouped runs' device launch order: column cost
                                   // buckets [B], ranks within the bucket [B], bucket histogram
+  uint32_t* gorder = nullptr;     // [B] the grouped runs' device-computed launch order (its own
+                                  // buffer: set_seeds' order stays for the next egr_frontier_run)
   uint32_t* ident = nullptr;      // [B] 0..B-1 (grouped runs: column order)
   uint32_t* seed_v = nullptr;     // [max_seeds] grouped by column
   float* seed_s = nullptr;
@@ -585,7 +595,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const size_t ms = (size_t)std::max<int64_t>(max_seeds, 1);
   if ((rc = dalloc(&f->seed_ptr, (size_t)n_cols + 1)) || (rc = dalloc(&f->seed_cnt, 2 * (size_t)n_cols)) ||
       (rc = dalloc(&f->order, (size_t)n_cols)) || (rc = dalloc(&f->ident, (size_t)n_cols)) ||
-      (rc = dalloc(&f->gcost, 2 * (size_t)n_cols + 64)) ||
+      (rc = dalloc(&f->gcost, 2 * (size_t)n_cols + 64)) || (rc = dalloc(&f->gorder, (size_t)n_cols)) ||
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
@@ -599,7 +609,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
     egr_frontier_free(f);
     return rc;
   }
-  if (getenv("EGRAPH_FRONTIER_PROFILE") &&
+  if (EGR_FR_PROFILE && getenv("EGRAPH_FRONTIER_PROFILE") &&
       (rc = dalloc(&f->prof, (size_t)n_cols * PROF_SLOTS * prof_w(f)))) {
     egr_frontier_free(f);
     return rc;
@@ -635,6 +645,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->seed_ptr);
   dfree(f->seed_cnt);
   dfree(f->order);
+  dfree(f->gorder);
   dfree(f->gcost);
   dfree(f->ident);
   dfree(f->seed_v);
@@ -751,10 +762,10 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                        seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, gbk,
                        gpos, ghist);
     hipLaunchKernelGGL(cost_order_kernel, dim3((unsigned)((f->B + 255) / 256)), dim3(256), 0, st,
-                       gbk, gpos, ghist, f->B, f->order);
+                       gbk, gpos, ghist, f->B, f->gorder);
     EGR_CHECK_LAUNCH();
   }
-  a.order = (sorted || !order) ? f->order : order;
+  a.order = sorted ? f->order : order ? order : f->gorder;
   a.seed_cnt = sorted ? f->seed_cnt : nullptr;
   a.out_ids = out_ids;
   a.out_scores = out_scores;

@@ -159,8 +159,12 @@ __device__ __forceinline__ int tab_find(const Tab<GT>& t, uint32_t v) {
   return -1;
 }
 
+// The column's work counters (egr_frontier_stats: CSR entries pulled / expanded, rows walked)
+// live in LDS (Shared::w_pull, w_expand, w_rows): a row walk adds one wave's sums per chunk from
+// one lane.  Kept per lane in registers they were live across every walk of the column and, at
+// the narrow table's 72 VGPRs, spilled to scratch and reloaded in every chunk.
 struct Work {
-  uint32_t pull = 0, expand = 0, rows = 0;
+  uint32_t* ctr;    // LDS: pull, expand, rows
 };
 
 // a top-k candidate's depth: reached within `hops` of the incident vertex (fl = depth + 1)
@@ -169,7 +173,10 @@ __device__ __forceinline__ bool cand_depth(uint8_t f, int hops) {
   return d != 0 && d <= (uint32_t)(hops + 1);
 }
 
-// diagnostics: per-wave sums of sub-step times (profiling builds of a phase only)
+// diagnostics: per-wave sums of sub-step times (profiling builds, -DEGR_FR_PROFILE=1, of a
+// phase only).  In the shipped build it holds nothing: its twelve 64-bit sums were live across
+// the whole row walk and cost ~24 scalar registers whether or not a run was profiled.
+#if EGR_FR_PROFILE
 struct Ticker {
   bool on = false;
   uint64_t t0 = 0;
@@ -183,6 +190,12 @@ struct Ticker {
     }
   }
 };
+#else
+struct Ticker {
+  static constexpr bool on = false;
+  __device__ __forceinline__ void tick(int) {}
+};
+#endif
 
 
 // Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
@@ -528,8 +541,10 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // diagnostics (profiling on, b >= 0): per-wave sums of sub-step times into slots 24..31
   Ticker tk;
-  tk.on = A.prof && b >= 0;
+#if EGR_FR_PROFILE
+  tk.on = FR_PROF_ON(A) && b >= 0;
   if (tk.on) tk.t0 = wall_clock64();
+#endif
   const bool prop_next = h + 1 < A.hops;
   const uint32_t par = (uint32_t)h & 1u;
   // walk h (SEEDS: h = -1) expands the members at depth h + REACH_AHEAD into reach level
@@ -599,10 +614,15 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     const Chunk cur = nxt;
     nxt = fetch(c_cur + 1);
     const uint32_t i = cur.i, kind = cur.kind, e0 = cur.e0, deg = cur.e1 - cur.e0;
-    if (kind) {
-      ++work.rows;
-      if (kind & K_PULL) work.pull += deg;
-      else work.expand += deg;
+    {   // the chunk's work counters: wave sums, one lane adds them (all 64 lanes active here)
+      const uint32_t sp = wave_incl_sum((kind & K_PULL) ? deg : 0u);
+      const uint32_t se = wave_incl_sum((kind && !(kind & K_PULL)) ? deg : 0u);
+      const uint64_t rows = __ballot(kind != 0u);
+      if (lane == 63) {
+        atomicAdd(work.ctr, sp);
+        atomicAdd(work.ctr + 1, se);
+        atomicAdd(work.ctr + 2, (uint32_t)__popcll(rows));
+      }
     }
     tk.tick(0);
     const bool light = deg <= (uint32_t)LMAX;
@@ -681,9 +701,11 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     }
     tk.tick(3);
   }
+#if EGR_FR_PROFILE
   if (tk.on && lane == 0)
     for (int k = 0; k < 12; ++k)
       A.prof[((size_t)b * PROF_SLOTS + 24 + k) * PROF_W + 1 + wave] = tk.sub[k];
+#endif
 }
 
 // ---- top-k keys: (score desc, vertex asc) as one u64, larger = better, 0 = none -----------
@@ -738,7 +760,7 @@ struct Shared {
 #endif
   unsigned long long base;
   uint64_t top[NWAVES][KMAXF];
-  uint32_t w_pull, w_expand, w_rows;
+  uint32_t w_pull, w_expand, w_rows;   // (contiguous: Work::ctr)
 };
 
 // candidate key of member slot p: reached within `hops`, not carrying the excluded label
@@ -774,7 +796,7 @@ __device__ __forceinline__ void wave_topk(const FArgs& A, const Tab<GT>& t, Shar
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if constexpr (!GT) {
     // diagnostics (profiling on): per-wave time of the candidate loads and of the k rounds
-    const bool prof = A.prof && b >= 0;
+    const bool prof = FR_PROF_ON(A) && b >= 0;
     const uint64_t tp0 = prof ? wall_clock64() : 0;
     uint64_t kk[MPT];
 #pragma unroll
@@ -855,12 +877,12 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
   const uint32_t tid = threadIdx.x;
   const int hops = A.hops;
   auto stamp = [&]() {
-    if (A.prof && tid == 0 && slot < PROF_SLOTS)
+    if (FR_PROF_ON(A) && tid == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
     ++slot;
   };
   auto wstamp = [&]() {
-    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+    if (FR_PROF_ON(A) && (tid & 63) == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   const uint32_t n = cnt;
@@ -906,19 +928,7 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
   stamp();
   // members -> pool (coalesced by member index)
   if (tid == 0) sh.base = A.pool_cap ? atomicAdd(A.pool_ctr, (unsigned long long)n) : 0ull;
-  {   // work counters: one LDS atomic per wave
-    uint32_t wp = work.pull, we = work.expand, wr = work.rows;
-    for (int o = 32; o > 0; o >>= 1) {
-      wp += __shfl_xor(wp, o);
-      we += __shfl_xor(we, o);
-      wr += __shfl_xor(wr, o);
-    }
-    if (lane == 0) {
-      atomicAdd(&sh.w_pull, wp);
-      atomicAdd(&sh.w_expand, we);
-      atomicAdd(&sh.w_rows, wr);
-    }
-  }
+  (void)work;      // (the work counters are in sh.w_*, complete after the last walk's barrier)
   __syncthreads();
   const unsigned long long base = sh.base;
   const bool keep = A.pool_cap && base + n <= A.pool_cap;
@@ -930,7 +940,7 @@ __device__ __forceinline__ bool finish_column(const FArgs& A, const Tab<GT>& t, 
       A.pool_d[base + i] = t.fl[p] & FL_DEPTH;
     }
   }
-  if (A.prof && tid == 0) A.prof[((size_t)b * PROF_SLOTS + 20) * PROF_W] = n;   // members
+  if (FR_PROF_ON(A) && tid == 0) A.prof[((size_t)b * PROF_SLOTS + 20) * PROF_W] = n;   // members
   if (tid == 0) {
     A.mem_off[b] = base;
     A.mem_cnt[b] = keep ? n : NO_NODE;
@@ -948,17 +958,17 @@ template <bool GT>
 __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Shared& sh, int b) {
   const uint32_t tid = threadIdx.x;
   const int hops = A.hops;
-  Work work;
+  Work work{&sh.w_pull};
   // phase-boundary timestamps (s_memrealtime, 100 MHz), thread 0, when profiling is on
   // (each wave's lane 0 also stamps its own finish before the barrier: wstamp)
   int slot = 0;
   auto stamp = [&]() {
-    if (A.prof && tid == 0 && slot < PROF_SLOTS)
+    if (FR_PROF_ON(A) && tid == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W] = wall_clock64();
     ++slot;
   };
   auto wstamp = [&]() {
-    if (A.prof && (tid & 63) == 0 && slot < PROF_SLOTS)
+    if (FR_PROF_ON(A) && (tid & 63) == 0 && slot < PROF_SLOTS)
       A.prof[((size_t)b * PROF_SLOTS + slot) * PROF_W + 1 + (tid >> 6)] = wall_clock64();
   };
   stamp();
@@ -1026,8 +1036,8 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   // reach level 1 (REACH_AHEAD pre-pass): the incident vertex's row, spread over the workgroup
   if (src_ok) {
     if (tid == 0) {
-      ++work.rows;
-      work.expand += ie1 - ie0;
+      atomicAdd(&sh.w_rows, 1u);
+      atomicAdd(&sh.w_expand, ie1 - ie0);
     }
     for (uint32_t e = ie0 + tid; e < ie1; e += FT) {
       const int q = tab_insert<GT>(t, e == ie0 + tid ? ic0 : A.cv[e].x);

@@ -17,6 +17,7 @@
 // gives; the frontier maps its inputs (seed vertices, incident vertices) through `perm` and
 // breaks top-k ties and writes its outputs with the original ids (`iperm`).
 #include <algorithm>
+#include <new>
 #include <numeric>
 
 #include "graph_dev.h"
@@ -166,24 +167,44 @@ int relayout(egr_snapshot* s, hipStream_t st) {
 
 }  // namespace
 
+// The layout is an optional second copy (~1.25x the canonical cv plus row pointers, perm, iperm
+// and labels): when it cannot be built -- device memory, a host allocation -- it is dropped and
+// the frontier reads the canonical arrays, which give the same results bit for bit.  Neither
+// function fails its caller: a graph that fits HBM without the layout still gets its snapshot
+// (egr_snapshot_create / egr_snapshot_from_csr) and its updates (egr_snapshot_update).
+static void layout_drop(egr_snapshot* s) {
+  layout_free(s);
+  (void)hipGetLastError();                  // (a failed allocation's status is not the caller's)
+}
+
 int layout_build(egr_snapshot* s, const uint32_t* row_ptr_host, const uint32_t* col_host) {
   if (!layout_enabled() || s->V <= 0) return EGR_OK;
   DeviceGuard guard(s->device);
-  if (!s->lay) s->lay = new FrLayout();
-  s->lay->order = locality_order(row_ptr_host, col_host, s->V);
-  const int rc = relayout(s, nullptr);
-  if (rc != EGR_OK) layout_free(s);
-  return rc;
+  int rc = EGR_ENOMEM;
+  try {
+    if (!s->lay) s->lay = new FrLayout();
+    s->lay->order = locality_order(row_ptr_host, col_host, s->V);
+    rc = relayout(s, nullptr);
+  } catch (const std::bad_alloc&) {
+    rc = EGR_ENOMEM;
+  }
+  if (rc != EGR_OK) layout_drop(s);
+  return EGR_OK;
 }
 
 int layout_extend(egr_snapshot* s, hipStream_t st) {
   if (!s->lay) return EGR_OK;
   DeviceGuard guard(s->device);
-  FrLayout* L = s->lay;
-  for (int64_t v = (int64_t)L->order.size(); v < s->V; ++v) L->order.push_back((uint32_t)v);
-  const int rc = relayout(s, st);
-  if (rc != EGR_OK) layout_free(s);         // (the frontier then reads the canonical arrays)
-  return rc;
+  int rc = EGR_ENOMEM;
+  try {
+    FrLayout* L = s->lay;
+    for (int64_t v = (int64_t)L->order.size(); v < s->V; ++v) L->order.push_back((uint32_t)v);
+    rc = relayout(s, st);
+  } catch (const std::bad_alloc&) {
+    rc = EGR_ENOMEM;
+  }
+  if (rc != EGR_OK) layout_drop(s);         // (the frontier then reads the canonical arrays)
+  return EGR_OK;
 }
 
 void layout_free(egr_snapshot* s) {

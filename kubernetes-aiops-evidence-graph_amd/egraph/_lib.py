@@ -142,6 +142,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_snapshot_version": (I64, [P]),
     "egr_locality_order": (C.c_int, [P, P, I64, P]),
     "egr_snapshot_within": (C.c_int, [P, P, I64, I32, P, P]),
+    "egr_snapshot_typed_neighbors": (C.c_int, [P, P, I64, I32, I32, I32, P, P, P, P]),
     "egr_frontier_max_vertices": (I64, [P]),
     "egr_graph_export_edges": (C.c_int, [P, I64, I64, P, P, P]),
     "egr_graph_add_edges_indexed": (C.c_int, [P, P, P, C.c_char_p, P, I32, P, I64, PI64]),
@@ -177,6 +178,13 @@ def _load() -> C.CDLL:
 
 
 lib = _load()
+
+
+def build_hash(path: Path | None = None) -> str:
+    """SHA-256 (first 16 hex digits) of the loaded libegraph.so: stamps counter summaries in
+    profiles/ so that a figure taken on another build is never read as this build's."""
+    import hashlib
+    return hashlib.sha256(Path(path or LIB_PATH).read_bytes()).hexdigest()[:16]
 
 
 def _load_pyhost():

@@ -482,6 +482,36 @@ class Snapshot:
                 "egr_snapshot_within")
         return out
 
+    OUT, IN = 1, 0      # typed_neighbors directions: (v)-[:T]->(u) / (v)<-[:T]-(u)
+
+    def typed_neighbors(self, vertices, rel_type: int, direction: int, label: int = -1,
+                        stream=None) -> list[np.ndarray]:
+        """One typed hop of a Cypher path pattern, per query vertex (egr_snapshot_typed_neighbors):
+        the neighbours u with (v)-[:rel_type]->(u) (direction OUT) or (v)<-[:rel_type]-(u) (IN)
+        and label index `label` (-1: any), in CSR order (u ascending), as int64 arrays.  Two
+        launches: the counts, then the matches into their segments."""
+        q = np.ascontiguousarray(vertices, np.int64)
+        n = len(q)
+        if n == 0:
+            return []
+        if rel_type < 0:                   # a relationship type the graph has never seen
+            return [np.empty(0, np.int64) for _ in range(n)]
+        st = L.stream_handle(self.dev) if stream is None else stream
+        dq = to_device(np.where(q >= 0, q, 0xFFFFFFFF).astype(np.uint32), self.dev)
+        cnt = torch.empty(n, dtype=torch.int32, device=self.dev)
+        L.check(L.lib.egr_snapshot_typed_neighbors(self._h, L.ptr(dq), n, int(rel_type), int(direction),
+                                                   int(label), None, None, L.ptr(cnt), st),
+                "egr_snapshot_typed_neighbors")
+        counts = cnt.cpu().numpy().astype(np.int64)
+        off = np.concatenate([[0], np.cumsum(counts)])
+        out = torch.empty(max(int(off[-1]), 1), dtype=torch.int32, device=self.dev)
+        doff = to_device(off[:-1], self.dev)
+        L.check(L.lib.egr_snapshot_typed_neighbors(self._h, L.ptr(dq), n, int(rel_type), int(direction),
+                                                   int(label), L.ptr(doff), L.ptr(out), L.ptr(cnt), st),
+                "egr_snapshot_typed_neighbors")
+        flat = out.cpu().numpy().view(np.uint32).astype(np.int64)
+        return [flat[off[i]:off[i + 1]] for i in range(n)]
+
     def download(self) -> dict[str, np.ndarray]:
         """Host copy of the device CSR (the layout of EvidenceGraph.csr()) and labels."""
         V, NE = self.n_vertices, self.n_entries

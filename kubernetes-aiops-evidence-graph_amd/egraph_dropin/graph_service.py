@@ -263,6 +263,162 @@ class GraphService:
             cls._snapshot, cls._plans, cls._frontiers = None, {}, {}
             return 1
 
+    # ---- typed path queries (neo4j.py:205-279) ---------------------------------------------
+    # Each Cypher MATCH step is one typed hop on the device snapshot (Snapshot.typed_neighbors,
+    # egr_snapshot_typed_neighbors); properties come from the host graph, as the reference's
+    # `dict(node)`.  Row semantics follow the Cypher text (oracle/graph_queries.py restates them
+    # on an edge list): one row per matched path, OPTIONAL MATCH rows with None, collect(DISTINCT)
+    # by first occurrence, the changed_at filter true only for timezone-aware datetimes (a Neo4j
+    # DATETIME; strings and naive datetimes compare to null).  Neo4j leaves the order of
+    # unordered rows unspecified; here it is match order: query vertices in vertex order,
+    # neighbours in CSR order.
+    OWNS_MAX_DEPTH = 16     # bound on the (p)<-[:OWNS*]-(d) expansion (k8s owner chains are 1-2)
+
+    @classmethod
+    def _props(cls, g, labels, vlabel, v: int) -> dict:
+        lab = labels[vlabel[v]]
+        vid = g.vertex_id(int(v))
+        return dict(g.node_props.get((lab, vid), {"id": vid}))
+
+    @classmethod
+    def _match_props(cls, g, label: str, **want) -> list[int]:
+        """MATCH (n:label {k: v, ...}) on properties: the vertices in vertex order."""
+        ids = [i for (lab, i), p in g.node_props.items()
+               if lab == label and all(k in p and p[k] == x for k, x in want.items())]
+        if not ids:
+            return []
+        vs = g.lookup_labeled(ids, label)
+        return sorted(int(v) for v in vs if v >= 0)
+
+    @staticmethod
+    def _index(names: list[str], name: str) -> int:
+        return names.index(name) if name in names else -1
+
+    @staticmethod
+    async def find_related_changes(incident_id: str, time_window_minutes: int = 30) -> list[dict]:
+        return GraphService.find_related_changes_sync(incident_id, time_window_minutes)
+
+    @classmethod
+    def find_related_changes_sync(cls, incident_id: str, time_window_minutes: int = 30,
+                                  now=None) -> list[dict]:
+        """MATCH (i:Incident {id})-[:AFFECTS]->(s), (s)<-[:APPLIES_TO]-(c:ChangeEvent) WHERE
+        c.changed_at >= datetime() - duration({minutes}) RETURN c ORDER BY c.changed_at DESC
+        (neo4j.py:205-229): the change events' property dicts."""
+        import datetime as dt
+        with cls._lock:
+            g = cls.graph()
+            if g.num_vertices == 0:
+                return []
+            incs = cls._match_props(g, "Incident", id=incident_id)
+            labels, types = g.labels(), g.rel_types()
+            ce = cls._index(labels, "ChangeEvent")
+            if not incs or ce < 0:
+                return []
+            snap = cls._snap()
+            targets = [s for row in snap.typed_neighbors(incs, cls._index(types, "AFFECTS"), snap.OUT)
+                       for s in row.tolist()]
+            changes = [c for row in snap.typed_neighbors(targets, cls._index(types, "APPLIES_TO"),
+                                                         snap.IN, ce) for c in row.tolist()]
+            vlabel = g.vertex_labels()
+            cutoff = (now or dt.datetime.now(dt.timezone.utc)) - dt.timedelta(minutes=time_window_minutes)
+            rows = []
+            for c in changes:
+                p = cls._props(g, labels, vlabel, c)
+                t = p.get("changed_at")
+                if isinstance(t, dt.datetime) and t.tzinfo is not None and t >= cutoff:
+                    rows.append(p)
+        rows.sort(key=lambda p: p["changed_at"], reverse=True)
+        return rows
+
+    @staticmethod
+    async def find_affected_by_node(node_name: str) -> list[dict]:
+        return GraphService.find_affected_by_node_sync(node_name)
+
+    @classmethod
+    def find_affected_by_node_sync(cls, node_name: str) -> list[dict]:
+        """MATCH (n:Node {name})<-[:SCHEDULED_ON]-(p:Pod), (p)<-[:OWNS*]-(d:Deployment)
+        OPTIONAL MATCH (d)<-[:SELECTS]-(s:Service) RETURN p, d, s (neo4j.py:232-252):
+        [{"pod", "deployment", "service" (None when no Service selects d)}], one per path."""
+        with cls._lock:
+            g = cls.graph()
+            if g.num_vertices == 0:
+                return []
+            labels, types = g.labels(), g.rel_types()
+            lp, ld, ls = (cls._index(labels, x) for x in ("Pod", "Deployment", "Service"))
+            nodes = cls._match_props(g, "Node", name=node_name)
+            if not nodes or lp < 0 or ld < 0:
+                return []
+            snap = cls._snap()
+            t_owns = cls._index(types, "OWNS")
+            vlabel = g.vertex_labels()
+            pods = [p for row in snap.typed_neighbors(nodes, cls._index(types, "SCHEDULED_ON"), snap.IN, lp)
+                    for p in row.tolist()]
+            # OWNS* backwards from every pod, one level of every open path per launch; a path
+            # is (its pod, its vertices' chain); relationships stay unique within a path
+            paths = [(i, (p,)) for i, p in enumerate(pods)]
+            found: list[list[tuple]] = [[] for _ in pods]   # per pod: (path vertices) ending at d
+            for _ in range(cls.OWNS_MAX_DEPTH):
+                if not paths or t_owns < 0:
+                    break
+                nb = snap.typed_neighbors([pv[-1] for _, pv in paths], t_owns, snap.IN)
+                nxt = []
+                for (i, pv), owners in zip(paths, nb):
+                    used = set(zip(pv[1:], pv[:-1]))            # (owner, owned) edges on the path
+                    for u in owners.tolist():
+                        if (u, pv[-1]) in used:
+                            continue
+                        q = pv + (u,)
+                        if vlabel[u] == ld:
+                            found[i].append(q)
+                        nxt.append((i, q))
+                paths = nxt
+            # per pod, the paths in depth-first order over CSR-ordered owners (lexicographic
+            # order of the vertex chains: a path comes before its extensions)
+            deps = [[q[-1] for q in sorted(f)] for f in found]
+            flat_d = [d for ds in deps for d in ds]
+            svcs = (snap.typed_neighbors(flat_d, cls._index(types, "SELECTS"), snap.IN, ls)
+                    if flat_d and ls >= 0 else [np.empty(0, np.int64) for _ in flat_d])
+            rows, j = [], 0
+            for p, ds in zip(pods, deps):
+                pp = cls._props(g, labels, vlabel, p)
+                for d in ds:
+                    dp = cls._props(g, labels, vlabel, d)
+                    ss = svcs[j].tolist()
+                    j += 1
+                    for s in ss or [None]:
+                        rows.append({"pod": dict(pp), "deployment": dict(dp),
+                                     "service": cls._props(g, labels, vlabel, s) if s is not None else None})
+        return rows
+
+    @staticmethod
+    async def get_service_dependencies(service_name: str, namespace: str) -> dict:
+        return GraphService.get_service_dependencies_sync(service_name, namespace)
+
+    @classmethod
+    def get_service_dependencies_sync(cls, service_name: str, namespace: str) -> dict:
+        """MATCH (s:Service {name, namespace}) OPTIONAL MATCH (s)-[:CALLS]->(down:Service)
+        OPTIONAL MATCH (up:Service)-[:CALLS]->(s) RETURN s, collect(DISTINCT down),
+        collect(DISTINCT up) (neo4j.py:255-279), the first matching service's record."""
+        none = {"service": None, "downstream": [], "upstream": []}
+        with cls._lock:
+            g = cls.graph()
+            if g.num_vertices == 0:
+                return none
+            svc = cls._match_props(g, "Service", name=service_name, namespace=namespace)
+            if not svc:
+                return none
+            labels, types = g.labels(), g.rel_types()
+            ls, t_calls = cls._index(labels, "Service"), cls._index(types, "CALLS")
+            snap = cls._snap()
+            down = snap.typed_neighbors([svc[0]], t_calls, snap.OUT, ls)[0]
+            up = snap.typed_neighbors([svc[0]], t_calls, snap.IN, ls)[0]
+            vlabel = g.vertex_labels()
+
+            def distinct(vs):
+                return [cls._props(g, labels, vlabel, v) for v in dict.fromkeys(vs.tolist())]
+            return {"service": cls._props(g, labels, vlabel, svc[0]),
+                    "downstream": distinct(down), "upstream": distinct(up)}
+
     @staticmethod
     async def get_incident_graph(incident_id: str, depth: int = 3,
                                  resolve_bare_uuid: bool = False) -> dict:

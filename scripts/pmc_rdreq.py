@@ -7,6 +7,7 @@ workload (config, batch, batches per launch) matches.
 Usage: python scripts/pmc_rdreq.py <pmc dir> <tag> <config> <batch> <batches_per_launch> [distinct]
 (distinct = how many different incident sets the launch's batches are; 1 = copies of one set)"""
 import csv
+import hashlib
 import json
 import os
 import sys
@@ -16,6 +17,7 @@ from pathlib import Path
 root, tag, config, batch, merge = Path(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
 distinct = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 REPO = Path(__file__).resolve().parents[1]
+LIB = Path(os.environ.get("EGRAPH_LIB", REPO / "kubernetes-aiops-evidence-graph_amd" / "lib" / "libegraph.so"))
 vals = defaultdict(list)
 for f in sorted(root.rglob("*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -40,6 +42,9 @@ rep = {
     "note": "bytes fetched past the XCD L2s: Infinity-Cache hits are counted (the 12-MB C3 CSR "
             "is Infinity-Cache resident), so this is an upper bound on HBM bytes",
     "source": str(root),
+    # the build the counters were taken on (egraph._lib.build_hash): bench.py reports this file's
+    # bytes as roofline.traffic only while it loads the same libegraph.so
+    "lib_hash": hashlib.sha256(LIB.read_bytes()).hexdigest()[:16],
 }
 (REPO / "profiles" / f"pmc_frontier_calibrated_{tag}.json").write_text(json.dumps(rep, indent=1))
 print(json.dumps(rep))

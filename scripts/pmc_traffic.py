@@ -6,6 +6,8 @@ float4 gathers and uncalibrated for the frontier's 8-B / 4-B gathers -- both raw
 kept).  Writes profiles/pmc_frontier.json and profiles/pmc_hop.json, which bench.py reads.
 Usage: python scripts/pmc_traffic.py <pmc output dir>"""
 import csv
+import hashlib
+import os
 import json
 import sys
 from collections import defaultdict
@@ -13,6 +15,7 @@ from pathlib import Path
 
 root = Path(sys.argv[1])
 REPO = Path(__file__).resolve().parents[1]
+LIB = Path(os.environ.get("EGRAPH_LIB", REPO / "kubernetes-aiops-evidence-graph_amd" / "lib" / "libegraph.so"))
 KERNELS = {"frontier": "frontier_lds_kernel", "hop": "hop_kernel<32, false>"}
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(root.rglob("*counter_collection.csv")):
@@ -37,6 +40,8 @@ for key in KERNELS:
         "tcc_ea0_wrreq_per_launch": mean.get("TCC_EA0_WRREQ_sum"),
         "hbm_bytes_per_launch": 2.0 * fetch_b + write_b,
         "correction": "2 x FETCH_SIZE (gfx950, MI355X_MICROARCH.md HBM section) + WRITE_SIZE",
+        "lib_hash": hashlib.sha256(LIB.read_bytes()).hexdigest()[:16],
+        "source": str(root),
     }
     (REPO / "profiles" / f"pmc_{key}.json").write_text(json.dumps(rep, indent=1))
     print(key, json.dumps(rep))

@@ -207,6 +207,57 @@ def test_bench_config_c3_merged_launch():
         bench.GROUPED = monkey
 
 
+def test_bench_headline_launch_m20():
+    """The exact launch the headline times (bench.py --steps 20 --warmup 5, the driver's run):
+    bench.setup("C3", B=1024, merge=20) -- 20 DIFFERENT incident sets, 20,480 columns in one
+    launch, the locality layout, the launch order computed on the device -- warmed up as main()
+    does (bench.warm_up: eager steps, Frontier.adapt() switching the wide-table retry on for the
+    columns that overflow the 7-per-CU narrow table, then HIP-graph capture and replays), then
+    replayed once more with poisoned outputs.  Every one of the 20,480 columns' top-k ids and
+    score bytes equals orc_frontier's on the same merged input, the rules over all 20 batches'
+    rows equal orc_rules_eval's, and some columns did overflow the narrow table and were
+    re-run by the wide retry (none reached the global-memory variant)."""
+    import bench
+    saved = bench.GROUPED
+    bench.GROUPED = "device"
+    try:
+        dev = torch.device("cuda", 0)
+        B, k, hops, M = 1024, 10, 3, 20
+        ctx = bench.setup("C3", B, k, 0, dev, merge=M)
+        assert ctx["distinct_batches"] == M and ctx["merge"] == M
+        step = bench.warm_up(ctx, hops, 5, dev)
+        assert step is bench.step_graph
+        lane = ctx["lanes"][0]
+        fr = lane["frontier"]
+        assert fr.retry_blocks > 0 and fr.wide_first == fr.FIRST_NARROW, "C3 runs narrow + retry"
+        fr.out_ids.fill_(-7)
+        fr.out_scores.fill_(float("nan"))
+        lane["rules"].mask.fill_(-7)
+        torch.cuda.synchronize()
+        ctx["sub"] = 0
+        for _ in range(M):                  # one timed-region's worth: a single replay of M batches
+            bench.step_graph(ctx, hops)
+        torch.cuda.synchronize()
+        st = fr.stats()
+        assert st["overflowed"] > 0, "the headline launch retries its overflowing columns"
+        assert st["global_columns"] == 0
+        g = ctx["graph"]
+        csr = g.csr()
+        vl, _, _, _ = g.export()
+        sv, sc, ss, src = ctx["lane_host"]
+        assert len(src) == B * M
+        e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k, hops)
+        ids = fr.out_ids.cpu().numpy().view(np.uint32).reshape(B * M, k)
+        sco = fr.out_scores.cpu().numpy().reshape(B * M, k)
+        for i in range(M):
+            sl = slice(i * B, (i + 1) * B)
+            np.testing.assert_array_equal(ids[sl], e_ids[sl], err_msg=f"batch {i}")
+            assert sco[sl].tobytes() == e_sc[sl].tobytes(), f"batch {i}"
+        _check_rules(lane["rules"].fetch(), ctx["lane_enc"])
+    finally:
+        bench.GROUPED = saved
+
+
 def test_c2_rules_dropin_and_frontier():
     import asyncio
     from types import SimpleNamespace
