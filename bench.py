@@ -52,6 +52,11 @@ sys.path.insert(0, str(REPO / "kubernetes-aiops-evidence-graph_amd"))
 
 METRIC = "incidents RCA-ranked/sec + edges/sec (3-hop propagation), 100k-pod graph"
 XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
+# The edge-cut projection's charge per RCCL collective on the critical path (a stated assumption,
+# not a measurement: RCCL refuses two ranks on one GPU, so the 8-GPU latency cannot be timed on
+# the 1-GPU box; small-message all-to-all / all-gather over 8 MI355X on xGMI are tens of us).
+# The JSON also carries the projection at 10 and 60 us.
+RCCL_COLL_LATENCY_US = 30.0
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # --merge default cap: a launch costs ~0.12 ms of tail + ~0.055 ms per C3 batch (0.0734 / 0.0653 /
 # 0.0626 ms per batch at 8 / 16 / 24 batches, profiles/r03_ab_merge_schedule.txt).  The M batches
@@ -1010,6 +1015,7 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     events: list = []
     for r in ctx["runs"]:
         r.sent_bytes, r.exchanges, r.link_bytes = 0, 0, 0
+    calls0 = ctx["comm"].calls
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -1020,6 +1026,7 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    coll_per_step = (ctx["comm"].calls - calls0) / max(args.steps, 1)
     if dist:
         elapsed = max_over_ranks(dist, elapsed, dev)
     # untimed: each partition's own compute (its kernels only, no exchange) per step, from HIP
@@ -1038,7 +1045,6 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     def chain_ms(q, c):
         return sum(a.elapsed_time(b) for a, b, t in q if t == c) / 3
     crit_ms = [max(chain_ms(q, "main"), chain_ms(q, "side")) + chain_ms(q, "tail") for q in parts]
-    overlap_on = not args.no_overlap
     B = args.batch
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -1049,6 +1055,12 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     achieved = hop_bytes / (hop_ms * 1e-3) / 1e9
     nnz = len(ctx["csr"]["col"])
     halo = max(r.halo_bytes_per_hop for r in ctx["runs"])
+    # collectives a GPU waits for on its critical path per step: with the reach chain on its own
+    # stream, one chain's exchanges (hops - 1; the other chain's overlap them) + the all-gather;
+    # serial, all of them.  (Steady state: one all-to-all per exchange; a calibrating or re-run
+    # pass issues more, which coll_per_step -- the timed steps' own count -- would show.)
+    overlap_on = not args.no_overlap
+    coll_crit = (args.hops - 1 + 1) if overlap_on else coll_per_step
     per_hop = max(1, args.steps * max(args.hops - 1, 1))
     sent = sent_t / per_hop
     link = link_t / max(args.steps, 1)
@@ -1078,8 +1090,18 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "link_bytes_per_step_max_rank": link,
             "reach_chain_overlap": overlap_on,
             "partition_critical_ms": crit_ms if overlap_on else part_ms,
-            "projected_ms_per_gpu": max(crit_ms if overlap_on else part_ms) + link / (XGMI_LINK_GBS * 1e6),
-            "projected_serial_ms_per_gpu": max(part_ms) + link / (XGMI_LINK_GBS * 1e6),
+            "collectives_per_step": coll_per_step,
+            "collectives_on_critical_path": coll_crit,
+            "collective_latency_us": RCCL_COLL_LATENCY_US,
+            "collective_latency_note": "bench.RCCL_COLL_LATENCY_US: a stated charge per RCCL "
+                                       "collective (not measured: RCCL refuses two ranks on one GPU)",
+            "projected_ms_per_gpu": max(crit_ms if overlap_on else part_ms) + link / (XGMI_LINK_GBS * 1e6)
+                                    + coll_crit * RCCL_COLL_LATENCY_US * 1e-3,
+            "projected_ms_per_gpu_at_latency_us": {
+                str(us): max(crit_ms if overlap_on else part_ms) + link / (XGMI_LINK_GBS * 1e6)
+                         + coll_crit * us * 1e-3 for us in (0, 10, 30, 60)},
+            "projected_serial_ms_per_gpu": max(part_ms) + link / (XGMI_LINK_GBS * 1e6)
+                                           + coll_per_step * RCCL_COLL_LATENCY_US * 1e-3,
             "projected_note": "max over partitions of their own device work per step (hops, reach "
                               "hops, candidates, top-k and the halo pack / unpack kernels; HIP events, "
                               "untimed steps) -- with the reach chain on its own stream, the longer "
@@ -1088,7 +1110,8 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
                               "from one rank to ONE peer over its xGMI link (point to point: the "
                               "peers' transfers run on separate links at once); what P GPUs running "
                               "one partition each would take per step (the in-process ms_per_step "
-                              "runs them one after another on one GPU)",
+                              "runs them one after another on one GPU) + the collectives on the "
+                              "critical path x collective_latency_us",
         },
         "roofline": {"bound": "hbm", "kernel": "hop_kernel (dense propagation hop, local partition)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

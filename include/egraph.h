@@ -330,19 +330,21 @@ int egr_plan_unpack_sparse(egr_plan* p, int32_t what, const uint32_t* recv_verte
                            const int64_t* in, int64_t n_entries, const int64_t* eseg,
                            const int64_t* rbase, int32_t P, void* stream);
 /* The same exchange with FIXED-CAPACITY peer slots and no host synchronisation (a halo exchange
- * per hop then never waits for the host: the all-to-all runs with equal splits of peer_cap
- * entries).  pack_cap: seg_dev[P + 1] on the device; a count pass, a scan and an emit pass
- * write peer q's entries to out[q * peer_cap * words_per_entry ...) in (row, column) order, its
- * entry count to counts_dev[q] (device int64), and *overflow_dev (device u32) gets 1 when a peer has more than peer_cap
- * entries (the excess is dropped: the caller re-runs the pass with larger slots).  unpack_cap:
- * sender s's entries are the first min(counts_dev[s], peer_cap) of its slot of `in` (the peers'
- * counts, exchanged beside the data); zero + scatter as egr_plan_unpack_sparse.  Both are
- * enqueued on `stream` only.                                                              */
+ * per hop then never waits for the host: ONE all-to-all with equal splits).  A slot is
+ * 1 + peer_cap * words_per_entry int64 words: a header word holding the sender's entry count
+ * for that peer, then the entries.  pack_cap: seg_dev[P + 1] on the device; a count pass, a scan
+ * and an emit pass write peer q's header and entries to out[q * slot ...) in (row, column) order
+ * (the counts also to counts_dev[q] when it is not NULL), and *overflow_dev (device u32) gets 1
+ * when a peer has more than peer_cap entries (the excess is dropped: the caller re-runs the pass
+ * with larger slots) or 2 when a row's emitted entries disagree with its count pass.
+ * unpack_cap: sender s's entries are the first min(header, peer_cap) of its slot of `in`; a
+ * header past peer_cap (the sender overflowed) sets *overflow_dev when it is not NULL; zero +
+ * scatter as egr_plan_unpack_sparse.  Both are enqueued on `stream` only. */
 int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, int64_t n,
                              const int64_t* seg_dev, int32_t P, int64_t* out, int64_t peer_cap,
                              int64_t* counts_dev, uint32_t* overflow_dev, void* stream);
 int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
-                               const int64_t* in, int64_t peer_cap, const int64_t* counts_dev,
+                               const int64_t* in, int64_t peer_cap, uint32_t* overflow_dev,
                                const int64_t* rbase, int32_t P, void* stream);
 
 /* ------------------------------------------------------------------------------------------

@@ -990,9 +990,14 @@ __global__ __launch_bounds__(256) void sx_count_rows_kernel(const float* __restr
 }
 
 // Pass 2 (after the exclusive scan of cnt into off): the entries of every row with work at its
-// offset within its peer's slot (off[r] - off[seg[q]]), in (row, column) order; the wave of
-// block 0 writes each peer's entry count off[seg[q + 1]] - off[seg[q]] and flags an overflow.
-// Entries past a slot's capacity are dropped.
+// offset within its peer's slot (off[r] - off[seg[q]]), in (row, column) order.  A slot is one
+// header word -- the peer's entry count off[seg[q + 1]] - off[seg[q]], which the wave of block 0
+// writes (and into counts[q] when given), flagging an overflow past the capacity -- then
+// peer_cap entries (x2 words for reach): the count travels in the slot itself, so an exchange is
+// ONE equal-split all-to-all.  Entries past a slot's capacity are dropped.  A row whose entries
+// do not end where the scan says (its count pass and its emit disagree: the hop's tile counts
+// and the scores no longer match) flags an overflow too, so the pass re-runs on the host-count
+// path instead of leaving gaps or overlaps in a slot.
 __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restrict__ X,
     const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
     const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
@@ -1002,10 +1007,12 @@ __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restri
   const int lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  const int64_t stride = 1 + peer_cap * (reach ? 2 : 1);   // header word + entries
   if (wave == 0) {
     for (int q = lane; q < P; q += 64) {
       const int64_t c = off[seg[q + 1]] - off[seg[q]];
-      counts[q] = c;
+      out[(size_t)q * stride] = c;
+      if (counts) counts[q] = c;
       if (c > peer_cap) atomicOr(overflow, 1u);
     }
   }
@@ -1029,7 +1036,7 @@ __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restri
       const int64_t rl = r - seg[q];
       int64_t pos = off[r] - off[seg[q]];
       const uint8_t* fl = nzf ? nzf + (size_t)v * ntiles : nullptr;
-      int64_t* dst = out + (size_t)q * peer_cap * (reach ? 2 : 1);
+      int64_t* dst = out + (size_t)q * stride + 1;
       for (uint64_t cs = m; cs; cs &= cs - 1ull) {
         const int b = 64 * (__ffsll((long long)cs) - 1) + lane;
         uint64_t w = 0;
@@ -1047,6 +1054,7 @@ __global__ __launch_bounds__(256) void sx_emit_rows_kernel(const float* __restri
         }
         pos += __popcll(bm);
       }
+      if (lane == 0 && pos != off[r + 1] - off[seg[q]]) atomicOr(overflow, 2u);
     }
   }
 }
@@ -1124,9 +1132,10 @@ __global__ __launch_bounds__(256) void sx_zero_kernel(float* __restrict__ X, uin
   }
 }
 
-// Fixed-capacity mode (peer_cap > 0, egr_plan_unpack_sparse_cap): sender s's entries are slots
-// [s * peer_cap, s * peer_cap + min(cnt[s], peer_cap)) of `in` (cnt: sender s's entry count);
-// n = P * peer_cap slots are scanned.
+// Fixed-capacity mode (peer_cap > 0, egr_plan_unpack_sparse_cap): sender s's slot starts at
+// word s * (1 + peer_cap * per) of `in`: its entry count, then its entries, of which the first
+// min(count, peer_cap) are scattered; n = P * peer_cap entry positions are scanned, and a count
+// past the capacity (the sender's slot overflowed) sets *ovf.
 __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ R, uint32_t V,
                                   int TW, uint32_t RS, int width, bool reach,
                                   const uint32_t* __restrict__ recv_vertex,
@@ -1134,13 +1143,19 @@ __global__ void sx_scatter_kernel(float* __restrict__ X, uint64_t* __restrict__ 
                                   const int64_t* __restrict__ eseg,
                                   const int64_t* __restrict__ rbase, int P,
                                   uint8_t* __restrict__ nzf, uint32_t ntiles,
-                                  int64_t peer_cap = 0, const int64_t* __restrict__ cnt = nullptr) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                  int64_t peer_cap = 0, uint32_t* __restrict__ ovf = nullptr) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   int s = 0;
   if (peer_cap > 0) {
     s = (int)(e / peer_cap);
-    if (e - (int64_t)s * peer_cap >= cnt[s]) return;      // (cnt: entries; past the slot: dropped)
+    const int64_t j = e - (int64_t)s * peer_cap;
+    const int64_t base = (int64_t)s * (1 + peer_cap * (reach ? 2 : 1));
+    const int64_t c = in[base];                            // the sender's header word
+    if (j == 0 && c > peer_cap && ovf) atomicOr(ovf, 1u);
+    if (j >= c) return;                                    // (past the count, or the slot: dropped)
+    in += base + 1;                                        // entry j of this slot
+    e = j;
   } else {
     while (s + 1 < P && eseg[s + 1] <= e) ++s;
   }
@@ -1954,7 +1969,7 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
                              const int64_t* seg_dev, int32_t P, int64_t* out, int64_t peer_cap,
                              int64_t* counts_dev, uint32_t* overflow_dev, void* stream) {
   if (!p || (what != 0 && what != 1) || n < 0 || P < 1 || P > EGR_SX_MAX_PEERS || !seg_dev ||
-      !counts_dev || !overflow_dev || peer_cap < 1 || (n > 0 && (!rows || !out)))
+      !overflow_dev || peer_cap < 1 || !out || (n > 0 && !rows))
     return egr::fail(EGR_EINVAL, "egr_plan_pack_sparse_cap: bad arguments");
   const bool reach = what == 1;
   if (reach ? !p->sources_set : p->hops_done < 1)
@@ -2001,9 +2016,9 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
 }
 
 int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
-                               const int64_t* in, int64_t peer_cap, const int64_t* counts_dev,
+                               const int64_t* in, int64_t peer_cap, uint32_t* overflow_dev,
                                const int64_t* rbase, int32_t P, void* stream) {
-  if (!p || (what != 0 && what != 1) || n_rows < 0 || P < 1 || peer_cap < 1 || !counts_dev ||
+  if (!p || (what != 0 && what != 1) || n_rows < 0 || P < 1 || peer_cap < 1 ||
       (n_rows > 0 && (!recv_vertex || !in || !rbase)))
     return egr::fail(EGR_EINVAL, "egr_plan_unpack_sparse_cap: bad arguments");
   const bool reach = what == 1;
@@ -2029,7 +2044,7 @@ int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_v
   hipLaunchKernelGGL(sx_scatter_kernel, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0,
                      st, X, R, V, p->TW, (uint32_t)p->RS, width, reach, recv_vertex, in,
                      slots, (const int64_t*)nullptr, rbase, P, nzf, (uint32_t)p->ntiles, peer_cap,
-                     counts_dev);
+                     overflow_dev);
   EGR_CHECK_LAUNCH();
   p->cand_valid = false;
   return EGR_OK;

@@ -620,15 +620,21 @@ class Plan:
                                              n, L.ptr(eseg), L.ptr(rbase), rbase.numel(),
                                              self._st(stream)), "egr_plan_unpack_sparse")
 
+    @staticmethod
+    def slot_words(what: str, peer_cap: int) -> int:
+        """int64 words of one peer slot of the fixed-capacity exchange: the header (the
+        sender's entry count for that peer), then peer_cap entries of 1 (scores) / 2 (reach)."""
+        return 1 + peer_cap * (2 if what == "reach" else 1)
+
     def pack_sparse_cap(self, what: str, rows: torch.Tensor, seg_dev: torch.Tensor, out: torch.Tensor,
-                        peer_cap: int, counts: torch.Tensor, overflow: torch.Tensor, stream=None) -> None:
-        """egr_plan_pack_sparse_cap: the non-zero entries into fixed slots of peer_cap entries
-        per peer (out: int64 [P * peer_cap * words per entry]; an entry is one word for scores,
-        two for reach), each peer's entry count into `counts` (device int64 [P]; past peer_cap
-        the entries are dropped and `overflow`, device int32 [1], is set); one launch, no
-        synchronisation."""
+                        peer_cap: int, overflow: torch.Tensor, counts: torch.Tensor | None = None,
+                        stream=None) -> None:
+        """egr_plan_pack_sparse_cap: the non-zero entries into fixed slots, one per peer
+        (out: int64 [P * slot_words]), each slot headed by its entry count; past peer_cap the
+        entries are dropped and `overflow` (device int32 [1]) is set.  `counts` (device int64
+        [P]), when given, gets the counts too.  One launch chain, no synchronisation."""
         P = seg_dev.numel() - 1
-        if out.numel() < P * peer_cap * (2 if what == "reach" else 1) or counts.numel() < P:
+        if out.numel() < P * self.slot_words(what, peer_cap) or (counts is not None and counts.numel() < P):
             raise ValueError("pack_sparse_cap: output slots or counts too small")
         L.check(L.lib.egr_plan_pack_sparse_cap(self._h, 1 if what == "reach" else 0, L.ptr(rows),
                                                rows.numel(), L.ptr(seg_dev), P, L.ptr(out), int(peer_cap),
@@ -636,10 +642,14 @@ class Plan:
                 "egr_plan_pack_sparse_cap")
 
     def unpack_sparse_cap(self, what: str, recv_vertex: torch.Tensor, entries: torch.Tensor,
-                          peer_cap: int, counts: torch.Tensor, rbase: torch.Tensor, stream=None) -> None:
+                          peer_cap: int, rbase: torch.Tensor, overflow: torch.Tensor | None = None,
+                          stream=None) -> None:
+        """egr_plan_unpack_sparse_cap: zero the received halo rows and scatter every sender's
+        slot (its header's count of entries, at most peer_cap); a header past peer_cap sets
+        `overflow` when given."""
         L.check(L.lib.egr_plan_unpack_sparse_cap(self._h, 1 if what == "reach" else 0,
                                                  L.ptr(recv_vertex), recv_vertex.numel(), L.ptr(entries),
-                                                 int(peer_cap), L.ptr(counts), L.ptr(rbase),
+                                                 int(peer_cap), L.ptr(overflow), L.ptr(rbase),
                                                  rbase.numel(), self._st(stream)),
                 "egr_plan_unpack_sparse_cap")
 

@@ -161,10 +161,12 @@ class TorchComm:
         self.group = group
         self.P = dist.get_world_size(group)
         self.gloo = dist.get_backend(group) == "gloo"
+        self.calls = 0          # collectives issued (each all_to_all_v is two: counts, then data)
 
     def all_gather(self, send: list[torch.Tensor]) -> list[torch.Tensor]:
         (x,) = send
         x = x.contiguous()
+        self.calls += 1
         if self.gloo:
             h = x.cpu()
             parts = [torch.empty_like(h) for _ in range(self.P)]
@@ -178,6 +180,7 @@ class TorchComm:
         """items = [(send, send_counts, recv, recv_counts)] for this process's one rank; rows
         send[off_q : off_q + send_counts[q]] go to rank q, recv is filled grouped by sender."""
         ((send, sc, recv, rc),) = items
+        self.calls += 1
         if self.gloo:
             hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
             self.dist.all_to_all_single(hr, hs, output_split_sizes=rc, input_split_sizes=sc,
@@ -192,6 +195,7 @@ class TorchComm:
         the per-sender counts]: sizes are exchanged first (one int64 per peer), then the data."""
         ((send, sc),) = items
         dev = send.device
+        self.calls += 2
         cnt = torch.tensor(sc, dtype=torch.int64)
         rcnt = torch.empty(self.P, dtype=torch.int64)
         if self.gloo:
@@ -217,6 +221,7 @@ class TorchComm:
         """items = [(send, recv)]: equal splits -- block q of send (numel / P) goes to rank q and
         block r of recv comes from rank r.  No split sizes, so nothing is read on the host."""
         ((send, recv),) = items
+        self.calls += 1
         if self.gloo:
             hr = torch.empty(recv.shape, dtype=recv.dtype)
             self.dist.all_to_all_single(hr, send.cpu(), group=self.group)
@@ -228,6 +233,7 @@ class TorchComm:
         """True if any rank's flag tensor (device int32 [1]) is non-zero (one all-reduce and one
         host read per call)."""
         (f,) = flags
+        self.calls += 1
         t = f.to(torch.int64).clone() if not self.gloo else f.to(torch.int64).cpu()
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
         return bool(t.item())
@@ -235,13 +241,19 @@ class TorchComm:
 
 class LocalComm:
     """All ranks in one process (tests, and a multi-partition single-GPU run): gathers are
-    concatenations, the all-to-all copies each sender's segment into its reader's buffer."""
+    concatenations, the all-to-all copies each sender's segment into its reader's buffer.
+    `calls` counts the collectives the P ranks would issue (one per call, as TorchComm)."""
+
+    def __init__(self):
+        self.calls = 0
 
     def all_gather(self, send: list[torch.Tensor]) -> list[torch.Tensor]:
+        self.calls += 1
         cat = torch.cat([s.to(send[0].device) for s in send])
         return [cat.to(s.device) for s in send]
 
     def all_to_all(self, items: list) -> None:
+        self.calls += 1
         P = len(items)
         s_off = [np.concatenate([[0], np.cumsum(sc)]) for _, sc, _, _ in items]
         r_off = [np.concatenate([[0], np.cumsum(rc)]) for _, _, _, rc in items]
@@ -255,6 +267,7 @@ class LocalComm:
 
 
     def all_to_all_fixed(self, items: list) -> None:
+        self.calls += 1
         P = len(items)
         for q in range(P):                       # reader
             recv = items[q][1]
@@ -266,9 +279,11 @@ class LocalComm:
                 recv[r * bq:(r + 1) * bq] = send[q * bs:(q + 1) * bs].to(recv.device)
 
     def any_flag(self, flags: list) -> bool:
+        self.calls += 1
         return any(bool(f.item()) for f in flags)
 
     def all_to_all_v(self, items: list) -> list:
+        self.calls += 2
         P = len(items)
         s_off = [np.concatenate([[0], np.cumsum(sc)]) for _, sc in items]
         out = []
@@ -353,40 +368,42 @@ class HaloOverflow(RuntimeError):
     the pass's results are incomplete and it must be run again (the slots have been grown)."""
 
 
+def _slot_words(what: str, cap: int) -> int:
+    """One peer slot of the fixed-capacity exchange: a header word (the sender's entry count
+    for that peer), then cap entries of one (scores) or two (reach) int64 words."""
+    return 1 + cap * (2 if what == "reach" else 1)
+
+
 def _fixed_bufs(r: "RankRun", what: str):
-    per = 2 if what == "reach" else 1
     P = r.lg.P
     cap = r.cap[what]
     b = r._fx.get(what)
     if b is None or b[0] != cap:
         dev = r.send.device
+        n = P * _slot_words(what, cap)
         b = r._fx[what] = (cap,
-                           torch.empty(P * cap * per, dtype=torch.int64, device=dev),   # send slots
-                           torch.empty(P * cap * per, dtype=torch.int64, device=dev),   # recv slots
-                           torch.zeros(P, dtype=torch.int64, device=dev),               # words sent
-                           torch.zeros(P, dtype=torch.int64, device=dev))               # words received
+                           torch.empty(n, dtype=torch.int64, device=dev),     # send slots
+                           torch.empty(n, dtype=torch.int64, device=dev))     # recv slots
     return b
 
 
 def _exchange_fixed(runs: list[RankRun], comm, what: str) -> None:
-    """The sparse halo exchange with fixed-capacity peer slots: device pack (counts and overflow
-    stay on the device), one equal-split all-to-all of the slots and one of the counts, device
-    unpack -- no host synchronisation per exchange (egr_plan_pack_sparse_cap)."""
-    items_d, items_c = [], []
+    """The sparse halo exchange with fixed-capacity peer slots: device pack (each slot headed by
+    its entry count; overflow stays on the device), ONE equal-split all-to-all of the slots,
+    device unpack (a header past the capacity sets the receiver's overflow flag too) -- no host
+    synchronisation per exchange (egr_plan_pack_sparse_cap)."""
+    items = []
     for r in runs:
-        cap, sbuf, rbuf, scnt, rcnt = _fixed_bufs(r, what)
-        r.eng.pack_sparse_cap(what, r.send, r.seg_dev, sbuf, cap, scnt, r.overflow)
-        per = 2 if what == "reach" else 1
-        r.sent_bytes += 8 * len(r.lg.send_counts) * cap * per + 8 * len(r.lg.send_counts)
-        r.link_bytes += (8 * cap * per + 8) if r.lg.P > 1 else 0
+        cap, sbuf, rbuf = _fixed_bufs(r, what)
+        r.eng.pack_sparse_cap(what, r.send, r.seg_dev, sbuf, cap, r.overflow)
+        r.sent_bytes += 8 * len(r.lg.send_counts) * _slot_words(what, cap)
+        r.link_bytes += 8 * _slot_words(what, cap) if r.lg.P > 1 else 0
         r.exchanges += 1
-        items_d.append((sbuf, rbuf))
-        items_c.append((scnt, rcnt))
-    comm.all_to_all_fixed(items_d)
-    comm.all_to_all_fixed(items_c)
+        items.append((sbuf, rbuf))
+    comm.all_to_all_fixed(items)
     for r in runs:
-        cap, _, rbuf, _, rcnt = _fixed_bufs(r, what)
-        r.eng.unpack_sparse_cap(what, r.recv_vertex, rbuf, cap, rcnt, r.recv_base)
+        cap, _, rbuf = _fixed_bufs(r, what)
+        r.eng.unpack_sparse_cap(what, r.recv_vertex, rbuf, cap, r.recv_base, r.overflow)
 
 
 def _exchange_sparse(runs: list[RankRun], comm, what: str) -> None:
@@ -442,6 +459,7 @@ def _exchange_sparse_py(runs: list[RankRun], comm, what: str) -> None:
         peer = torch.searchsorted(seg_t[1:], row, right=True)
         local = (row - seg_t[peer]) * width + (nz % width)       # index inside the peer's segment
         counts = torch.bincount(peer, minlength=len(r.lg.send_counts)).cpu().tolist()
+        r.max_seen[what] = max(r.max_seen.get(what, 0), max(counts, default=0))   # (slot calibration)
         if what == "scores":
             if int(np.diff(seg).max(initial=0)) * width >= 1 << 32:
                 raise ValueError("sparse score exchange: a peer segment's (row, column) index "
@@ -549,13 +567,7 @@ def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k:
                 xch(runs, comm, "reach")
     if overlap:
         main.wait_stream(side)
-    if use_fixed:
-        if comm.any_flag([r.overflow for r in runs]):
-            for r in runs:
-                r.cap = {}                # the re-run calibrates again over the host counts
-                r.overflows += 1
-            raise HaloOverflow("a halo exchange overflowed its fixed peer slots (run again)")
-    elif fixed and sparse:
+    if fixed and sparse and not use_fixed:
         # calibration: the slots hold 1.5x the largest per-peer entry count of this pass (the
         # same on every rank: the all-to-all needs equal block sizes)
         for what in ("scores", "reach"):
@@ -563,20 +575,33 @@ def run_partitioned(runs: list[RankRun], comm, hops: int, exclude_label: int, k:
             m = _max_over_ranks(comm, m)
             for r in runs:
                 r.cap[what] = max(1024, (3 * m) // 2 + 1)
+    # the candidate lists travel in one all-gather, each rank's with its overflow flag as a last
+    # element: every rank learns whether any slot of the pass overflowed without an all-reduce
     cands = []
+    shape = None
     for r in runs:
         r.eng.candidates(exclude_label)
         ids, sc = r.eng.topk(exclude_label)
         lid = ids.to(torch.int64) & 0xFFFFFFFF
         g = torch.where(lid == NO_NODE, torch.full_like(lid, NO_NODE),
                         r.gid[torch.clamp(lid, max=len(r.lg.gid) - 1)])
-        cands.append(torch.stack([g.to(torch.float64), sc.to(torch.float64)], dim=0))
+        c = torch.stack([g.to(torch.float64), sc.to(torch.float64)], dim=0)
+        shape = c.shape
+        cands.append(torch.cat([c.reshape(-1), r.overflow.to(torch.float64).reshape(1)]))
     gathered = comm.all_gather(cands)
+    if use_fixed:
+        flags = gathered[0].view(-1, cands[0].numel())[:, -1]
+        if bool((flags != 0).any().item()):
+            for r in runs:
+                r.cap = {}                # the re-run calibrates again over the host counts
+                r.overflows += 1
+            raise HaloOverflow("a halo exchange overflowed its fixed peer slots (run again)")
     out = []
     for r, allc in zip(runs, gathered):
+        allc = allc.view(-1, cands[0].numel())[:, :-1].reshape(-1, *shape[1:])
         P = allc.shape[0] // 2
-        ids = allc.view(P, 2, *cands[0].shape[1:])[:, 0].permute(1, 0, 2).reshape(cands[0].shape[1], -1)
-        scs = allc.view(P, 2, *cands[0].shape[1:])[:, 1].permute(1, 0, 2).reshape(cands[0].shape[1], -1)
+        ids = allc.view(P, 2, *shape[1:])[:, 0].permute(1, 0, 2).reshape(shape[1], -1)
+        scs = allc.view(P, 2, *shape[1:])[:, 1].permute(1, 0, 2).reshape(shape[1], -1)
         # (score desc, id asc): stable sort by id, then stable sort by -score
         o1 = torch.argsort(ids, dim=1, stable=True)
         ids, scs = torch.gather(ids, 1, o1), torch.gather(scs, 1, o1)

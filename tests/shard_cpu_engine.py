@@ -106,12 +106,13 @@ class CpuEngine:
             return self._words(r).view(np.int64)                         # [n][W] words
         return self.x[r].view(np.int32).astype(np.int64) & 0xFFFFFFFF    # [n][B] value bits
 
-    def pack_sparse_cap(self, what, rows, seg_dev, out, peer_cap, counts, overflow):
+    def pack_sparse_cap(self, what, rows, seg_dev, out, peer_cap, overflow, counts=None):
         r = rows.numpy().view(np.uint32)
         seg = seg_dev.numpy()
         vals = self._row_words(what, r)
         width = vals.shape[1] if vals.ndim == 2 else 0
         per = 2 if what == "reach" else 1
+        stride = 1 + peer_cap * per               # header word (the entry count) + the entries
         o = out.numpy()
         for q in range(len(seg) - 1):
             ent = []
@@ -120,32 +121,38 @@ class CpuEngine:
                     ent.append(((i - seg[q]) * width + b, int(vals[i, b])))
             if len(ent) > peer_cap:
                 overflow[0] = 1
-            counts[q] = len(ent)                  # entries, uncapped (the receiver clamps)
+            o[q * stride] = len(ent)              # entries, uncapped (the receiver clamps)
+            if counts is not None:
+                counts[q] = len(ent)
             ent = ent[:peer_cap]
-            base = q * peer_cap * per
+            base = q * stride + 1
             for j, (idx, w) in enumerate(ent):
                 if per == 2:
                     o[base + 2 * j], o[base + 2 * j + 1] = idx, w          # w: the signed word
                 else:
                     o[base + j] = (idx << 32) | w
 
-    def unpack_sparse_cap(self, what, recv_vertex, entries, peer_cap, counts, rbase):
+    def unpack_sparse_cap(self, what, recv_vertex, entries, peer_cap, rbase, overflow=None):
         rv = recv_vertex.numpy().view(np.uint32)
         e = entries.numpy()
         rb = rbase.numpy()
         per = 2 if what == "reach" else 1
+        stride = 1 + peer_cap * per
         width = self.W if what == "reach" else self.padded_cols
         if what == "reach":
             self.R[rv] = False
         else:
             self.x[rv] = 0.0
         for s in range(len(rb)):
-            for j in range(min(int(counts[s]), peer_cap)):
+            n = int(e[s * stride])
+            if n > peer_cap and overflow is not None:
+                overflow[0] = 1
+            for j in range(min(n, peer_cap)):
                 if per == 2:
-                    idx = int(e[(s * peer_cap + j) * 2])
-                    w = int(e[(s * peer_cap + j) * 2 + 1]) & 0xFFFFFFFFFFFFFFFF
+                    idx = int(e[s * stride + 1 + 2 * j])
+                    w = int(e[s * stride + 2 + 2 * j]) & 0xFFFFFFFFFFFFFFFF
                 else:
-                    x = int(e[s * peer_cap + j])
+                    x = int(e[s * stride + 1 + j])
                     idx, w = x >> 32, x & 0xFFFFFFFF
                 row = rv[rb[s] + idx // width]
                 b = idx % width

@@ -223,7 +223,7 @@ def test_bench_headline_launch_m20():
     try:
         dev = torch.device("cuda", 0)
         B, k, hops, M = 1024, 10, 3, 20
-        ctx = bench.setup("C3", B, k, 0, dev, merge=M)
+        ctx = bench.setup("C3", B, k, 0, dev, pool_entries=-1, merge=M)
         assert ctx["distinct_batches"] == M and ctx["merge"] == M
         step = bench.warm_up(ctx, hops, 5, dev)
         assert step is bench.step_graph

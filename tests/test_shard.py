@@ -105,7 +105,11 @@ def _rank_main(rank, P, port, q, sparse=True, fixed=False):
             shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
             assert run.cap["scores"] >= 1024
             reset()
+            c0 = comm.calls
             shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
+            # a steady-state pass: one all-to-all per exchange (2 score + 2 reach) and the
+            # candidates' all-gather, which also carries the overflow flags -- 5 collectives
+            assert comm.calls - c0 == 5, comm.calls - c0
             run.cap = {"scores": 2, "reach": 2}
             reset()
             (ids, scores), = shard.run_partitioned_retry([run], comm, 3, inc, 6, reset)
