@@ -108,8 +108,7 @@ struct FArgs {
   uint32_t* spill_n;
   const uint32_t* retry_list;   // the retry kernel's input list and count (drained through
   const uint32_t* retry_n;      // the retry_next work counter)
-  float* lsnew;                 // [B][LLIMIT] pull results by member index (a geometry with
-                                // FR_DBUF keeps the seeds' values by slot there instead)
+  float* lsnew;                 // [B][LLIMIT] pull results by member index
   // global tables (one per resident workgroup of the fallback kernel)
   uint32_t* gkeys;              // [nbig][gcap]
   float* gs;                    // [nbig][gcap]
@@ -140,8 +139,6 @@ namespace fr_wide {
 #define FR_LLIMIT 4608
 #define FR_BLOOM_LOG 15
 #define FR_WAVES_PER_EU 4
-#define FR_HUBCHAIN 2
-#define FR_DBUF 0
 #define FR_KERNELS 7
 #define FR_LMAX 16
 #define FR_FIND_SELECT 1
@@ -152,8 +149,6 @@ namespace fr_wide {
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_HUBCHAIN
-#undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
 #undef FR_HEAD
@@ -173,8 +168,6 @@ namespace fr_narrow {
 #define FR_LLIMIT 1152
 #define FR_BLOOM_LOG 14
 #define FR_WAVES_PER_EU 7
-#define FR_HUBCHAIN 2
-#define FR_DBUF 0
 #define FR_KERNELS 1
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
@@ -185,8 +178,6 @@ namespace fr_narrow {
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_HUBCHAIN
-#undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
 #undef FR_HEAD
@@ -206,8 +197,6 @@ namespace fr_mid {
 #define FR_LLIMIT 2112
 #define FR_BLOOM_LOG 15
 #define FR_WAVES_PER_EU 4
-#define FR_HUBCHAIN 2
-#define FR_DBUF 0
 #define FR_KERNELS 1
 #define FR_LMAX 16
 #define FR_FIND_SELECT 1
@@ -218,8 +207,6 @@ namespace fr_mid {
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_HUBCHAIN
-#undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
 #undef FR_HEAD
@@ -237,8 +224,6 @@ namespace fr_fallback {
 #define FR_LLIMIT 192
 #define FR_BLOOM_LOG 10
 #define FR_WAVES_PER_EU 4
-#define FR_HUBCHAIN 2
-#define FR_DBUF 0
 #define FR_KERNELS 4
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
@@ -249,8 +234,6 @@ namespace fr_fallback {
 #undef FR_LLIMIT
 #undef FR_BLOOM_LOG
 #undef FR_WAVES_PER_EU
-#undef FR_HUBCHAIN
-#undef FR_DBUF
 #undef FR_LMAX
 #undef FR_FIND_SELECT
 #undef FR_HEAD
@@ -579,8 +562,6 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   const uint32_t lcap = f->narrow ? fr_narrow::LCAP : fr_wide::LCAP;
   // pull results by member index: the narrow kernel and the wide retry index the same buffer
   const uint32_t llimit = std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT);
-  static_assert(!fr_narrow::DBUF || fr_narrow::LCAP <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
-                "FR_DBUF: the narrow kernel keeps its seed values by slot in lsnew's column stride");
   static_assert(fr_mid::LLIMIT <= std::max(fr_narrow::LLIMIT, fr_wide::LLIMIT),
                 "the mid kernel's pull results by member index fit lsnew's column stride");
   // fallback table: 2 x nextpow2(V) slots, never more than half full

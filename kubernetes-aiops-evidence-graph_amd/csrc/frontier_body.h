@@ -5,16 +5,14 @@
 // Geometry of this instantiation (set by the includer, csrc/frontier.hip):
 //   FR_FT threads per workgroup, FR_LCAP LDS table slots, FR_LLIMIT members before a column
 //   overflows to the global-memory variant, FR_BLOOM_LOG filter bits (log2), FR_WAVES_PER_EU,
-//   FR_HUBCHAIN (hub-row fmaf chains: 1 = v_readlane operands in every lane, 2 = the pairs
-//   through the wave's LDS scratch, one lane), FR_DBUF (1: two slot-indexed score buffers; a
-//   pull reads hop h's and writes hop h + 1's directly, seed add and need-bit clearing
-//   included, so no copy phase follows the walk; 0: pull results by member index in HBM and a
-//   copy phase), FR_LMAX (light-row limit), FR_FIND_SELECT (1: branch-free probe rounds, see
-//   find_batch), FR_HEAD (light-row entries probed in the row's lane; the rest of the row is
-//   spread over the wave, see light_row; 0: all in-lane).  Every combination instantiated by
-//   frontier.hip is a shipped path; FR_DBUF 1 is instantiated by none since late round 4 (the
-//   narrow and mid tables trade the second score buffer for one more workgroup per CU,
-//   profiles/r04_ab_one_buffer.txt) and stays for the measured A/B history.
+//   FR_LMAX (light-row limit), FR_FIND_SELECT (1: branch-free probe rounds, see find_batch),
+//   FR_HEAD (light-row entries probed in the row's lane; the rest of the row is spread over the
+//   wave, see light_row; 0: all in-lane).  Every combination instantiated by frontier.hip is a
+//   shipped path.  Pull results go by member index to HBM (lsnew) and a copy phase moves them
+//   into the one LDS score buffer after each walk (round 2's second slot-indexed buffer, with
+//   no copy phase, lost to the extra workgroup per CU its LDS paid for:
+//   profiles/r04_ab_one_buffer.txt; git history holds that variant, and the v_readlane hub
+//   chains, r02_ab_hubchain.txt).
 constexpr int FT = FR_FT;                   // threads per workgroup
 constexpr int NWAVES = FT / 64;
 constexpr uint32_t LCAP = FR_LCAP;          // LDS table slots
@@ -32,14 +30,12 @@ constexpr uint32_t BLOOM_WORDS = (1u << BLOOM_LOG) / 32;  // rejects absent keys
 constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candidate registers)
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
-constexpr bool DBUF = FR_DBUF;
-constexpr int CHAIN_W = 64;                 // hub-chain scratch pairs per wave (FR_HUBCHAIN 2)
-static_assert(FR_HUBCHAIN == 1 || FR_HUBCHAIN == 2, "hub-row chain scheme");
+constexpr int CHAIN_W = 64;                 // hub-chain / tail pair scratch per wave
 
 
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
 // insertion order (u16 in LDS, u32 in the global variant) and snew the pull results by member
-// index (FR_DBUF: the second score buffer, by slot).
+// index.
 template <bool GT>
 struct Tab {
   using MT = typename std::conditional<GT, uint32_t, uint16_t>::type;
@@ -53,10 +49,7 @@ struct Tab {
   uint32_t* count;  // LDS
   uint32_t* ovf;    // LDS
   uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
-  float2* chain;    // LDS: per-wave hub-chain scratch [NWAVES][64] (FR_HUBCHAIN 2), or null
-  // FR_DBUF (LDS tables): snew is the slot-indexed buffer the walk writes (hop h + 1's scores)
-  // and s0g the column's seed values by slot, in global memory (read by the seeds' pullers)
-  const float* s0g = nullptr;
+  float2* chain;    // LDS: per-wave hub-chain / tail pair scratch [NWAVES][64]
 
   __device__ __forceinline__ uint32_t key(uint32_t p) const { return keys[p]; }
   __device__ __forceinline__ float& sc(uint32_t p) const { return s[p]; }
@@ -359,7 +352,6 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
                                           uint32_t kind, int h, float& acc, Ticker& tk) {
   constexpr int NH = FR_HEAD ? FR_HEAD : LMAX;
   static_assert(NH % LB == 0 && NH <= LMAX && LMAX - NH <= 16, "light-row head");
-  static_assert(FR_HEAD == 0 || FR_HUBCHAIN == 2, "light-row tails use the hub-chain scratch");
   const uint32_t dh = min(dl, (uint32_t)NH);
   uint32_t c[NH];
   float w[NH];
@@ -469,25 +461,14 @@ __device__ __forceinline__ float readlane_f(float x, int l) {
 // fmaf(w, +0, acc) == acc for finite w and acc != -0 (acc starts at +0 and no fmaf of finite
 // operands turns it into -0), so the chain over the non-zero entries, in lane (= CSR) order,
 // equals the chain over every entry.  Hub rows are mostly non-members: the chain shrinks to the
-// few members' terms.  `rem` = entries left in the row (>= 1, wave-uniform); the result is in
-// every lane (FR_HUBCHAIN 1) or in lane m (2).
-//   FR_HUBCHAIN 1: v_readlane operands of each set ballot bit, in every lane
-//   FR_HUBCHAIN 2: the non-zero pairs compacted into the wave's LDS scratch (mbcnt rank) and
-//                  lane m runs the chain from 16-B LDS reads (one lane, 4-cycle dependent fmas)
-__device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32_t rem, int m,
-                                          float& hacc, float2* chain) {
-  (void)rem;
+// few members' terms.  The non-zero pairs are compacted into the wave's LDS scratch (mbcnt rank)
+// and lane m runs the chain from 16-B LDS reads (one lane, 4-cycle dependent fmas); the result
+// is in lane m.
+__device__ __forceinline__ void hub_chain(float w, float x, bool present, int m, float& hacc,
+                                          float2* chain) {
   const bool nz = present && x != 0.f;
-  uint64_t mk = __ballot(nz);
+  const uint64_t mk = __ballot(nz);
   if (mk == 0) return;                      // (wave-uniform)
-#if FR_HUBCHAIN == 1
-  (void)m; (void)chain;
-  while (mk) {
-    const int j = __ffsll((long long)mk) - 1;
-    mk &= mk - 1;
-    hacc = fmaf(readlane_f(w, j), readlane_f(x, j), hacc);
-  }
-#else
   const int lane = threadIdx.x & 63;
   const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
@@ -516,7 +497,6 @@ __device__ __forceinline__ void hub_chain(float w, float x, bool present, uint32
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#endif
 }
 
 // One pass over the members [0, n) present when it starts, a wave taking 64 at a time.
@@ -560,22 +540,13 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   // together (e.g. the incident's Node hubs, all reached at one level) spread over different
   // waves.  The next chunk's selection and row_ptr loads are issued before the current chunk is
   // walked (a member's kind cannot change during the pass: see the comment above).
-  // FR_DBUF pulls (DW): every member of the walk writes its hop h + 1 score into the other
-  // buffer (0 when not pulled, + s0 for a seed), clears its hop-h need bit and, after the last
-  // pull, gets NEED_EXCL when it is a candidate carrying the excluded label.
-  constexpr bool DW = DBUF && !GT && PH == PULL;
-  const bool last_pull = h == A.hops - 1;
-  const bool mark_excl = DW && last_pull && A.exclude >= 0;
-  constexpr uint32_t NOP = 0xFFFFFFFFu;
   struct Chunk {
     uint32_t i, kind, e0, e1;
-    uint32_t p;      // DW: the member's slot | (0x100 | label) << 16 for a candidate (NOP: none)
-    float s0;        // DW: the member's seed value (0 unless a seed)
   };
   const uint32_t nch = (n + FT - 1) / FT;
   auto member_of = [&](uint32_t c) { return wave + NWAVES * (lane + 64u * c); };
   auto fetch = [&](uint32_t c) {
-    Chunk ch{member_of(c), 0u, 0u, 0u, NOP, 0.f};
+    Chunk ch{member_of(c), 0u, 0u, 0u};
     uint32_t v = 0;
     if (c < nch && ch.i < n) {
       uint32_t p = t.mlist[ch.i];
@@ -588,15 +559,6 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         const uint32_t nd = t.need[p];
         if ((((nd >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
           ch.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
-        if constexpr (DW) {
-          // the hop-h bit is consumed here (the copy phase of the single-buffer scheme cleared
-          // it); expansions of this walk set the other parity's bit of the same word
-          if (((nd >> par) & 1u) && !last_pull)
-            atomicAnd(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), ~((1u << par) << ((p & 3u) * 8u)));
-          ch.p = p;
-          if (f & FL_SEED) ch.s0 = t.s0g[p];
-          if (mark_excl && is_cand(f)) ch.p |= (0x100u | A.vlabel[v]) << 16;   // candidate | label
-        }
       }
     }
     if (ch.kind) {
@@ -668,7 +630,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
         if (hkind & K_PULL) {
           const float w = __uint_as_float(ce.y);
           const float x = q >= 0 ? t.sc(q) : 0.f;
-          hub_chain(w, x, q >= 0, hdeg - base, m, hacc, chain);
+          hub_chain(w, x, q >= 0, m, hacc, chain);
         }
         tk.tick(10);
         if ((hkind & (K_REACH | K_PROP)) && act) grow_entry<GT>(t, u, q, hkind, h);
@@ -687,16 +649,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       }
     }
     tk.tick(2);
-    if constexpr (DW) {
-      if (cur.p != NOP) {
-        const uint32_t p = cur.p & 0xFFFFu;
-        // = the copy (pulled ? acc : +0) then the seed add (+ s0): the same fadd, bit for bit
-        // (s0 is +0 for a non-seed, and r + +0 == r: r is never -0)
-        t.snew[p] = ((kind & K_PULL) ? acc : 0.f) + cur.s0;
-        if (mark_excl && (cur.p >> 16) == (0x100u | (uint8_t)A.exclude))
-          atomicOr(reinterpret_cast<uint32_t*>(t.need) + (p >> 2), (uint32_t)NEED_EXCL << ((p & 3u) * 8u));
-      }
-    } else if constexpr (PH == PULL) {
+    if constexpr (PH == PULL) {
       if (kind & K_PULL) t.snew[i] = acc;
     }
     tk.tick(3);
@@ -752,12 +705,8 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
 
 struct Shared {
   uint32_t count, ovf, item;
-#if FR_HUBCHAIN == 2
-  float2 chain[NWAVES][CHAIN_W];   // hub-row chain pairs, one row per wave
+  float2 chain[NWAVES][CHAIN_W];   // hub-row chain / light-row tail pairs, one row per wave
 #define SH_CHAIN (&sh.chain[0][0])
-#else
-#define SH_CHAIN nullptr
-#endif
   unsigned long long base;
   uint64_t top[NWAVES][KMAXF];
   uint32_t w_pull, w_expand, w_rows;   // (contiguous: Work::ctr)
@@ -1021,11 +970,9 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
         const float s0 = unord(*reinterpret_cast<unsigned int*>(&t.s[q]));
         t.sc(q) = s0;
         r = make_uint2((uint32_t)q, __float_as_uint(s0));
-        if constexpr (DBUF && !GT) const_cast<float*>(t.s0g)[q] = s0;   // read by its pullers
       }
     }
-    if constexpr (!(DBUF && !GT)) A.seed_rep[i] = r;
-    else (void)r;
+    A.seed_rep[i] = r;
   }
   if (tid == 0 && src_ok) {       // (a find of a seed is unaffected by concurrent inserts)
     const int q = tab_insert<GT>(t, src);
@@ -1055,25 +1002,6 @@ __device__ __forceinline__ bool run_column(const FArgs& A, const Tab<GT>& t, Sha
   ovf = phase_sync(sh, cnt);
   stamp();
   if (ovf) return false;
-  if constexpr (DBUF && !GT) {
-    // two slot-indexed score buffers: pull h reads t.s / t.snew alternately and writes the
-    // other one (the copy, the seed add and the excluded-label marks happen in the walk)
-    float* const sbuf[2] = {t.s, t.snew};
-    for (int h = 0; h < hops; ++h) {
-      Tab<GT> th = t;
-      th.s = sbuf[h & 1];
-      th.snew = sbuf[(h + 1) & 1];
-      row_phase<GT, PULL>(A, th, cnt, h, work, h == hops - 1 ? b : -1);
-      wstamp();
-      ovf = phase_sync(sh, cnt);
-      stamp();
-      if (ovf) return false;
-      stamp();                      // (an empty copy phase: the profile's slots keep their meaning)
-    }
-    Tab<GT> tf = t;
-    tf.s = sbuf[hops & 1];
-    return finish_column<GT>(A, tf, sh, b, cnt, work, slot);
-  }
   for (int h = 0; h < hops; ++h) {
     // pull hop h (+ the expansion for hop h + 1 and reach level h + 3, in the same walk)
     const uint32_t n0 = cnt;
@@ -1128,16 +1056,7 @@ struct LdsTab {
   uint32_t needw[LCAP / 4];
   uint16_t mlist[LLIMIT];
   uint32_t bloom[BLOOM_WORDS];
-#if FR_DBUF
-  float s2[LCAP];              // the second slot-indexed score buffer (FR_DBUF)
-#endif
 };
-#define LDS_S_PTR L.s
-#if FR_DBUF
-#define LSNEW_PTR L.s2
-#else
-#define LSNEW_PTR (A.lsnew + (size_t)b * LLIMIT)
-#endif
 
 // One column in the LDS table: clear, run, and on overflow hand the column on (A.ovf_list).
 __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh) {
@@ -1147,9 +1066,6 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   for (int i = 0; i < LPPT; ++i) {
     L.keys[tid + i * FT] = EMPTY;
     L.s[tid + i * FT] = 0.f;
-#if FR_DBUF
-    L.s2[tid + i * FT] = 0.f;
-#endif
   }
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.flw[i] = 0;
   for (uint32_t i = tid; i < LCAP / 4; i += FT) L.needw[i] = 0;
@@ -1159,9 +1075,8 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
     sh.w_pull = sh.w_expand = sh.w_rows = 0;
   }
   __syncthreads();
-  Tab<false> t{L.keys, LDS_S_PTR, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, LSNEW_PTR, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN,
-               A.lsnew + (size_t)b * LCAP};   // (FR_DBUF: seed values by slot; LCAP <= lsnew's stride)
+  Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
+               L.mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN};
   if (!run_column<false>(A, t, sh, b) && tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
@@ -1256,6 +1171,4 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   }
 }
 #endif
-#undef LSNEW_PTR
 #undef SH_CHAIN
-#undef LDS_S_PTR
