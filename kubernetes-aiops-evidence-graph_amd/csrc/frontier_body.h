@@ -439,12 +439,17 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     // (an absent or unpulled term is (+0, +0): fmaf leaves acc unchanged, acc != -0)
     const int a0 = max((int)off - (int)r0, 0);
     const int a1 = min((int)(off + tl) - (int)r0, 64);
-    if ((kind & K_PULL) && a0 < a1) {
-      float2 pw[LMAX - NH];
+    // (two pairs a step, the wave leaving as soon as no lane has more: most tails are one to
+    // four entries, and holding all LMAX - NH pairs at once was the walk's register peak)
+    const bool pulls = (kind & K_PULL) && a0 < a1;
 #pragma unroll
-      for (int y = 0; y < LMAX - NH; ++y) pw[y] = pr[min(a0 + y, 63)];
-#pragma unroll
-      for (int y = 0; y < LMAX - NH; ++y) acc = a0 + y < a1 ? fmaf(pw[y].x, pw[y].y, acc) : acc;
+    for (int y = 0; y < LMAX - NH; y += 2) {
+      if (!__any(pulls && a0 + y < a1)) break;
+      const float2 p0 = pr[min(a0 + y, 63)], p1 = pr[min(a0 + y + 1, 63)];
+      if (pulls) {
+        acc = a0 + y < a1 ? fmaf(p0.x, p0.y, acc) : acc;
+        acc = a0 + y + 1 < a1 ? fmaf(p1.x, p1.y, acc) : acc;
+      }
     }
     tk.tick(6);
     wave_sync_lds();                              // (read before the next round's marks)
