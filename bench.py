@@ -446,7 +446,7 @@ def step(ctx, hops: int, ev=None):
     plan.topk(ctx["inc_label"])
 
 
-def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 300) -> dict:
+def dropin_rules(ctx, dev, reps: int = 5, n_single: int = 1024) -> dict:
     """The drop-in API end to end (host-bound; reported beside `value`, never as it):
       * batch: RulesEngine.rank_incidents_batch on the bench batch (evidence dicts in, ranked
         hypothesis dicts out: native encode, one packed upload, egr_rules_eval, one packed

@@ -146,6 +146,26 @@ int egr_rules_eval_small(const egr_rule_table* table, const uint32_t* row_flags,
                          const uint32_t* row_vocab, const uint32_t* row_node, const double* row_err,
                          int32_t n_rows, const egr_rules_out* out, void* stream);
 
+/* The single-incident rules server: egr_rules_eval_small's job without a kernel launch per
+ * call.  A one-wave kernel stays resident while calls keep coming, polling a mailbox in
+ * mapped coherent host memory; post() writes one incident's encoded rows (at most 1024, host
+ * arrays) and returns at once; poll() returns 1 once the incident's outputs are ready and
+ * copies them into the caller's arrays (mask[1], n_hyp[1], S = n_rules + 1 slots each, the
+ * layout of egr_rules_eval's outputs), 0 while pending -- and starts the wave again when it
+ * has left (it leaves after ~2 ms without a request, ~2 s in all, or at free(); a
+ * device-wide synchronize waits for it meanwhile).  One
+ * incident in flight per server; post() refuses (EGR_ESTATE) while one is pending.  Same
+ * outputs as egr_rules_eval, bit for bit (the same per-incident device code).  The drop-in's
+ * idle generate_hypotheses calls (activities.py:124-170, one incident per activity). */
+typedef struct egr_rules_server egr_rules_server;
+int egr_rules_server_create(const egr_rule_table* table, int32_t device, egr_rules_server** out);
+int egr_rules_server_post(egr_rules_server* s, const uint32_t* row_flags, const uint32_t* row_vocab,
+                          const uint32_t* row_node, const double* row_err, int32_t n_rows);
+int egr_rules_server_poll(egr_rules_server* s, uint32_t* mask, uint8_t* n_hyp, uint8_t* order_conf,
+                          uint8_t* order_rank, double* confidence, double* final_score,
+                          double* strength);
+void egr_rules_server_free(egr_rules_server* s);
+
 /* Ranker (A6) over arbitrary hypothesis lists.  List j owns entries [list_off[j], list_off[j+1]).
  *   score = confidence * cat_weight; if support > 0: *= 1 + min(support,5)*0.05;
  *   *= 1 + strength*0.2; final = round(score, 4); stable sort descending.

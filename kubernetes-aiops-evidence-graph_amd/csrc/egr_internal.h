@@ -30,6 +30,19 @@ int fail(int code, const std::string& msg);
                                           std::to_string(__LINE__) + "): " + hipGetErrorString(e_)); \
   } while (0)
 
+// ---- the current device for a scope (host) ----------------------------------------------
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 // ---- Python-exact float rounding -----------------------------------------------------------
 // round(x, nd) in CPython (Objects/floatobject.c, double_round) is: take the exact binary value
 // of x, round x*10^nd to an integer q half-to-even, return the double nearest to q/10^nd.

@@ -54,18 +54,6 @@ FrLayoutView layout_view(const egr_snapshot* s);
 
 namespace egr {
 
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
 template <typename T>
 inline int dalloc(T** p, size_t count) {
   if (count == 0) count = 1;

@@ -17,7 +17,9 @@
 //     by counting, with the unknown fallback (:230-231, :457-478).
 // The per-incident working set is a few KB, so the kernel is latency- not bandwidth-bound for
 // realistic batches; its HBM cost is one read of the rows.
+#include <cstring>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -300,6 +302,66 @@ __global__ __launch_bounds__(64) void rules_small_kernel(const SmallRows a) {
 }
 
 // Stand-alone ranker: one wave per hypothesis list, stable descending order by counting.
+// ---- the single-incident rules server (egr_rules_server_*) --------------------------------
+// A one-wave kernel that stays resident while single generate_hypotheses calls keep coming:
+// the host writes an incident's encoded rows into a mailbox in fine-grained (coherent) mapped
+// host memory and bumps `req`; the wave, polling `req` across PCIe, evaluates the incident
+// (rules_incident, the batched kernel's own per-incident code) straight into the mailbox's
+// output block and publishes `ack` = req with a system-scope release.  A call then costs the
+// PCIe round trips (~a few us) instead of a kernel launch and its event (~20-25 us, with a
+// launch-queue tail the host enqueue itself shows: profiles/r05_dropin_latency_*.txt).
+// Exit conditions every run reaches: the host's `stop`, SRV_IDLE_POLLS polls without a request
+// (~2 ms: a device-wide synchronize waits for the resident wave, so it does not linger) or
+// SRV_MAX_POLLS polls in all (~2 s); the wave then clears `alive`, and the host launches it
+// again on the next call that finds it gone.
+constexpr int kSrvRows = 1024;      // (activity incidents are ~100 rows; the C3 generator's up to ~300)
+struct alignas(64) SrvMailbox {
+  uint64_t req;                 // host: sequence number of the posted incident (written last)
+  uint64_t ack;                 // device: the last sequence number evaluated (outputs ready)
+  uint32_t stop;                // host: leave now
+  uint32_t alive;               // host sets 1 before a launch; the wave clears it as it leaves
+  int32_t n_rows;
+  uint32_t pad;
+  uint32_t flags[kSrvRows], vocab[kSrvRows], node[kSrvRows];
+  double err[kSrvRows];
+  // outputs of the incident (S = n_rules + 1 <= EGR_MAX_RULES + 1 slots)
+  uint32_t mask;
+  uint8_t n_hyp;
+  uint8_t order_conf[EGR_MAX_RULES + 1], order_rank[EGR_MAX_RULES + 1];
+  double confidence[EGR_MAX_RULES + 1], final_score[EGR_MAX_RULES + 1], strength[EGR_MAX_RULES + 1];
+};
+constexpr uint64_t SRV_IDLE_POLLS = 1000;
+constexpr uint64_t SRV_MAX_POLLS = 1000000;
+
+__global__ __launch_bounds__(64) void rules_server_kernel(const RulesDev* __restrict__ D,
+                                                          SrvMailbox* mb) {
+  __shared__ uint32_t node_key[kNodeSlots];
+  __shared__ uint32_t node_cnt[kNodeSlots];
+  const int lane = threadIdx.x;
+  uint64_t last = __hip_atomic_load(&mb->ack, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint64_t idle = 0;
+  for (uint64_t it = 0; it < SRV_MAX_POLLS; ++it) {
+    const uint64_t req = __hip_atomic_load(&mb->req, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__hip_atomic_load(&mb->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+    if (req != last) {
+      const int n = min(max(mb->n_rows, 0), kSrvRows);
+      const egr_rules_out out{&mb->mask, &mb->n_hyp, mb->order_conf, mb->order_rank,
+                              mb->confidence, mb->final_score, mb->strength};
+      rules_incident(D, mb->flags, mb->vocab, mb->node, mb->err, 0, n, 0, out, node_key, node_cnt);
+      __atomic_thread_fence(__ATOMIC_RELEASE);    // (the outputs before the ack, system-wide)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      if (lane == 0) __hip_atomic_store(&mb->ack, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      last = req;
+      idle = 0;
+    } else if (++idle >= SRV_IDLE_POLLS) {
+      break;
+    } else {
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  if (lane == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void rank_kernel(
     const double* __restrict__ conf, const double* __restrict__ catw,
     const double* __restrict__ support, const double* __restrict__ strength,
@@ -474,6 +536,121 @@ extern "C" int egr_rules_eval_small(const egr_rule_table* table, const uint32_t*
   hipLaunchKernelGGL(rules_small_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
+}
+
+struct egr_rules_server {
+  int device = 0;
+  const RulesDev* D = nullptr;
+  SrvMailbox* h = nullptr;      // host view of the mailbox (mapped, coherent)
+  SrvMailbox* d = nullptr;      // the device's address of the same bytes
+  hipStream_t st = nullptr;     // the server wave's own stream
+  int S = 0;
+  uint64_t seq = 0;             // last posted sequence number
+  bool launched = false;
+};
+
+static int srv_launch(egr_rules_server* s) {
+  __atomic_store_n(&s->h->alive, 1u, __ATOMIC_RELEASE);
+  hipLaunchKernelGGL(rules_server_kernel, dim3(1), dim3(64), 0, s->st, s->D, s->d);
+  EGR_CHECK_LAUNCH();
+  s->launched = true;
+  return EGR_OK;
+}
+
+extern "C" int egr_rules_server_create(const egr_rule_table* table, int32_t device,
+                                       egr_rules_server** out) {
+  if (!table || !out || table->n_rules < 0 || table->n_rules > EGR_MAX_RULES)
+    return egr::fail(EGR_EINVAL, "egr_rules_server_create: bad arguments");
+  for (int r = 0; r < table->n_rules; ++r)
+    if (table->rules[r].n_conds < 0 || table->rules[r].n_conds > EGR_MAX_CONDS)
+      return egr::fail(EGR_EINVAL, "egr_rules_server_create: n_conds out of range");
+  *out = nullptr;
+  egr::DeviceGuard guard(device);
+  auto* s = new egr_rules_server();
+  s->device = device;
+  s->S = table->n_rules + 1;
+  hipError_t e = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking);
+  void* h = nullptr;
+  if (e == hipSuccess) e = hipHostMalloc(&h, sizeof(SrvMailbox), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    s->h = static_cast<SrvMailbox*>(h);
+    std::memset(s->h, 0, sizeof(SrvMailbox));
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, h, 0);
+    s->d = static_cast<SrvMailbox*>(d);
+  }
+  int rc = e == hipSuccess ? EGR_OK : egr::fail(EGR_EDEVICE, std::string("egr_rules_server_create: ") +
+                                                             hipGetErrorString(e));
+  if (rc == EGR_OK) rc = rules_table_dev(*table, s->st, &s->D);
+  if (rc != EGR_OK) {
+    egr_rules_server_free(s);
+    return rc;
+  }
+  *out = s;
+  return EGR_OK;
+}
+
+extern "C" int egr_rules_server_post(egr_rules_server* s, const uint32_t* row_flags,
+                                     const uint32_t* row_vocab, const uint32_t* row_node,
+                                     const double* row_err, int32_t n_rows) {
+  if (!s || n_rows < 0 || n_rows > kSrvRows ||
+      (n_rows > 0 && (!row_flags || !row_vocab || !row_node || !row_err)))
+    return egr::fail(EGR_EINVAL, "egr_rules_server_post: bad arguments (at most 1024 rows)");
+  SrvMailbox* m = s->h;
+  if (__atomic_load_n(&m->ack, __ATOMIC_ACQUIRE) != s->seq)
+    return egr::fail(EGR_ESTATE, "egr_rules_server_post: the previous incident is still pending");
+  if (n_rows > 0) {
+    std::memcpy(m->flags, row_flags, sizeof(uint32_t) * n_rows);
+    std::memcpy(m->vocab, row_vocab, sizeof(uint32_t) * n_rows);
+    std::memcpy(m->node, row_node, sizeof(uint32_t) * n_rows);
+    std::memcpy(m->err, row_err, sizeof(double) * n_rows);
+  }
+  m->n_rows = n_rows;
+  __atomic_store_n(&m->req, ++s->seq, __ATOMIC_RELEASE);     // (the rows before the request)
+  if (!__atomic_load_n(&m->alive, __ATOMIC_ACQUIRE)) {
+    egr::DeviceGuard guard(s->device);
+    return srv_launch(s);
+  }
+  return EGR_OK;
+}
+
+extern "C" int egr_rules_server_poll(egr_rules_server* s, uint32_t* mask, uint8_t* n_hyp,
+                                     uint8_t* order_conf, uint8_t* order_rank, double* confidence,
+                                     double* final_score, double* strength) {
+  if (!s || !mask || !n_hyp || !order_conf || !order_rank || !confidence || !final_score || !strength)
+    return egr::fail(EGR_EINVAL, "egr_rules_server_poll: bad arguments");
+  SrvMailbox* m = s->h;
+  if (__atomic_load_n(&m->ack, __ATOMIC_ACQUIRE) != s->seq) {
+    // the wave left (idle or lifetime bound) before it saw this request: start another one,
+    // which picks the pending request up (it starts from the last acknowledged number)
+    if (!__atomic_load_n(&m->alive, __ATOMIC_ACQUIRE)) {
+      egr::DeviceGuard guard(s->device);
+      const int rc = srv_launch(s);
+      if (rc != EGR_OK) return rc;
+    }
+    return 0;
+  }
+  const int S = s->S;
+  *mask = m->mask;
+  *n_hyp = m->n_hyp;
+  std::memcpy(order_conf, m->order_conf, S);
+  std::memcpy(order_rank, m->order_rank, S);
+  std::memcpy(confidence, m->confidence, sizeof(double) * S);
+  std::memcpy(final_score, m->final_score, sizeof(double) * S);
+  std::memcpy(strength, m->strength, sizeof(double) * S);
+  return 1;
+}
+
+extern "C" void egr_rules_server_free(egr_rules_server* s) {
+  if (!s) return;
+  egr::DeviceGuard guard(s->device);
+  if (s->h) {
+    __atomic_store_n(&s->h->stop, 1u, __ATOMIC_RELEASE);
+    if (s->launched && s->st) (void)hipStreamSynchronize(s->st);   // (the wave leaves at its next poll)
+    (void)hipHostFree(s->h);
+  }
+  if (s->st) (void)hipStreamDestroy(s->st);
+  delete s;
 }
 
 extern "C" int egr_rank(const double* confidence, const double* cat_weight, const double* support,

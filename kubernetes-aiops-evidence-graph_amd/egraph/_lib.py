@@ -161,6 +161,10 @@ SIGNATURES: dict[str, tuple] = {
     "egr_host_free": (C.c_int, [P]),
     "egr_rules_eval_small": (C.c_int, [C.POINTER(EgrRuleTable), P, P, P, P, I32, C.POINTER(EgrRulesOut), P]),
     "egr_rules_eval_staged": (C.c_int, [C.POINTER(EgrRuleTable), P, P, P, P, I64, I64, I64, I32, P]),
+    "egr_rules_server_create": (C.c_int, [C.POINTER(EgrRuleTable), I32, C.POINTER(P)]),
+    "egr_rules_server_post": (C.c_int, [P, P, P, P, P, I32]),
+    "egr_rules_server_poll": (C.c_int, [P, P, P, P, P, P, P, P]),
+    "egr_rules_server_free": (None, [P]),
 }
 
 

@@ -4,10 +4,12 @@ The reference runs one RulesEngine.generate_hypotheses + HypothesisRanker.rank p
 inside each Temporal activity (src/services/workflow/activities.py:124-170); activities run
 concurrently in one worker.  Here:
 
-  RulesRunner   one egr_rules_eval launch per call.  Small batches (the single-incident
-                calls of the activities) are ZERO-COPY: the kernel reads the encoded rows from,
-                and writes its outputs to, pinned host memory mapped into the GPU address space
-                (egr_host_alloc), so a call is one kernel launch with no DMA copies.  Large
+  RulesRunner   one egr_rules_eval launch per call.  A single incident of at most 1024 rows
+                (the activities' calls) goes to the resident rules server (egr_rules_server_*):
+                a one-wave kernel polling a mailbox in mapped host memory, so the call is two
+                PCIe round trips and no kernel launch.  Other small batches are ZERO-COPY: the
+                kernel reads the encoded rows from, and writes its outputs to, pinned host memory
+                mapped into the GPU address space (egr_host_alloc).  Large
                 batches go through a device buffer: the columns go up in ONE host-to-device copy
                 and the seven outputs come back in ONE device-to-host copy, issued with the
                 kernel in one library call (egr_rules_eval_staged).  Either way the caller waits
@@ -24,6 +26,7 @@ from __future__ import annotations
 import asyncio
 import contextlib
 import gc
+import os
 import time
 
 import numpy as np
@@ -78,10 +81,39 @@ class RulesRunner:
         self.mode = ""                                # "small" / "zero_copy" / "staged"
         self._layouts: dict = {}
         self._small_out = None                        # EgrRulesOut of the single-incident layout
+        self._srv = None                              # the rules server (created on first use)
+        self._srv_wait = None
 
     # a single incident of at most this many rows travels in the kernel's arguments
     # (egr_rules_eval_small): one launch, no copies, no PCIe reads by the kernel
     SMALL_ROWS = 128
+
+    # the single-incident path through the resident rules server (False: one small kernel
+    # launch per call, egr_rules_eval_small; $EGRAPH_RULES_SERVER=0 for A/B runs)
+    USE_SERVER = os.environ.get("EGRAPH_RULES_SERVER", "1") != "0"
+    SERVER_ROWS = 1024                            # the server's mailbox (egr_rules_server_post)
+
+    def _server(self):
+        if self._srv is None:
+            import ctypes as C
+            h = C.c_void_p()
+            L.check(L.lib.egr_rules_server_create(self.cat.table, self.dev.index or 0, C.byref(h)),
+                    "egr_rules_server_create")
+            self._srv = h
+            S = self.S
+            a8 = (S + 7) // 8 * 8
+            # one output block per call: mask u32 @0, n_hyp u8 @8, order_conf / order_rank (S
+            # bytes each), confidence / final_score / strength (S doubles each)
+            self._srv_off = (0, 8, 16, 16 + a8, 16 + 2 * a8, 16 + 2 * a8 + 8 * S, 16 + 2 * a8 + 16 * S)
+            self._srv_bytes = 16 + 2 * a8 + 24 * S
+            self._srv_wait = _ServerWait(self)
+        return self._srv
+
+    def __del__(self):
+        h = getattr(self, "_srv", None)
+        if h is not None and getattr(L, "lib", None) is not None:
+            self._srv = None
+            L.lib.egr_rules_server_free(h)
 
     def _layout(self, rows: int, B: int):
         key = (rows, B)
@@ -174,6 +206,15 @@ class RulesRunner:
         self.off, self.in_bytes, self.total = self._layout(rows, B)
         st = self.stream
         small = B == 1 and rows <= self.SMALL_ROWS
+        if B == 1 and rows <= self.SERVER_ROWS and self.USE_SERVER:
+            srv = self._server()
+            f = enc.flags.ctypes.data if rows else None
+            L.check(L.lib.egr_rules_server_post(srv, f, enc.vocab.ctypes.data if rows else None,
+                                                enc.node.ctypes.data if rows else None,
+                                                enc.err.ctypes.data if rows else None, rows),
+                    "egr_rules_server_post")
+            self.mode = "server"
+            return self._srv_wait.arm()
         if (small or rows <= self.ZERO_COPY_ROWS) and (self.mapped is None or self.mapped.nbytes < self.total):
             self.mapped = MappedBuffer(max(self.total, 1 << 20))
             self._small_out = None
@@ -221,6 +262,8 @@ class RulesRunner:
         """Host copies of the last launch's outputs (after its event completed): the output
         block is copied once and the seven arrays are views of that copy."""
         B, S = self._B, self.S
+        if self.mode == "server":
+            return self._srv_wait.result()
         lo = self.off["mask"][0]
         o, nb = self.off["str"]
         blk = self.hnp[lo:o + nb].copy()
@@ -238,6 +281,10 @@ class RulesRunner:
     def run_sync(self, enc: EncodedBatch) -> RulesResult:
         self.launch(enc).synchronize()
         return self.results()
+
+    def sync_last(self) -> None:
+        """Wait for the last launch (whichever path it took)."""
+        (self._srv_wait if self.mode == "server" else self.event).synchronize()
 
     # the first SPIN_S of a launch's wait spin on its event without yielding (a single
     # incident's round trip is ~25-30 us, and every event-loop hop adds several us); past it
@@ -259,6 +306,44 @@ class RulesRunner:
             if time.perf_counter() - t0 > self.SPIN_S:
                 await asyncio.sleep(0)              # long launch: poll from the loop
         return self.results()
+
+
+class _ServerWait:
+    """The event-like handle of a rules-server call (query / synchronize, as a torch.cuda.Event
+    is used by RulesRunner.run / run_sync): query() polls the mailbox and, once the incident is
+    done, holds its outputs in a fresh block (the arrays of the RulesResult are views of it)."""
+    __slots__ = ("r", "blk", "done", "_args")
+
+    def __init__(self, runner: RulesRunner):
+        self.r, self.blk, self.done, self._args = runner, None, False, None
+
+    def arm(self) -> "_ServerWait":
+        r = self.r
+        self.blk = np.empty(r._srv_bytes, np.uint8)
+        base = self.blk.ctypes.data
+        self._args = tuple(base + o for o in r._srv_off)
+        self.done = False
+        return self
+
+    def query(self) -> bool:
+        if not self.done:
+            rc = L.lib.egr_rules_server_poll(self.r._srv, *self._args)
+            if rc < 0:
+                L.check(rc, "egr_rules_server_poll")
+            self.done = rc == 1
+        return self.done
+
+    def synchronize(self) -> None:
+        while not self.query():
+            pass
+
+    def result(self) -> RulesResult:
+        S, o, b = self.r.S, self.r._srv_off, self.blk
+        return RulesResult(b[o[0]:o[0] + 4].view(np.uint32), b[o[1]:o[1] + 1],
+                           b[o[2]:o[2] + S].reshape(1, S), b[o[3]:o[3] + S].reshape(1, S),
+                           b[o[4]:o[4] + 8 * S].view(np.float64).reshape(1, S),
+                           b[o[5]:o[5] + 8 * S].view(np.float64).reshape(1, S),
+                           b[o[6]:o[6] + 8 * S].view(np.float64).reshape(1, S))
 
 
 def concat(encs: list[EncodedBatch]) -> EncodedBatch:
@@ -300,13 +385,43 @@ class RulesBatcher:
 
     async def submit(self, incident_id, evidence: list[dict], ranked: bool) -> list[dict]:
         """One incident's hypothesis list (generate_hypotheses, ranked or not)."""
+        self.calls += 1
+        if not self.busy:
+            return await self._single_idle(str(incident_id), evidence, ranked)
+        # (a launch is running: this call joins the next one)
         loop = asyncio.get_running_loop()
         call = _Call([str(incident_id)], [evidence], ranked, loop.create_future(), True)
-        self.calls += 1
         self.queue.append(call)
-        if self.busy:                  # (a launch is running: this call joins the next one)
-            return await call.fut
-        return await self._launch_idle(loop, call)
+        return await call.fut
+
+    async def _single_idle(self, incident_id: str, evidence: list[dict], ranked: bool) -> list[dict]:
+        """An idle batcher's lone call, run in the caller's task with no queue entry, future or
+        second task: encode (raising what the reference raises, to this caller only), the
+        launch (the rules server for a single incident), the dicts.  Calls that arrive while it
+        runs queue up and go out together from a drain task afterwards.  (Fewer objects per call
+        than the queued path: the activities' one-incident calls see fewer collector pauses.)"""
+        self.busy = True
+        launched = False
+        try:
+            enc = encode_batch([evidence], self.cat, out=self.runner.input_views)
+            self.launches += 1
+            launched = True
+            res = await self.runner.run(enc)
+            launched = False
+            with gc_paused():
+                lists = hypothesis_lists(self.cat, res, [incident_id], enc.evidence_ids, ranked)
+                if not ranked:
+                    FUSED.register(self.cat, res, lists, (0,))
+            return lists[0]
+        except asyncio.CancelledError:
+            if launched:                     # (the next launch reuses the buffers / mailbox)
+                self.runner.sync_last()
+            raise
+        finally:
+            if self.queue:
+                asyncio.get_running_loop().create_task(self._drain())   # stays busy until empty
+            else:
+                self.busy = False
 
     async def submit_many(self, incident_ids: list, evidence_lists: list, ranked: bool
                           ) -> list[list[dict]]:
@@ -377,7 +492,7 @@ class RulesBatcher:
             # its kernel runs: finish the launch here -- the next launch reuses its buffers --
             # and serve the other calls of the batch, then let the cancellation through
             try:
-                self.runner.event.synchronize()
+                self.runner.sync_last()
                 res = self.runner.results()
             except BaseException as e:                      # noqa: BLE001 (re-raised below)
                 self._fail(ok, e)

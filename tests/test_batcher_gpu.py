@@ -30,17 +30,19 @@ def test_runner_matches_oracle():
     cat = catalog.default()
     runner = RulesRunner(cat)
     # zero-copy (mapped host memory) for small batches, the staged device buffer above
-    # ZERO_COPY_ROWS; grows, then reuses the buffers with a smaller batch
-    # and a single incident of <= 128 rows in the kernel arguments (egr_rules_eval_small)
+    # ZERO_COPY_ROWS; grows, then reuses the buffers with a smaller batch; a single incident
+    # of <= 1024 rows through the resident rules server (egr_rules_server_*)
     seen = set()
-    for n, big in ((1, False), (3, False), (700, False), (40, False), (2000, False), (0, False),
-                   (5, False), (1, True), (1, False)):
+    # (rep: one incident of its first list repeated -- 30x: 129..1024 rows, still the server's;
+    # 600x: past its mailbox, zero-copy)
+    for n, rep in ((1, 0), (3, 0), (700, 0), (40, 0), (2000, 0), (0, 0), (5, 0), (1, 600),
+                   (1, 30), (1, 0)):
         lists = [evidence_fuzz.random_evidence(rng) for _ in range(n)]
-        if big:
-            lists = [(lists[0] or [{"id": "x"}]) * 200]   # one incident of > 128 rows
+        if rep:
+            lists = [(lists[0] or [{"id": "x"}]) * rep]
         enc = encode_batch(lists, cat)
         res = runner.run_sync(enc)
-        want = ("small" if n == 1 and enc.n_rows <= runner.SMALL_ROWS else
+        want = ("server" if n == 1 and enc.n_rows <= runner.SERVER_ROWS else
                 "zero_copy" if enc.n_rows <= runner.ZERO_COPY_ROWS else "staged")
         assert runner.mode == want
         seen.add(want)
@@ -51,7 +53,58 @@ def test_runner_matches_oracle():
         assert res.final_score.tobytes() == exp["final_score"].tobytes()
         assert res.confidence.tobytes() == exp["confidence"].tobytes()
         assert res.strength.tobytes() == exp["strength"].tobytes()
-    assert seen == {"small", "zero_copy", "staged"}
+    assert seen == {"server", "zero_copy", "staged"}
+
+
+def _check_one(res, enc, cat):
+    exp = oracle.rules_eval(cat.table, enc.flags, enc.vocab, enc.node, enc.err, enc.seg_off)
+    np.testing.assert_array_equal(res.mask, exp["mask"])
+    np.testing.assert_array_equal(res.n_hyp, exp["n_hyp"])
+    np.testing.assert_array_equal(res.order_rank, exp["order_rank"])
+    np.testing.assert_array_equal(res.order_conf, exp["order_conf"])
+    assert res.final_score.tobytes() == exp["final_score"].tobytes()
+    assert res.confidence.tobytes() == exp["confidence"].tobytes()
+    assert res.strength.tobytes() == exp["strength"].tobytes()
+
+
+def test_rules_server_sequence_idle_exit_and_small_kernel(golden):
+    """The resident rules server (egr_rules_server_*): every golden case posted one after
+    another through the same mailbox -- each result equals the C oracle and the one-launch
+    small kernel's, so no request reads a previous one's rows or outputs; the server wave leaves
+    after ~2 ms idle and the next call starts it again; a pending post is refused."""
+    import time
+    from egraph import catalog
+    from egraph.batcher import RulesRunner
+    from egraph.encode import encode_batch
+    from egraph import _lib as L
+    cat = catalog.default()
+    srv, small = RulesRunner(cat), RulesRunner(cat)
+    small.USE_SERVER = False
+    cases = golden["rules"]["cases"]
+    n_small = 0
+    for i, case in enumerate(cases):
+        enc = encode_batch([case["evidence"]], cat)
+        if enc.n_rows > RulesRunner.SMALL_ROWS:
+            continue
+        a = srv.run_sync(enc)
+        assert srv.mode == "server"
+        _check_one(a, enc, cat)
+        if i % 7 == 0:
+            b = small.run_sync(enc)
+            assert small.mode == "small"
+            for x, y in zip(a.__dict__.values(), b.__dict__.values()):
+                assert x.tobytes() == y.tobytes()
+            n_small += 1
+        if i in (100, 500):
+            time.sleep(0.05)                   # idle past the wave's ~2 ms: it leaves, and
+            e0 = encode_batch([[]], cat)       # the next post starts it again
+            _check_one(srv.run_sync(e0), e0, cat)
+            h = srv._srv                       # one incident in flight: a second post is refused
+            assert L.lib.egr_rules_server_post(h, None, None, None, None, 0) == L.EGR_OK
+            # (unless the wave has already answered the first: a PCIe round trip or two)
+            assert L.lib.egr_rules_server_post(h, None, None, None, None, 0) in (L.EGR_ESTATE, L.EGR_OK)
+            srv._srv_wait.arm().synchronize()
+    assert n_small > 100
 
 
 def test_concurrent_calls_coalesce_and_match_golden(golden):
