@@ -269,9 +269,10 @@ def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) ->
 def warm_up(ctx, hops: int, warmup: int, dev, rank: int = 0, engine: str = "frontier",
             graphs: bool = True):
     """The untimed part of a run, as main() does it: `warmup` eager steps (at least one per lane
-    and launch group), then -- frontier -- two looks of Frontier.adapt() at the stats (the
-    wide-table retry for graphs whose columns overflow the narrow table; mid- or wide-first when
-    most do) with warm-up steps after each, then the lanes captured as HIP graphs and replayed
+    and launch group), then -- frontier -- two looks of Frontier.adapt() at the stats (overflow
+    handling for graphs whose columns overflow the narrow table: continuation regions, the wide
+    retry behind them; mid- or wide-first when most do) with warm-up steps after each, then the
+    lanes captured as HIP graphs and replayed
     `warmup` times.  Returns the step function of the timed region."""
     M = ctx.get("merge", 1)
     run_step = step_frontier if engine == "frontier" else step
@@ -280,16 +281,18 @@ def warm_up(ctx, hops: int, warmup: int, dev, rank: int = 0, engine: str = "fron
         run_step(ctx, hops)
     torch.cuda.synchronize(dev)
     if engine == "frontier":
-        # graphs with large 3-hop neighbourhoods (the dense C4): columns that overflow the
-        # narrow table get the wide-table retry from here on (egraph.graph.Frontier.adapt)
+        # graphs with large 3-hop neighbourhoods: columns that overflow the narrow table continue
+        # in global-memory regions inside the grid from here on, the wide-table retry behind
+        # them (egraph.graph.Frontier.adapt)
         # most columns overflowing the narrow table: the mid table first; a second look after the
         # next warm-up steps moves to wide-first if most columns overflow that one too
         for check in range(2):
             for lane in ctx["lanes"]:
                 fr = lane["frontier"]
                 if fr.adapt(fr.stats()):
-                    log(f"[rank {rank}] wide-table retry on ({fr.retry_blocks} blocks), first "
-                        f"table {FIRST_TABLE[fr.wide_first]}")
+                    log(f"[rank {rank}] overflow handling on (wide retry {fr.retry_blocks} blocks, "
+                        f"{fr.continuation_regions} continuation regions), first table "
+                        f"{FIRST_TABLE[fr.wide_first]}")
             for _ in range(max(warmup, 1)):
                 run_step(ctx, hops)
             torch.cuda.synchronize(dev)

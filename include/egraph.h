@@ -385,8 +385,8 @@ int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_v
  *                         pulls (col + val read), CSR entries read by expansions (col only),
  *                         rows walked (row_ptr pairs), members, columns handed on by an LDS
  *                         kernel (the narrow one and, with the retry on, the wide one), pool
- *                         entries used, valid seed entries, -1 (reserved), columns ranked by
- *                         the global-memory variant.
+ *                         entries used, valid seed entries, columns finished in a
+ *                         continuation region, columns ranked by the global-memory variant.
  *   egr_frontier_read_* : dense copies like egr_plan_read_* (scores [V][n_cols] row-major,
  *                         reach [ceil(n_cols/64)][V]); EGR_ESTATE-free but a column whose
  *                         members did not fit the pool reads as all zero.
@@ -402,6 +402,15 @@ typedef struct egr_frontier egr_frontier;
  * overflow and skip the launch).  Takes effect from the next run (capture it into a graph
  * after setting it).                                                                       */
 int egr_frontier_set_retry(egr_frontier* f, int32_t blocks);
+/* With the retry on and the narrow table first: a column that overflows the narrow table
+ * continues in its own workgroup, in one of `regions` global-memory table regions (8192 slots,
+ * 6144 members each; claimed one per overflowing column per run, cleared by the workgroup
+ * after use), instead of waiting for the wide retry grid that runs after the narrow one --
+ * the costliest columns start first, so they finish while the grid runs.  What overflows a
+ * region, or finds none left, goes to the global-memory variant.  0 = off (the default).
+ * Same results either way; EGR_EINVAL outside 0..4096; synchronises the device when it
+ * allocates (about 128 KB per region).                                                     */
+int egr_frontier_set_continuation(egr_frontier* f, int32_t regions);
 /* Top-k-only frontiers with the retry on: the first table every column tries, for graphs where
  * most columns overflow the narrow one (the narrow attempt would be wasted work).  `on` = 0: the
  * narrow table; 1: EVERY column straight to the wide grid; 2: a 2.8k-slot mid table first (four

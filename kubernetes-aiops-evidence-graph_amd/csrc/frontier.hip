@@ -33,6 +33,10 @@
 // column with more members than the table's limit is flagged and redone by the next table, and
 // last by the global-memory variant of the same code (a table of >= 2V slots per resident
 // workgroup, never overflows), launched unconditionally (it drains an empty work list at once).
+// A narrow-table overflow (pruned C3: 0.56 % of the columns, 1.2-1.6k members) continues in its
+// own workgroup instead, in a global-memory region (egr_frontier_set_continuation): those columns
+// start early, costliest first, and finish while the grid runs -- the serial wide-retry grid
+// after it was 6.6 % of the launch (C3 -3 % per step, profiles/r05_ab_continuation.txt).
 //
 // (Round 3 measured a two-phase alternative for top-k runs -- discover the column's member set
 // and its member-restricted local CSR first, then propagate in LDS only -- at 0.14-0.16 ms per
@@ -67,6 +71,11 @@ constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents t
 constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
 constexpr int MAX_HOPS = 60;
 constexpr int PROF_SLOTS = 40;
+// a continuation region (egr_frontier_set_continuation): 8192 slots (2048 four-slot buckets),
+// members up to 6144 (load 0.75) -- more than the wide LDS table's 4608, so what the wide retry
+// used to take fits.  Keys, scores, flags, need bits, then the member list and pull results.
+constexpr uint32_t CONT_CAP = 8192, CONT_LIMIT = 6144;
+constexpr size_t CONT_REGION_BYTES = 10 * (size_t)CONT_CAP + 8 * (size_t)CONT_LIMIT;
 
 struct FArgs {
   const uint32_t* row_ptr;
@@ -119,8 +128,15 @@ struct FArgs {
   uint32_t gcap;
   unsigned long long* prof;     // [B][PROF_SLOTS] wall-clock stamps per phase, or nullptr
   // [0] CSR entries gathered by pulls (col + val), [1] entries read by expansions (col),
-  // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed
+  // [2] rows walked (row_ptr pairs), [3] members, [4] columns that overflowed an LDS table,
+  // [5] columns finished in a continuation region
   unsigned long long* stats;
+  // overflow continuation (egr_frontier_set_continuation): cont_n global-memory table regions
+  // of CONT_REGION_BYTES from cont_base, claimed through *cont_ctr (zeroed with the run's
+  // counters)
+  unsigned long long* cont_ctr;
+  uint32_t cont_n;
+  uint8_t* cont_base;
 };
 
 struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
@@ -304,7 +320,7 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 __global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf,
                                                           uint32_t* ghist) {
   const int tid = threadIdx.x;
-  if (tid < 7) ctr[tid] = 0;
+  if (tid < 8) ctr[tid] = 0;
   if (tid < 4) ovf[tid] = 0;
   if (ghist) ghist[tid] = 0;      // (64 threads = COST_BUCKETS)
 }
@@ -381,7 +397,7 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
     run += x;
   }
   if (tid == SCAN_T - 1) ptr[B] = part[SCAN_T - 1];
-  if (tid < 7) ctr[tid] = 0;      // the next run's pool / stats counters and overflow lists
+  if (tid < 8) ctr[tid] = 0;      // the next run's pool / stats counters and overflow lists
   if (tid < 4) ovf[tid] = 0;
   for (int c = c0; c < c1; ++c) atomicAdd(&hist[cost_bucket(cost[c])], 1u);
   __syncthreads();
@@ -527,7 +543,12 @@ struct egr_frontier {
   bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
   int64_t last_n_seeds = -1;      // seed entries of the last grouped run (-1: the last run was
                                   // a set_seeds run; its valid count is seed_ptr[B])
+  // overflow continuation regions (egr_frontier_set_continuation; cont_n = 0: off)
+  uint32_t cont_n = 0;
+  uint8_t* cont_base = nullptr;
 };
+
+
 
 // default persistent grid of the wide-table second chance ($EGRAPH_FRONTIER_WIDE_RETRY, or
 // egr_frontier_set_retry): two 78-KB workgroups per CU on 256 CUs
@@ -580,7 +601,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       (rc = dalloc(&f->seed_v, ms)) || (rc = dalloc(&f->seed_s, ms)) ||
       (rc = dalloc(&f->seed_rep, ms)) ||
       (rc = dalloc(&f->pool_v, f->pool_cap)) || (rc = dalloc(&f->pool_s, f->pool_cap)) ||
-      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 7)) ||
+      (rc = dalloc(&f->pool_d, f->pool_cap)) || (rc = dalloc(&f->ctr, 8)) ||
       (rc = dalloc(&f->mem_off, (size_t)n_cols)) || (rc = dalloc(&f->mem_cnt, (size_t)n_cols)) ||
       (rc = dalloc(&f->ovf, 2 * (size_t)n_cols + 4)) || (rc = dalloc(&f->all_n, 1)) ||
       (rc = dalloc(&f->gkeys, gcap * f->nbig)) || (rc = dalloc(&f->gs, gcap * f->nbig)) ||
@@ -601,7 +622,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
       hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
-      hipMemset(f->ctr, 0, 7 * 8) != hipSuccess) {
+      hipMemset(f->ctr, 0, 8 * 8) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
   }
@@ -648,6 +669,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->gfl);
   dfree(f->gneed);
   dfree(f->gmlist);
+  dfree(f->cont_base);
   delete f;
 }
 
@@ -802,7 +824,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     if (f->first == 2 && rb > 0) {
       // mid-first: every column in the 2.8k-slot table; what overflows it takes the wide retry
       FArgs am = an;
-      hipLaunchKernelGGL(fr_mid::frontier_lds_kernel, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
+      hipLaunchKernelGGL(fr_mid::frontier_lds_kernel<false>, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
       EGR_CHECK_LAUNCH();
       hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
                          dim3(fr_wide::FT), 0, st, a);
@@ -817,8 +839,23 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                          dim3(fr_wide::FT), 0, st, aw);
       EGR_CHECK_LAUNCH();
       skipped_lds = true;
+    } else if (rb > 0 && f->cont_n > 0) {
+      // continuation: an overflowing column finishes in its own workgroup, in a global-memory
+      // region, while the grid runs (no serial retry after it); what overflows a region too, or
+      // finds none left, goes straight to the global-memory variant's list
+      FArgs ac = an;
+      ac.ovf_n = a.ovf_n;
+      ac.ovf_list = a.ovf_list;
+      ac.ovf_cap = a.ovf_cap;
+      ac.cont_ctr = f->ctr + 7;
+      // ($EGRAPH_FRONTIER_CONT_DRY: the continuation kernel with no region -- a test hook that
+      // prices its code against the plain kernel's)
+      ac.cont_n = getenv("EGRAPH_FRONTIER_CONT_DRY") ? 0u : f->cont_n;
+      ac.cont_base = f->cont_base;
+      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel<true>, dim3(f->B), dim3(fr_narrow::FT), 0, st, ac);
+      EGR_CHECK_LAUNCH();
     } else {
-      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
+      hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel<false>, dim3(f->B), dim3(fr_narrow::FT), 0, st, an);
       EGR_CHECK_LAUNCH();
       if (rb > 0) {
         hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
@@ -827,7 +864,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
       }
     }
   } else {
-    hipLaunchKernelGGL(fr_wide::frontier_lds_kernel, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
+    hipLaunchKernelGGL(fr_wide::frontier_lds_kernel<false>, dim3(f->B), dim3(fr_wide::FT), 0, st, a);
     EGR_CHECK_LAUNCH();
   }
   // the overflow fallback: one-wave workgroups (they are dispatched as soon as one SIMD has
@@ -917,6 +954,29 @@ int egr_frontier_set_retry(egr_frontier* f, int32_t blocks) {
   return EGR_OK;
 }
 
+int egr_frontier_set_continuation(egr_frontier* f, int32_t regions) {
+  if (!f || regions < 0 || regions > 4096)
+    return egr::fail(EGR_EINVAL, "egr_frontier_set_continuation: bad arguments (0..4096 regions)");
+  if ((uint32_t)regions > f->cont_n) {
+    DeviceGuard guard(f->s->device);
+    EGR_HIP(hipDeviceSynchronize());            // runs in flight still use the old regions
+    dfree(f->cont_base);
+    f->cont_base = nullptr;
+    f->cont_n = 0;
+    const size_t n = (size_t)regions;
+    int rc;
+    if ((rc = dalloc(&f->cont_base, n * CONT_REGION_BYTES))) return rc;
+    // every region: keys EMPTY, scores / flags / need zero (a used region is left so again)
+    if (hipMemset(f->cont_base, 0, n * CONT_REGION_BYTES) != hipSuccess)
+      return egr::fail(EGR_EDEVICE, "egr_frontier_set_continuation: region init failed");
+    for (size_t r = 0; r < n; ++r)
+      if (hipMemset(f->cont_base + r * CONT_REGION_BYTES, 0xFF, 4 * (size_t)CONT_CAP) != hipSuccess)
+        return egr::fail(EGR_EDEVICE, "egr_frontier_set_continuation: region init failed");
+  }
+  f->cont_n = (uint32_t)regions;
+  return EGR_OK;
+}
+
 int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
   // out8 holds 9 values (egraph.h: out9)
   if (!f || !out8) return egr::fail(EGR_EINVAL, "egr_frontier_stats: NULL argument");
@@ -933,7 +993,7 @@ int egr_frontier_stats(const egr_frontier* f, int64_t* out8, void* stream) {
   for (int i = 0; i < 5; ++i) out8[i] = (int64_t)h[i + 1];
   out8[5] = (int64_t)h[0];
   out8[6] = f->last_n_seeds < 0 ? (int64_t)nu : f->last_n_seeds;
-  out8[7] = -1;   // reserved (a corrupt-key counter of earlier debug builds): not counted
+  out8[7] = (int64_t)h[6];   // columns finished in a continuation region
   return EGR_OK;
 }
 

@@ -1063,8 +1063,67 @@ struct LdsTab {
   uint32_t bloom[BLOOM_WORDS];
 };
 
-// One column in the LDS table: clear, run, and on overflow hand the column on (A.ovf_list).
-__device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh) {
+// The rest of a column that overflowed the LDS table, in the same workgroup: run again from its
+// seeds in a global-memory table region of its own (A.cont_*: 2k-slot-bucket tables, claimed one
+// per column and run from a counter zeroed with the run's counters -- a region is used by one
+// workgroup per run, so no other XCD's L2 holds a stale line of it), then the region's every
+// slot cleared for the next run.  The overflowing columns start early (costliest first), so
+// finishing them here, while the grid runs, leaves no serial retry tail after it.  False (the
+// caller hands the column on) when the regions are used up or the column overflows this table too.
+// (Inlined: a noinline call measured +37 % on the whole kernel, profiles/r05_ab_continuation.txt.)
+template <bool CONT>
+__device__ __forceinline__ bool continue_column(const FArgs& A, int b, Shared& sh) {
+  if constexpr (!CONT) {
+    return false;
+  } else {
+    const uint32_t tid = threadIdx.x;
+    __syncthreads();                         // (every wave is past the LDS attempt's sh reads)
+    if (tid == 0) {
+      sh.item = atomicAdd(A.cont_ctr, 1u);
+      sh.count = 0;
+      sh.ovf = 0;
+      sh.w_pull = sh.w_expand = sh.w_rows = 0;
+    }
+    __syncthreads();
+    const uint32_t r = sh.item;
+    if (r >= A.cont_n) return false;
+    // (profiling builds: slot 38 keeps the column's first stamp -- run_column restamps the
+    // phases from slot 0 -- and slot 39 the continuation's start and end)
+    const size_t pb = (size_t)b * PROF_SLOTS * PROF_W;
+    if (FR_PROF_ON(A) && tid == 0) {
+      A.prof[pb + 38 * PROF_W] = A.prof[pb];
+      A.prof[pb + 39 * PROF_W] = wall_clock64();
+    }
+    // one allocation, region r at cont_base + r * CONT_REGION_BYTES, its arrays at fixed offsets
+    // (one base register pair for all six: the continuation adds no live pointers of its own
+    // to the kernel, whose register budget its LDS path shares)
+    uint8_t* rb = A.cont_base + (size_t)r * CONT_REGION_BYTES;
+    constexpr uint32_t cap = CONT_CAP;
+    Tab<true> g{reinterpret_cast<uint32_t*>(rb), reinterpret_cast<float*>(rb + 4 * cap), rb + 8 * cap,
+                rb + 9 * cap, reinterpret_cast<uint32_t*>(rb + 10 * cap),
+                reinterpret_cast<float*>(rb + 10 * cap + 4 * CONT_LIMIT), cap, CONT_LIMIT, &sh.count,
+                &sh.ovf, nullptr, SH_CHAIN};
+    const bool ok = run_column<true>(A, g, sh, b);
+    if (ok && tid == 0) atomicAdd(&A.stats[5], 1ull);
+    if (FR_PROF_ON(A) && tid == 0) A.prof[pb + 39 * PROF_W + 1] = wall_clock64();
+    __syncthreads();
+    // every slot back to empty (an overflowed column may have inserted past its member list)
+    for (uint32_t i = tid; i < cap; i += FT) {
+      g.keys[i] = EMPTY;
+      g.s[i] = 0.f;
+      g.fl[i] = 0;
+      g.need[i] = 0;
+    }
+    return ok;
+  }
+}
+
+// One column in the LDS table: clear, run, and on overflow either continue it in a global
+// region (CONT) or hand it on (A.ovf_list).  `row`: the row of A.lsnew that holds the column's
+// pull results by member index.  (The row pointer is formed here, not by the caller: a pointer
+// argument stays live through the column and costs the narrow kernel 20 B of scratch.)
+template <bool CONT>
+__device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Shared& sh, uint32_t row) {
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < BLOOM_WORDS; i += FT) L.bloom[i] = 0;
 #pragma unroll
@@ -1081,19 +1140,24 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   }
   __syncthreads();
   Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, A.lsnew + (size_t)b * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN};
-  if (!run_column<false>(A, t, sh, b) && tid == 0) {
+               L.mlist, A.lsnew + (size_t)row * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN};
+  if (run_column<false>(A, t, sh, b)) return;
+  if (tid == 0) atomicAdd(&A.stats[4], 1ull);
+  if (continue_column<CONT>(A, b, sh)) return;
+  if (tid == 0) {
     const uint32_t i = atomicAdd(A.ovf_n, 1u);
     if (i < A.ovf_cap) A.ovf_list[i] = (uint32_t)b;
     else A.spill_list[atomicAdd(A.spill_n, 1u)] = (uint32_t)b;
-    atomicAdd(&A.stats[4], 1ull);
   }
 }
 
 // The kernels this geometry launches (FR_KERNELS: 1 = frontier_lds_kernel, 2 =
 // frontier_lds_retry_kernel, 4 = frontier_global_kernel).
 #if FR_KERNELS & 1
-// One workgroup per column, in launch order (A.order).
+// One workgroup per column, in launch order (A.order).  CONT: an overflowing column continues in
+// a global-memory region (continue_column; a separate instantiation, so the plain kernel carries
+// none of that code).
+template <bool CONT>
 __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(FR_WAVES_PER_EU)))
 void frontier_lds_kernel(const FArgs A) {
   __shared__ LdsTab L;
@@ -1104,7 +1168,7 @@ void frontier_lds_kernel(const FArgs A) {
     A.seed_cnt[b] = 0;                      // zero for the next set_seeds
     A.seed_cnt[A.B + b] = 0;
   }
-  lds_column(A, b, L, sh);
+  lds_column<CONT>(A, b, L, sh, (uint32_t)b);
 }
 #endif
 
@@ -1126,7 +1190,8 @@ void frontier_lds_retry_kernel(const FArgs A) {
     __syncthreads();
     const uint32_t i = sh.item;
     if (i >= n) break;
-    lds_column(A, (int)A.retry_list[i], L, sh);
+    const uint32_t b = A.retry_list[i];
+    lds_column<false>(A, (int)b, L, sh, b);
     __syncthreads();              // the next column clears the table this one used
   }
 }

@@ -132,6 +132,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_frontier_shape": (C.c_int, [P, P, P]),
     "egr_frontier_stats": (C.c_int, [P, P, P]),
     "egr_frontier_set_retry": (C.c_int, [P, I32]),
+    "egr_frontier_set_continuation": (C.c_int, [P, I32]),
     "egr_frontier_set_wide_first": (C.c_int, [P, I32]),
     "egr_frontier_read_scores": (C.c_int, [P, P, P]),
     "egr_frontier_phase_times": (C.c_int, [P, P, I64, P]),

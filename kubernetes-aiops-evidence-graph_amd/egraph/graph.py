@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 from collections.abc import Iterable, Sequence
 
 import numpy as np
@@ -768,6 +769,7 @@ class Frontier:
         self.out_ids = torch.empty(n_cols * k, dtype=torch.int32, device=self.dev)
         self.out_scores = torch.empty(n_cols * k, dtype=torch.float32, device=self.dev)
         self.retry_blocks = 0
+        self.continuation_regions = 0
         self.wide_first = self.FIRST_NARROW
         self._mid_checked = False
         self._adapt_calls = 0
@@ -818,15 +820,26 @@ class Frontier:
         return self.out_ids.view(self.B, self.k), self.out_scores.view(self.B, self.k)
 
     STATS = ("pull_entries", "expand_entries", "rows", "members", "overflowed", "pool_used",
-             "seed_entries", "corrupt_keys", "global_columns")
+             "seed_entries", "continued", "global_columns")
 
     RETRY_BLOCKS = 512          # two wide workgroups per CU
+    # global-memory regions in which a narrow-table overflow continues inside the grid
+    # (egr_frontier_set_continuation), switched on with the retry; $EGRAPH_FRONTIER_CONTINUATION
+    # overrides (0 = off: the wide retry grid after the narrow one)
+    CONTINUATION_REGIONS = int(os.environ.get("EGRAPH_FRONTIER_CONTINUATION", "128"))
 
     def set_retry(self, blocks: int) -> None:
         """Wide-table second chance for the columns that overflow the narrow table (see
         egr_frontier_set_retry); 0 turns it off."""
         L.check(L.lib.egr_frontier_set_retry(self._h, int(blocks)), "egr_frontier_set_retry")
         self.retry_blocks = int(blocks)
+
+    def set_continuation(self, regions: int) -> None:
+        """Finish the narrow table's overflowing columns inside the grid, each in a global-memory
+        region of its own (egr_frontier_set_continuation); 0 = off."""
+        L.check(L.lib.egr_frontier_set_continuation(self._h, int(regions)),
+                "egr_frontier_set_continuation")
+        self.continuation_regions = int(regions)
 
     # the first table a column tries (egr_frontier_set_wide_first): narrow, the wide grid, or the
     # 2.8k-slot mid table (then the wide grid for what overflows it)
@@ -861,6 +874,8 @@ class Frontier:
         if self.retry_blocks == 0:
             if st["overflowed"] > 0:
                 self.set_retry(min(self.RETRY_BLOCKS, self.B))
+                if self.CONTINUATION_REGIONS > 0:
+                    self.set_continuation(self.CONTINUATION_REGIONS)
                 if over:
                     self.set_wide_first(self.FIRST_MID)
                 return True
@@ -872,15 +887,11 @@ class Frontier:
         return False
 
     def stats(self, stream=None) -> dict:
-        """Work counters of the last run (synchronous).  `corrupt_keys` is present only in
-        debug builds (-DEGR_FR_GUARDS), where the kernel checks every member key it walks."""
+        """Work counters of the last run (synchronous)."""
         out = np.zeros(9, np.int64)
         L.check(L.lib.egr_frontier_stats(self._h, _addr(out), self._st(stream)),
                 "egr_frontier_stats")
-        d = dict(zip(self.STATS, out.tolist()))
-        if d["corrupt_keys"] < 0:
-            del d["corrupt_keys"]
-        return d
+        return dict(zip(self.STATS, out.tolist()))
 
     def phase_times(self, stream=None) -> np.ndarray | None:
         """[B, 40, 1 + waves] s_memrealtime stamps (100 MHz): per phase boundary the stamp

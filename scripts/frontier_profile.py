@@ -46,6 +46,23 @@ def main():
         bench.step_frontier(ctx, args.hops)
     torch.cuda.synchronize()
     raw = ctx["frontier"].phase_times()
+    cont = np.nonzero(raw[:, 39, 0] > 0)[0]     # columns finished in a continuation region
+    if len(cont):
+        # their first stamp was moved to slot 38 (run_column restamped the phases)
+        t0 = np.where(raw[:, 39, 0] > 0, raw[:, 38, 0], raw[:, 0, 0]).astype(np.float64)
+        base = t0.min()
+        cs, ce = raw[cont, 39, 0].astype(np.float64), raw[cont, 39, 1].astype(np.float64)
+        ends = raw[:, :20, 0].max(1).astype(np.float64)
+        span = (np.maximum(ends.max(), ce.max()) - base) / 100.0
+        st = (t0[cont] - base) / 100.0
+        print(f"continued columns: {len(cont)}; start (us after the first column) p50 "
+              f"{np.percentile(st, 50):.1f} max {st.max():.1f}; narrow attempt mean "
+              f"{((cs - t0[cont]) / 100.0).mean():.1f} us; continuation mean "
+              f"{((ce - cs) / 100.0).mean():.1f} max {((ce - cs) / 100.0).max():.1f} us; last "
+              f"continuation end {(ce.max() - base) / 100.0:.1f} us of a {span:.1f}-us launch; "
+              f"members p50 {np.percentile(raw[cont, 20, 0], 50):.0f} max {raw[cont, 20, 0].max()}")
+        raw = raw.copy()
+        raw[cont, 0, 0] = raw[cont, 38, 0]
     members = raw[:, 20, 0].astype(np.int64)
     full = raw.astype(np.float64) * 10.0 / 1000.0   # -> us
     full[:, 20, 0] = 0

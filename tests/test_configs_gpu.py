@@ -211,12 +211,13 @@ def test_bench_headline_launch_m20():
     """The exact launch the headline times (bench.py --steps 20 --warmup 5, the driver's run):
     bench.setup("C3", B=1024, merge=20) -- 20 DIFFERENT incident sets, 20,480 columns in one
     launch, the locality layout, the launch order computed on the device -- warmed up as main()
-    does (bench.warm_up: eager steps, Frontier.adapt() switching the wide-table retry on for the
-    columns that overflow the 7-per-CU narrow table, then HIP-graph capture and replays), then
+    does (bench.warm_up: eager steps, Frontier.adapt() switching the overflow handling on for the
+    columns that overflow the 7-per-CU narrow table -- continuation regions, the wide retry
+    behind them -- then HIP-graph capture and replays), then
     replayed once more with poisoned outputs.  Every one of the 20,480 columns' top-k ids and
     score bytes equals orc_frontier's on the same merged input, the rules over all 20 batches'
     rows equal orc_rules_eval's, and some columns did overflow the narrow table and were
-    re-run by the wide retry (none reached the global-memory variant)."""
+    finished in continuation regions inside the grid (none reached the global-memory variant)."""
     import bench
     saved = bench.GROUPED
     bench.GROUPED = "device"
@@ -241,6 +242,8 @@ def test_bench_headline_launch_m20():
         st = fr.stats()
         assert st["overflowed"] > 0, "the headline launch retries its overflowing columns"
         assert st["global_columns"] == 0
+        if fr.CONTINUATION_REGIONS > 0:      # ... each finished in its own workgroup, in a region
+            assert fr.continuation_regions > 0 and st["continued"] == st["overflowed"], st
         g = ctx["graph"]
         csr = g.csr()
         vl, _, _, _ = g.export()

@@ -36,6 +36,9 @@ class _Probe(Frontier):
         self.calls.append(("first", int(mode)))
         self.wide_first = int(mode)
 
+    def set_continuation(self, regions: int) -> None:
+        self.calls.append(("continuation", regions))
+
 
 def _st(overflowed: int) -> dict:
     return {"overflowed": overflowed}
@@ -50,10 +53,13 @@ def test_no_overflow_keeps_narrow():
 def test_few_overflows_retry_only():
     f = _Probe(1024)
     assert f.adapt(_st(115))                         # C3: ~0.5 % of the columns
-    assert f.calls == [("retry", min(f.RETRY_BLOCKS, 1024))]
+    # (overflowing columns continue in global-memory regions inside the grid, unless switched off)
+    assert f.calls == [("retry", min(f.RETRY_BLOCKS, 1024))] + (
+        [("continuation", f.CONTINUATION_REGIONS)] if f.CONTINUATION_REGIONS > 0 else [])
     assert f.wide_first == f.FIRST_NARROW
+    n = len(f.calls)
     assert not f.adapt(_st(1000))                    # settled: no second look in narrow mode
-    assert len(f.calls) == 1
+    assert len(f.calls) == n
 
 
 def test_most_overflow_mid_first_then_kept():

@@ -70,7 +70,8 @@ def _check(g, sv, sc, ss, src, B, hops=3, k=10, exclude=None, pool_entries=0, sc
                                  order=_dev(order))
     np.testing.assert_array_equal(g_ids.cpu().numpy().view(np.uint32), e_ids)
     assert g_sc.cpu().numpy().tobytes() == e_sc.tobytes()
-    assert fr.stats().get("corrupt_keys", 0) == 0     # counted in debug (guard) builds only
+    st = fr.stats()
+    assert 0 <= st["continued"] <= st["overflowed"]
     if scores:
         assert fr.read_scores().cpu().numpy().tobytes() == exp.tobytes()     # bit-identical
         np.testing.assert_array_equal(fr.read_reach().cpu().numpy().view(np.uint64), er)
@@ -153,33 +154,47 @@ def test_frontier_overflow_fallback_mixed():
 
 
 @pytest.mark.parametrize("mode", ["pool", "pruned", "pruned_wide_retry", "narrow_unpruned",
-                                  "retry_grid_7", "retry_grid_7_big_hubs"])
+                                  "retry_grid_7", "retry_grid_7_big_hubs", "continue_64",
+                                  "continue_64_big_hubs", "continue_5"])
 def test_frontier_global_table_reuse(mode, monkeypatch):
     """More overflowing columns than global-variant workgroups (32): each workgroup reuses its
     table across columns and must leave it clean (wide table with a pool, narrow table pruned,
     the same with the wide-table retry on its default 512-block grid, narrow table with pruning
     switched off).  retry_grid_7: the wide retry on a 7-block persistent grid, so each block
     takes ~21 of the 150 hub columns in turn (its LDS table reused); _big_hubs: hubs past the
-    wide table's 4608 members, so the retry hands every one of them on to the global variant."""
+    wide table's 4608 members, so the retry hands every one of them on to the global variant.
+    continue_64: the retry on with 64 continuation regions -- each of the first 64 overflowing
+    hub columns finishes in its own workgroup, in a global-memory region, the rest go to the
+    global variant; the runs repeat, so every region is reused from the state its last column
+    left; _big_hubs: ~6000 members per hub column, at a region's 6144-member limit;
+    continue_5: 5 regions, most hub columns find none left."""
     if mode == "narrow_unpruned":
         monkeypatch.setenv("EGRAPH_FRONTIER_NO_PRUNE", "1")
     if mode == "pruned_wide_retry":
         monkeypatch.setenv("EGRAPH_FRONTIER_WIDE_RETRY", "1")
     # retry_grid_7: ~2000 members per hub column (over the narrow table's 1152, within the
     # wide 4608); otherwise ~6000 (past both LDS tables)
-    leaves = 1000 if mode == "retry_grid_7" else 3000
+    leaves = 1000 if mode in ("retry_grid_7", "continue_64", "continue_5") else 3000
     g, sv, sc, ss, src = _hub_world(n_leaves=leaves, n_cols=300)   # 150 hub columns
-    if mode.startswith("retry_grid"):
+    if mode.startswith(("retry_grid", "continue")):
         from egraph.graph import Frontier
         real_run = Frontier.run
 
         def run(self, *a, **kw):                    # the retry switched on before the run
             self.set_retry(7)
+            self.set_continuation(int(mode.split("_")[1]) if mode.startswith("continue") else 0)
             return real_run(self, *a, **kw)
         monkeypatch.setattr(Frontier, "run", run)
     fr = _check(g, sv, sc, ss, src, len(src), k=10, pool_entries=0 if mode == "pool" else -1,
                 scores=mode == "pool")
-    assert fr.stats()["overflowed"] >= 33
+    st = fr.stats()
+    assert st["overflowed"] >= 33
+    if mode == "continue_64":
+        assert st["continued"] == 64 and st["global_columns"] == st["overflowed"] - 64, st
+    if mode == "continue_5":
+        assert st["continued"] == 5 and st["global_columns"] == st["overflowed"] - 5, st
+    if mode == "continue_64_big_hubs":       # (each column ends in a region or the global variant)
+        assert st["continued"] + st["global_columns"] == st["overflowed"], st
 
 
 def test_frontier_edge_inputs():
