@@ -266,6 +266,9 @@ def set_lane_seeds(lane: dict, seeds: tuple, B: int, snap, dev, row_ptr=None) ->
             lane["order"] = torch.from_numpy(launch_order(gp, gv, rp).view(np.int32)).to(dev)
 
 
+GRAPH_MERGE_MAX = 8      # eager launches from this many batches per launch up (main())
+
+
 def warm_up(ctx, hops: int, warmup: int, dev, rank: int = 0, engine: str = "frontier",
             graphs: bool = True):
     """The untimed part of a run, as main() does it: `warmup` eager steps (at least one per lane
@@ -1299,8 +1302,12 @@ def main():
     ap.add_argument("--storm-keep-evidence", action="store_true",
                     help="A/B: the engine keeps every incident's evidence rows (no release)")
     ap.add_argument("--no-graph", action="store_true",
-                    help="frontier: enqueue each batch eagerly instead of replaying the lane's "
-                         "captured HIP graph")
+                    help="frontier: enqueue each launch eagerly instead of replaying the lane's "
+                         "captured HIP graph (the default from --merge 8 up: five kernel launches "
+                         "per M batches cost less than a graph launch, -1.5 %% per step at M=20, "
+                         "profiles/r05_ab_graph_eager.txt)")
+    ap.add_argument("--graph", action="store_true",
+                    help="frontier: replay captured HIP graphs at any --merge (A/B)")
     ap.add_argument("--seed-input", default="grouped", choices=["grouped", "grouped-host-order", "sort"],
                     help="grouped: seeds grouped by incident as resident input, launch order on "
                          "the device per step (egr_frontier_run_grouped); grouped-host-order: the "
@@ -1360,7 +1367,9 @@ def main():
                 merge=max(1, args.merge) if args.engine == "frontier" else 1,
                 replicate=args.replicate_batches)
     M = ctx["merge"]
-    graphs = args.engine == "frontier" and not args.no_graph
+    # captured graphs pay off while a launch carries few batches; at M >= 8 the eager launch's
+    # five kernel launches are cheaper than hipGraphLaunch (profiles/r05_ab_graph_eager.txt)
+    graphs = args.engine == "frontier" and not args.no_graph and (args.graph or M < GRAPH_MERGE_MAX)
     run_step = warm_up(ctx, args.hops, args.warmup, dev, rank,
                        engine=args.engine, graphs=graphs)
 

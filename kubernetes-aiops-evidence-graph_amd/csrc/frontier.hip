@@ -418,11 +418,14 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
 // the sum over its seeds of 1 + the seed vertex's degree (the predictor set_seeds sorts by;
 // original ids, canonical row_ptr).  Order within a bucket is arbitrary -- results do not depend
 // on the order.  Two many-block kernels (one block with a serial histogram was 128 us at 40k
-// columns): the first computes 64 columns per block (4 lanes per column), ranks them inside the
-// block with LDS atomics and claims each bucket's block total with ONE global atomic on the
-// histogram `ghist` (zeroed by clear_counters_kernel ahead of it); the second scans the 64-bucket
-// histogram in one wave per block and scatters each column to its slot.
-__global__ __launch_bounds__(256) void grouped_cost_kernel(const uint32_t* __restrict__ seed_ptr,
+// columns): the first computes 64 columns per block (16 lanes per column: C3's ~74 seeds per
+// column are ~5 rounds of two dependent loads, not ~19 at 4 lanes -- 12.6 us per 20k-column
+// launch), ranks them inside the block with LDS atomics and claims each bucket's block total
+// with ONE global atomic on the histogram `ghist` (zeroed by clear_counters_kernel ahead of it;
+// 64 columns per block keep those atomics few); the second scans the 64-bucket histogram in one
+// wave per block and scatters each column to its slot.
+constexpr int COST_LANES = 16, COST_T = 64 * COST_LANES;
+__global__ __launch_bounds__(COST_T) void grouped_cost_kernel(const uint32_t* __restrict__ seed_ptr,
                                                           const uint32_t* __restrict__ seed_v,
                                                           uint32_t n_seeds, int B,
                                                           const uint32_t* __restrict__ row_ptr,
@@ -431,19 +434,19 @@ __global__ __launch_bounds__(256) void grouped_cost_kernel(const uint32_t* __res
                                                           uint32_t* __restrict__ ghist) {
   __shared__ uint32_t hist[COST_BUCKETS];
   __shared__ uint32_t base[COST_BUCKETS];
-  const int tid = threadIdx.x, q = tid & 3;
-  const int c = (int)(blockIdx.x * 64 + (tid >> 2));
+  const int tid = threadIdx.x, q = tid & (COST_LANES - 1);
+  const int c = (int)(blockIdx.x * 64 + tid / COST_LANES);
   if (tid < COST_BUCKETS) hist[tid] = 0;
   uint32_t sum = 0;
   if (c < B) {
     const uint32_t s0 = min(seed_ptr[c], n_seeds), s1 = max(s0, min(seed_ptr[c + 1], n_seeds));
-    for (uint32_t i = s0 + q; i < s1; i += 4) {
+    for (uint32_t i = s0 + q; i < s1; i += COST_LANES) {
       const uint32_t v = seed_v[i];
       if (v < V) sum += 1u + row_ptr[v + 1] - row_ptr[v];
     }
   }
-  sum += __shfl_xor(sum, 1, 64);
-  sum += __shfl_xor(sum, 2, 64);
+#pragma unroll
+  for (int o = 1; o < COST_LANES; o <<= 1) sum += __shfl_xor(sum, o, 64);
   __syncthreads();
   const int bk = cost_bucket(sum);
   uint32_t lpos = 0;
@@ -761,7 +764,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     uint32_t* gbk = f->gcost;
     uint32_t* gpos = f->gcost + f->B;
     uint32_t* ghist = f->gcost + 2 * (size_t)f->B;
-    hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 63) / 64)), dim3(256), 0, st,
+    hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 63) / 64)), dim3(COST_T), 0, st,
                        seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, gbk,
                        gpos, ghist);
     hipLaunchKernelGGL(cost_order_kernel, dim3((unsigned)((f->B + 255) / 256)), dim3(256), 0, st,

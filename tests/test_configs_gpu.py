@@ -213,8 +213,8 @@ def test_bench_headline_launch_m20():
     launch, the locality layout, the launch order computed on the device -- warmed up as main()
     does (bench.warm_up: eager steps, Frontier.adapt() switching the overflow handling on for the
     columns that overflow the 7-per-CU narrow table -- continuation regions, the wide retry
-    behind them -- then HIP-graph capture and replays), then
-    replayed once more with poisoned outputs.  Every one of the 20,480 columns' top-k ids and
+    behind them -- then, at M = 20, eager launches: main() captures HIP graphs only below
+    bench.GRAPH_MERGE_MAX batches per launch), then launched once more with poisoned outputs.  Every one of the 20,480 columns' top-k ids and
     score bytes equals orc_frontier's on the same merged input, the rules over all 20 batches'
     rows equal orc_rules_eval's, and some columns did overflow the narrow table and were
     finished in continuation regions inside the grid (none reached the global-memory variant)."""
@@ -226,8 +226,9 @@ def test_bench_headline_launch_m20():
         B, k, hops, M = 1024, 10, 3, 20
         ctx = bench.setup("C3", B, k, 0, dev, pool_entries=-1, merge=M)
         assert ctx["distinct_batches"] == M and ctx["merge"] == M
-        step = bench.warm_up(ctx, hops, 5, dev)
-        assert step is bench.step_graph
+        graphs = M < bench.GRAPH_MERGE_MAX          # (as main(): eager launches at M = 20)
+        step = bench.warm_up(ctx, hops, 5, dev, graphs=graphs)
+        assert step is (bench.step_graph if graphs else bench.step_frontier)
         lane = ctx["lanes"][0]
         fr = lane["frontier"]
         assert fr.retry_blocks > 0 and fr.wide_first == fr.FIRST_NARROW, "C3 runs narrow + retry"
@@ -236,8 +237,8 @@ def test_bench_headline_launch_m20():
         lane["rules"].mask.fill_(-7)
         torch.cuda.synchronize()
         ctx["sub"] = 0
-        for _ in range(M):                  # one timed-region's worth: a single replay of M batches
-            bench.step_graph(ctx, hops)
+        for _ in range(M):                  # one timed-region's worth: a single launch of M batches
+            step(ctx, hops)
         torch.cuda.synchronize()
         st = fr.stats()
         assert st["overflowed"] > 0, "the headline launch retries its overflowing columns"
