@@ -342,35 +342,44 @@ def step_frontier(ctx, hops: int, ev=None):
 
 
 def lane_step(lane, hops: int, inc_label: int, ev=None, fork_join: bool = False):
-    """One batch on one lane (the current stream): rules on the lane's side stream, then the
-    seed preparation and the frontier run.  fork_join (graph capture): the side stream forks
-    from the current stream and joins it again after the frontier launch."""
+    """One batch on one lane (the current stream): the rules on the lane's side stream, then the
+    seed preparation and the frontier run.  Eager: launched with stream handles, not stream
+    contexts (those cost ~40 us of host time ahead of the frontier's chain,
+    profiles/r05_timeline_eager.txt); the rules kernel runs while the host enqueues that chain
+    -- enqueued after it instead, it shares the CUs with the frontier kernel and slows it more
+    than it saves.  fork_join (graph capture): the side stream forks from the current stream
+    and joins it again after the frontier launch."""
     fr = lane["frontier"]
     side = lane["side"]
     cur = torch.cuda.current_stream()
-    if side is not None:
-        if fork_join:
+    st = cur.cuda_stream
+    if fork_join:
+        if side is not None:
             side.wait_stream(cur)
-        with torch.cuda.stream(side):
+            with torch.cuda.stream(side):
+                lane["rules"].launch()
+        else:
             lane["rules"].launch()
     else:
-        lane["rules"].launch()
+        lane["rules"].launch(side.cuda_stream if side is not None else st)
+
     def run():
         if "grouped" in lane:
-            fr.run_grouped(*lane["grouped"], lane["sources"], hops, inc_label, order=lane["order"])
+            fr.run_grouped(*lane["grouped"], lane["sources"], hops, inc_label, order=lane["order"],
+                           stream=st)
         else:
-            fr.run(lane["sources"], hops, inc_label)
+            fr.run(lane["sources"], hops, inc_label, stream=st)
     if "grouped" not in lane:
-        fr.set_seeds(*lane["seeds"])
+        fr.set_seeds(*lane["seeds"], stream=st)
     if ev is not None:
         a, b = ev.pop()
-        a.record()
+        a.record(cur)
         run()
-        b.record()
+        b.record(cur)
         ev.done.append((a, b))
     else:
         run()
-    if side is not None and fork_join:
+    if fork_join and side is not None:
         cur.wait_stream(side)
 
 
@@ -429,6 +438,12 @@ class EventPool(list):
         super().__init__((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                          for _ in range(n))
         self.done: list = []
+        # (torch creates an event's HIP event at its first record: do that here, not in the
+        # timed region)
+        for a, b in self:
+            a.record()
+            b.record()
+        torch.cuda.synchronize()
 
 
 def step(ctx, hops: int, ev=None):

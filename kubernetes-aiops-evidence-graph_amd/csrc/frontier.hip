@@ -137,6 +137,7 @@ struct FArgs {
   unsigned long long* cont_ctr;
   uint32_t cont_n;
   uint8_t* cont_base;
+  uint32_t* ghist;              // the grouped cost histogram: zeroed by the run's last kernel
 };
 
 struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
@@ -317,12 +318,10 @@ __device__ __forceinline__ SeedRun seed_run(const uint32_t* __restrict__ sv,
 
 // A run's pool / stats counters and overflow-list heads cleared in one launch (one graph node
 // instead of two fill nodes in a captured replay: each node costs its own dispatch gap).
-__global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf,
-                                                          uint32_t* ghist) {
+__global__ __launch_bounds__(64) void clear_counters_kernel(unsigned long long* ctr, uint32_t* ovf) {
   const int tid = threadIdx.x;
   if (tid < 8) ctr[tid] = 0;
   if (tid < 4) ovf[tid] = 0;
-  if (ghist) ghist[tid] = 0;      // (64 threads = COST_BUCKETS)
 }
 
 // cnt[c] += seeds of column c; cost[c] += 1 + degree of each seed vertex (a cheap predictor of
@@ -421,7 +420,8 @@ __global__ __launch_bounds__(SCAN_T) void seed_scan_kernel(uint32_t* cnt, int B,
 // columns): the first computes 64 columns per block (16 lanes per column: C3's ~74 seeds per
 // column are ~5 rounds of two dependent loads, not ~19 at 4 lanes -- 12.6 us per 20k-column
 // launch), ranks them inside the block with LDS atomics and claims each bucket's block total
-// with ONE global atomic on the histogram `ghist` (zeroed by clear_counters_kernel ahead of it;
+// with ONE global atomic on the histogram `ghist` (zero at its start: the previous run's last
+// kernel cleared it;
 // 64 columns per block keep those atomics few); the second scans the 64-bucket histogram in one
 // wave per block and scatters each column to its slot.
 constexpr int COST_LANES = 16, COST_T = 64 * COST_LANES;
@@ -460,12 +460,21 @@ __global__ __launch_bounds__(COST_T) void grouped_cost_kernel(const uint32_t* __
   }
 }
 
+// (It also clears the run's counters -- block 0, ahead of the frontier kernel that counts into
+// them -- so a grouped run launches no clear_counters_kernel of its own; the histogram is
+// zeroed again by the run's last kernel, frontier_global_kernel, for the next run.  A position
+// past B, which only a histogram left dirty by an aborted run could give, is dropped.)
 __global__ __launch_bounds__(256) void cost_order_kernel(const uint32_t* __restrict__ gbk,
                                                         const uint32_t* __restrict__ gpos,
                                                         const uint32_t* __restrict__ ghist, int B,
-                                                        uint32_t* __restrict__ order) {
+                                                        uint32_t* __restrict__ order,
+                                                        unsigned long long* ctr, uint32_t* ovf) {
   __shared__ uint32_t pre[COST_BUCKETS];
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    if (tid < 8) ctr[tid] = 0;
+    if (tid < 4) ovf[tid] = 0;
+  }
   if (tid < COST_BUCKETS) {                      // exclusive scan of the histogram, one wave
     const uint32_t x = ghist[tid];
     uint32_t inc = x;
@@ -477,7 +486,10 @@ __global__ __launch_bounds__(256) void cost_order_kernel(const uint32_t* __restr
   }
   __syncthreads();
   const int c = (int)(blockIdx.x * 256 + tid);
-  if (c < B) order[pre[gbk[c]] + gpos[c]] = (uint32_t)c;
+  if (c < B) {
+    const uint32_t pos = pre[gbk[c]] + gpos[c];
+    if (pos < (uint32_t)B) order[pos] = (uint32_t)c;
+  }
 }
 
 __global__ void seed_scatter_kernel(const uint32_t* __restrict__ sv, const uint32_t* __restrict__ sc,
@@ -625,7 +637,8 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
       hipMemset(f->gneed, 0, gcap * f->nbig) != hipSuccess ||
       hipMemset(f->mem_cnt, 0xFF, (size_t)n_cols * 4) != hipSuccess ||
       hipMemset(f->seed_cnt, 0, (size_t)n_cols * 8) != hipSuccess ||
-      hipMemset(f->ctr, 0, 8 * 8) != hipSuccess) {
+      hipMemset(f->ctr, 0, 8 * 8) != hipSuccess ||
+      hipMemset(f->gcost, 0, (2 * (size_t)n_cols + 64) * 4) != hipSuccess) {
     egr_frontier_free(f);
     return egr::fail(EGR_EDEVICE, "egr_frontier_create: table init failed");
   }
@@ -733,9 +746,10 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                              int32_t hops, int32_t exclude_label, uint32_t* out_ids,
                              float* out_scores, hipStream_t st) {
   const egr_snapshot* s = f->s;
-  if (!(sorted && f->ctr_clean)) {
-    hipLaunchKernelGGL(clear_counters_kernel, dim3(1), dim3(64), 0, st, f->ctr, f->ovf,
-                       (!sorted && !order) ? f->gcost + 2 * (size_t)f->B : (uint32_t*)nullptr);
+  // (a grouped run with its order computed on the device clears its counters in
+  // cost_order_kernel: one launch fewer)
+  if (!(sorted && f->ctr_clean) && !(!sorted && !order)) {
+    hipLaunchKernelGGL(clear_counters_kernel, dim3(1), dim3(64), 0, st, f->ctr, f->ovf);
     EGR_CHECK_LAUNCH();
   }
   FArgs a{};
@@ -768,7 +782,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
                        seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, gbk,
                        gpos, ghist);
     hipLaunchKernelGGL(cost_order_kernel, dim3((unsigned)((f->B + 255) / 256)), dim3(256), 0, st,
-                       gbk, gpos, ghist, f->B, f->gorder);
+                       gbk, gpos, ghist, f->B, f->gorder, f->ctr, f->ovf);
     EGR_CHECK_LAUNCH();
   }
   a.order = sorted ? f->order : order ? order : f->gorder;
@@ -802,6 +816,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.prof = f->prof;
   if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
   a.stats = f->ctr + 1;
+  a.ghist = f->gcost + 2 * (size_t)f->B;
   bool skipped_lds = false;       // no LDS kernel ran: the set_seeds counters were not consumed
   if (getenv("EGRAPH_FRONTIER_GLOBAL_ONLY")) {
     // (a test hook: every column through the global-memory variant, as if every LDS kernel had

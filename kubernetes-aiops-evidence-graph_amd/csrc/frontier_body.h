@@ -1202,6 +1202,8 @@ void frontier_lds_retry_kernel(const FArgs A) {
 __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
   __shared__ Shared sh;
   const uint32_t tid = threadIdx.x;
+  // (every run ends with this kernel: it leaves the grouped cost histogram zero for the next)
+  if (A.ghist && blockIdx.x == 0 && tid < 64) A.ghist[tid] = 0;
   const size_t cap = A.gcap;
   Tab<true> t{A.gkeys + blockIdx.x * cap, A.gs + blockIdx.x * cap, A.gfl + blockIdx.x * cap,
               A.gneed + blockIdx.x * cap, A.gmlist + (size_t)blockIdx.x * A.V,
