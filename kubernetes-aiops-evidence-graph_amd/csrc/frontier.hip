@@ -556,6 +556,9 @@ struct egr_frontier {
   bool ran = false;
   bool cnt_clean = true;          // seed_cnt is zero in stream order (the run's kernel zeroes it)
   bool ctr_clean = false;         // ctr / ovf zeroed by the last set_seeds, no run since
+  // test hooks, read once at creation ($EGRAPH_FRONTIER_NO_PRUNE, _GLOBAL_ONLY, _WIDE_RETRY,
+  // _CONT_DRY: see frontier_run_impl) -- a run pays no environment scans
+  bool env_no_prune = false, env_global_only = false, env_wide_retry = false, env_cont_dry = false;
   int64_t last_n_seeds = -1;      // seed entries of the last grouped run (-1: the last run was
                                   // a set_seeds run; its valid count is seed_ptr[B])
   // overflow continuation regions (egr_frontier_set_continuation; cont_n = 0: off)
@@ -589,6 +592,10 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   f->B = n_cols;
   f->k = k;
   f->max_seeds = max_seeds;
+  f->env_no_prune = getenv("EGRAPH_FRONTIER_NO_PRUNE") != nullptr;
+  f->env_global_only = getenv("EGRAPH_FRONTIER_GLOBAL_ONLY") != nullptr;
+  f->env_wide_retry = getenv("EGRAPH_FRONTIER_WIDE_RETRY") != nullptr;
+  f->env_cont_dry = getenv("EGRAPH_FRONTIER_CONT_DRY") != nullptr;
   // sized with headroom so the snapshot can grow by incremental updates (egr_snapshot_update)
   const int64_t vmax = std::min<int64_t>(s->V + s->V / 4 + 4096, (int64_t)EGR_NO_NODE - 1);
   f->vmax = vmax;
@@ -765,7 +772,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.k = f->k;
   a.exclude = exclude_label;
   // ($EGRAPH_FRONTIER_NO_PRUNE: every member exact in a top-k run too -- a test hook)
-  a.prune = (f->pool_cap == 0 && !getenv("EGRAPH_FRONTIER_NO_PRUNE")) ? 1 : 0;
+  a.prune = (f->pool_cap == 0 && !f->env_no_prune) ? 1 : 0;
   a.seed_ptr = seed_ptr;
   a.seed_vert = seed_v;
   a.seed_val = seed_s;
@@ -818,7 +825,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.stats = f->ctr + 1;
   a.ghist = f->gcost + 2 * (size_t)f->B;
   bool skipped_lds = false;       // no LDS kernel ran: the set_seeds counters were not consumed
-  if (getenv("EGRAPH_FRONTIER_GLOBAL_ONLY")) {
+  if (f->env_global_only) {
     // (a test hook: every column through the global-memory variant, as if every LDS kernel had
     // handed it on)
     a.ovf_list = const_cast<uint32_t*>(a.order);
@@ -836,7 +843,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     an.ovf_n = f->ovf + 2;
     an.ovf_list = f->ovf + 4 + f->B;
     const int32_t rb = f->retry_blocks >= 0 ? f->retry_blocks
-                       : getenv("EGRAPH_FRONTIER_WIDE_RETRY") ? RETRY_BLOCKS : 0;
+                       : f->env_wide_retry ? RETRY_BLOCKS : 0;
     an.ovf_cap = rb > 0 ? (uint32_t)f->B : 0u;     // every overflowing column gets the retry
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
     if (f->first == 2 && rb > 0) {
@@ -868,7 +875,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
       ac.cont_ctr = f->ctr + 7;
       // ($EGRAPH_FRONTIER_CONT_DRY: the continuation kernel with no region -- a test hook that
       // prices its code against the plain kernel's)
-      ac.cont_n = getenv("EGRAPH_FRONTIER_CONT_DRY") ? 0u : f->cont_n;
+      ac.cont_n = f->env_cont_dry ? 0u : f->cont_n;
       ac.cont_base = f->cont_base;
       hipLaunchKernelGGL(fr_narrow::frontier_lds_kernel<true>, dim3(f->B), dim3(fr_narrow::FT), 0, st, ac);
       EGR_CHECK_LAUNCH();

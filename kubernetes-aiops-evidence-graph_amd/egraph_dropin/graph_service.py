@@ -35,6 +35,7 @@ import torch
 
 from egraph import ops
 from egraph._lib import pyhost
+from egraph.batcher import gc_paused
 from egraph.device import to_device
 from egraph.graph import EvidenceGraph
 from egraph.seeds import seeds_for_batch
@@ -171,6 +172,14 @@ class GraphService:
 
     @classmethod
     def _rank_locked(cls, incident_ids, evidence_lists, hops, k, stages=None):
+        # (the cyclic GC deferred while the call builds its seed arrays and ~k entity dicts per
+        # incident: collections triggered by those allocations traverse the whole heap -- the
+        # graph's and the callers' evidence objects -- and find nothing to free)
+        with gc_paused():
+            return cls._rank_body(incident_ids, evidence_lists, hops, k, stages)
+
+    @classmethod
+    def _rank_body(cls, incident_ids, evidence_lists, hops, k, stages=None):
         g = cls.graph()
         if g.num_vertices == 0:
             return [[] for _ in incident_ids]
