@@ -58,6 +58,7 @@ XGMI_LINK_GBS = 153.0          # one xGMI link, GB/s (MI355X_MICROARCH.md)
 # The JSON also carries the projection at 10 and 60 us.
 RCCL_COLL_LATENCY_US = 30.0
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0   # MI355X_MICROARCH.md: the eight XCD L2s together, ~34.5 TB/s
 # --merge default cap: a launch costs ~0.12 ms of tail + ~0.055 ms per C3 batch (0.0734 / 0.0653 /
 # 0.0626 ms per batch at 8 / 16 / 24 batches, profiles/r03_ab_merge_schedule.txt).  The M batches
 # of a launch are M different incident sets, all open in the graph (M x B incidents): 20 sets
@@ -863,6 +864,12 @@ def frontier_roofline(ctx, run_ms: float, B: int, k: int, step_ms: float) -> tup
                              "write requests, profiles/pmc_frontier_calibrated*.json; counts "
                              "Infinity-Cache hits (C3 CSR resident there): upper bound on HBM bytes",
              "avg_launch_ms": run_ms, "algorithmic_bytes_per_launch": nbytes,
+             # the same bytes against the L2 roof: the C3 CSR (~5.5 MB) is re-read by every
+             # column from L2 / the Infinity Cache, so neither bandwidth binds -- the kernel is
+             # bound by dependent-load latency and issue (the stall counters in
+             # profiles/r05_pmc_*.txt)
+             "l2_roof": {"achieved": achieved, "peak": L2_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / L2_PEAK_GBS},
              # with batches in flight, launches overlap: per batch the GPU delivers nbytes
              # in one step's wall time
              "achieved_per_step": nbytes / (step_ms * 1e-3) / 1e9,

@@ -37,6 +37,7 @@ struct FrLayout {
   size_t temp_bytes = 0;
   int64_t cap_v = 0, cap_e = 0, V = 0;
   std::vector<uint32_t> order;    // internal -> original (host copy, extended by updates)
+  int64_t v_ordered = 0;          // vertices when `order` was last computed by locality_order
 };
 
 namespace {
@@ -110,6 +111,15 @@ __global__ void __launch_bounds__(256) lay_rows_kernel(const uint32_t* __restric
   out_label[i] = vlabel[o];
 }
 
+// the vertices an update appended keep their own ids: perm / iperm are the identity on [v0, V)
+__global__ void __launch_bounds__(256) lay_tail_kernel(uint32_t v0, uint32_t V, uint32_t* __restrict__ perm,
+                                                       uint32_t* __restrict__ iperm) {
+  const uint32_t i = v0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= V) return;
+  perm[i] = i;
+  iperm[i] = i;
+}
+
 inline unsigned lgrid(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + 255) / 256); }
 
 bool layout_enabled() {
@@ -117,12 +127,17 @@ bool layout_enabled() {
   return !(e && e[0] == '0');
 }
 
-// (re)lay the device arrays of s->lay from the canonical snapshot for lay->order (its size is V)
-int relayout(egr_snapshot* s, hipStream_t st) {
+// (re)lay the device arrays of s->lay from the canonical snapshot for lay->order (its size is V).
+// tail_from > 0: the device perm / iperm are current for [0, tail_from) and `order` only appended
+// identity entries after it (an update's new vertices) -- those are filled on the device, so the
+// call copies nothing from the host and does not wait for the stream; 0: both uploaded from
+// `order` (and the host waits for the copy of its stack buffer).
+int relayout(egr_snapshot* s, hipStream_t st, int64_t tail_from = 0) {
   FrLayout* L = s->lay;
   const int64_t V = s->V, NE = s->NE;
   int rc = EGR_OK;
   if (L->cap_v < V) {
+    tail_from = 0;                          // (new arrays: nothing on the device is current)
     const int64_t c = V + V / 4 + 1024;
     dfree(L->row_ptr);
     dfree(L->vlabel);
@@ -149,10 +164,17 @@ int relayout(egr_snapshot* s, hipStream_t st) {
     EGR_HIP(hipMemset(L->cv, 0, (size_t)(c + 2) * sizeof(uint2)));
     L->cap_e = c;
   }
-  std::vector<uint32_t> perm((size_t)V);
-  for (int64_t i = 0; i < V; ++i) perm[L->order[(size_t)i]] = (uint32_t)i;
-  EGR_HIP(hipMemcpyAsync(L->iperm, L->order.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
-  EGR_HIP(hipMemcpyAsync(L->perm, perm.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
+  const bool full = tail_from <= 0;
+  std::vector<uint32_t> perm;
+  if (full) {
+    perm.resize((size_t)V);
+    for (int64_t i = 0; i < V; ++i) perm[L->order[(size_t)i]] = (uint32_t)i;
+    EGR_HIP(hipMemcpyAsync(L->iperm, L->order.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
+    EGR_HIP(hipMemcpyAsync(L->perm, perm.data(), (size_t)V * 4, hipMemcpyHostToDevice, st));
+  } else if (tail_from < V) {
+    hipLaunchKernelGGL(lay_tail_kernel, dim3(lgrid(V - tail_from)), dim3(256), 0, st,
+                       (uint32_t)tail_from, (uint32_t)V, L->perm, L->iperm);
+  }
   hipLaunchKernelGGL(lay_deg_kernel, dim3(lgrid(V + 1)), dim3(256), 0, st, s->row_ptr, L->iperm,
                      (uint32_t)V, L->deg);
   size_t tb = L->temp_bytes;
@@ -160,7 +182,7 @@ int relayout(egr_snapshot* s, hipStream_t st) {
   hipLaunchKernelGGL(lay_rows_kernel, dim3(lgrid(V)), dim3(256), 0, st, s->row_ptr, s->cv, s->vlabel,
                      L->iperm, L->perm, L->row_ptr, (uint32_t)V, L->cv, L->vlabel);
   EGR_CHECK_LAUNCH();
-  EGR_HIP(hipStreamSynchronize(st));        // (perm lives on the host stack until here)
+  if (full) EGR_HIP(hipStreamSynchronize(st));   // (perm lives on the host stack until here)
   L->V = V;
   return EGR_OK;
 }
@@ -184,6 +206,7 @@ int layout_build(egr_snapshot* s, const uint32_t* row_ptr_host, const uint32_t* 
   try {
     if (!s->lay) s->lay = new FrLayout();
     s->lay->order = locality_order(row_ptr_host, col_host, s->V);
+    s->lay->v_ordered = s->V;
     rc = relayout(s, nullptr);
   } catch (const std::bad_alloc&) {
     rc = EGR_ENOMEM;
@@ -192,14 +215,30 @@ int layout_build(egr_snapshot* s, const uint32_t* row_ptr_host, const uint32_t* 
   return EGR_OK;
 }
 
+// After an update: the new vertices go after the old ones with their own ids (the device fills
+// that tail, nothing is copied from the host and the host does not wait), every row re-laid on
+// the device (the rows' offsets moved).  Appended vertices are not placed by locality, so once
+// the graph has grown by a quarter since the order was computed, the order is recomputed from
+// the current CSR (one column download) and uploaded whole.
 int layout_extend(egr_snapshot* s, hipStream_t st) {
   if (!s->lay) return EGR_OK;
   DeviceGuard guard(s->device);
   int rc = EGR_ENOMEM;
   try {
     FrLayout* L = s->lay;
-    for (int64_t v = (int64_t)L->order.size(); v < s->V; ++v) L->order.push_back((uint32_t)v);
-    rc = relayout(s, st);
+    const int64_t v0 = (int64_t)L->order.size();
+    if (s->V - L->v_ordered > L->v_ordered / 4 && (int64_t)s->row_ptr_host.size() == s->V + 1) {
+      std::vector<uint32_t> col((size_t)s->NE);
+      EGR_HIP(hipStreamSynchronize(st));
+      if (s->NE > 0)
+        EGR_HIP(hipMemcpy(col.data(), s->col, (size_t)s->NE * 4, hipMemcpyDeviceToHost));
+      L->order = locality_order(s->row_ptr_host.data(), col.data(), s->V);
+      L->v_ordered = s->V;
+      rc = relayout(s, st);
+    } else {
+      for (int64_t v = v0; v < s->V; ++v) L->order.push_back((uint32_t)v);
+      rc = relayout(s, st, v0 > 0 ? v0 : 0);
+    }
   } catch (const std::bad_alloc&) {
     rc = EGR_ENOMEM;
   }

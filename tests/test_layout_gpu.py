@@ -72,16 +72,22 @@ def test_layout_equals_canonical_and_oracle(monkeypatch, pool):
         assert torch.equal(fa.read_reach(), fb.read_reach())
 
 
-def test_layout_follows_snapshot_updates(monkeypatch):
+@pytest.mark.parametrize("per", [20, 300])
+def test_layout_follows_snapshot_updates(monkeypatch, per):
     """After incremental updates (new incidents, vertices and edges MERGEd on the host and synced
-    to the device) the laid-out frontier still equals a fresh snapshot and the oracle."""
+    to the device) the laid-out frontier still equals a fresh snapshot and the oracle.  per=20:
+    the new vertices are appended to the order (their perm / iperm filled on the device);
+    per=300: the graph grows by more than a quarter, so the update recomputes the locality order
+    from the current CSR and uploads it whole."""
     from egraph import synth
-    c, g, cases, sv, sc, ss, src = _world(pods=3000, B=64, seed=41)
+    # (per=300: a small cluster, so its incidents' new vertices are more than a quarter of it)
+    c, g, cases, sv, sc, ss, src = _world(pods=3000 if per == 20 else 300, B=64, seed=41)
     inc = g.labels().index("Incident")
     snap = _snap(g, monkeypatch, True)
-    more = synth.make_incidents(c, 40, seed=99)
+    v_start = g.num_vertices
+    more = synth.make_incidents(c, 2 * per, seed=99)
     for j in range(2):
-        part = more[20 * j: 20 * j + 20]
+        part = more[per * j: per * j + per]
         for case in part:
             g.merge_nodes([e["id"] for e in case.entities], [e["type"] for e in case.entities])
             g.merge_edges([r["source_id"] for r in case.relations],
@@ -89,7 +95,9 @@ def test_layout_follows_snapshot_updates(monkeypatch):
                           [r["relation_type"] for r in case.relations])
         nv, ne = snap.sync(g)
         assert nv > 0 and ne > 0
-        allc = cases + more[: 20 * j + 20]
+        allc = cases + more[: per * j + per]
+        if per == 300 and j == 0:
+            assert g.num_vertices > 1.25 * v_start, "the re-order path needs a quarter's growth"
         sv2, sc2, ss2 = synth.seeds_for_batch(g, [x.evidence for x in allc])
         src2 = g.lookup([f"incident:{x.incident['id']}" for x in allc]).astype(np.uint32)
         _, ia, sa = _run(snap, sv2, sc2, ss2, src2, inc)
