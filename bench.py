@@ -334,25 +334,24 @@ def step_frontier(ctx, hops: int, ev=None):
         return None
     lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]
     ctx["tick"] += 1
-    if lane["main"] is None:
-        lane_step(lane, hops, ctx["inc_label"], ev)
-    else:
-        with torch.cuda.stream(lane["main"]):
-            lane_step(lane, hops, ctx["inc_label"], ev)
+    # (the lane's stream by handle: no stream context to enter and leave)
+    lane_step(lane, hops, ctx["inc_label"], ev, cur=lane["main"])
     return lane
 
 
-def lane_step(lane, hops: int, inc_label: int, ev=None, fork_join: bool = False):
+def lane_step(lane, hops: int, inc_label: int, ev=None, fork_join: bool = False, cur=None):
     """One batch on one lane (the current stream): the rules on the lane's side stream, then the
     seed preparation and the frontier run.  Eager: launched with stream handles, not stream
     contexts (those cost ~40 us of host time ahead of the frontier's chain,
     profiles/r05_timeline_eager.txt); the rules kernel runs while the host enqueues that chain
     -- enqueued after it instead, it shares the CUs with the frontier kernel and slows it more
-    than it saves.  fork_join (graph capture): the side stream forks from the current stream
+    than it saves, with the frontier on a high-priority stream and the rules on a low-priority
+    one too (profiles/r05_ab_rules_last.txt).  fork_join (graph capture): the side stream forks from the current stream
     and joins it again after the frontier launch."""
     fr = lane["frontier"]
     side = lane["side"]
-    cur = torch.cuda.current_stream()
+    if cur is None:
+        cur = torch.cuda.current_stream()
     st = cur.cuda_stream
     if fork_join:
         if side is not None:
