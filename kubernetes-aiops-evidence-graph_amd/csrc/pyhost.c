@@ -2581,6 +2581,12 @@ static PyObject* entity_rows(PyObject* self, PyObject* args) {
   /* (the cyclic GC deferred while ~3 objects per entity are created, as the hypothesis
    * assembly does: collections triggered by them traverse the caller's whole heap) */
   const int gc_was = PyGC_Disable();
+  /* the id strings are scattered over the heap (one per graph vertex) and each entity takes a
+   * reference to one: their headers are prefetched PF entities ahead, so the cache misses of
+   * the reference counts overlap instead of queueing one by one */
+  enum { PF = 16 };
+  for (Py_ssize_t j = 0; j < PF && j < n; ++j)
+    if (ids[j] < (uint32_t)NV) __builtin_prefetch(PyList_GET_ITEM(vids, ids[j]), 1, 0);
   for (Py_ssize_t b = 0; b < B; ++b) {
     Py_ssize_t m = 0;
     while (m < k && ids[b * k + m] != NO_NODE) ++m;
@@ -2588,6 +2594,8 @@ static PyObject* entity_rows(PyObject* self, PyObject* args) {
     if (!row) goto fail;
     PyList_SET_ITEM(out, b, row);
     for (Py_ssize_t r = 0; r < m; ++r) {
+      const Py_ssize_t jp = b * k + r + PF;
+      if (jp < n && ids[jp] < (uint32_t)NV) __builtin_prefetch(PyList_GET_ITEM(vids, ids[jp]), 1, 0);
       const uint32_t v = ids[b * k + r];
       const uint8_t l = lab[b * k + r];
       if ((Py_ssize_t)v >= NV || (Py_ssize_t)l >= NL) {
