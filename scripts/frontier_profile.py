@@ -113,6 +113,34 @@ def main():
     end = t[:, used - 1] - t[:, 0].min()
     print(f"column total: mean {total.mean():.1f} p50 {np.percentile(total, 50):.1f} "
           f"max {total.max():.1f} us; starts span {start.max():.1f} us; last end {end.max():.1f} us")
+    # the grid's drain: column slots busy over time (a slot = one resident workgroup; the
+    # narrow geometry holds 7 per CU), and how well the launch order predicted the durations
+    slots = 7 * torch.cuda.get_device_properties(dev).multi_processor_count
+    mk = end.max()
+    busy = total.sum() / (slots * mk)
+    last_start = start.max()
+    order = ctx["lanes"][0]["order"] if ctx["lanes"][0].get("order") is not None else None
+    pos = np.empty(len(start), np.int64)
+    pos[np.argsort(start, kind="stable")] = np.arange(len(start))
+    q10 = np.percentile(end, [90, 99])
+    tail_cols = total[start >= np.percentile(start, 95)]
+    rk = np.corrcoef(pos, np.argsort(np.argsort(-total)))[0, 1]
+    print(f"drain: slot occupancy {busy:.3f} over a {mk:.1f}-us makespan ({slots} slots); the "
+          f"last column starts at {last_start:.1f} us ({mk - last_start:.1f} us before the end); "
+          f"90 / 99 % of columns ended by {q10[0]:.1f} / {q10[1]:.1f} us; the last 5 % of starts "
+          f"last {tail_cols.mean():.1f} us (all {total.mean():.1f}); rank correlation of start "
+          f"order with duration order {rk:.3f}")
+    hist = np.histogram(end, bins=20, range=(0, mk))[0]
+    running = [int(((start <= x) & (end > x)).sum()) for x in np.linspace(0, mk, 41)[1:-1]]
+    print("columns running at 2.5 % steps of the makespan:", running)
+    rep["drain"] = {"slot_occupancy": float(busy), "makespan_us": float(mk),
+                    "last_start_us": float(last_start), "running": running,
+                    "ends_hist": hist.tolist(), "order_rank_corr": float(rk)}
+    del order
+    if args.out:
+        # per column (index = column id): start / duration (us) and members, for offline
+        # predictor studies (scripts/launch_order_study.py)
+        np.savez(Path(args.out).with_suffix(".npz"), start=start, total=total, members=members)
     rep["column_total"] = {"mean_us": float(total.mean()), "max_us": float(total.max())}
     rep["start_span_us"] = float(start.max())
     rep["makespan_us"] = float(end.max())
