@@ -1,0 +1,98 @@
+"""Where the drop-in's concurrent single calls spend their time (GPU box; diagnostic).
+
+The bench's pattern (bench.py dropin_rules `concurrent`): 1024 incidents, each its own
+generate_hypotheses + HypothesisRanker.rank call, all in flight at once.  The batcher's stages
+are wrapped with wall-clock accumulators -- the coalesced encode, the launch call, the wait for
+the results, the assembly and delivery -- and what is left of the round is the per-call Python
+(tasks, coroutines, futures, the ranker's fused reuse).
+  python scripts/concurrent_stages.py [n_incidents]
+"""
+import asyncio
+import gc
+import sys
+import time
+from pathlib import Path
+from types import SimpleNamespace
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "kubernetes-aiops-evidence-graph_amd")]
+
+from egraph import batcher as B  # noqa: E402
+
+ACC: dict = {}
+
+
+def timed(name, fn):
+    def w(*a, **k):
+        t = time.perf_counter()
+        try:
+            return fn(*a, **k)
+        finally:
+            ACC[name] = ACC.get(name, 0.0) + time.perf_counter() - t
+    return w
+
+
+def timed_async(name, fn):
+    async def w(*a, **k):
+        t = time.perf_counter()
+        try:
+            return await fn(*a, **k)
+        finally:
+            ACC[name] = ACC.get(name, 0.0) + time.perf_counter() - t
+    return w
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    from egraph import synth
+    from src.services.rca import rules_engine as RE
+    from src.services.rca.hypothesis_ranker import HypothesisRanker
+    B.encode_batch = timed("encode", B.encode_batch)
+    B.RulesRunner.launch = timed("launch call", B.RulesRunner.launch)
+    B.RulesRunner.run = timed_async("run (launch + wait)", B.RulesRunner.run)
+    # the wait's parts: the loop turn after the launch, then the event polls
+    _sleep = asyncio.sleep
+
+    async def sleep(d, *a):
+        t = time.perf_counter()
+        try:
+            return await _sleep(d, *a)
+        finally:
+            ACC["loop turns in run"] = ACC.get("loop turns in run", 0.0) + time.perf_counter() - t
+            ACC["loop turns (count)"] = ACC.get("loop turns (count)", 0) + 1e-3
+    B.asyncio = SimpleNamespace(**{k: getattr(asyncio, k) for k in dir(asyncio) if not k.startswith("__")})
+    B.asyncio.sleep = sleep
+    B.RulesRunner.results = timed("results copy", B.RulesRunner.results)
+    B.RulesBatcher._finish = timed("assemble + deliver", B.RulesBatcher._finish)
+    cl = synth.build_cluster(synth.CONFIGS["C3"])
+    cases = synth.make_incidents(cl, n, seed=1000)
+    ev = [x.evidence for x in cases]
+    incs = [SimpleNamespace(id=f"inc-{i}") for i in range(n)]
+    eng = RE.RulesEngine()
+    ranker = HypothesisRanker()
+
+    async def one(i):
+        return ranker.rank(await eng.generate_hypotheses(incs[i], ev[i]))
+
+    async def rounds(k):
+        ts = []
+        for _ in range(k):
+            gc.collect()
+            ACC.clear()
+            t0 = time.perf_counter()
+            await asyncio.gather(*[one(i) for i in range(n)])
+            ts.append((time.perf_counter() - t0, dict(ACC)))
+        return ts
+
+    asyncio.run(rounds(1))
+    ts = asyncio.run(rounds(5))
+    t, acc = min(ts, key=lambda x: x[0])
+    print(f"{n} concurrent calls: best {t * 1e3:.2f} ms -> {n / t:,.0f} incidents/s")
+    for k, v in acc.items():
+        print(f"  {k:>22}: {v * 1e3:7.3f} ms")
+    rest = t - acc.get("encode", 0) - acc.get("run (launch + wait)", 0) - acc.get("assemble + deliver", 0)
+    print(f"  {'the rest (per-call)':>22}: {rest * 1e3:7.3f} ms ({rest / n * 1e6:.2f} us per call)")
+
+
+if __name__ == "__main__":
+    main()
