@@ -394,6 +394,15 @@ class RulesBatcher:
         self.queue.append(call)
         return await call.fut
 
+    def queued(self, incident_id, evidence: list[dict], ranked: bool) -> asyncio.Future:
+        """submit()'s path while a launch runs, as a plain call: the future of a call queued for
+        the next launch (the caller awaits it -- one coroutine frame fewer per concurrent call
+        than awaiting submit()).  Only while self.busy."""
+        self.calls += 1
+        fut = asyncio.get_running_loop().create_future()
+        self.queue.append(_Call([str(incident_id)], [evidence], ranked, fut, True))
+        return fut
+
     async def _single_idle(self, incident_id: str, evidence: list[dict], ranked: bool) -> list[dict]:
         """An idle batcher's lone call, run in the caller's task with no queue entry, future or
         second task: encode (raising what the reference raises, to this caller only), the
@@ -551,6 +560,12 @@ class RulesBatcher:
             lists = hypothesis_lists(self.cat, sub, ids, eids, ranked)
             if not ranked:             # the kernel ranked them too: HypothesisRanker.rank reuses it
                 FUSED.register(self.cat, sub, lists, range(len(lists)))
+            if len(ids) == len(cs):    # (every call one incident: concurrent single calls)
+                for c, lst in zip(cs, lists):
+                    f = c.fut
+                    if not f.done():
+                        f.set_result(lst if c.single else [lst])
+                continue
             pos = 0
             for c in cs:
                 n = len(c.incident_ids)

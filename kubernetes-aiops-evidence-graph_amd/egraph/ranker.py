@@ -167,8 +167,8 @@ class FusedRanks:
         """Rank `hyps` from its record if it is exactly a registered list; else None."""
         if not hyps or not isinstance(hyps[0], dict):
             return None
-        with self.lock:
-            rec = self.recs.get(hyps[0].get("id"))
+        # (one C-level get: atomic under the GIL against register()'s locked updates)
+        rec = self.recs.get(hyps[0].get("id"))
         if rec is None or len(hyps) != len(rec[0]):
             self.misses += 1
             return None

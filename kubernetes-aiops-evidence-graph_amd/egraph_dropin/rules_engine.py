@@ -97,7 +97,10 @@ class RulesEngine:
 
     async def generate_hypotheses(self, incident, evidence: list[dict]) -> list[dict]:
         """Generate hypotheses by matching evidence against rules (rules_engine.py:199-233)."""
-        return await _batcher(self.catalog, self.device).submit(incident.id, evidence, False)
+        b = _batcher(self.catalog, self.device)
+        # (a launch in flight: the call joins the next one through its future directly)
+        return await (b.queued(incident.id, evidence, False) if b.busy
+                      else b.submit(incident.id, evidence, False))
 
     async def generate_hypotheses_batch(self, incidents: list, evidence_lists: list[list[dict]]
                                         ) -> list[list[dict]]:
