@@ -156,7 +156,14 @@ int egr_rules_eval_small(const egr_rule_table* table, const uint32_t* row_flags,
  * device-wide synchronize waits for it meanwhile).  One
  * incident in flight per server; post() refuses (EGR_ESTATE) while one is pending.  Same
  * outputs as egr_rules_eval, bit for bit (the same per-incident device code).  The drop-in's
- * idle generate_hypotheses calls (activities.py:124-170, one incident per activity). */
+ * idle generate_hypotheses calls (activities.py:124-170, one incident per activity).
+ * Contract: a handle is single-caller -- post() and poll() from one thread at a time (its
+ * sequence number is a plain counter).  The wave clears its `alive` word as it leaves with no
+ * handshake: a post() or poll() that races that exit can queue one redundant wave behind the
+ * leaving one (it idles ~2 ms and leaves) -- a wasted launch, never a wrong or lost answer,
+ * since every wave starts from the last acknowledged request.  A request that is never
+ * acknowledged (a wave that faulted) leaves post() refusing with EGR_ESTATE: the caller bounds
+ * its wait on poll() and replaces the handle (egraph/batcher.py: _ServerWait, 5 s). */
 typedef struct egr_rules_server egr_rules_server;
 int egr_rules_server_create(const egr_rule_table* table, int32_t device, egr_rules_server** out);
 int egr_rules_server_post(egr_rules_server* s, const uint32_t* row_flags, const uint32_t* row_vocab,

@@ -69,6 +69,7 @@ constexpr uint8_t FL_DEPTH = 0x3F;          // fl: depth + 1 in the low bits
 constexpr uint8_t FL_SEED = 0x40;           // the member is one of the column's seeds
 constexpr uint8_t FL_CLAIM = 0x80;          // a seed entry already represents this vertex
 constexpr uint8_t NEED_EXCL = 0x80;         // need: a candidate carrying the excluded label
+constexpr uint8_t NEED_REC = 0x04;          // need: the member's row slots are recorded (FR_REC)
 constexpr int MAX_HOPS = 60;
 constexpr int PROF_SLOTS = 40;
 // a continuation region (egr_frontier_set_continuation): 8192 slots (2048 four-slot buckets),
@@ -138,6 +139,8 @@ struct FArgs {
   uint32_t cont_n;
   uint8_t* cont_base;
   uint32_t* ghist;              // the grouped cost histogram: zeroed by the run's last kernel
+  uint16_t* rec;                // [B][REC_STRIDE] row slot records of the narrow table (FR_REC;
+                                // nullptr: off)
 };
 
 struct alignas(8) Pair2 { uint32_t c0, v0, c1, v1; };   // two CSR entries, 8-B aligned
@@ -189,6 +192,13 @@ namespace fr_narrow {
 #define FR_LMAX 12
 #define FR_FIND_SELECT 0
 #define FR_HEAD 4
+// row slot records (frontier_body.h, FR_REC): measured and off -- with mixed walks a wave still
+// runs the probe code for its unrecorded rows, VALU fell 6.4 % and the launch 0.3 %, behind the
+// plain kernel's registers (profiles/r06_ab_row_records.txt); -DEGR_FR_NARROW_REC=1 builds it
+#ifndef EGR_FR_NARROW_REC
+#define EGR_FR_NARROW_REC 0
+#endif
+#define FR_REC EGR_FR_NARROW_REC
 #include "frontier_body.h"
 #undef FR_FT
 #undef FR_LCAP
@@ -462,8 +472,10 @@ __global__ __launch_bounds__(COST_T) void grouped_cost_kernel(const uint32_t* __
 
 // (It also clears the run's counters -- block 0, ahead of the frontier kernel that counts into
 // them -- so a grouped run launches no clear_counters_kernel of its own; the histogram is
-// zeroed again by the run's last kernel, frontier_global_kernel, for the next run.  A position
-// past B, which only a histogram left dirty by an aborted run could give, is dropped.)
+// zeroed again by the run's last kernel, frontier_global_kernel, for the next run; a run that
+// returned before enqueueing that kernel leaves egr_frontier::ghist_dirty set and the next
+// grouped run clears the histogram first.  A position past B cannot occur then; it is dropped
+// rather than written out of bounds.)
 __global__ __launch_bounds__(256) void cost_order_kernel(const uint32_t* __restrict__ gbk,
                                                         const uint32_t* __restrict__ gpos,
                                                         const uint32_t* __restrict__ ghist, int B,
@@ -559,11 +571,19 @@ struct egr_frontier {
   // test hooks, read once at creation ($EGRAPH_FRONTIER_NO_PRUNE, _GLOBAL_ONLY, _WIDE_RETRY,
   // _CONT_DRY: see frontier_run_impl) -- a run pays no environment scans
   bool env_no_prune = false, env_global_only = false, env_wide_retry = false, env_cont_dry = false;
+  // a grouped run's cost histogram may hold counts: set when grouped_cost_kernel is enqueued,
+  // cleared once the run's last kernel (which zeroes the histogram) is enqueued -- a run that
+  // returns between the two (a failed launch) leaves it set, and the next grouped run clears the
+  // histogram first instead of ordering its columns by stale counts
+  bool ghist_dirty = false;
   int64_t last_n_seeds = -1;      // seed entries of the last grouped run (-1: the last run was
                                   // a set_seeds run; its valid count is seed_ptr[B])
   // overflow continuation regions (egr_frontier_set_continuation; cont_n = 0: off)
   uint32_t cont_n = 0;
   uint8_t* cont_base = nullptr;
+  // the narrow table's row slot records ([B][fr_narrow::REC_STRIDE] u16; nullptr: off, e.g. a
+  // member-pool frontier or $EGRAPH_FRONTIER_NO_REC)
+  uint16_t* rec = nullptr;
 };
 
 
@@ -633,6 +653,11 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
     egr_frontier_free(f);
     return rc;
   }
+  if (fr_narrow::REC && f->narrow && !getenv("EGRAPH_FRONTIER_NO_REC") &&
+      (rc = dalloc(&f->rec, (size_t)n_cols * fr_narrow::REC_STRIDE))) {
+    egr_frontier_free(f);
+    return rc;
+  }
   if (EGR_FR_PROFILE && getenv("EGRAPH_FRONTIER_PROFILE") &&
       (rc = dalloc(&f->prof, (size_t)n_cols * PROF_SLOTS * prof_w(f)))) {
     egr_frontier_free(f);
@@ -693,6 +718,7 @@ void egr_frontier_free(egr_frontier* f) {
   dfree(f->gneed);
   dfree(f->gmlist);
   dfree(f->cont_base);
+  dfree(f->rec);
   delete f;
 }
 
@@ -785,6 +811,8 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     uint32_t* gbk = f->gcost;
     uint32_t* gpos = f->gcost + f->B;
     uint32_t* ghist = f->gcost + 2 * (size_t)f->B;
+    if (f->ghist_dirty) EGR_HIP(hipMemsetAsync(ghist, 0, COST_BUCKETS * sizeof(uint32_t), st));
+    f->ghist_dirty = true;
     hipLaunchKernelGGL(grouped_cost_kernel, dim3((unsigned)((f->B + 63) / 64)), dim3(COST_T), 0, st,
                        seed_ptr, seed_v, (uint32_t)n_seeds, f->B, s->row_ptr, (uint32_t)s->V, gbk,
                        gpos, ghist);
@@ -820,6 +848,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   a.gmlist = f->gmlist;
   a.gcap = f->gcap;
   a.lsnew = f->lsnew;
+  a.rec = f->rec;
   a.prof = f->prof;
   if (f->prof) EGR_HIP(hipMemsetAsync(f->prof, 0, (size_t)f->B * PROF_SLOTS * prof_w(f) * 8, st));
   a.stats = f->ctr + 1;
@@ -899,6 +928,7 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
   else
     hipLaunchKernelGGL(fr_fallback::frontier_global_kernel, dim3(f->nbig), dim3(fr_fallback::FT), 0, st, a);
   EGR_CHECK_LAUNCH();
+  f->ghist_dirty = false;         // (the kernel just enqueued zeroes the histogram)
   f->ran = true;
   f->ctr_clean = false;
   // the narrow / wide LDS kernels zero each column's set_seeds counters as they consume them;

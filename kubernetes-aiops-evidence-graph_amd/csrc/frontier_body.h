@@ -31,6 +31,18 @@ constexpr int MPT = (LLIMIT + FT - 1) / FT; // members per thread (top-k candida
 constexpr int PROF_W = NWAVES + 1;          // per slot: post-barrier stamp + each wave's finish
 static_assert(LCAP % FT == 0 && LLIMIT <= LCAP && NWAVES <= 8, "frontier geometry");
 constexpr int CHAIN_W = 64;                 // hub-chain / tail pair scratch per wave
+// Row slot records (FR_REC, round 6): a light row's neighbour slots, once resolved by the hash
+// probe (and the inserts of the walk that resolved them), are stored in the column's record
+// region -- LMAX u16 per member index, 0xFFFF = absent -- and every later walk of the row reads
+// them instead of probing again.  A slot never moves, so a recorded slot stays valid; an absent
+// entry is recorded only by a walk after which nothing is inserted any more (see rec_walk in
+// row_phase), so it stays absent.  Rows longer than LMAX (hubs) are probed in every walk.
+#ifndef FR_REC
+#define FR_REC 0
+#endif
+constexpr bool REC = FR_REC != 0;
+constexpr size_t REC_STRIDE = (size_t)LLIMIT * LMAX;   // u16 per column
+constexpr uint16_t REC_ABSENT = 0xFFFFu;
 
 
 // The table of one column.  keys/s/fl are indexed by slot; mlist lists the member slots in
@@ -50,6 +62,7 @@ struct Tab {
   uint32_t* ovf;    // LDS
   uint32_t* bloom;  // LDS variant: BLOOM_BITS-bit membership filter (nullptr: none)
   float2* chain;    // LDS: per-wave hub-chain / tail pair scratch [NWAVES][64]
+  uint16_t* rec;    // the column's row slot records [LLIMIT][LMAX] (nullptr: off; LDS tables only)
 
   __device__ __forceinline__ uint32_t key(uint32_t p) const { return keys[p]; }
   __device__ __forceinline__ float& sc(uint32_t p) const { return s[p]; }
@@ -307,18 +320,28 @@ __device__ __forceinline__ void set_need(const Tab<GT>& t, uint32_t q, uint32_t 
   atomicOr(reinterpret_cast<uint32_t*>(t.need) + (q >> 2), (1u << par) << ((q & 3u) * 8u));
 }
 
+// K_REC: the row's slots are recorded (read them, no probe); K_MKREC: record them in this walk
+constexpr uint32_t K_REC = 16u, K_MKREC = 32u;
+
 // Insertion side of a row entry (after its probe): q = the slot if present, else insert.
+// Returns the entry's slot after it (-1: absent and not inserted, or the table overflowed).
 template <bool GT>
-__device__ __forceinline__ void grow_entry(const Tab<GT>& t, uint32_t key, int q, uint32_t kind,
-                                           int h) {
-  if (q < 0 && (kind & (K_NOINS | K_REACH)) == K_NOINS) return;
+__device__ __forceinline__ int grow_entry(const Tab<GT>& t, uint32_t key, int q, uint32_t kind,
+                                          int h) {
+  if (q < 0 && (kind & (K_NOINS | K_REACH)) == K_NOINS) return -1;
   const int qq = q >= 0 ? q : tab_insert<GT>(t, key);
-  if (qq < 0) return;
+  if (qq < 0) return -1;
   if (kind & K_REACH) {   // walk h builds reach level h + 1 + REACH_AHEAD (fl = depth + 1)
     const uint8_t fo = t.fl[qq];
     if ((fo & FL_DEPTH) == 0) t.fl[qq] = fo | (uint8_t)(h + 2 + REACH_AHEAD);   // all write this
   }
   if (kind & K_PROP) set_need<GT>(t, (uint32_t)qq, (uint32_t)(h + 1) & 1u);
+  return qq;
+}
+
+__device__ __forceinline__ int rec_slot(uint32_t w, int hi) {   // u16 hi of a packed word
+  const uint32_t s = hi ? (w >> 16) : (w & 0xFFFFu);
+  return s == REC_ABSENT ? -1 : (int)s;
 }
 
 // Inclusive sum over the wave's 64 lanes (every lane active): DPP row shifts inside each row of
@@ -349,10 +372,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 // continues its chain in CSR order.
 template <bool GT>
 __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint32_t e0, uint32_t dl,
-                                          uint32_t kind, int h, float& acc, Ticker& tk) {
+                                          uint32_t kind, int h, float& acc, Ticker& tk, uint32_t mi) {
   constexpr int NH = FR_HEAD ? FR_HEAD : LMAX;
   static_assert(NH % LB == 0 && NH <= LMAX && LMAX - NH <= 16, "light-row head");
+  constexpr bool RC = REC && !GT;
   const uint32_t dh = min(dl, (uint32_t)NH);
+  const bool hr = RC && (kind & K_REC) && dh != 0;     // slots recorded: no probe
+  const bool mr = RC && (kind & K_MKREC) && dh != 0;   // record them in this walk
+  uint16_t* const rr = RC ? t.rec + (size_t)mi * LMAX : nullptr;
   uint32_t c[NH];
   float w[NH];
   // two entries per 16-B load (8-B aligned: gfx950 global loads need only dword alignment);
@@ -367,6 +394,13 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     c[x + 1] = ce.c1;
     w[x + 1] = __uint_as_float(ce.v1);
   }
+  // the head's recorded slots: LB u16 per 8-B word pair (record rows are LMAX * 2 B, 8-B aligned)
+  uint2 rw[NH / LB];
+#pragma unroll
+  for (int sb = 0; sb < NH / LB; ++sb) {
+    rw[sb] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (hr && (uint32_t)(sb * LB) < dh) rw[sb] = *reinterpret_cast<const uint2*>(rr + sb * LB);
+  }
   tk.tick(4);
 #pragma unroll
   for (int sb = 0; sb < NH / LB; ++sb) {
@@ -376,7 +410,16 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
 #pragma unroll
     for (int x = 0; x < LB; ++x) key[x] = c[sb * LB + x];
     int q[LB];
-    find_batch<GT, LB>(t, key, nq, q);
+    if (!RC || __any(!hr && nq != 0u)) {
+      find_batch<GT, LB>(t, key, hr ? 0u : nq, q);
+    } else {
+#pragma unroll
+      for (int x = 0; x < LB; ++x) q[x] = -1;
+    }
+    if (hr) {
+#pragma unroll
+      for (int x = 0; x < LB; ++x) q[x] = rec_slot(x < 2 ? rw[sb].x : rw[sb].y, x & 1);
+    }
     tk.tick(5);
     if (kind & K_PULL) {
       float xs[LB];
@@ -394,10 +437,18 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
 #endif
     }
     tk.tick(6);
+    int rq[LB];
+#pragma unroll
+    for (int x = 0; x < LB; ++x) rq[x] = q[x];
     if (kind & (K_REACH | K_PROP)) {
 #pragma unroll
       for (int x = 0; x < LB; ++x)
-        if ((uint32_t)x < nq) grow_entry<GT>(t, key[x], q[x], kind, h);
+        if ((uint32_t)x < nq) rq[x] = grow_entry<GT>(t, key[x], q[x], kind, h);
+    }
+    if (mr && nq != 0u) {   // the batch's slots after its inserts (-1 -> REC_ABSENT)
+      const uint32_t u0 = (uint32_t)rq[0] & 0xFFFFu, u1 = (uint32_t)rq[1] & 0xFFFFu;
+      const uint32_t u2 = (uint32_t)rq[2] & 0xFFFFu, u3 = (uint32_t)rq[3] & 0xFFFFu;
+      *reinterpret_cast<uint2*>(rr + sb * LB) = make_uint2(u0 | (u1 << 16), u2 | (u3 << 16));
     }
     tk.tick(7);
   }
@@ -427,12 +478,32 @@ __device__ __forceinline__ void light_row(const FArgs& A, const Tab<GT>& t, uint
     const uint2 ce = valid ? A.cv[oe0 + NH + (pos - ooff)] : make_uint2(0u, 0u);
     const uint32_t key1[1] = {ce.x};
     int q1[1];
-    find_batch<GT, 1>(t, key1, valid ? 1u : 0u, q1);
+    // a recorded row's tail entry: its slot from the owner's record (owner member index by
+    // shuffle), no probe
+    uint16_t* trec = nullptr;
+    bool thr = false;
+    uint32_t tslot = REC_ABSENT;
+    if constexpr (RC) {
+      const uint32_t omi = (uint32_t)__shfl((int)mi, o, 64);
+      trec = t.rec + (size_t)omi * LMAX + NH + (pos - ooff);
+      thr = valid && (okind & K_REC);
+      if (thr) tslot = *trec;
+    }
+    if (!RC || __any(valid && !thr)) {
+      find_batch<GT, 1>(t, key1, (valid && !thr) ? 1u : 0u, q1);
+    } else {
+      q1[0] = -1;
+    }
+    if (thr) q1[0] = tslot == REC_ABSENT ? -1 : (int)tslot;
     tk.tick(5);
     const bool term = q1[0] >= 0 && (okind & K_PULL);
     const float x = term ? t.sc((uint32_t)q1[0]) : 0.f;
     pr[lane] = make_float2(term ? __uint_as_float(ce.y) : 0.f, x);
-    if (valid && (okind & (K_REACH | K_PROP))) grow_entry<GT>(t, ce.x, q1[0], okind, h);
+    int tq = q1[0];
+    if (valid && (okind & (K_REACH | K_PROP))) tq = grow_entry<GT>(t, ce.x, q1[0], okind, h);
+    if constexpr (RC) {
+      if (valid && (okind & K_MKREC)) *trec = tq < 0 ? REC_ABSENT : (uint16_t)tq;
+    }
     tk.tick(7);
     wave_sync_lds();
     // each row's lane continues its chain over its positions in this window, in CSR order
@@ -550,6 +621,14 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
   };
   const uint32_t nch = (n + FT - 1) / FT;
   auto member_of = [&](uint32_t c) { return wave + NWAVES * (lane + 64u * c); };
+  // Row slot records (REC): a walk with a later walk records the light rows it walks for the
+  // first time.  Every such walk either inserts every absent entry of the rows it walks (reach
+  // rows, and expansions without K_NOINS: the record holds a slot for each entry), or is the
+  // pruned walk of hop hops - 2 (K_NOINS), after which nothing is inserted any more (its last
+  // walk pulls only, and reach level hops + 1 is never built): an absent entry it records stays
+  // absent.  The member's NEED_REC bit says the record exists (set here, read by the next walks'
+  // fetch; a hub row's bit is ignored -- hubs are never recorded).
+  const bool rec_walk = REC && !GT && t.rec != nullptr && h + 1 < A.hops;
   auto fetch = [&](uint32_t c) {
     Chunk ch{member_of(c), 0u, 0u, 0u};
     uint32_t v = 0;
@@ -558,12 +637,24 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       v = t.key(p);
       const uint8_t f = t.fl[p];
       if (reach_lvl && (f & FL_DEPTH) == reach_fl) ch.kind |= K_REACH;
+      uint32_t nd = 0;
       if constexpr (PH == SEEDS) {
         if (f & FL_SEED) ch.kind |= K_PROP | noins;
       } else {
-        const uint32_t nd = t.need[p];
+        nd = t.need[p];
         if ((((nd >> par) & 1u) || (f & FL_SEED)) && (!prune_now || is_cand(f)))
           ch.kind |= K_PULL | (prop_next ? K_PROP | noins : 0u);
+      }
+      if constexpr (REC && !GT) {
+        if (ch.kind && t.rec) {
+          if (nd & NEED_REC) {
+            ch.kind |= K_REC;
+          } else if (rec_walk) {
+            ch.kind |= K_MKREC;
+            atomicOr(reinterpret_cast<uint32_t*>(t.need) + (p >> 2),
+                     (uint32_t)NEED_REC << ((p & 3u) * 8u));
+          }
+        }
       }
     }
     if (ch.kind) {
@@ -594,7 +685,7 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
     tk.tick(0);
     const bool light = deg <= (uint32_t)LMAX;
     float acc = 0.f;
-    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk);
+    light_row<GT>(A, t, e0, light ? deg : 0u, kind, h, acc, tk, i);
     tk.tick(1);
     // hub rows, one 64-entry segment at a time across the wave; the next segment's entries (of
     // this hub, or the first of the next one) are loaded before the current one is probed
@@ -658,6 +749,16 @@ __device__ __forceinline__ void row_phase(const FArgs& A, const Tab<GT>& t, uint
       if (kind & K_PULL) t.snew[i] = acc;
     }
     tk.tick(3);
+#ifdef EGR_FR_VALU_PAD
+    {   // perturbation builds only (scripts/build_variant.sh): EGR_FR_VALU_PAD extra VALU
+        // instructions per chunk that change no result -- what a VALU instruction costs the
+        // launch (profiles/r06_ab_valu_perturbation.txt)
+      uint32_t z = (uint32_t)lane;
+#pragma unroll
+      for (int k = 0; k < EGR_FR_VALU_PAD; ++k) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(z) : "v"(lane));
+      asm volatile("" ::"v"(z));
+    }
+#endif
   }
 #if EGR_FR_PROFILE
   if (tk.on && lane == 0)
@@ -1140,7 +1241,8 @@ __device__ __forceinline__ void lds_column(const FArgs& A, int b, LdsTab& L, Sha
   }
   __syncthreads();
   Tab<false> t{L.keys, L.s, reinterpret_cast<uint8_t*>(L.flw), reinterpret_cast<uint8_t*>(L.needw),
-               L.mlist, A.lsnew + (size_t)row * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN};
+               L.mlist, A.lsnew + (size_t)row * LLIMIT, LCAP, LLIMIT, &sh.count, &sh.ovf, L.bloom, SH_CHAIN,
+               (REC && A.rec) ? A.rec + (size_t)row * REC_STRIDE : nullptr};
   if (run_column<false>(A, t, sh, b)) return;
   if (tid == 0) atomicAdd(&A.stats[4], 1ull);
   if (continue_column<CONT>(A, b, sh)) return;
@@ -1244,3 +1346,4 @@ __global__ __launch_bounds__(FT, 2) void frontier_global_kernel(const FArgs A) {
 }
 #endif
 #undef SH_CHAIN
+#undef FR_REC

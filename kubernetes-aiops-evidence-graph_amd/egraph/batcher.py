@@ -115,6 +115,14 @@ class RulesRunner:
             self._srv = None
             L.lib.egr_rules_server_free(h)
 
+    def _server_failed(self) -> None:
+        """A server request went unanswered past _ServerWait.TIMEOUT_S (its wave faulted or
+        never ran): drop the handle -- free() stops the wave, which leaves at its next poll --
+        so the next single call creates a fresh server instead of being refused forever."""
+        h, self._srv, self._srv_wait = self._srv, None, None
+        if h is not None:
+            L.lib.egr_rules_server_free(h)
+
     def _layout(self, rows: int, B: int):
         key = (rows, B)
         hit = self._layouts.get(key)
@@ -303,7 +311,10 @@ class RulesRunner:
             await asyncio.sleep(0)
         t0 = time.perf_counter()
         while not ev.query():
-            if time.perf_counter() - t0 > self.SPIN_S:
+            dt = time.perf_counter() - t0
+            if dt > self.SPIN_S:
+                if self.mode == "server" and dt > _ServerWait.TIMEOUT_S:
+                    ev.expire()                     # raises; the next call gets a new server
                 await asyncio.sleep(0)              # long launch: poll from the loop
         return self.results()
 
@@ -333,9 +344,20 @@ class _ServerWait:
             self.done = rc == 1
         return self.done
 
+    # a request unanswered this long is lost: the wave polls its mailbox every few us while
+    # resident and is relaunched when it has left, so only a faulted wave gets here
+    TIMEOUT_S = 5.0
+
     def synchronize(self) -> None:
+        t0 = time.perf_counter()
         while not self.query():
-            pass
+            if time.perf_counter() - t0 > self.TIMEOUT_S:
+                self.expire()
+
+    def expire(self) -> None:
+        self.r._server_failed()
+        raise RuntimeError(f"egr_rules_server: no answer within {self.TIMEOUT_S} s "
+                           "(the server was dropped; the next call starts a new one)")
 
     def result(self) -> RulesResult:
         S, o, b = self.r.S, self.r._srv_off, self.blk
@@ -435,7 +457,10 @@ class RulesBatcher:
     async def submit_many(self, incident_ids: list, evidence_lists: list, ranked: bool
                           ) -> list[list[dict]]:
         """Several incidents as ONE call (it raises as a whole if any row makes the
-        reference raise, as the reference's loop over them would)."""
+        reference raise, as the reference's loop over them would).  No incidents: [] at once
+        (a call with nothing to launch never joins a batch)."""
+        if not incident_ids and not evidence_lists:
+            return []
         loop = asyncio.get_running_loop()
         call = _Call([str(i) for i in incident_ids], list(evidence_lists), ranked, loop.create_future())
         self.calls += 1
@@ -560,7 +585,7 @@ class RulesBatcher:
             lists = hypothesis_lists(self.cat, sub, ids, eids, ranked)
             if not ranked:             # the kernel ranked them too: HypothesisRanker.rank reuses it
                 FUSED.register(self.cat, sub, lists, range(len(lists)))
-            if len(ids) == len(cs):    # (every call one incident: concurrent single calls)
+            if all(len(c.incident_ids) == 1 for c in cs):   # (concurrent single calls)
                 for c, lst in zip(cs, lists):
                     f = c.fut
                     if not f.done():

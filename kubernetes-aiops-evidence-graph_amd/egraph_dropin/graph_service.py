@@ -281,7 +281,11 @@ class GraphService:
     # DATETIME; strings and naive datetimes compare to null).  Neo4j leaves the order of
     # unordered rows unspecified; here it is match order: query vertices in vertex order,
     # neighbours in CSR order.
-    OWNS_MAX_DEPTH = 16     # bound on the (p)<-[:OWNS*]-(d) expansion (k8s owner chains are 1-2)
+    # The (p)<-[:OWNS*]-(d) expansion runs until no open path is left, as Cypher's unbounded
+    # variable-length match does: relationships are unique within a path, so it terminates.  A
+    # relationship is identified by its (owner, owned) vertex pair: the reference writes every
+    # relation with MERGE (source)-[r:TYPE]->(target) (neo4j.py:122, :152), so there is at most
+    # one OWNS relationship per ordered pair and pair uniqueness is relationship uniqueness.
 
     @classmethod
     def _props(cls, g, labels, vlabel, v: int) -> dict:
@@ -305,7 +309,9 @@ class GraphService:
 
     @staticmethod
     async def find_related_changes(incident_id: str, time_window_minutes: int = 30) -> list[dict]:
-        return GraphService.find_related_changes_sync(incident_id, time_window_minutes)
+        # (in a worker thread: the body takes the service lock, which a ranking call holds for
+        # its whole run, and waits on device copies -- the event loop stays free)
+        return await asyncio.to_thread(GraphService.find_related_changes_sync, incident_id, time_window_minutes)
 
     @classmethod
     def find_related_changes_sync(cls, incident_id: str, time_window_minutes: int = 30,
@@ -341,7 +347,9 @@ class GraphService:
 
     @staticmethod
     async def find_affected_by_node(node_name: str) -> list[dict]:
-        return GraphService.find_affected_by_node_sync(node_name)
+        # (in a worker thread: the body takes the service lock, which a ranking call holds for
+        # its whole run, and waits on device copies -- the event loop stays free)
+        return await asyncio.to_thread(GraphService.find_affected_by_node_sync, node_name)
 
     @classmethod
     def find_affected_by_node_sync(cls, node_name: str) -> list[dict]:
@@ -366,9 +374,7 @@ class GraphService:
             # is (its pod, its vertices' chain); relationships stay unique within a path
             paths = [(i, (p,)) for i, p in enumerate(pods)]
             found: list[list[tuple]] = [[] for _ in pods]   # per pod: (path vertices) ending at d
-            for _ in range(cls.OWNS_MAX_DEPTH):
-                if not paths or t_owns < 0:
-                    break
+            while paths and t_owns >= 0:
                 nb = snap.typed_neighbors([pv[-1] for _, pv in paths], t_owns, snap.IN)
                 nxt = []
                 for (i, pv), owners in zip(paths, nb):
@@ -401,7 +407,9 @@ class GraphService:
 
     @staticmethod
     async def get_service_dependencies(service_name: str, namespace: str) -> dict:
-        return GraphService.get_service_dependencies_sync(service_name, namespace)
+        # (in a worker thread: the body takes the service lock, which a ranking call holds for
+        # its whole run, and waits on device copies -- the event loop stays free)
+        return await asyncio.to_thread(GraphService.get_service_dependencies_sync, service_name, namespace)
 
     @classmethod
     def get_service_dependencies_sync(cls, service_name: str, namespace: str) -> dict:
@@ -431,7 +439,8 @@ class GraphService:
     @staticmethod
     async def get_incident_graph(incident_id: str, depth: int = 3,
                                  resolve_bare_uuid: bool = False) -> dict:
-        return GraphService.get_incident_graphs([incident_id], depth, resolve_bare_uuid)[0]
+        return (await asyncio.to_thread(GraphService.get_incident_graphs, [incident_id], depth,
+                                        resolve_bare_uuid))[0]
 
     @classmethod
     def get_incident_graphs(cls, incident_ids: list[str], depth: int = 3,

@@ -21,7 +21,9 @@ from __future__ import annotations
 
 import datetime as _dt
 
-OWNS_MAX_DEPTH = 16       # (the drop-in bounds the OWNS* expansion the same way)
+# OWNS* is expanded without a depth bound, as Cypher does: relationships are unique within a
+# path (one relationship per ordered vertex pair and type -- the reference MERGEs them), so the
+# expansion ends.
 
 
 def _props(labels, ids, props, v):
@@ -77,8 +79,6 @@ def affected_by_node(labels, ids, edges, props, node_name):
             stack = [(p, frozenset(), 0)]
             while stack:
                 cur, used, depth = stack.pop()
-                if depth >= OWNS_MAX_DEPTH:
-                    continue
                 nxt = []
                 for u in inn.get((cur, "OWNS"), []):
                     if (u, cur) in used:

@@ -139,6 +139,42 @@ def test_concurrent_calls_coalesce_and_match_golden(golden):
         assert record(hyps) == golden_record(case["expected"]), case["name"]
 
 
+def test_coalesced_batch_calls_of_mixed_sizes(golden):
+    """Batch calls coalesced into one launch -- an empty one, two-incident ones, single
+    incidents -- each get their own lists: the one-incident-per-call delivery is taken only when
+    every call holds one incident (an empty call beside a two-incident call also sums to one
+    incident per call)."""
+    import rca_oracle
+    from src.services.rca import rules_engine as RE
+    eng = RE.RulesEngine()
+    cases = golden["rules"]["cases"][:9]
+
+    def strip(hs):
+        return [{k: v for k, v in h.items() if k != "id"} for h in hs]
+
+    async def go():
+        b = RE._batcher(eng.catalog, eng.device)
+        first = asyncio.ensure_future(eng.generate_hypotheses(_Inc("a"), cases[0]["evidence"]))
+        await asyncio.sleep(0)            # `first` has launched: the next calls coalesce
+        assert b.busy
+        calls = [eng.generate_hypotheses_batch([], []),
+                 eng.generate_hypotheses_batch([_Inc("a")] * 2, [cases[1]["evidence"], cases[2]["evidence"]]),
+                 eng.generate_hypotheses(_Inc("a"), cases[3]["evidence"]),
+                 eng.generate_hypotheses_batch([], []),
+                 eng.generate_hypotheses_batch([_Inc("a")] * 2, [cases[4]["evidence"], cases[5]["evidence"]]),
+                 eng.generate_hypotheses_batch([_Inc("a")], [cases[6]["evidence"]])]
+        return await first, await asyncio.gather(*calls)
+
+    first, (e0, two1, one, e1, two2, one1) = asyncio.run(go())
+    exp = [rca_oracle.generate("a", c["evidence"]) for c in cases]
+    assert strip(first) == exp[0]
+    assert e0 == [] and e1 == []
+    assert [strip(x) for x in two1] == exp[1:3]
+    assert strip(one) == exp[3]
+    assert [strip(x) for x in two2] == exp[4:6]
+    assert len(one1) == 1 and strip(one1[0]) == exp[6]
+
+
 def test_error_raises_in_its_own_call_only(golden):
     from src.services.rca import rules_engine as RE
     eng = RE.RulesEngine()

@@ -79,6 +79,69 @@ def test_typed_queries_known_answer():
         GS.reset()
 
 
+def test_owner_chain_depth_and_cycle():
+    """(p)<-[:OWNS*]-(d:Deployment) has no depth bound: an owner chain 24 levels deep (past the
+    old bound of 16) reaches its Deployment, and an OWNS cycle ends by relationship uniqueness."""
+    E = [("node:n", "Node", {"name": "n"}), ("pod:ns:p", "Pod", {"name": "p"}),
+         ("pod:ns:q", "Pod", {"name": "q"}), ("deployment:ns:deep", "Deployment", {"name": "deep"}),
+         ("deployment:ns:c1", "Deployment", {"name": "c1"}), ("replicaset:ns:c2", "ReplicaSet", {})]
+    R = [("pod:ns:p", "node:n", "SCHEDULED_ON"), ("pod:ns:q", "node:n", "SCHEDULED_ON")]
+    prev = "pod:ns:p"
+    for j in range(23):
+        E.append((f"owner:ns:o{j}", "ReplicaSet", {}))
+        R.append((f"owner:ns:o{j}", prev, "OWNS"))
+        prev = f"owner:ns:o{j}"
+    R.append(("deployment:ns:deep", prev, "OWNS"))
+    # q <- c2 <- c1 <- c2 (a cycle through c1, a Deployment)
+    R += [("replicaset:ns:c2", "pod:ns:q", "OWNS"), ("deployment:ns:c1", "replicaset:ns:c2", "OWNS"),
+          ("replicaset:ns:c2", "deployment:ns:c1", "OWNS")]
+    GS = _load(E, R)
+    try:
+        got = asyncio.run(GS.find_affected_by_node("n"))
+        assert {(r["pod"]["name"], r["deployment"]["name"]) for r in got} == {("p", "deep"), ("q", "c1")}
+        _check_all(GS, [], ["n"], [])
+    finally:
+        GS.reset()
+
+
+def test_typed_query_leaves_the_event_loop_free():
+    """A typed query waits for the service lock (held here by another thread, as a ranking call
+    holds it for its whole run) in a worker thread: the event loop keeps running other tasks."""
+    import threading
+    import time
+    E, R, _ = known_answer_world()
+    GS = _load(E, R)
+    try:
+        GS.find_affected_by_node_sync("node-a")          # (snapshot built outside the timing)
+        held = threading.Event()
+
+        def holder():
+            with GS._lock:
+                held.set()
+                time.sleep(0.4)
+        th = threading.Thread(target=holder)
+        th.start()
+        held.wait()
+
+        async def go():
+            ticks = 0
+
+            async def ticker():
+                nonlocal ticks
+                while True:
+                    await asyncio.sleep(0.01)
+                    ticks += 1
+            t = asyncio.ensure_future(ticker())
+            rows = await GS.find_affected_by_node("node-a")
+            t.cancel()
+            return rows, ticks
+        rows, ticks = asyncio.run(go())
+        th.join()
+        assert rows and ticks >= 10
+    finally:
+        GS.reset()
+
+
 def _with_props(cl, rng, n_changes: int, incidents: list[str]):
     """A synthetic cluster's vertices as the collectors would write them: Nodes with `name`,
     Services / Pods / Deployments with `name` + `namespace` (parsed from the id scheme), plus
