@@ -901,7 +901,7 @@ class _TimedPlan:
     def __getattr__(self, name):
         return getattr(self._p, name)
 
-    def _timed(self, fn, *a, tail: bool = False):
+    def _timed(self, fn, *a, tail: bool = False, what: str = ""):
         if self._part is None:
             return fn(*a)
         x, y = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -914,7 +914,7 @@ class _TimedPlan:
         side = shard._SIDE.get(torch.cuda.current_device())
         chain = "tail" if tail else ("side" if side is not None and torch.cuda.current_stream() == side
                                      else "main")
-        self._part.append((x, y, chain))
+        self._part.append((x, y, chain, what or getattr(fn, "__name__", "?")))
         return r
 
     def hop(self):
@@ -940,16 +940,16 @@ class _TimedPlan:
     # the halo exchange's own device work (pack before, unpack after the transfer) runs on the
     # partition's GPU too: counted in its compute (the pack's host read of the peer sizes included)
     def pack_sparse(self, *a, **k):
-        return self._timed(lambda: self._p.pack_sparse(*a, **k))
+        return self._timed(lambda: self._p.pack_sparse(*a, **k), what="pack_sparse")
 
     def unpack_sparse(self, *a, **k):
-        return self._timed(lambda: self._p.unpack_sparse(*a, **k))
+        return self._timed(lambda: self._p.unpack_sparse(*a, **k), what="unpack_sparse")
 
     def pack_sparse_cap(self, *a, **k):
-        return self._timed(lambda: self._p.pack_sparse_cap(*a, **k))
+        return self._timed(lambda: self._p.pack_sparse_cap(*a, **k), what="pack_sparse_cap")
 
     def unpack_sparse_cap(self, *a, **k):
-        return self._timed(lambda: self._p.unpack_sparse_cap(*a, **k))
+        return self._timed(lambda: self._p.unpack_sparse_cap(*a, **k), what="unpack_sparse_cap")
 
     def pack_scores(self, *a):
         return self._timed(self._p.pack_scores, *a)
@@ -1065,13 +1065,19 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
     for _ in range(3):
         shard_step(ctx, args.hops, args.k, None, parts)
     torch.cuda.synchronize(dev)
-    part_ms = [sum(a.elapsed_time(b) for a, b, _ in q) / 3 for q in parts]
+    part_ms = [sum(a.elapsed_time(b) for a, b, _, _ in q) / 3 for q in parts]
     # the critical path of a partition with the reach chain on its own stream: the longer of the
     # two chains, then the tail (what one GPU running the partition waits for, if the chains
     # overlap; the in-process ms_per_step with and without --no-overlap measures that they do)
     def chain_ms(q, c):
-        return sum(a.elapsed_time(b) for a, b, t in q if t == c) / 3
+        return sum(a.elapsed_time(b) for a, b, t, _ in q if t == c) / 3
     crit_ms = [max(chain_ms(q, "main"), chain_ms(q, "side")) + chain_ms(q, "tail") for q in parts]
+    # the slowest partition's calls by chain and kind (ms per step)
+    slow = parts[int(np.argmax(crit_ms))]
+    breakdown: dict = {}
+    for a, b, t, w in slow:
+        key = f"{t}:{w}"
+        breakdown[key] = breakdown.get(key, 0.0) + a.elapsed_time(b) / 3
     B = args.batch
     ms = elapsed / args.steps * 1e3
     hop_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -1104,6 +1110,9 @@ def shard_main(args, world: int, rank: int, dev: torch.device, dist) -> None:
             "partitions": ctx["P"], "incidents": B, "hops": args.hops, "k": args.k,
             "parallelism": f"edge-cut x{ctx['P']}" + (" (one process)" if world == 1 else ""),
             "local_vertices": [len(r.lg.gid) for r in ctx["runs"]],
+            "owned_vertices": [int(r.lg.n_owned) for r in ctx["runs"]],
+            "halo_over_owned": [round(len(r.lg.halo_rows) / max(r.lg.n_owned, 1), 3) for r in ctx["runs"]],
+            "slowest_partition_breakdown_ms": {k: round(v, 4) for k, v in sorted(breakdown.items())},
             "halo_bytes_per_hop_max_rank": halo,
             "halo_exchange": "dense" if args.dense_halo else
                              "sparse, host-read peer counts" if args.halo_host_counts else
@@ -1493,10 +1502,65 @@ def main():
     if rank == 0 and args.engine == "frontier" and not args.no_dropin:
         out["dropin_rules"] = dropin_rules(ctx, dev)
         out["dropin_graph"] = dropin_graph(ctx, dev, args.hops, args.k)
+    if "cpu_baseline" in out:
+        reference_speedups(out)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+CALIBRATION = REPO / "profiles" / "r06_standin_calibration.json"
+
+
+def reference_speedups(out: dict) -> None:
+    """cpu_baseline.speedup_vs_reference and .end_to_end_speedup: the GPU figures over the
+    reference's own Python rules path on this host's cores.  That path cannot run here (the
+    reference does not travel to the GPU box); its pinned restatement oracle/rca_oracle.py is
+    timed instead (python_rules_path), and oracle/calibrate_standin.py measured, in the build
+    container, how much longer the real reference takes on the same C3-shaped incidents: the
+    median over interleaved pairs of rounds with a distribution-free 95 % interval
+    (profiles/r06_standin_calibration.json).  reference rate = stand-in rate / that ratio; the
+    interval of each speed-up is the ratio's interval carried through."""
+    cb = out["cpu_baseline"]
+    try:
+        cal = json.loads(CALIBRATION.read_text())
+        r = float(cal["bench_workload_ratio"])
+        lo, hi = (float(x) for x in cal["bench_workload_ratio_ci95"])
+    except (OSError, KeyError, ValueError) as e:
+        cb["speedup_vs_reference"] = {"value": None, "note": f"no calibration: {e}"}
+        return
+    py = cb["python_rules_path"]["value"]
+    ref, ref_lo, ref_hi = py / r, py / hi, py / lo       # the reference's incidents/s, interval
+    cb["reference_rules_path"] = {
+        "value": ref, "ci95": [ref_lo, ref_hi], "unit": "incidents/s", "cores": 1,
+        "derivation": f"python_rules_path {py:.0f}/s / calibration ratio {r:.4f} "
+                      f"(95 % CI {lo:.4f} .. {hi:.4f}, {CALIBRATION.name})"}
+
+    def ratio(x: float) -> dict:
+        return {"value": x / ref, "ci95": [x / ref_hi, x / ref_lo]}
+    cb["speedup_vs_reference"] = {
+        **ratio(out["value"]),
+        "what": "the headline (GPU stage on resident, pre-encoded columns: rules + 3-hop "
+                "propagation + reach + top-k per incident) over the reference's Python rules path "
+                "(dicts in, dicts out; it has no graph stage without Neo4j)"}
+    e2e: dict = {"what": "the drop-in's Python API end to end (evidence dicts in, hypothesis "
+                         "dicts out) against the reference's rules path, same host"}
+    dr = out.get("dropin_rules")
+    if dr:
+        e2e["rules_batch"] = {**ratio(dr["value"]), "what": "RulesEngine.rank_incidents_batch, 1024 "
+                                                           "incidents per call"}
+        conc = dr.get("concurrent", {}).get("value")
+        if conc:
+            e2e["concurrent_single_calls"] = {**ratio(conc), "what": "1024 concurrent "
+                                              "generate_hypotheses + rank calls"}
+        one, ref_one = dr.get("single_call_us", {}).get("p50"), dr.get("reference_single_call_us", {}).get("p50")
+        if one and ref_one:
+            # the reference's per-call time = the stand-in's measured p50 x the ratio
+            e2e["single_call_p50"] = {"value": ref_one * r / one, "ci95": [ref_one * lo / one, ref_one * hi / one],
+                                      "what": "one incident per call, idle engine (the activity's "
+                                              "pattern, activities.py:124-170): reference p50 / drop-in p50"}
+    cb["end_to_end_speedup"] = e2e
 
 
 if __name__ == "__main__":

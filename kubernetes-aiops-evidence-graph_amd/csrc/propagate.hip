@@ -115,8 +115,12 @@ struct HopArgs {
   const uint32_t* seed_tiles;
   const float* xin;
   float* xout;
-  uint8_t* nzout;     // partitioned plans: [V][ntiles] "row v's tile holds a non-zero" of xout
-  uint32_t ntiles;    // (nullptr otherwise: the flags cost nothing on the unpartitioned path)
+  uint8_t* nzout;     // [V][ntiles] per row tile of xout: its non-zero count (the sparse halo pack
+  uint32_t ntiles;    // reads only non-zero tiles; the next hop skips gathers of zero tiles)
+  // [V][ntiles] the same flags of xin (0 = the tile is all +0), read by the zero-tile skip
+  // (hop_kernel<G, false, true>); xbytes = V * TW * 4, the buffer range of one tile of xin
+  const uint8_t* nzin;
+  uint32_t xbytes;
   uint32_t V;
   uint32_t nchunks;
 };
@@ -128,16 +132,28 @@ struct Batch {
   uint32_t u[NB];
   float w[NB];
   uint32_t n;
+  uint32_t la, lb;   // the row's (live) entry range [la, lb): n = lb - la
 };
 
 // Stage a chunk's row offsets (relative to its first entry) and up to CSR_CAP column ids (and
 // values) in LDS: every global load is issued before the first LDS store.
+// With nz (the hop's input tile flags, [V][ntiles]; a chunk of at most CSR_CAP entries): each
+// staged entry's neighbour tile flag is loaded once the column ids have arrived, and the LIVE
+// entries (flag != 0: x[col][tile] may hold a non-zero) are compacted in entry order into
+// s_live, with the per-64-entry live masks s_segm and their exclusive prefix counts s_segp --
+// live_before(x) = s_segp[x / 64] + popc(s_segm[x / 64] below bit x % 64).
+constexpr uint32_t NSEG = CSR_CAP / 64;
 template <int ROWS, bool VAL>
 __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr,
                                             const uint32_t* __restrict__ col,
                                             const float* __restrict__ val, uint32_t v0,
                                             uint32_t nrows, uint32_t e0, uint32_t e1,
-                                            uint32_t* s_rp, uint32_t* s_col, float* s_val) {
+                                            uint32_t* s_rp, uint32_t* s_col, float* s_val,
+                                            const uint8_t* __restrict__ nz = nullptr,
+                                            uint32_t ntiles = 0, uint32_t tile = 0,
+                                            uint16_t* s_live = nullptr, uint64_t* s_segm = nullptr,
+                                            uint32_t* s_segp = nullptr,
+                                            const uint32_t* __restrict__ seed_tiles = nullptr) {
   constexpr int PER = CSR_CAP / 256;
   const uint32_t tid = threadIdx.x;
   const uint32_t nst = min(e1 - e0, CSR_CAP);
@@ -151,6 +167,43 @@ __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr
       const uint32_t i = min(tid + k * 256u, nst - 1u);
       cc[k] = col[e0 + i];
       if constexpr (VAL) ww[k] = val[e0 + i];
+    }
+  }
+  if (nz || seed_tiles) {
+    // (the first hop: live = the neighbour has a seed in this tile, its per-vertex tile mask)
+    uint8_t ff[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      ff[k] = tid + k * 256u >= nst ? 0
+            : nz ? nz[(size_t)cc[k] * ntiles + tile]
+                 : (uint8_t)((seed_tiles[cc[k]] >> (tile & 31u)) & 1u);
+    // entry i = tid + 256 k: wave w of pass k covers the 64 entries of segment 4 k + w
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    uint64_t mk[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      mk[k] = __ballot(ff[k] != 0);
+      if (lane == 0) s_segm[4 * k + wv] = mk[k];
+    }
+    __syncthreads();
+    if (tid < 64) {                          // exclusive prefix of the NSEG segment counts
+      uint32_t c = tid < NSEG ? (uint32_t)__popcll(s_segm[tid]) : 0u, inc = c;
+#pragma unroll
+      for (int o = 1; o < (int)NSEG; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if ((int)tid >= o) inc += y;
+      }
+      if (tid < NSEG) s_segp[tid + 1] = inc;
+      if (tid == 0) s_segp[0] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (ff[k] != 0) {
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk[k] >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mk[k], 0u));
+        s_live[s_segp[4 * k + wv] + r] = (uint16_t)(tid + k * 256u);
+      }
     }
   }
   if (tid < nrows) s_rp[tid] = rp_t - e0;
@@ -175,12 +228,22 @@ __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr
 #define EGR_HOP_XCD_REMAP 0
 #endif
 
-template <int G, bool FROM_SEEDS>
+// SKIP (not FROM_SEEDS): the zero-tile skip -- a row's fmaf chain runs over its LIVE entries
+// only, those whose neighbour tile of xin may hold a non-zero (tile flags A.nzin, compacted per
+// chunk by stage_chunk), in CSR order: a skipped entry's x are all +0 and fmaf(w, +0, acc) ==
+// acc (acc != -0), so the result is bit-identical.  A row with no live entry gathers nothing (its
+// batch loads go through a buffer descriptor at an out-of-range offset: zeros, no fetch, and the
+// loop keeps its branch-free form).  Hops 2 and 3 of a 3-hop C3 batch gather a non-zero tile
+// for 9 % / 34 % of their entries, C4 2 % / 15 % (scripts/tile_sparsity.py).
+template <int G, bool FROM_SEEDS, bool SKIP = false>
 __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
   __shared__ uint32_t s_rp[ROWS + 1];
   __shared__ uint32_t s_col[CSR_CAP];
   __shared__ float s_val[CSR_CAP];
+  __shared__ uint16_t s_live[SKIP ? CSR_CAP : 1];        // the chunk's live entries (SKIP)
+  __shared__ uint64_t s_segm[SKIP ? NSEG : 1];
+  __shared__ uint32_t s_segp[SKIP ? NSEG + 1 : 1];
   const uint32_t tid = threadIdx.x, gl = tid % G, grp = tid / G;
   const uint32_t V = A.V;
 #if EGR_HOP_XCD_REMAP
@@ -196,7 +259,11 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   const uint32_t v0 = A.chunk_start[chunk], v1 = A.chunk_start[chunk + 1];
   const uint32_t nrows = v1 - v0;
   const uint32_t e0 = A.row_ptr[v0], e1 = A.row_ptr[v1];
-  stage_chunk<ROWS, true>(A.row_ptr, A.col, A.val, v0, nrows, e0, e1, s_rp, s_col, s_val);
+  // (a lone row longer than CSR_CAP -- its own chunk -- gathers every entry)
+  const bool live_on = SKIP && e1 - e0 <= CSR_CAP;
+  stage_chunk<ROWS, true>(A.row_ptr, A.col, A.val, v0, nrows, e0, e1, s_rp, s_col, s_val,
+                          live_on && !FROM_SEEDS ? A.nzin : nullptr, A.ntiles, tile, s_live, s_segm,
+                          s_segp, live_on && FROM_SEEDS ? A.seed_tiles : nullptr);
   if (grp >= nrows) return;  // no barrier below
 
   const uint32_t lo = tile * TW + 4 * gl;  // first column of this lane
@@ -204,20 +271,52 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   const size_t toff = (size_t)tile * V * TW;
   const float4* __restrict__ X = reinterpret_cast<const float4*>(A.xin + toff);
   float4* __restrict__ Y = reinterpret_cast<float4*>(A.xout + toff);
+  // one gather of neighbour u's tile; SKIP: through a buffer descriptor, `none` = an
+  // out-of-range offset (zeros, nothing fetched)
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)(A.xin + (SKIP ? toff : 0)), 0,
+                                                    SKIP ? (int)A.xbytes : 0, 0x00020000);
+  auto gather = [&](uint32_t u, bool none) -> float4 {
+    if constexpr (SKIP) {
+      const uint32_t off = none ? 0x80000000u : (u * (uint32_t)G + gl) * 16u;
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)off, 0, 0);
+      return make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]),
+                         __uint_as_float(q[3]));
+    } else {
+      return X[(size_t)u * G + gl];
+    }
+  };
+  // live entries before staged entry x (live_on), and the entry of live index i
+  auto live_before = [&](uint32_t x) -> uint32_t {
+    const uint32_t sg = x >> 6, bt = x & 63u;
+    return s_segp[sg] + (bt ? (uint32_t)__popcll(s_segm[sg] & ((1ull << bt) - 1ull)) : 0u);
+  };
+  auto entry = [&](uint32_t i) -> uint32_t {
+    if constexpr (SKIP) return live_on ? (uint32_t)s_live[min(i, CSR_CAP - 1u)] : i;
+    return i;
+  };
 
-  // NB entries of row r; slots past the row's end repeat its last neighbour at weight 0
+  // NB (live) entries of row r; slots past the row's end repeat its last one at weight 0
   auto issue = [&](uint32_t r, Batch<FROM_SEEDS>& bt) {
     const uint32_t a = s_rp[r], b = s_rp[r + 1];
-    const uint32_t n = b - a;
+    uint32_t la = a, lb = b;
+    if constexpr (SKIP) {
+      if (live_on) {
+        la = live_before(a);
+        lb = live_before(b);
+      }
+    }
+    const uint32_t n = lb - la;
     bt.n = n;
+    bt.la = la;
+    bt.lb = lb;
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-      const uint32_t jj = a + min((uint32_t)t, n > 0u ? n - 1u : 0u);
+      const uint32_t jj = entry(la + min((uint32_t)t, n > 0u ? n - 1u : 0u));
       const uint32_t u = n > 0u ? s_col[min(jj, CSR_CAP - 1u)] : v0 + r;
       bt.u[t] = u;
       bt.w[t] = (uint32_t)t < n ? s_val[min(jj, CSR_CAP - 1u)] : 0.f;
       if constexpr (FROM_SEEDS) bt.m[t] = A.seed_tiles[u];
-      else bt.x[t] = X[(size_t)u * G + gl];
+      else bt.x[t] = gather(u, n == 0u);
     }
   };
   auto seed_gather = [&](uint32_t u, float w, float4& acc) {
@@ -243,13 +342,13 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
     // tail of rows with more than NB entries, NT gathers per batch (deployments, services,
     // Node hubs); slots past the end repeat the last entry at weight 0
     constexpr int NT = 4;
-    const uint32_t b = s_rp[r + 1];
-    for (uint32_t j = s_rp[r] + NB; j < b; j += NT) {
+    const uint32_t b = bt.lb;
+    for (uint32_t j = bt.la + NB; j < b; j += NT) {
       uint32_t u[NT];
       float w[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const uint32_t jj = min(j + t, b - 1u);
+        const uint32_t jj = entry(min(j + t, b - 1u));
         u[t] = jj < CSR_CAP ? s_col[jj] : A.col[e0 + jj];
         w[t] = j + t < b ? (jj < CSR_CAP ? s_val[jj] : A.val[e0 + jj]) : 0.f;
       }
@@ -263,7 +362,7 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       } else {
         float4 x[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) x[t] = X[(size_t)u[t] * G + gl];
+        for (int t = 0; t < NT; ++t) x[t] = gather(u[t], false);
 #pragma unroll
         for (int t = 0; t < NT; ++t) fma4(w[t], x[t], acc);
       }
@@ -278,9 +377,9 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
     Y[(size_t)v * G + gl] = acc;
 #endif
     if (A.nzout) {
-      // the row's non-zero count in this tile for the sparse halo pack (TW = 4G <= 128 columns:
-      // a byte): summed over the G lanes of the row's group (contiguous lanes, all active for
-      // the same row); -0.0 counts as non-zero, as the pack sends it
+      // the row's non-zero count in this tile -- for the sparse halo pack and the next hop's
+      // zero-tile skip (TW = 4G <= 128 columns: a byte): summed over the G lanes of the row's
+      // group (contiguous lanes, all active for the same row); -0.0 counts as non-zero
       int c = (__float_as_uint(acc.x) != 0u) + (__float_as_uint(acc.y) != 0u) +
               (__float_as_uint(acc.z) != 0u) + (__float_as_uint(acc.w) != 0u);
 #pragma unroll
@@ -738,11 +837,16 @@ __global__ void pack_scores_kernel(const float* __restrict__ X, uint32_t V, int 
 
 __global__ void unpack_scores_kernel(float* __restrict__ X, uint32_t V, int TW, int Bpad,
                                      const uint32_t* __restrict__ rows,
-                                     const uint32_t* __restrict__ src, const float* __restrict__ in) {
+                                     const uint32_t* __restrict__ src, const float* __restrict__ in,
+                                     uint8_t* __restrict__ nzf) {
   const uint32_t v = rows[blockIdx.x];
   const size_t o = (size_t)src[blockIdx.x] * Bpad;
   for (int b = threadIdx.x; b < Bpad; b += blockDim.x)
     X[((size_t)(b / TW) * V + v) * TW + (b % TW)] = in[o + b];
+  // a whole row written: every tile may hold a non-zero (the next hop gathers them all)
+  const int ntiles = Bpad / TW;
+  if (nzf)
+    for (int t = threadIdx.x; t < ntiles; t += blockDim.x) nzf[(size_t)v * ntiles + t] = 0xFF;
 }
 
 __global__ void pack_reach_kernel(const uint64_t* __restrict__ R, uint32_t RS, int W,
@@ -1199,6 +1303,7 @@ struct egr_plan {
   // since the last unpack (it clears only those, once the buffer has been zeroed in full)
   uint8_t* nzf[2] = {nullptr, nullptr};
   bool xzeroed[2] = {false, false};
+  bool skip_zero = true;             // hop_kernel's zero-tile skip ($EGRAPH_HOP_NO_SKIP=1: off)
   uint64_t* reach[2] = {nullptr, nullptr};
   int rcur = 0;
   int reach_hops = -1;  // -1: sources not set
@@ -1279,8 +1384,10 @@ std::vector<uint32_t> build_chunks(const std::vector<uint32_t>& rp, uint32_t V, 
 }
 
 template <int G>
-void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds) {
-  if (seeds) hipLaunchKernelGGL((hop_kernel<G, true>), grid, dim3(256), 0, st, a);
+void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool skip) {
+  if (seeds && skip) hipLaunchKernelGGL((hop_kernel<G, true, true>), grid, dim3(256), 0, st, a);
+  else if (seeds) hipLaunchKernelGGL((hop_kernel<G, true>), grid, dim3(256), 0, st, a);
+  else if (skip) hipLaunchKernelGGL((hop_kernel<G, false, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((hop_kernel<G, false>), grid, dim3(256), 0, st, a);
 }
 
@@ -1313,15 +1420,20 @@ int plan_hop(egr_plan* p, void* stream) {
   a.xin = seeds ? nullptr : p->x[p->xcur];
   a.xout = p->x[seeds ? 0 : 1 - p->xcur];
   a.nzout = p->nzf[seeds ? 0 : 1 - p->xcur];
+  // (the skip's buffer offsets are 32-bit: one tile of xin must span < 2 GB, V < 4.2M at TW 128)
+  // (the first hop skips by the seed tile masks, the others by xin's tile flags)
+  const bool skip = p->skip_zero && (uint64_t)s->V * p->TW * 4 < (1ull << 31);
+  a.nzin = skip && !seeds ? p->nzf[p->xcur] : nullptr;
+  a.xbytes = skip && !seeds ? (uint32_t)((uint64_t)s->V * p->TW * 4) : 0u;
   a.ntiles = (uint32_t)p->ntiles;
   a.V = (uint32_t)s->V;
   a.nchunks = p->nchunks;
   const dim3 grid(p->nchunks * p->ntiles);
   switch (p->TW) {
-    case 128: launch_hop_g<32>(a, grid, st, seeds); break;
-    case 64: launch_hop_g<16>(a, grid, st, seeds); break;
-    case 16: launch_hop_g<4>(a, grid, st, seeds); break;
-    default: launch_hop_g<1>(a, grid, st, seeds); break;
+    case 128: launch_hop_g<32>(a, grid, st, seeds, skip); break;
+    case 64: launch_hop_g<16>(a, grid, st, seeds, skip); break;
+    case 16: launch_hop_g<4>(a, grid, st, seeds, skip); break;
+    default: launch_hop_g<1>(a, grid, st, seeds, skip); break;
   }
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
@@ -1458,9 +1570,18 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
       (rc = dalloc(&p->cand_cnt, ncnt)) || (rc = dalloc(&p->cand_off, ncnt)) ||
       (rc = dalloc(&p->cand_list, p->cand_enabled ? (size_t)V * p->B : 1)) ||
       (rc = dalloc(&p->counter, 1)) || (rc = dalloc(&p->chunk_start, chunks.size())) ||
-      (rc = dalloc(&p->rchunk_start, rchunks.size()))) {
+      (rc = dalloc(&p->rchunk_start, rchunks.size())) ||
+      (rc = dalloc(&p->nzf[0], (size_t)V * p->ntiles)) || (rc = dalloc(&p->nzf[1], (size_t)V * p->ntiles))) {
     egr_plan_free(p);
     return rc;
+  }
+  p->skip_zero = getenv("EGRAPH_HOP_NO_SKIP") == nullptr;
+  // every hop writes its rows' tile flags (a hop reads only flags its predecessor wrote); zero
+  // them once so that no stale byte is ever read
+  if (hipMemset(p->nzf[0], 0, (size_t)V * p->ntiles) != hipSuccess ||
+      hipMemset(p->nzf[1], 0, (size_t)V * p->ntiles) != hipSuccess) {
+    egr_plan_free(p);
+    return egr::fail(EGR_EDEVICE, "plan flag init failed");
   }
   // the count pass never writes cand_cnt[B*NG], so the scan's last slot is the grand total
   if (hipMemcpy(p->chunk_start, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1774,13 +1895,13 @@ int egr_plan_set_owned(egr_plan* p, int64_t n_owned) {
   p->nchunks = (uint32_t)chunks.size() - 1;
   p->rnchunks = (uint32_t)rchunks.size() - 1;
   for (int b = 0; b < 2; ++b) {
+    const size_t nb = (size_t)p->s->V * p->ntiles;
     if (!p->nzf[b]) {
-      const size_t nb = (size_t)p->s->V * p->ntiles;
       const int rc = dalloc(&p->nzf[b], nb);
       if (rc != EGR_OK) return rc;
-      if (hipMemset(p->nzf[b], 0, nb) != hipSuccess)
-        return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: flag init failed");
     }
+    if (hipMemset(p->nzf[b], 0, nb) != hipSuccess)
+      return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: flag init failed");
     p->xzeroed[b] = false;
   }
   p->owned = (uint32_t)n_owned;
@@ -1810,7 +1931,7 @@ int egr_plan_unpack_scores(egr_plan* p, const uint32_t* rows, const uint32_t* sr
   p->xzeroed[p->xcur] = false;              // full halo rows written: no tile tracking
   DeviceGuard guard(p->s->device);
   hipLaunchKernelGGL(unpack_scores_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream,
-                     p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->Bpad, rows, src, in);
+                     p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->Bpad, rows, src, in, p->nzf[p->xcur]);
   EGR_CHECK_LAUNCH();
   p->cand_valid = false;
   return EGR_OK;

@@ -63,6 +63,27 @@ def test_propagation_reach_topk_equal_oracle(B):
     np.testing.assert_array_equal(scores.cpu().numpy(), e_sc)
 
 
+@pytest.mark.parametrize("B", [37, 600])
+def test_zero_tile_skip_off_is_bit_identical(B, monkeypatch):
+    """The hop's zero-tile skip (live-entry compaction by the input's tile flags, and by the
+    seed tile masks in the first hop) against the full gather ($EGRAPH_HOP_NO_SKIP=1, read at
+    plan creation): the same scores bit for bit, both equal to the oracle."""
+    g, sv, sc, ss, src = _small_world(B, seed=5, pods=1500)
+    snap = g.snapshot()
+    got = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("EGRAPH_HOP_NO_SKIP", "1")
+        plan = snap.plan(B, max_seeds=len(sv), k=5)
+        plan.set_seeds(_dev(sv), _dev(sc), _dev(ss))
+        plan.set_sources(_dev(src))
+        plan.run(hops=4)
+        got.append(plan.read_scores().cpu().numpy())
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv, sc, ss, B, 4)
+    assert got[0].tobytes() == exp.tobytes() and got[1].tobytes() == exp.tobytes()
+
+
 @pytest.mark.parametrize("tw", [4, 16, 64, 128])
 def test_tile_width_override(tw, monkeypatch):
     B = 200
