@@ -571,6 +571,10 @@ struct egr_frontier {
   // test hooks, read once at creation ($EGRAPH_FRONTIER_NO_PRUNE, _GLOBAL_ONLY, _WIDE_RETRY,
   // _CONT_DRY: see frontier_run_impl) -- a run pays no environment scans
   bool env_no_prune = false, env_global_only = false, env_wide_retry = false, env_cont_dry = false;
+  // $EGRAPH_FRONTIER_MID_CONT=1: the mid table's overflows continue in regions too (off by
+  // default: at C4 its 1,559 overflowing columns per 20-batch launch take 30 % longer that way
+  // than through the serial wide retry, profiles/r06_ab_c4_mid_continuation.txt)
+  bool env_mid_cont = false;
   // a grouped run's cost histogram may hold counts: set when grouped_cost_kernel is enqueued,
   // cleared once the run's last kernel (which zeroes the histogram) is enqueued -- a run that
   // returns between the two (a failed launch) leaves it set, and the next grouped run clears the
@@ -616,6 +620,7 @@ int egr_frontier_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds
   f->env_global_only = getenv("EGRAPH_FRONTIER_GLOBAL_ONLY") != nullptr;
   f->env_wide_retry = getenv("EGRAPH_FRONTIER_WIDE_RETRY") != nullptr;
   f->env_cont_dry = getenv("EGRAPH_FRONTIER_CONT_DRY") != nullptr;
+  f->env_mid_cont = getenv("EGRAPH_FRONTIER_MID_CONT") != nullptr;
   // sized with headroom so the snapshot can grow by incremental updates (egr_snapshot_update)
   const int64_t vmax = std::min<int64_t>(s->V + s->V / 4 + 4096, (int64_t)EGR_NO_NODE - 1);
   f->vmax = vmax;
@@ -877,8 +882,17 @@ static int frontier_run_impl(egr_frontier* f, const uint32_t* seed_ptr, const ui
     a.prof = nullptr;   // the wide kernels' stamp layout differs: only the narrow pass is profiled
     if (f->first == 2 && rb > 0) {
       // mid-first: every column in the 2.8k-slot table; what overflows it takes the wide retry
+      // -- or, with $EGRAPH_FRONTIER_MID_CONT, continues in its own workgroup in a global-memory
+      // region (as the narrow table's do), the retry taking what finds no region
       FArgs am = an;
-      hipLaunchKernelGGL(fr_mid::frontier_lds_kernel<false>, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
+      if (f->cont_n > 0 && f->env_mid_cont) {
+        am.cont_ctr = f->ctr + 7;
+        am.cont_n = f->env_cont_dry ? 0u : f->cont_n;
+        am.cont_base = f->cont_base;
+        hipLaunchKernelGGL(fr_mid::frontier_lds_kernel<true>, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
+      } else {
+        hipLaunchKernelGGL(fr_mid::frontier_lds_kernel<false>, dim3(f->B), dim3(fr_mid::FT), 0, st, am);
+      }
       EGR_CHECK_LAUNCH();
       hipLaunchKernelGGL(fr_wide::frontier_lds_retry_kernel, dim3(std::min(rb, f->B)),
                          dim3(fr_wide::FT), 0, st, a);

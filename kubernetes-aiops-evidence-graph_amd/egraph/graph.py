@@ -827,6 +827,8 @@ class Frontier:
     # (egr_frontier_set_continuation), switched on with the retry; $EGRAPH_FRONTIER_CONTINUATION
     # overrides (0 = off: the wide retry grid after the narrow one)
     CONTINUATION_REGIONS = int(os.environ.get("EGRAPH_FRONTIER_CONTINUATION", "128"))
+    MAX_CONTINUATION_REGIONS = 4096     # (egr_frontier_set_continuation's bound; 128 KB each)
+    MID_CONTINUATION = os.environ.get("EGRAPH_FRONTIER_MID_CONT") is not None
 
     def set_retry(self, blocks: int) -> None:
         """Wide-table second chance for the columns that overflow the narrow table (see
@@ -883,6 +885,13 @@ class Frontier:
         self._mid_checked = True        # (one check of a mid-first run)
         if over:
             self.set_wide_first(self.FIRST_WIDE)
+            return True
+        # ($EGRAPH_FRONTIER_MID_CONT: the mid table's overflowing columns continue in regions
+        # too -- enough for all of them, with headroom -- instead of the serial wide retry; off
+        # by default: 30 % slower at C4, profiles/r06_ab_c4_mid_continuation.txt)
+        want = min(self.MAX_CONTINUATION_REGIONS, (st["overflowed"] * 5 + 3) // 4)
+        if self.MID_CONTINUATION and self.CONTINUATION_REGIONS > 0 and want > self.continuation_regions:
+            self.set_continuation(want)
             return True
         return False
 

@@ -262,6 +262,58 @@ def test_bench_headline_launch_m20():
         bench.GROUPED = saved
 
 
+@pytest.mark.parametrize("mid_cont", [False, True])
+def test_c4_launch_m20(mid_cont, monkeypatch):
+    """C4 through the replicated frontier as bench.py --config C4 --steps 20 times it: 20
+    different incident sets in one launch of 20,480 columns, warmed up as main() does -- the
+    narrow table overflows, adapt() starts every column in the mid table, whose overflowing
+    columns take the wide retry (the default) or, with $EGRAPH_FRONTIER_MID_CONT, continue
+    inside the grid, each in a region adapt()'s second look sized for all of them (no serial
+    wide retry, no global-memory variant).  Every column's top-k ids and score bytes equal
+    orc_frontier's."""
+    import bench
+    from egraph.graph import Frontier
+    if mid_cont:
+        monkeypatch.setenv("EGRAPH_FRONTIER_MID_CONT", "1")        # (read at frontier creation)
+        monkeypatch.setattr(Frontier, "MID_CONTINUATION", True)
+    saved = bench.GROUPED
+    bench.GROUPED = "device"
+    try:
+        dev = torch.device("cuda", 0)
+        B, k, hops, M = 1024, 10, 3, 20
+        ctx = bench.setup("C4", B, k, 0, dev, pool_entries=-1, merge=M)
+        step = bench.warm_up(ctx, hops, 5, dev, graphs=M < bench.GRAPH_MERGE_MAX)
+        lane = ctx["lanes"][0]
+        fr = lane["frontier"]
+        assert fr.wide_first == fr.FIRST_MID and fr.retry_blocks > 0
+        fr.out_ids.fill_(-7)
+        fr.out_scores.fill_(float("nan"))
+        torch.cuda.synchronize()
+        ctx["sub"] = 0
+        for _ in range(M):
+            step(ctx, hops)
+        torch.cuda.synchronize()
+        st = fr.stats()
+        assert st["overflowed"] > 0 and st["global_columns"] == 0, st
+        if mid_cont:
+            assert fr.continuation_regions >= st["overflowed"] and st["continued"] == st["overflowed"], st
+        else:
+            assert st["continued"] == 0, st
+        g = ctx["graph"]
+        csr = g.csr()
+        vl, _, _, _ = g.export()
+        sv, sc, ss, src = ctx["lane_host"]
+        e_ids, e_sc = _oracle_topk(g, csr, vl, sv, sc, ss, src, k, hops)
+        ids = fr.out_ids.cpu().numpy().view(np.uint32).reshape(B * M, k)
+        sco = fr.out_scores.cpu().numpy().reshape(B * M, k)
+        for i in range(M):
+            sl = slice(i * B, (i + 1) * B)
+            np.testing.assert_array_equal(ids[sl], e_ids[sl], err_msg=f"batch {i}")
+            assert sco[sl].tobytes() == e_sc[sl].tobytes(), f"batch {i}"
+    finally:
+        bench.GROUPED = saved
+
+
 def test_c2_rules_dropin_and_frontier():
     import asyncio
     from types import SimpleNamespace
