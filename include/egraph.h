@@ -373,6 +373,20 @@ int egr_plan_pack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* rows, in
 int egr_plan_unpack_sparse_cap(egr_plan* p, int32_t what, const uint32_t* recv_vertex, int64_t n_rows,
                                const int64_t* in, int64_t peer_cap, uint32_t* overflow_dev,
                                const int64_t* rbase, int32_t P, void* stream);
+/* One whole halo exchange over an RCCL communicator, for callers that are not torch (SURVEY.md
+ * §8b's egr_halo_allgather; egraph/shard.py's TorchComm path issues the same three steps): the
+ * pack above into send_slots (P slots of 1 + peer_cap * (what ? 2 : 1) int64 words, device), ONE
+ * ncclAllToAll of the slots over xGMI into recv_slots, the unpack above -- enqueued on `stream`,
+ * no host synchronisation.  rccl_comm: an ncclComm_t of exactly P ranks (this rank's), e.g. from
+ * ncclCommInitRank; send_rows / send_seg_dev / recv_vertex / recv_base_dev as the pack / unpack
+ * above (egraph.shard.LocalGraph holds them).  *overflow_dev != 0 afterwards: a slot overflowed,
+ * re-run the pass with a larger peer_cap.  Replaces the cross-partition part of the single-host
+ * apoc.path.subgraphAll traversal (neo4j.py:169-202) for graphs split over GPUs. */
+int egr_plan_halo_exchange(egr_plan* p, int32_t what, const uint32_t* send_rows, int64_t n_send,
+                           const int64_t* send_seg_dev, int32_t P, int64_t peer_cap,
+                           int64_t* send_slots, int64_t* recv_slots, const uint32_t* recv_vertex,
+                           int64_t n_recv, const int64_t* recv_base_dev, uint32_t* overflow_dev,
+                           void* rccl_comm, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Frontier engine: the same A8 + A9 + top-k results as a plan's egr_plan_run, computed per

@@ -124,6 +124,7 @@ SIGNATURES: dict[str, tuple] = {
     "egr_plan_unpack_sparse": (C.c_int, [P, I32, P, I64, P, I64, P, P, I32, P]),
     "egr_plan_pack_sparse_cap": (C.c_int, [P, I32, P, I64, P, I32, P, I64, P, P, P]),
     "egr_plan_unpack_sparse_cap": (C.c_int, [P, I32, P, I64, P, I64, P, P, I32, P]),
+    "egr_plan_halo_exchange": (C.c_int, [P, I32, P, I64, P, I32, I64, P, P, P, I64, P, P, P, P]),
     "egr_frontier_create": (C.c_int, [P, I32, I64, I32, I64, C.POINTER(P)]),
     "egr_frontier_free": (None, [P]),
     "egr_frontier_set_seeds": (C.c_int, [P, P, P, P, I64, P]),

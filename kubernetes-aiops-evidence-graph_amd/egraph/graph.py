@@ -654,6 +654,23 @@ class Plan:
                                                  rbase.numel(), self._st(stream)),
                 "egr_plan_unpack_sparse_cap")
 
+    def halo_exchange_rccl(self, what: str, rows: torch.Tensor, seg_dev: torch.Tensor,
+                           peer_cap: int, send_slots: torch.Tensor, recv_slots: torch.Tensor,
+                           recv_vertex: torch.Tensor, rbase: torch.Tensor, overflow: torch.Tensor,
+                           rccl_comm: int, stream=None) -> None:
+        """egr_plan_halo_exchange: pack_sparse_cap, ONE ncclAllToAll of the slots over the RCCL
+        communicator `rccl_comm` (an ncclComm_t address of P ranks), unpack_sparse_cap -- the
+        C-ABI path for callers without torch.distributed (egraph/shard.py's TorchComm issues
+        the same steps through torch)."""
+        P = seg_dev.numel() - 1
+        if min(send_slots.numel(), recv_slots.numel()) < P * self.slot_words(what, peer_cap):
+            raise ValueError("halo_exchange_rccl: slot buffers too small")
+        L.check(L.lib.egr_plan_halo_exchange(self._h, 1 if what == "reach" else 0, L.ptr(rows),
+                                             rows.numel(), L.ptr(seg_dev), P, int(peer_cap),
+                                             L.ptr(send_slots), L.ptr(recv_slots), L.ptr(recv_vertex),
+                                             recv_vertex.numel(), L.ptr(rbase), L.ptr(overflow),
+                                             rccl_comm, self._st(stream)), "egr_plan_halo_exchange")
+
     def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
         n = vertex.numel()
         if not (col.numel() == n == val.numel()):
@@ -782,6 +799,23 @@ class Frontier:
 
     def _st(self, stream):
         return L.stream_handle(self.dev) if stream is None else stream
+
+    def halo_exchange_rccl(self, what: str, rows: torch.Tensor, seg_dev: torch.Tensor,
+                           peer_cap: int, send_slots: torch.Tensor, recv_slots: torch.Tensor,
+                           recv_vertex: torch.Tensor, rbase: torch.Tensor, overflow: torch.Tensor,
+                           rccl_comm: int, stream=None) -> None:
+        """egr_plan_halo_exchange: pack_sparse_cap, ONE ncclAllToAll of the slots over the RCCL
+        communicator `rccl_comm` (an ncclComm_t address of P ranks), unpack_sparse_cap -- the
+        C-ABI path for callers without torch.distributed (egraph/shard.py's TorchComm issues
+        the same steps through torch)."""
+        P = seg_dev.numel() - 1
+        if min(send_slots.numel(), recv_slots.numel()) < P * self.slot_words(what, peer_cap):
+            raise ValueError("halo_exchange_rccl: slot buffers too small")
+        L.check(L.lib.egr_plan_halo_exchange(self._h, 1 if what == "reach" else 0, L.ptr(rows),
+                                             rows.numel(), L.ptr(seg_dev), P, int(peer_cap),
+                                             L.ptr(send_slots), L.ptr(recv_slots), L.ptr(recv_vertex),
+                                             recv_vertex.numel(), L.ptr(rbase), L.ptr(overflow),
+                                             rccl_comm, self._st(stream)), "egr_plan_halo_exchange")
 
     def set_seeds(self, vertex: torch.Tensor, col: torch.Tensor, val: torch.Tensor, stream=None):
         n = vertex.numel()

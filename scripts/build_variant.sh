@@ -13,5 +13,5 @@ mkdir -p build/exp_$NAME lib/exp_$NAME
 /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
   -I../include -I$CS --offload-arch=gfx950 $FLAGS -c $CS/$FILE -o build/exp_$NAME/$FILE.o
 OBJS=$(ls build/*.o | grep -v "/$FILE.o")
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o lib/exp_$NAME/libegraph.so $OBJS build/exp_$NAME/$FILE.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o lib/exp_$NAME/libegraph.so $OBJS build/exp_$NAME/$FILE.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built lib/exp_$NAME/libegraph.so"
