@@ -130,9 +130,12 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
     from egraph.rca import RulesDeviceBatch
     t0 = time.time()
     # --merge M: the M batches of one launch are M DIFFERENT incident sets (distinct_batches);
-    # every one of them is open in the graph, so the graph holds M x B incidents.  Each rank
+    # every one of them is open in the graph, so the graph holds M x B incidents.  --pipeline P
+    # lanes: each lane's launches carry their OWN M sets (P x M distinct sets in all -- lanes
+    # in flight at once never share columns, whose common rows would meet in L2).  Each rank
     # builds its own graph with its own incident sets (per-GPU work fixed: weak scaling)
-    n_sets = merge if (merge > 1 and not replicate) else 1
+    per_lane = merge if merge > 1 else 1
+    n_sets = 1 if replicate else per_lane * max(pipeline, 1)
     g, batches = make_world(config, B, n_sets, seed0=1000 + rank * n_sets)
     evidence, sv, sc, ss, src = batches[0]
     enc = encode_batch(evidence, catalog.default())
@@ -148,32 +151,40 @@ def setup(config: str, B: int, k: int, rank: int, dev: torch.device, pipeline: i
         # seeds at its own column offset, the rules over the M batches' rows): the hardware
         # dispatcher hands the columns out costliest-first across all M batches, so batch i's
         # tail runs beside batch i+1's columns inside one launch on one stream
-        # (batch i = batches[i]; --replicate-batches (A/B only): M copies of batch 0, round 3's
-        # launch, whose adjacent copies share L2 lines)
+        # (lane l's batch i = batches[l * M + i]; --replicate-batches (A/B only): M copies of
+        # batch 0, round 3's launch, whose adjacent copies share L2 lines)
         Bm = B * merge
-        if merge > 1:
-            parts = [batches[i % n_sets] for i in range(merge)]
-            msv, msc, mss, msrc = merge_batches([p[1:] for p in parts], B)
-            lane_seeds = tuple(to_device(a, dev) for a in (msv, msc, mss))
-            lane_src = to_device(msrc, dev)
-            lane_rules = encode_batch([ev for p in parts for ev in p[0]], catalog.default())
-            lane_enc, lane_host = lane_rules, (msv, msc, mss, msrc)
-            n_seeds = len(msv)
-        else:
-            lane_seeds, lane_src, lane_rules, n_seeds = seeds, sources, rules, len(sv)
-            lane_enc, lane_host = enc, (sv, sc, ss, src)
+        lane_in = []
+        for ln in range(max(pipeline, 1)):
+            if merge > 1:
+                parts = [batches[(ln * merge + i) % n_sets] for i in range(merge)]
+                msv, msc, mss, msrc = merge_batches([p[1:] for p in parts], B)
+                lane_in.append((tuple(to_device(a, dev) for a in (msv, msc, mss)), to_device(msrc, dev),
+                                encode_batch([ev for p in parts for ev in p[0]], catalog.default()),
+                                (msv, msc, mss, msrc)))
+            else:
+                ev_l, sv_l, sc_l, ss_l, src_l = batches[ln % n_sets]
+                if ln == 0:
+                    lane_in.append((seeds, sources, rules, (sv, sc, ss, src)))
+                else:
+                    lane_in.append((tuple(to_device(a, dev) for a in (sv_l, sc_l, ss_l)),
+                                    to_device(src_l, dev), encode_batch(ev_l, catalog.default()),
+                                    (sv_l, sc_l, ss_l, src_l)))
+        n_seeds = max(len(x[3][0]) for x in lane_in)
+        lane_enc = lane_in[0][2] if merge > 1 else enc
+        lane_host = lane_in[0][3]
         # pool_entries=-1: top-k only, as GraphService runs it (the last pull then skips the
         # members outside the candidate set); 0 keeps every member's score for inspection
         fr = snap.frontier(Bm, max_seeds=n_seeds, k=k, pool_entries=pool_entries)
         lanes = build_lanes(snap, Bm, n_seeds, k, pipeline, pool_entries, dev,
-                            [(fr, lane_rules, lane_seeds, lane_src)]
-                            + [(None, lane_rules if merge > 1 else enc, lane_seeds, lane_src)] * (pipeline - 1))
+                            [(fr if ln == 0 else None, x[2], x[0], x[1]) for ln, x in enumerate(lane_in)])
         torch.cuda.synchronize(dev)
     inc_label = g.labels().index("Incident")
     return dict(config=config, graph=g, snap=snap, plan=plan, frontier=fr, rules=rules, seeds=seeds, sources=sources,
                 lanes=lanes, tick=0, merge=merge, sub=0, enc=enc, seed_host=(sv, sc, ss), src_host=src, inc_label=inc_label,
                 evidence=evidence, incident_ids=[str(e[0]["incident_id"]) for e in evidence],
-                distinct_batches=n_sets, incidents_in_graph=n_sets * B,
+                distinct_batches=min(n_sets, per_lane), incidents_in_graph=n_sets * B,
+                distinct_sets=n_sets,
                 # lane 0's launch input on the host (all M batches: seeds, incident vertices,
                 # encoded rows): what the parity test of the headline launch checks against
                 lane_host=lane_host, lane_enc=lane_enc)
@@ -1473,6 +1484,7 @@ def main():
             "lanes": args.pipeline if args.engine == "frontier" else 1,
             "batches_per_launch": M,
             "distinct_batches_per_launch": ctx["distinct_batches"],
+            "distinct_incident_sets": ctx["distinct_sets"],
             "frontier_layout": "locality order (csrc/layout.hip)" if frontier_layout_on() else "canonical",
             "first_table": (FIRST_TABLE[ctx["lanes"][0]["frontier"].wide_first]
                             if args.engine == "frontier" else None),
