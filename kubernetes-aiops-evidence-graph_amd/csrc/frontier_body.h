@@ -206,6 +206,11 @@ struct Ticker {
 
 // Lockstep probe of NQ keys (the first nq valid): every round reads one bucket for every key
 // still unresolved, so a lane's NQ probe sequences share round trips.
+// (EGR_FR_LIGHT_BLOOM=0, an A/B build: the branchy light-row probe skips the membership filter
+// and goes straight to the buckets.)
+#ifndef EGR_FR_LIGHT_BLOOM
+#define EGR_FR_LIGHT_BLOOM 1
+#endif
 #if FR_FIND_SELECT
 template <bool GT, int NQ>
 __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&key)[NQ], uint32_t nq,
@@ -270,7 +275,7 @@ __device__ __forceinline__ void find_batch(const Tab<GT>& t, const uint32_t (&ke
     q[x] = -1;
     if ((uint32_t)x < nq) pend |= 1u << x;
   }
-  if constexpr (!GT) {
+  if constexpr (!GT && EGR_FR_LIGHT_BLOOM) {
     // the filter: a key whose bit is clear is not a member
     uint32_t bw[NQ];
 #pragma unroll

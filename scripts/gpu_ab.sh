@@ -13,6 +13,13 @@ ARGS=${BENCH_ARGS:-"--steps 20 --warmup 5 --no-cpu-baseline --no-dropin --dense-
 if [ -n "$TESTS" ]; then          # (parity of the default build, the candidate)
   timeout -k 10 400 python -u -m pytest $TESTS -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
   echo "tests ok: $(tail -1 $OUT/pytest.log)"
+  if [ -n "$VARIANT_TESTS" ]; then  # (and of every variant build)
+    for a in $ALTS; do
+      n=$(basename $(dirname $a))
+      EGRAPH_LIB=$PWD/$a timeout -k 10 400 python -u -m pytest $TESTS -x -q --timeout 200 --timeout-method thread > $OUT/pytest_$n.log 2>&1
+      echo "tests ok ($n): $(tail -1 $OUT/pytest_$n.log)"
+    done
+  fi
 fi
 for r in $(seq 1 ${REPS:-3}); do
   for a in base $ALTS $ENV_ALTS; do
