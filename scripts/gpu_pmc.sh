@@ -32,7 +32,7 @@ for p in $PASSES; do
     tcp) run tcp TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum ;;
   esac
 done
-python3 scripts/pmc_summary.py $OUT frontier_lds_kernel frontier_lds_retry_kernel "hop_kernel<32, false>" > $OUT/summary.txt
+python3 scripts/pmc_summary.py $OUT frontier_lds_kernel frontier_lds_retry_kernel "hop_kernel<32, false, " > $OUT/summary.txt
 cat $OUT/summary.txt
 if [ -n "$PMC_TAG" ] && [ -d $OUT/rdreq ]; then
   python3 scripts/pmc_rdreq.py $OUT/rdreq $PMC_TAG ${PMC_CONFIG:-C3} 1024 20 20 > /dev/null

@@ -16,7 +16,7 @@ from pathlib import Path
 root = Path(sys.argv[1])
 REPO = Path(__file__).resolve().parents[1]
 LIB = Path(os.environ.get("EGRAPH_LIB", REPO / "kubernetes-aiops-evidence-graph_amd" / "lib" / "libegraph.so"))
-KERNELS = {"frontier": "frontier_lds_kernel", "hop": "hop_kernel<32, false>"}
+KERNELS = {"frontier": "frontier_lds_kernel", "hop": "hop_kernel<32, false, "}   # (round 6: <G, FROM_SEEDS, SKIP>)
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(root.rglob("*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
