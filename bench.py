@@ -337,10 +337,11 @@ _GRAPH_NAME = {"C2": "10k-pod", "C3": "100k-pod", "C4": "400k-pod (1M-vertex)"}
 
 def step_frontier(ctx, hops: int, ev=None):
     """One pass; `ev` (EventPool) times the frontier run on its stream.  The rules launch does
-    not depend on the graph stages (nor they on it), so it goes to a second stream: its waves
-    (35 VGPRs, no LDS) co-reside with the frontier kernel's (101 VGPRs x 4 per SIMD) instead of
-    running in front of the seed preparation.  The timed region ends with a device-wide
-    synchronize, which joins every stream."""
+    not depend on the graph stages (nor they on it), so it goes to a second stream, enqueued
+    first: its waves (35 VGPRs, no LDS) run while the host enqueues the frontier chain and the
+    cost / order kernels run, ahead of the narrow kernel, whose workgroups (72 VGPRs, seven
+    waves per SIMD) then fill the CUs (the launch chain).  The timed region ends
+    with a device-wide synchronize, which joins every stream."""
     if not _launch_due(ctx):
         return None
     lane = ctx["lanes"][ctx["tick"] % len(ctx["lanes"])]

@@ -178,7 +178,8 @@ namespace fr_wide {
 namespace fr_narrow {
 // hub-row chains through LDS, one lane (+4 % at three batches in flight,
 // profiles/r02_ab_hubchain.txt); one LDS score buffer (pull results by member index in HBM and
-// a copy phase) and a 2^14-bit filter: 22 KB and 72 VGPRs (14 spilled), seven workgroups per
+// a copy phase) and a 2^14-bit filter: 22 KB and 72 VGPRs (3 spilled in the plain kernel, 18
+// in the continuation instantiation <true> the headline runs), seven workgroups per
 // CU (-1.7 % against six at 24 KB with a 2^15-bit filter, profiles/r04_ab_one_buffer.txt).  Round 2's two slot-indexed buffers
 // (no copy phase, +2.5 % at five per CU, profiles/r02_ab_frontier_session3.txt) lost to the
 // sixth workgroup once the light-row tails cut the registers: C3 -4.5 %
