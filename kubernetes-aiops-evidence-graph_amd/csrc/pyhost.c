@@ -1968,16 +1968,26 @@ done:
   return result;
 }
 
-/* ---- fused-rank reuse (egraph/ranker.py FusedRanks.apply) ---------------------------------
- * fused_apply(hyps, rec) -> the ranked list, False (not the registered list: a miss), or
- * None (a value this path does not compare without Python: FusedRanks.apply decides).
- * rec = FusedRanks.register's record (ids, catalog, slots, conf, strength, final, orank, cat)
- * with cat = (R, rule categories, rule support counts, (confidence, category, support,
- * strength) of the unknown hypothesis), all plain values.  The checks are FusedRanks.apply's, in its
- * order: every dict is an exact dict with the registered id at its position and the four
- * ranker inputs the kernel emitted; then final_score / rank are written as egr_rank would. */
+/* ---- fused-rank reuse (egraph/ranker.py FusedRanks) ----------------------------------------
+ * A launch's fields travel as ONE bytes block `blk` of m rows (FusedRanks.register packs it with
+ * numpy); row j (stride FR_STRIDE(S), S = R + 1 slots): order_conf u8[S] @0, order_rank u8[S] @S,
+ * then from a8 = (2S + 7) & ~7 confidence f64[S], signal_strength f64[S], final_score f64[S].
+ * A record is (ids tuple, catalog, blk, j, cat) with cat = (R, rule categories, rule support
+ * counts, (confidence, category, support, strength) of the unknown hypothesis).
+ *
+ * fused_records(lists, blk, cat_obj, cat) -> [(first id, record)] for the non-empty lists
+ * (lists[j] = row j), so that registering a launch's lists costs no Python loop.
+ *
+ * fused_apply(hyps, rec) -> the ranked list, False (not the registered list: a miss), or None
+ * (a value this path does not compare without Python: FusedRanks.apply decides).  The checks are
+ * FusedRanks.apply's, in its order: every dict is an exact dict with the registered id at its
+ * position and the four ranker inputs the kernel emitted; then final_score / rank are written as
+ * egr_rank would. */
 static PyObject *f_confidence, *f_category, *f_support, *f_final, *f_rank, *f_unknown, *f_half,
     *f_zero;
+
+static inline Py_ssize_t fr_a8(Py_ssize_t S) { return (2 * S + 7) & ~(Py_ssize_t)7; }
+static inline Py_ssize_t fr_stride(Py_ssize_t S) { return fr_a8(S) + 24 * S; }
 
 /* v (borrowed, NULL = missing -> dflt) == want for plain numbers: 1 / 0, -1 = not plain */
 static inline int f_num_eq(PyObject* v, PyObject* dflt, PyObject* want) {
@@ -1985,25 +1995,90 @@ static inline int f_num_eq(PyObject* v, PyObject* dflt, PyObject* want) {
   if (!(PyFloat_CheckExact(v) || PyLong_CheckExact(v) || PyBool_Check(v))) return -1;
   return PyObject_RichCompareBool(v, want, Py_EQ);   /* built-in numbers: no user code */
 }
+/* the same against a float64 the kernel wrote (Python's int == float semantics kept: a non-float
+ * value is compared through a float object) */
+static inline int f_num_eq_d(PyObject* v, PyObject* dflt, double want) {
+  if (v == NULL) v = dflt;
+  if (PyFloat_CheckExact(v)) return PyFloat_AS_DOUBLE(v) == want;
+  if (!(PyLong_CheckExact(v) || PyBool_Check(v))) return -1;
+  PyObject* w = PyFloat_FromDouble(want);
+  if (!w) return -1;
+  const int eq = PyObject_RichCompareBool(v, w, Py_EQ);
+  Py_DECREF(w);
+  return eq;
+}
 
-static PyObject* fused_apply(PyObject* self, PyObject* args) {
-  PyObject *hyps, *rec;
-  if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &hyps, &PyTuple_Type, &rec)) return NULL;
-  if (PyTuple_GET_SIZE(rec) < 8 || !PyTuple_Check(PyTuple_GET_ITEM(rec, 7))) Py_RETURN_NONE;
-  PyObject *ids = PyTuple_GET_ITEM(rec, 0), *slots = PyTuple_GET_ITEM(rec, 2),
-           *conf = PyTuple_GET_ITEM(rec, 3), *strength = PyTuple_GET_ITEM(rec, 4),
-           *final = PyTuple_GET_ITEM(rec, 5), *orank = PyTuple_GET_ITEM(rec, 6);
+static PyObject* fused_records(PyObject* self, PyObject* args) {
+  PyObject *lists, *blk, *catobj, *cat;
+  if (!PyArg_ParseTuple(args, "O!O!OO!", &PyList_Type, &lists, &PyBytes_Type, &blk, &catobj,
+                        &PyTuple_Type, &cat))
+    return NULL;
+  Py_ssize_t R;
+  PyObject *cats, *sups, *unk;
+  if (!PyArg_ParseTuple(cat, "nOOO", &R, &cats, &sups, &unk)) return NULL;
+  const Py_ssize_t m = PyList_GET_SIZE(lists), S = R + 1;
+  if (R < 0 || PyBytes_GET_SIZE(blk) < m * fr_stride(S)) {
+    PyErr_SetString(PyExc_ValueError, "fused_records: the block is smaller than its rows");
+    return NULL;
+  }
+  PyObject* out = PyList_New(0);
+  if (!out) return NULL;
+  for (Py_ssize_t j = 0; j < m; ++j) {
+    PyObject* hyps = PyList_GET_ITEM(lists, j);
+    if (!PyList_Check(hyps)) {
+      PyErr_SetString(PyExc_TypeError, "fused_records: a hypothesis list is not a list");
+      goto fail;
+    }
+    const Py_ssize_t n = PyList_GET_SIZE(hyps);
+    if (n == 0) continue;
+    PyObject* ids = PyTuple_New(n);
+    if (!ids) goto fail;
+    for (Py_ssize_t p = 0; p < n; ++p) {
+      PyObject* h = PyList_GET_ITEM(hyps, p);
+      PyObject* hid = PyDict_Check(h) ? PyDict_GetItemWithError(h, k_id) : NULL;
+      if (!hid) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_KeyError, "id");
+        Py_DECREF(ids);
+        goto fail;
+      }
+      Py_INCREF(hid);
+      PyTuple_SET_ITEM(ids, p, hid);
+    }
+    PyObject* rec = Py_BuildValue("(OOOnO)", ids, catobj, blk, j, cat);
+    PyObject* kr = rec ? PyTuple_Pack(2, PyTuple_GET_ITEM(ids, 0), rec) : NULL;
+    Py_DECREF(ids);
+    Py_XDECREF(rec);
+    if (!kr || PyList_Append(out, kr) < 0) { Py_XDECREF(kr); goto fail; }
+    Py_DECREF(kr);
+  }
+  return out;
+fail:
+  Py_DECREF(out);
+  return NULL;
+}
+
+static PyObject* fused_verify_apply(PyObject* hyps, PyObject* rec) {
+  if (PyTuple_GET_SIZE(rec) != 5 || !PyTuple_Check(PyTuple_GET_ITEM(rec, 4))) Py_RETURN_NONE;
+  PyObject *ids = PyTuple_GET_ITEM(rec, 0), *blk = PyTuple_GET_ITEM(rec, 2);
+  const Py_ssize_t row = PyLong_AsSsize_t(PyTuple_GET_ITEM(rec, 3));
+  if (row < 0) { PyErr_Clear(); Py_RETURN_NONE; }
   PyObject *cats, *sups, *unk;
   Py_ssize_t R;
-  if (!PyArg_ParseTuple(PyTuple_GET_ITEM(rec, 7), "nOOO", &R, &cats, &sups, &unk)) return NULL;
-  const Py_ssize_t n = PyList_GET_SIZE(hyps);
-  if (!PyTuple_Check(ids) || !PyList_Check(slots) || !PyList_Check(orank) || PyTuple_GET_SIZE(ids) != n ||
-      PyList_GET_SIZE(slots) != n || PyList_GET_SIZE(orank) != n || !PyList_Check(conf) ||
-      !PyList_Check(strength) || !PyList_Check(final) || !PyTuple_Check(cats) || !PyTuple_Check(sups) ||
-      !PyTuple_Check(unk) || PyTuple_GET_SIZE(unk) != 4)
+  if (!PyArg_ParseTuple(PyTuple_GET_ITEM(rec, 4), "nOOO", &R, &cats, &sups, &unk)) return NULL;
+  const Py_ssize_t n = PyList_GET_SIZE(hyps), S = R + 1;
+  if (!PyTuple_Check(ids) || PyTuple_GET_SIZE(ids) != n || !PyBytes_Check(blk) ||
+      PyBytes_GET_SIZE(blk) < (row + 1) * fr_stride(S) || !PyTuple_Check(cats) ||
+      !PyTuple_Check(sups) || !PyTuple_Check(unk) || PyTuple_GET_SIZE(unk) != 4 ||
+      PyTuple_GET_SIZE(cats) < R || PyTuple_GET_SIZE(sups) < R)
     Py_RETURN_NONE;
+  const unsigned char* rb = (const unsigned char*)PyBytes_AS_STRING(blk) + row * fr_stride(S);
+  const unsigned char *slots = rb, *orank = rb + S;
+  double conf[64], strength[64], final[64];
   Py_ssize_t pos[64];
-  if (n > 64 || R >= 64) Py_RETURN_NONE;
+  if (n > 64 || R >= 64 || n > S) Py_RETURN_NONE;
+  memcpy(conf, rb + fr_a8(S), 8 * S);
+  memcpy(strength, rb + fr_a8(S) + 8 * S, 8 * S);
+  memcpy(final, rb + fr_a8(S) + 16 * S, 8 * S);
   for (Py_ssize_t q = 0; q < 64; ++q) pos[q] = -1;
   for (Py_ssize_t p = 0; p < n; ++p) {
     PyObject* h = PyList_GET_ITEM(hyps, p);
@@ -2015,20 +2090,19 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
     PyObject* want_id = PyTuple_GET_ITEM(ids, p);
     if (hid == NULL || !PyUnicode_CheckExact(hid) || !PyUnicode_CheckExact(want_id)) Py_RETURN_NONE;
     if (PyUnicode_Compare(hid, want_id) != 0) Py_RETURN_FALSE;
-    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(slots, p));
-    if (slot < 0 || slot > R) { PyErr_Clear(); Py_RETURN_NONE; }
-    PyObject *wc, *wcat, *wsup, *wst;
+    const Py_ssize_t slot = slots[p];
+    if (slot > R) Py_RETURN_NONE;
+    int eq;
+    PyObject *wcat, *wsup;
     if (slot == R) {
-      wc = PyTuple_GET_ITEM(unk, 0); wcat = PyTuple_GET_ITEM(unk, 1);
-      wsup = PyTuple_GET_ITEM(unk, 2); wst = PyTuple_GET_ITEM(unk, 3);
+      wcat = PyTuple_GET_ITEM(unk, 1);
+      wsup = PyTuple_GET_ITEM(unk, 2);
+      eq = f_num_eq(c, f_half, PyTuple_GET_ITEM(unk, 0));
     } else {
-      if (slot >= PyList_GET_SIZE(conf) || slot >= PyList_GET_SIZE(strength) ||
-          slot >= PyTuple_GET_SIZE(cats) || slot >= PyTuple_GET_SIZE(sups))
-        Py_RETURN_NONE;
-      wc = PyList_GET_ITEM(conf, slot); wcat = PyTuple_GET_ITEM(cats, slot);
-      wsup = PyTuple_GET_ITEM(sups, slot); wst = PyList_GET_ITEM(strength, slot);
+      wcat = PyTuple_GET_ITEM(cats, slot);
+      wsup = PyTuple_GET_ITEM(sups, slot);
+      eq = f_num_eq_d(c, f_half, conf[slot]);
     }
-    int eq = f_num_eq(c, f_half, wc);
     if (eq < 0) { PyErr_Clear(); Py_RETURN_NONE; }
     if (!eq) Py_RETURN_FALSE;
     if (cg == NULL) cg = f_unknown;
@@ -2036,7 +2110,8 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
     if (PyUnicode_Compare(cg, wcat) != 0) Py_RETURN_FALSE;
     if ((eq = f_num_eq(sp, f_zero, wsup)) < 0) { PyErr_Clear(); Py_RETURN_NONE; }
     if (!eq) Py_RETURN_FALSE;
-    if ((eq = f_num_eq(st, f_zero, wst)) < 0) { PyErr_Clear(); Py_RETURN_NONE; }
+    eq = slot == R ? f_num_eq(st, f_zero, PyTuple_GET_ITEM(unk, 3)) : f_num_eq_d(st, f_zero, strength[slot]);
+    if (eq < 0) { PyErr_Clear(); Py_RETURN_NONE; }
     if (!eq) Py_RETURN_FALSE;
     if (pos[slot] >= 0) Py_RETURN_NONE;          /* (a slot twice: not a kernel list) */
     pos[slot] = p;
@@ -2045,9 +2120,8 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
   PyObject* out = PyList_New(n);
   if (!out) return NULL;
   for (Py_ssize_t q = 0; q < n; ++q) {
-    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(orank, q));
-    if (slot < 0 || slot > R || pos[slot] < 0 || slot >= PyList_GET_SIZE(final)) {
-      PyErr_Clear();
+    const Py_ssize_t slot = orank[q];
+    if (slot > R || pos[slot] < 0) {
       Py_DECREF(out);
       Py_RETURN_NONE;
     }
@@ -2057,8 +2131,9 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
   }
   for (Py_ssize_t p = 0; p < n; ++p) {
     PyObject* h = PyList_GET_ITEM(hyps, p);
-    const Py_ssize_t slot = PyLong_AsSsize_t(PyList_GET_ITEM(slots, p));
-    if (PyDict_SetItem(h, f_final, PyList_GET_ITEM(final, slot)) < 0) { Py_DECREF(out); return NULL; }
+    PyObject* f = PyFloat_FromDouble(final[slots[p]]);
+    if (!f || PyDict_SetItem(h, f_final, f) < 0) { Py_XDECREF(f); Py_DECREF(out); return NULL; }
+    Py_DECREF(f);
   }
   for (Py_ssize_t q = 0; q < n; ++q) {
     PyObject* r = PyLong_FromSsize_t(q + 1);
@@ -2070,6 +2145,42 @@ static PyObject* fused_apply(PyObject* self, PyObject* args) {
     Py_DECREF(r);
   }
   return out;
+}
+
+static PyObject* fused_apply(PyObject* self, PyObject* args) {
+  PyObject *hyps, *rec;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyList_Type, &hyps, &PyTuple_Type, &rec)) return NULL;
+  return fused_verify_apply(hyps, rec);
+}
+
+/* fused_rank(recs, hyps) -> FusedRanks.apply for an exact list, lookup included: the ranked list
+ * (a hit), 0 (a miss: no record of that first id, another length, or fused_apply's False), 1
+ * (not a candidate: empty, or a first item that is not a dict; counted as neither), or None (a
+ * value only Python compares: FusedRanks.apply's statements decide). */
+static PyObject* fused_rank(PyObject* self, PyObject* args) {
+  PyObject *recs, *hyps;
+  if (!PyArg_ParseTuple(args, "O!O!", &PyDict_Type, &recs, &PyList_Type, &hyps)) return NULL;
+  if (PyList_GET_SIZE(hyps) == 0) return PyLong_FromLong(1);
+  PyObject* h0 = PyList_GET_ITEM(hyps, 0);
+  if (!PyDict_Check(h0)) return PyLong_FromLong(1);
+  if (!PyDict_CheckExact(h0)) Py_RETURN_NONE;
+  PyObject *hid, *rec;
+  if (dget(h0, k_id, &hid)) Py_RETURN_NONE;
+  if (hid == NULL) hid = Py_None;
+  rec = PyDict_GetItemWithError(recs, hid);
+  if (rec == NULL) {
+    if (PyErr_Occurred()) { PyErr_Clear(); Py_RETURN_NONE; }   /* (an unhashable id: Python raises) */
+    return PyLong_FromLong(0);
+  }
+  if (!PyTuple_Check(rec) || PyTuple_GET_SIZE(rec) < 1 || !PyTuple_Check(PyTuple_GET_ITEM(rec, 0)))
+    Py_RETURN_NONE;
+  if (PyTuple_GET_SIZE(PyTuple_GET_ITEM(rec, 0)) != PyList_GET_SIZE(hyps)) return PyLong_FromLong(0);
+  Py_INCREF(rec);                                  /* (the checks below may run no Python code,
+                                                      but hold the record anyway) */
+  PyObject* r = fused_verify_apply(hyps, rec);
+  Py_DECREF(rec);
+  if (r == Py_False) { Py_DECREF(r); return PyLong_FromLong(0); }
+  return r;
 }
 
 /* ---- seed attachment candidates as keys (egraph/seeds.py SeedCandidates.per_column keys=True)
@@ -2642,6 +2753,8 @@ static PyMethodDef methods[] = {
     {"attach_idx", attach_idx, METH_VARARGS, "first present candidate per row + the ids before it"},
     {"str_blob", str_blob, METH_O, "list of str -> (UTF-8 blob, int64 offsets)"},
     {"fused_apply", fused_apply, METH_VARARGS, "verify + apply a registered fused ranking"},
+    {"fused_rank", fused_rank, METH_VARARGS, "FusedRanks.apply for an exact list, lookup included"},
+    {"fused_records", fused_records, METH_VARARGS, "a launch's hypothesis lists -> fused-rank records"},
     {"seed_attach", seed_attach, METH_VARARGS, "evidence rows -> attached (vertex, column, strength) seeds"},
     {"encode_rows", encode_rows, METH_VARARGS, "evidence dicts -> row columns"},
     {"assemble", assemble, METH_VARARGS, "kernel outputs -> hypothesis dicts"},

@@ -549,6 +549,20 @@ class RulesBatcher:
         still waiting (none is left pending)."""
         try:
             with gc_paused():
+                if enc.n_incidents == len(ok):
+                    # every call is one incident (concurrent single calls): one assembly, one
+                    # registration, one future per call, no per-call bookkeeping arrays
+                    r0 = ok[0].ranked
+                    if all(c.ranked == r0 for c in ok):
+                        lists = hypothesis_lists(self.cat, res, [c.incident_ids[0] for c in ok],
+                                                 enc.evidence_ids, r0)
+                        if not r0:
+                            FUSED.register(self.cat, res, lists, range(len(lists)))
+                        for c, lst in zip(ok, lists):
+                            f = c.fut
+                            if not f.done():
+                                f.set_result(lst if c.single else [lst])
+                        return
                 if len(ok) == 1:               # (a lone call: its lists are the whole result)
                     c = ok[0]
                     lists = hypothesis_lists(self.cat, res, c.incident_ids, enc.evidence_ids, c.ranked)

@@ -122,9 +122,10 @@ _RUNNERS: dict = {}
 
 class FusedRanks:
     """The rules kernel's ranking of the lists it generated, for rank() to reuse (module doc).
-    A record keeps the list's hypothesis ids and a reference to its launch's results (row i);
-    the fields to verify and the final scores / order are read from those results only when
-    rank() asks, so registering a list costs one tuple."""
+    A launch's fields are packed once into one bytes block (row j = list j: the slot order, the
+    kernel's order, confidence, signal strength and final score per slot); a record keeps the
+    list's hypothesis ids, the block and its row, and is built in native code
+    (csrc/pyhost.c fused_records), so registering a launch's lists runs no Python loop."""
 
     def __init__(self, capacity: int = 1 << 16):
         self.capacity = capacity
@@ -132,39 +133,50 @@ class FusedRanks:
         self.lock = threading.Lock()
         self.hits = self.misses = 0
 
+    @staticmethod
+    def pack(res, sel) -> bytes:
+        """The block of rows `sel` of a launch's results (csrc/pyhost.c's fused-rank layout)."""
+        S = res.confidence.shape[1]
+        a8 = (2 * S + 7) // 8 * 8
+        buf = np.zeros((len(sel), a8 + 24 * S), np.uint8)
+        buf[:, :S] = res.order_conf[sel]
+        buf[:, S:2 * S] = res.order_rank[sel]
+        for k, a in enumerate((res.confidence, res.strength, res.final_score)):
+            buf[:, a8 + 8 * S * k:a8 + 8 * S * (k + 1)] = \
+                np.ascontiguousarray(a[sel], np.float64).view(np.uint8)
+        return buf.tobytes()
+
     def register(self, cat, res, lists: list[list[dict]], rows) -> None:
-        """lists[j] = the unranked dicts of result row rows[j] (confidence order).  The rows'
-        fields are converted to Python numbers here, once per launch (whole arrays), so that
-        rank() -- called once per list, often one list per call -- does no numpy work."""
+        """lists[j] = the unranked dicts of result row rows[j] (confidence order)."""
         rows = list(rows)
         if not rows:
             return
-        sel = np.asarray(rows, np.int64)
-        conf = res.confidence[sel].tolist()
-        strength = res.strength[sel].tolist()
-        final = res.final_score[sel].tolist()
-        oconf = res.order_conf[sel].tolist()
-        orank = res.order_rank[sel].tolist()
+        blk = self.pack(res, np.asarray(rows, np.int64))
         u = cat.unknown
         # what the native check (pyhost.fused_apply) compares against, read from the catalog
         # now as apply() would read it
         ncat = (cat.n_rules, tuple(r["category"] for r in cat.rules),
                 tuple(len(r["conditions"]) for r in cat.rules),
                 (u["confidence"], u["category"], u["support_count"], u["signal_strength"]))
-        recs = []
-        for j, hyps in enumerate(lists):
-            if hyps:
-                n = len(hyps)
-                recs.append((hyps[0]["id"], (tuple(h["id"] for h in hyps), cat, oconf[j][:n],
-                                              conf[j], strength[j], final[j], orank[j][:n], ncat)))
+        recs = L.pyhost.fused_records(lists if type(lists) is list else list(lists), blk, cat, ncat)
         with self.lock:
-            for key, rec in recs:
-                self.recs[key] = rec
+            self.recs.update(recs)
             while len(self.recs) > self.capacity:
                 self.recs.popitem(last=False)
 
     def apply(self, hyps: list) -> list | None:
         """Rank `hyps` from its record if it is exactly a registered list; else None."""
+        if type(hyps) is list:
+            # lookup, checks and writes in native code (csrc/pyhost.c fused_rank); None: a value
+            # it leaves to the Python statements below
+            r = L.pyhost.fused_rank(self.recs, hyps)
+            if r is not None:
+                if type(r) is int:                 # 0: a miss; 1: not a candidate (not counted)
+                    if r == 0:
+                        self.misses += 1
+                    return None
+                self.hits += 1
+                return r
         if not hyps or not isinstance(hyps[0], dict):
             return None
         # (one C-level get: atomic under the GIL against register()'s locked updates)
@@ -172,18 +184,14 @@ class FusedRanks:
         if rec is None or len(hyps) != len(rec[0]):
             self.misses += 1
             return None
-        if type(hyps) is list:
-            # the same checks and writes in native code (csrc/pyhost.c fused_apply); None: a
-            # value it leaves to the Python statement below
-            r = L.pyhost.fused_apply(hyps, rec)
-            if r is not None:
-                if r is False:
-                    self.misses += 1
-                    return None
-                self.hits += 1
-                return r
-        ids, cat, slots, conf, strength, final, orank, _ = rec
+        ids, cat, blk, row, _ = rec
         R, rules, u = cat.n_rules, cat.rules, cat.unknown
+        S = R + 1
+        a8 = (2 * S + 7) // 8 * 8
+        rb = np.frombuffer(blk, np.uint8, a8 + 24 * S, row * (a8 + 24 * S))
+        slots, orank = rb[:len(hyps)].tolist(), rb[S:S + len(hyps)].tolist()
+        conf, strength, final = (rb[a8 + 8 * S * k:a8 + 8 * S * (k + 1)].view(np.float64).tolist()
+                                 for k in range(3))
         for h, hid, slot in zip(hyps, ids, slots):
             if not isinstance(h, dict) or h.get("id") != hid:
                 self.misses += 1

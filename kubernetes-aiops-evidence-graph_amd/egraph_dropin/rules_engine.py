@@ -88,16 +88,28 @@ class RulesEngine:
         self.rules = DIAGNOSIS_RULES if catalog is None else [
             {**r, "category": HypothesisCategory(r["category"])} for r in catalog.rules]
         self.device = device
+        self._last = None              # (event loop, its batcher): the previous call's, read once
+
+    def _batcher(self) -> RulesBatcher:
+        # one call per incident: the common case is the previous call's loop (the engine holds
+        # its catalog, so the catalog cannot change under it)
+        loop = asyncio.get_running_loop()
+        last = self._last
+        if last is not None and last[0] is loop:
+            return last[1]
+        b = _batcher(self.catalog, self.device)
+        self._last = (loop, b)
+        return b
 
     async def _run(self, incidents, evidence_lists, ranked: bool) -> list[list[dict]]:
         if len(incidents) != len(evidence_lists):
             raise ValueError("incidents and evidence_lists differ in length")
-        return await _batcher(self.catalog, self.device).submit_many(
+        return await self._batcher().submit_many(
             [inc.id for inc in incidents], evidence_lists, ranked)
 
     async def generate_hypotheses(self, incident, evidence: list[dict]) -> list[dict]:
         """Generate hypotheses by matching evidence against rules (rules_engine.py:199-233)."""
-        b = _batcher(self.catalog, self.device)
+        b = self._batcher()
         # (a launch in flight: the call joins the next one through its future directly)
         return await (b.queued(incident.id, evidence, False) if b.busy
                       else b.submit(incident.id, evidence, False))

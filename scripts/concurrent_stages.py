@@ -43,7 +43,12 @@ def timed_async(name, fn):
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n = int(args[0]) if args else 1024
+    # --ballast=M: M million small dicts kept alive (a process heap like the bench's, which holds
+    # the C3 graph and 20 incident sets); --singles: the bench's 1024 one-at-a-time calls first
+    ballast_m = next((float(a.split("=")[1]) for a in sys.argv if a.startswith("--ballast=")), 0.0)
+    ballast = [{"i": i, "s": "x"} for i in range(int(ballast_m * 1e6))]
     from egraph import synth
     from src.services.rca import rules_engine as RE
     from src.services.rca.hypothesis_ranker import HypothesisRanker
@@ -64,15 +69,32 @@ def main():
     B.asyncio.sleep = sleep
     B.RulesRunner.results = timed("results copy", B.RulesRunner.results)
     B.RulesBatcher._finish = timed("assemble + deliver", B.RulesBatcher._finish)
-    cl = synth.build_cluster(synth.CONFIGS["C3"])
-    cases = synth.make_incidents(cl, n, seed=1000)
-    ev = [x.evidence for x in cases]
+    if "--bench-ctx" in sys.argv:
+        # the bench's own workload object (bench.setup: the C3 graph, 20 incident sets) and its
+        # engine on an explicit device, as bench.py dropin_rules builds them
+        import torch
+        sys.path.insert(0, str(REPO))
+        import bench
+        dev = torch.device("cuda", 0)
+        ctx = bench.setup("C3", n, 10, 0, dev, merge=20)
+        ev = ctx["evidence"]
+        eng = RE.RulesEngine(device=dev if "--no-device" not in sys.argv else None)
+    else:
+        cl = synth.build_cluster(synth.CONFIGS["C3"])
+        cases = synth.make_incidents(cl, n, seed=1000)
+        ev = [x.evidence for x in cases]
+        eng = RE.RulesEngine()
     incs = [SimpleNamespace(id=f"inc-{i}") for i in range(n)]
-    eng = RE.RulesEngine()
     ranker = HypothesisRanker()
 
     async def one(i):
         return ranker.rank(await eng.generate_hypotheses(incs[i], ev[i]))
+
+    if "--singles" in sys.argv:
+        async def singles():
+            for i in range(n):
+                await one(i)
+        asyncio.run(singles())
 
     async def rounds(k):
         ts = []
@@ -87,7 +109,9 @@ def main():
     asyncio.run(rounds(1))
     ts = asyncio.run(rounds(5))
     t, acc = min(ts, key=lambda x: x[0])
-    print(f"{n} concurrent calls: best {t * 1e3:.2f} ms -> {n / t:,.0f} incidents/s")
+    print(f"{n} concurrent calls{' ' + ' '.join(sys.argv[2:]) if len(sys.argv) > 2 else ''}: "
+          f"best {t * 1e3:.2f} ms -> {n / t:,.0f} incidents/s (rounds "
+          f"{[round(x[0] * 1e3, 2) for x in ts]}; ballast {len(ballast)})")
     for k, v in acc.items():
         print(f"  {k:>22}: {v * 1e3:7.3f} ms")
     rest = t - acc.get("encode", 0) - acc.get("run (launch + wait)", 0) - acc.get("assemble + deliver", 0)

@@ -95,3 +95,26 @@ def test_capacity_evicts_oldest():
     assert len(fr.recs) == 10
     assert fr.apply(copy.deepcopy(hyps[0])) is None
     assert fr.apply(copy.deepcopy(hyps[-1])) is not None
+
+
+def test_python_path_equals_the_native_one():
+    """A list subclass skips the native check (pyhost.fused_apply): FusedRanks.apply's own
+    statements read the same packed row and must give the same ranking, and miss the same edits."""
+    from egraph.ranker import FusedRanks
+
+    class Hyps(list):
+        pass
+    rng = random.Random(11)
+    lists = [evidence_fuzz.random_evidence(rng) for _ in range(120)]
+    cat, res, hyps = _generated(lists)
+    fr = FusedRanks()
+    fr.register(cat, res, hyps, range(len(hyps)))
+    for h in hyps:
+        want = rca_oracle.rank(copy.deepcopy(h))
+        got = fr.apply(Hyps(copy.deepcopy(h)))
+        assert got is not None and record(got) == record(want)
+        assert record(fr.apply(copy.deepcopy(h))) == record(want)
+    multi = [h for h in hyps if len(h) >= 2]
+    h = Hyps(copy.deepcopy(multi[0]))
+    h[-1]["signal_strength"] = 0.123
+    assert fr.apply(h) is None
