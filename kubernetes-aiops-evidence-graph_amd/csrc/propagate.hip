@@ -123,6 +123,10 @@ struct HopArgs {
   uint32_t xbytes;
   uint32_t V;
   uint32_t nchunks;
+  // the chunks of one row longer than CSR_CAP (egr_plan::long_chunk): with SKIP they run in a
+  // launch of their own (hop_kernel<G, *, true, true>), so the main launch's chunks all compact
+  const uint32_t* long_chunks;
+  uint32_t nlong;
 };
 
 template <bool SEEDS>
@@ -227,6 +231,9 @@ __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr
 #ifndef EGR_HOP_XCD_REMAP
 #define EGR_HOP_XCD_REMAP 0
 #endif
+#ifndef EGR_HOP_STORE_SKIP
+#define EGR_HOP_STORE_SKIP 1
+#endif
 
 // SKIP (not FROM_SEEDS): the zero-tile skip -- a row's fmaf chain runs over its LIVE entries
 // only, those whose neighbour tile of xin may hold a non-zero (tile flags A.nzin, compacted per
@@ -235,7 +242,15 @@ __device__ __forceinline__ void stage_chunk(const uint32_t* __restrict__ row_ptr
 // batch loads go through a buffer descriptor at an out-of-range offset: zeros, no fetch, and the
 // loop keeps its branch-free form).  Hops 2 and 3 of a 3-hop C3 batch gather a non-zero tile
 // for 9 % / 34 % of their entries, C4 2 % / 15 % (scripts/tile_sparsity.py).
-template <int G, bool FROM_SEEDS, bool SKIP = false>
+// SKIP also skips the STORE of a row tile that came out all +0 and holds no seed of the row
+// (seed_add_kernel adds into the tiles the seed tile mask marks, so those are always written):
+// its flag (count 0) is the tile's value, and every reader of the scores goes through the flags
+// (the next hop's gathers, top-k, the read-back, the packs: egr_plan::xsparse).
+// LONG (with SKIP): the launch over the chunks of a lone row longer than CSR_CAP, which the main
+// SKIP launch leaves out -- their entries are not compacted, and each gather of a neighbour tile
+// goes through its flag (a zero tile's memory may be stale since the store skip); the main launch's
+// chunks then all take the compacted path, with no per-gather flag test in the hot loop.
+template <int G, bool FROM_SEEDS, bool SKIP = false, bool LONG = false>
 __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
   constexpr int TW = 4 * G, GROUPS = 256 / G, ROWS = HopGeo<G>::ROWS;
   __shared__ uint32_t s_rp[ROWS + 1];
@@ -255,12 +270,17 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
 #else
   const uint32_t lb = blockIdx.x;
 #endif
-  const uint32_t tile = lb / A.nchunks, chunk = lb % A.nchunks;
+  const uint32_t tile = LONG ? lb / A.nlong : lb / A.nchunks;
+  const uint32_t chunk = LONG ? A.long_chunks[lb % A.nlong] : lb % A.nchunks;
   const uint32_t v0 = A.chunk_start[chunk], v1 = A.chunk_start[chunk + 1];
   const uint32_t nrows = v1 - v0;
   const uint32_t e0 = A.row_ptr[v0], e1 = A.row_ptr[v1];
-  // (a lone row longer than CSR_CAP -- its own chunk -- gathers every entry)
-  const bool live_on = SKIP && e1 - e0 <= CSR_CAP;
+  // (a lone row longer than CSR_CAP -- its own chunk -- gathers every entry; with SKIP it is the
+  // LONG launch's, and the main launch leaves it: uniform in the block, before any barrier)
+  if constexpr (SKIP && !LONG) {
+    if (e1 - e0 > CSR_CAP) return;
+  }
+  constexpr bool live_on = SKIP && !LONG;
   stage_chunk<ROWS, true>(A.row_ptr, A.col, A.val, v0, nrows, e0, e1, s_rp, s_col, s_val,
                           live_on && !FROM_SEEDS ? A.nzin : nullptr, A.ntiles, tile, s_live, s_segm,
                           s_segp, live_on && FROM_SEEDS ? A.seed_tiles : nullptr);
@@ -285,13 +305,19 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       return X[(size_t)u * G + gl];
     }
   };
+  // a lone row longer than CSR_CAP (not compacted): its zero tiles are not gathered either -- since
+  // the store skip, a zero tile's memory may be stale, so its flag is what it holds
+  auto dead = [&](uint32_t u) -> bool {
+    if constexpr (SKIP && LONG) return A.nzin[(size_t)u * A.ntiles + tile] == 0;
+    return false;
+  };
   // live entries before staged entry x (live_on), and the entry of live index i
   auto live_before = [&](uint32_t x) -> uint32_t {
     const uint32_t sg = x >> 6, bt = x & 63u;
     return s_segp[sg] + (bt ? (uint32_t)__popcll(s_segm[sg] & ((1ull << bt) - 1ull)) : 0u);
   };
   auto entry = [&](uint32_t i) -> uint32_t {
-    if constexpr (SKIP) return live_on ? (uint32_t)s_live[min(i, CSR_CAP - 1u)] : i;
+    if constexpr (live_on) return (uint32_t)s_live[min(i, CSR_CAP - 1u)];
     return i;
   };
 
@@ -300,7 +326,7 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
     const uint32_t a = s_rp[r], b = s_rp[r + 1];
     uint32_t la = a, lb = b;
     if constexpr (SKIP) {
-      if (live_on) {
+      if constexpr (live_on) {
         la = live_before(a);
         lb = live_before(b);
       }
@@ -316,7 +342,7 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       bt.u[t] = u;
       bt.w[t] = (uint32_t)t < n ? s_val[min(jj, CSR_CAP - 1u)] : 0.f;
       if constexpr (FROM_SEEDS) bt.m[t] = A.seed_tiles[u];
-      else bt.x[t] = gather(u, n == 0u);
+      else bt.x[t] = gather(u, n == 0u || dead(u));
     }
   };
   auto seed_gather = [&](uint32_t u, float w, float4& acc) {
@@ -362,30 +388,32 @@ __global__ __launch_bounds__(256) void hop_kernel(const HopArgs A) {
       } else {
         float4 x[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) x[t] = gather(u[t], false);
+        for (int t = 0; t < NT; ++t) x[t] = gather(u[t], dead(u[t]));
 #pragma unroll
         for (int t = 0; t < NT; ++t) fma4(w[t], x[t], acc);
       }
     }
-#if EGR_HOP_NT_STORE
-    // streaming store: the output tile is not re-read in this hop, so keep it from evicting
-    // the input tile the gathers re-read from the Infinity Cache
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(f4v{acc.x, acc.y, acc.z, acc.w},
-                                reinterpret_cast<f4v*>(&Y[(size_t)v * G + gl]));
-#else
-    Y[(size_t)v * G + gl] = acc;
-#endif
-    if (A.nzout) {
-      // the row's non-zero count in this tile -- for the sparse halo pack and the next hop's
-      // zero-tile skip (TW = 4G <= 128 columns: a byte): summed over the G lanes of the row's
-      // group (contiguous lanes, all active for the same row); -0.0 counts as non-zero
-      int c = (__float_as_uint(acc.x) != 0u) + (__float_as_uint(acc.y) != 0u) +
-              (__float_as_uint(acc.z) != 0u) + (__float_as_uint(acc.w) != 0u);
+    // the row's non-zero count in this tile -- for the sparse halo pack, the next hop's zero-tile
+    // skip and the readers of a skipped store (TW = 4G <= 128 columns: a byte): summed over the
+    // G lanes of the row's group (contiguous lanes, all active for the same row); -0.0 counts
+    // as non-zero
+    int c = (__float_as_uint(acc.x) != 0u) + (__float_as_uint(acc.y) != 0u) +
+            (__float_as_uint(acc.z) != 0u) + (__float_as_uint(acc.w) != 0u);
 #pragma unroll
-      for (int o = 1; o < G; o <<= 1) c += __shfl_xor(c, o, 64);
-      if (gl == 0) A.nzout[(size_t)v * A.ntiles + tile] = (uint8_t)c;
+    for (int o = 1; o < G; o <<= 1) c += __shfl_xor(c, o, 64);
+    // (SKIP: an all-+0 tile without a seed of this row is not written; c is uniform in the group)
+    if (!SKIP || !EGR_HOP_STORE_SKIP || c != 0 || ((A.seed_tiles[v] >> tbit) & 1u)) {
+#if EGR_HOP_NT_STORE
+      // streaming store: the output tile is not re-read in this hop, so keep it from evicting
+      // the input tile the gathers re-read from the Infinity Cache
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(f4v{acc.x, acc.y, acc.z, acc.w},
+                                  reinterpret_cast<f4v*>(&Y[(size_t)v * G + gl]));
+#else
+      Y[(size_t)v * G + gl] = acc;
+#endif
     }
+    if (gl == 0) A.nzout[(size_t)v * A.ntiles + tile] = (uint8_t)c;
   };
 
   Batch<FROM_SEEDS> ba, bb;
@@ -611,6 +639,15 @@ __global__ void reach_export_kernel(const uint64_t* __restrict__ R, uint32_t RS,
 }
 
 // ---- top-k -----------------------------------------------------------------------------------
+// One score of the tiled buffer; nz (the buffer's tile flags when its last hop skipped the stores
+// of all-+0 tiles, egr_plan::xsparse; else nullptr): a tile flagged 0 reads as +0 without a load.
+__device__ __forceinline__ float x_at(const float* __restrict__ X, const uint8_t* __restrict__ nz,
+                                      uint32_t ntiles, uint32_t V, int TW, uint32_t v, int b) {
+  const uint32_t tile = (uint32_t)(b / TW);
+  if (nz && nz[(size_t)v * ntiles + tile] == 0) return 0.f;
+  return X[((size_t)tile * V + v) * TW + (b % TW)];
+}
+
 struct Cand {
   float s;
   uint32_t v;
@@ -679,7 +716,8 @@ __device__ __forceinline__ void wave_emit_topk(float (&Ls)[KMAX], uint32_t (&Lv)
 __global__ __launch_bounds__(256) void topk_partial_kernel(
     const float* __restrict__ X, const uint64_t* __restrict__ R, uint32_t RS,
     const uint8_t* __restrict__ vlabel, int exclude_label, uint32_t V, uint32_t VC, int TW, int B,
-    int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v) {
+    int n_chunks, float* __restrict__ part_s, uint32_t* __restrict__ part_v,
+    const uint8_t* __restrict__ nz, uint32_t nzt) {
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int CW = TW < 64 ? TW : 64, nsub = TW / CW;
@@ -719,7 +757,7 @@ __global__ __launch_bounds__(256) void topk_partial_kernel(
         const uint32_t v = vb + t * rps;
         const bool cand = (wd[t] & bit) && !(exclude_label >= 0 && lab[t] == (uint8_t)exclude_label);
         wd[t] = cand;
-        xs[t] = cand ? Xt[(size_t)v * TW + cx] : 0.f;
+        xs[t] = cand && !(nz && nz[(size_t)v * nzt + tile] == 0) ? Xt[(size_t)v * TW + cx] : 0.f;
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t)
@@ -767,7 +805,8 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 __global__ __launch_bounds__(256) void topk_cand_kernel(
     const float* __restrict__ X, const uint32_t* __restrict__ off, uint32_t NG,
     const uint32_t* __restrict__ cand_list, uint32_t V, int TW, int B, int k,
-    uint32_t* __restrict__ out_ids, float* __restrict__ out_scores) {
+    uint32_t* __restrict__ out_ids, float* __restrict__ out_scores, const uint8_t* __restrict__ nz,
+    uint32_t ntiles) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -788,7 +827,8 @@ __global__ __launch_bounds__(256) void topk_cand_kernel(
 #pragma unroll
     for (int t = 0; t < 4; ++t) vv[t] = i0 + t * 64u < n ? Lb[i0 + t * 64u] : NO_NODE;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) ss[t] = vv[t] != NO_NODE ? Xc[(size_t)vv[t] * TW] : 0.f;
+    for (int t = 0; t < 4; ++t)
+      ss[t] = vv[t] != NO_NODE && !(nz && nz[(size_t)vv[t] * ntiles + b / TW] == 0) ? Xc[(size_t)vv[t] * TW] : 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (vv[t] != NO_NODE) list_insert(Ls, Lv, ss[t], vv[t]);
@@ -797,12 +837,13 @@ __global__ __launch_bounds__(256) void topk_cand_kernel(
 }
 
 __global__ void scores_rowmajor_kernel(const float* __restrict__ X, uint32_t V, int TW, int B,
-                                       float* __restrict__ out) {
+                                       float* __restrict__ out, const uint8_t* __restrict__ nz,
+                                       uint32_t ntiles) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)V * B) return;
   const uint32_t v = (uint32_t)(i / B);
   const int b = (int)(i % B);
-  out[i] = X[((size_t)(b / TW) * V + v) * TW + (b % TW)];
+  out[i] = x_at(X, nz, ntiles, V, TW, v, b);
 }
 
 __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
@@ -829,10 +870,11 @@ __global__ void induced_kernel(const uint32_t* __restrict__ row_ptr,
 // ---- halo exchange of a partitioned graph (egraph/shard.py): rows of the tiled scores and of
 // the row-major reach words to / from dense [n][Bpad] / [n][W] buffers.  One block per row.
 __global__ void pack_scores_kernel(const float* __restrict__ X, uint32_t V, int TW, int Bpad,
-                                   const uint32_t* __restrict__ rows, float* __restrict__ out) {
+                                   const uint32_t* __restrict__ rows, float* __restrict__ out,
+                                   const uint8_t* __restrict__ nz, uint32_t ntiles) {
   const uint32_t v = rows[blockIdx.x];
   for (int b = threadIdx.x; b < Bpad; b += blockDim.x)
-    out[(size_t)blockIdx.x * Bpad + b] = X[((size_t)(b / TW) * V + v) * TW + (b % TW)];
+    out[(size_t)blockIdx.x * Bpad + b] = x_at(X, nz, ntiles, V, TW, v, b);
 }
 
 __global__ void unpack_scores_kernel(float* __restrict__ X, uint32_t V, int TW, int Bpad,
@@ -963,7 +1005,7 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     const uint64_t* __restrict__ R, uint32_t V, int TW, uint32_t RS, int width, bool reach,
     const uint32_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ seg, int P,
     const int64_t* __restrict__ off, const uint32_t* __restrict__ masks, int MW,
-    int64_t* __restrict__ out, int64_t cap) {
+    int64_t* __restrict__ out, int64_t cap, const uint8_t* __restrict__ nzf, uint32_t ntiles) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
   for (int64_t r = (int64_t)blockIdx.x * SX_ROWS + wv; r < n; r += (int64_t)gridDim.x * SX_ROWS) {
   uint32_t mk[EGR_SX_MASK_WORDS];
@@ -985,7 +1027,10 @@ __global__ __launch_bounds__(256) void sx_emit_kernel(const float* __restrict__ 
     const int g = base + half < nset ? kth_bit(mk, MW, base + half) : -1;
     const int b = g >= 0 ? 32 * g + hl : width;
     uint64_t w = 0;
-    const bool nz = b < width && sx_value(X, R, V, TW, RS, v, b, reach, &w);
+    // (a 32-column group spans several tiles below TW = 32: the count pass read only flagged
+    // tiles, and a tile flagged 0 may hold stale memory since the hop's store skip)
+    const bool nz = b < width && (!nzf || nzf[(size_t)v * ntiles + b / TW] != 0) &&
+                    sx_value(X, R, V, TW, RS, v, b, reach, &w);
     const uint64_t m = __ballot(nz);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
     const uint32_t mine = half ? hi : lo;
@@ -1294,6 +1339,8 @@ struct egr_plan {
   int n_chunks = 0;          // top-k full-scan chunks
   uint32_t nchunks = 0;      // hop row chunks per tile
   uint32_t* chunk_start = nullptr;
+  uint32_t nlong = 0;        // hop chunks of one row longer than CSR_CAP, and their indices
+  uint32_t* long_chunk = nullptr;
   uint32_t rnchunks = 0;     // reach row chunks
   uint32_t* rchunk_start = nullptr;
   float* x[2] = {nullptr, nullptr};
@@ -1304,6 +1351,9 @@ struct egr_plan {
   uint8_t* nzf[2] = {nullptr, nullptr};
   bool xzeroed[2] = {false, false};
   bool skip_zero = true;             // hop_kernel's zero-tile skip ($EGRAPH_HOP_NO_SKIP=1: off)
+  // x[i]'s last hop skipped the stores of all-+0 tiles: its flags nzf[i] say which tiles hold
+  // scores, and every reader goes through them (a tile flagged 0 may hold stale memory)
+  bool xsparse[2] = {false, false};
   uint64_t* reach[2] = {nullptr, nullptr};
   int rcur = 0;
   int reach_hops = -1;  // -1: sources not set
@@ -1383,12 +1433,36 @@ std::vector<uint32_t> build_chunks(const std::vector<uint32_t>& rp, uint32_t V, 
   return cs;
 }
 
+// The chunks of one row longer than CSR_CAP (hop_kernel's LONG launch) -> p->long_chunk / nlong
+int set_long_chunks(egr_plan* p, const std::vector<uint32_t>& cs) {
+  std::vector<uint32_t> lc;
+  const std::vector<uint32_t>& rp = p->s->row_ptr_host;
+  for (size_t c = 0; c + 1 < cs.size(); ++c)
+    if (rp[cs[c + 1]] - rp[cs[c]] > CSR_CAP) lc.push_back((uint32_t)c);
+  if (lc.size() > p->nlong || !p->long_chunk) {
+    dfree(p->long_chunk);
+    p->long_chunk = nullptr;
+    const int rc = dalloc(&p->long_chunk, std::max<size_t>(lc.size(), 1));
+    if (rc != EGR_OK) return rc;
+  }
+  if (!lc.empty() &&
+      hipMemcpy(p->long_chunk, lc.data(), lc.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return egr::fail(EGR_EDEVICE, "long chunk table upload failed");
+  p->nlong = (uint32_t)lc.size();
+  return EGR_OK;
+}
+
 template <int G>
-void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool skip) {
+void launch_hop_g(const HopArgs& a, dim3 grid, hipStream_t st, bool seeds, bool skip, uint32_t ntiles) {
   if (seeds && skip) hipLaunchKernelGGL((hop_kernel<G, true, true>), grid, dim3(256), 0, st, a);
   else if (seeds) hipLaunchKernelGGL((hop_kernel<G, true>), grid, dim3(256), 0, st, a);
   else if (skip) hipLaunchKernelGGL((hop_kernel<G, false, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((hop_kernel<G, false>), grid, dim3(256), 0, st, a);
+  if (skip && a.nlong > 0) {                    // the lone long rows' chunks (see hop_kernel)
+    const dim3 lg(a.nlong * ntiles);
+    if (seeds) hipLaunchKernelGGL((hop_kernel<G, true, true, true>), lg, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((hop_kernel<G, false, true, true>), lg, dim3(256), 0, st, a);
+  }
 }
 
 template <int RG>
@@ -1399,6 +1473,9 @@ void launch_reach_g(const egr_plan* p, hipStream_t st) {
 }
 
 uint32_t reach_rows(int RG) { return RG == 1 ? ReachGeo<1>::ROWS : ReachGeo<2>::ROWS; }
+
+// the current scores' tile flags for a reader, when the last hop skipped zero-tile stores
+const uint8_t* x_flags(const egr_plan* p) { return p->xsparse[p->xcur] ? p->nzf[p->xcur] : nullptr; }
 
 // One propagation hop (+ its own-row seed add).
 int plan_hop(egr_plan* p, void* stream) {
@@ -1428,12 +1505,14 @@ int plan_hop(egr_plan* p, void* stream) {
   a.ntiles = (uint32_t)p->ntiles;
   a.V = (uint32_t)s->V;
   a.nchunks = p->nchunks;
+  a.long_chunks = p->long_chunk;
+  a.nlong = p->nlong;
   const dim3 grid(p->nchunks * p->ntiles);
   switch (p->TW) {
-    case 128: launch_hop_g<32>(a, grid, st, seeds, skip); break;
-    case 64: launch_hop_g<16>(a, grid, st, seeds, skip); break;
-    case 16: launch_hop_g<4>(a, grid, st, seeds, skip); break;
-    default: launch_hop_g<1>(a, grid, st, seeds, skip); break;
+    case 128: launch_hop_g<32>(a, grid, st, seeds, skip, a.ntiles); break;
+    case 64: launch_hop_g<16>(a, grid, st, seeds, skip, a.ntiles); break;
+    case 16: launch_hop_g<4>(a, grid, st, seeds, skip, a.ntiles); break;
+    default: launch_hop_g<1>(a, grid, st, seeds, skip, a.ntiles); break;
   }
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(seed_add_kernel, dim3((unsigned)((std::max<int64_t>(p->max_seeds, 1) + 255) / 256)),
@@ -1441,6 +1520,7 @@ int plan_hop(egr_plan* p, void* stream) {
                      (uint32_t)p->TW, (uint32_t)s->V, a.xout, a.nzout, a.ntiles);
   EGR_CHECK_LAUNCH();
   p->xcur = seeds ? 0 : 1 - p->xcur;
+  p->xsparse[p->xcur] = skip;
   ++p->hops_done;
   p->cand_valid = false;
   return EGR_OK;
@@ -1590,6 +1670,10 @@ int egr_plan_create(const egr_snapshot* s, int32_t n_cols, int64_t max_seeds, in
     egr_plan_free(p);
     return egr::fail(EGR_EDEVICE, "plan table upload failed");
   }
+  if ((rc = set_long_chunks(p, chunks)) != EGR_OK) {
+    egr_plan_free(p);
+    return rc;
+  }
   *out = p;
   return EGR_OK;
 }
@@ -1612,6 +1696,7 @@ void egr_plan_free(egr_plan* p) {
   dfree(p->cand_list);
   dfree(p->counter);
   dfree(p->chunk_start);
+  dfree(p->long_chunk);
   dfree(p->rchunk_start);
   dfree(p->sx_off);
   for (int k = 0; k < 2; ++k) {
@@ -1754,7 +1839,8 @@ int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* 
   const uint32_t V = (uint32_t)p->s->V;
   if (p->cand_valid && p->cand_exclude == exclude_label) {
     hipLaunchKernelGGL(topk_cand_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->x[p->xcur],
-                       p->cand_off, p->NG, p->cand_list, V, p->TW, p->B, p->k, out_ids, out_scores);
+                       p->cand_off, p->NG, p->cand_list, V, p->TW, p->B, p->k, out_ids, out_scores,
+                       x_flags(p), (uint32_t)p->ntiles);
     EGR_CHECK_LAUNCH();
     return EGR_OK;
   }
@@ -1762,7 +1848,7 @@ int egr_plan_topk(egr_plan* p, int32_t exclude_label, uint32_t* out_ids, float* 
   hipLaunchKernelGGL(topk_partial_kernel, dim3((waves + 3) / 4), dim3(256), 0, st,
                      p->x[p->xcur], p->reach[p->rcur], (uint32_t)p->RS, p->s->vlabel, exclude_label, V,
                      p->owned, p->TW,
-                     p->B, p->n_chunks, p->part_s, p->part_v);
+                     p->B, p->n_chunks, p->part_s, p->part_v, x_flags(p), (uint32_t)p->ntiles);
   EGR_CHECK_LAUNCH();
   hipLaunchKernelGGL(topk_merge_kernel, dim3((p->B + 3) / 4), dim3(256), 0, st, p->part_s,
                      p->part_v, p->TW, p->B, p->n_chunks, p->k, out_ids, out_scores);
@@ -1786,7 +1872,8 @@ int egr_plan_read_scores(const egr_plan* p, float* out, void* stream) {
   DeviceGuard guard(p->s->device);
   const size_t n = (size_t)p->s->V * p->B;
   hipLaunchKernelGGL(scores_rowmajor_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->B, out);
+                     (hipStream_t)stream, p->x[p->xcur], (uint32_t)p->s->V, p->TW, p->B, out,
+                     x_flags(p), (uint32_t)p->ntiles);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
@@ -1894,6 +1981,7 @@ int egr_plan_set_owned(egr_plan* p, int64_t n_owned) {
     return egr::fail(EGR_EDEVICE, "egr_plan_set_owned: chunk table upload failed");
   p->nchunks = (uint32_t)chunks.size() - 1;
   p->rnchunks = (uint32_t)rchunks.size() - 1;
+  EGR_TRY(set_long_chunks(p, chunks));
   for (int b = 0; b < 2; ++b) {
     const size_t nb = (size_t)p->s->V * p->ntiles;
     if (!p->nzf[b]) {
@@ -1917,7 +2005,7 @@ int egr_plan_pack_scores(const egr_plan* p, const uint32_t* rows, int64_t n, flo
   const float* X = p->hops_done == 0 ? nullptr : p->x[p->xcur];
   if (!X) return egr::fail(EGR_ESTATE, "egr_plan_pack_scores: run a hop first");
   hipLaunchKernelGGL(pack_scores_kernel, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, X,
-                     (uint32_t)p->s->V, p->TW, p->Bpad, rows, out);
+                     (uint32_t)p->s->V, p->TW, p->Bpad, rows, out, x_flags(p), (uint32_t)p->ntiles);
   EGR_CHECK_LAUNCH();
   return EGR_OK;
 }
@@ -2041,7 +2129,7 @@ int egr_plan_pack_sparse(egr_plan* p, int32_t what, const uint32_t* rows, int64_
   // the device works while the copy and the host's synchronisation round trip are in flight
   hipLaunchKernelGGL(sx_emit_kernel, sxg, dim3(256), 0, st, X, R, V, p->TW,
                      (uint32_t)p->RS, width, reach, rows, (int64_t)n, dseg, P, p->sx_off, p->sx_mask,
-                     MW, out, cap);
+                     MW, out, cap, reach ? nullptr : p->nzf[p->xcur], (uint32_t)p->ntiles);
   EGR_CHECK_LAUNCH();
   EGR_HIP(hipStreamSynchronize(st));
   const int64_t* bound = pbound;

@@ -84,6 +84,65 @@ def test_zero_tile_skip_off_is_bit_identical(B, monkeypatch):
     assert got[0].tobytes() == exp.tobytes() and got[1].tobytes() == exp.tobytes()
 
 
+def _hub_world(n=5000):
+    from egraph.graph import EvidenceGraph
+    g = EvidenceGraph()
+    g.merge_nodes([f"p{i}" for i in range(n)] + ["hub", "inc"], ["Pod"] * n + ["Node", "Incident"])
+    g.merge_edges([f"p{i}" for i in range(n)] + ["inc"], ["hub"] * n + ["p0"],
+                  ["SCHEDULED_ON"] * n + ["AFFECTS"])
+    return g
+
+
+@pytest.mark.parametrize("world", ["small", "hub"])
+def test_reused_plan_reads_no_stale_tiles(world):
+    """The hop does not store a row tile that came out all +0 (and holds no seed of the row):
+    such a tile keeps whatever an earlier run left in it, and every reader goes through the tile
+    flags.  A plan run first with seeds in every tile, then with seeds in the first tile only,
+    must give the second run's scores, top-k (candidate lists and full scan) and packed rows
+    exactly as a fresh plan / the oracle do -- including the hub row longer than the 2048-entry
+    LDS stage, whose gathers are not compacted ("hub")."""
+    B = 300                                                     # three 128-column tiles
+    rng = np.random.default_rng(7)
+    if world == "small":
+        g, sv, sc, ss, src = _small_world(B, seed=17, pods=1500)
+    else:
+        g = _hub_world()
+        n = 5000
+        sv = rng.integers(0, n, 4000).astype(np.uint32)
+        sc = rng.integers(0, B, 4000).astype(np.uint32)
+        ss = rng.random(4000).astype(np.float32)
+        src = np.full(B, n + 1, np.uint32)
+    first = sc < 128                                            # the second run: tile 0 only
+    sv2, sc2, ss2 = sv[first], sc[first], ss[first]
+    assert len(sv2) and (~first).any()
+    snap = g.snapshot()
+    plan = snap.plan(B, max_seeds=len(sv), k=6)
+    assert plan.tile_width == 128
+    for vv, cc, s_ in ((sv, sc, ss), (sv2, sc2, ss2)):
+        plan.set_seeds(_dev(vv), _dev(cc), _dev(s_))
+        plan.set_sources(_dev(src))
+        ids, scores = plan.run(hops=3)
+    csr = g.csr()
+    exp = oracle.propagate(csr["row_ptr"], csr["col"], csr["val"], sv2, sc2, ss2, B, 3)
+    assert plan.read_scores().cpu().numpy().tobytes() == exp.tobytes()
+    er = oracle.reach(csr["row_ptr"], csr["col"], src, 3)
+    vl, _, _, _ = g.export()
+    eids, esc = oracle.topk(exp, er, vl, -1, 6)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), eids)
+    np.testing.assert_array_equal(scores.cpu().numpy(), esc)
+    inc = g.labels().index("Incident")
+    ids2, sc_2 = plan.topk(exclude_label=inc)                   # (no lists for it: the full scan)
+    eids2, esc2 = oracle.topk(exp, er, vl, inc, 6)
+    np.testing.assert_array_equal(ids2.cpu().numpy().view(np.uint32), eids2)
+    np.testing.assert_array_equal(sc_2.cpu().numpy(), esc2)
+    rows = np.sort(rng.choice(exp.shape[0], size=64, replace=False)).astype(np.uint32)
+    out = torch.empty((64, 384), dtype=torch.float32, device="cuda")
+    plan.pack_scores(_dev(rows), out)
+    torch.cuda.synchronize()
+    packed = out.cpu().numpy()[:, :B]
+    assert packed.tobytes() == np.ascontiguousarray(exp[rows]).tobytes()
+
+
 @pytest.mark.parametrize("tw", [4, 16, 64, 128])
 def test_tile_width_override(tw, monkeypatch):
     B = 200
@@ -164,12 +223,8 @@ def test_candidates_entry_point_and_exclusions(exclude):
 
 def test_hub_rows_longer_than_the_lds_stage():
     """A vertex whose CSR row exceeds the 2048 staged entries takes the global-read path."""
-    from egraph.graph import EvidenceGraph
-    g = EvidenceGraph()
     n = 5000
-    g.merge_nodes([f"p{i}" for i in range(n)] + ["hub", "inc"], ["Pod"] * n + ["Node", "Incident"])
-    g.merge_edges([f"p{i}" for i in range(n)] + ["inc"], ["hub"] * n + ["p0"],
-                  ["SCHEDULED_ON"] * n + ["AFFECTS"])
+    g = _hub_world(n)
     B = 64
     rng = np.random.default_rng(0)
     sv = rng.integers(0, n, 3000).astype(np.uint32)
