@@ -771,6 +771,35 @@ static inline uint64_t w_str_hash(PyObject* o) {
   return h ? h : 1u;
 }
 
+/* Software pipelining of the workers' row reads: a row costs a chain of dependent cache misses
+ * (the dict, its keys table, each value object), so a worker touches rows ahead of the one it
+ * works on -- row j + 6's dict, row j + 3's keys table, row j + 1's values -- and the misses of
+ * the next rows overlap the current row's work.  Prefetches only: no value is used. */
+static inline void row_prefetch(PyObject* evs, Py_ssize_t j, Py_ssize_t n) {
+  if (j + 6 < n) __builtin_prefetch(PyList_GET_ITEM(evs, j + 6));
+  if (j + 3 < n) {
+    PyObject* d = PyList_GET_ITEM(evs, j + 3);
+    if (PyDict_CheckExact(d)) {
+      const char* k = (const char*)((PyDictObject*)d)->ma_keys;
+      __builtin_prefetch(k);
+      __builtin_prefetch(k + 64);
+      __builtin_prefetch(k + 128);
+      __builtin_prefetch(k + 192);
+      __builtin_prefetch(k + 256);
+    }
+  }
+  if (j + 1 < n) {
+    PyObject* d = PyList_GET_ITEM(evs, j + 1);
+    if (PyDict_CheckExact(d)) {
+      Py_ssize_t pos = 0;
+      PyObject *key, *v;
+      Py_hash_t h;
+      int c = 0;
+      while (c++ < 16 && _PyDict_Next(d, &pos, &key, &v, &h)) __builtin_prefetch(v);
+    }
+  }
+}
+
 typedef struct {
   PyObject* const* lists;    /* the evidence lists (exact lists; their items are read in place) */
   const int64_t* base;       /* first row of each incident */
@@ -782,14 +811,25 @@ typedef struct {
   uint64_t* phash;           /* per row with a node name: its characters' hash (0: not a str) */
   PyObject** ids5;           /* per incident: its first five rows' ids (borrowed; NULL = none) */
   uint8_t* redo;             /* per row: 1 = encode on the calling thread */
+  Py_ssize_t* next;          /* the next unclaimed incident (shared by the call's jobs) */
 } WJob;
+
+/* Incidents per claim of the workers' shared cursor: rows differ in cost (a pod row reads a
+ * dozen keys, an event row two), so a static split by row counts left threads idle behind the
+ * slowest; claims of a few incidents balance them. */
+#define W_CHUNK 8
 
 static void* w_main(void* arg) {
   const WJob* J = (const WJob*)arg;
-  for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
+  for (;;) {
+  const Py_ssize_t c0 = __atomic_fetch_add(J->next, (Py_ssize_t)W_CHUNK, __ATOMIC_RELAXED);
+  if (c0 >= J->i1) break;
+  const Py_ssize_t c1 = c0 + W_CHUNK < J->i1 ? c0 + W_CHUNK : J->i1;
+  for (Py_ssize_t i = c0; i < c1; ++i) {
     PyObject* evs = J->lists[i];
     const Py_ssize_t n = PyList_GET_SIZE(evs);
     for (Py_ssize_t j = 0; j < n; ++j) {
+      row_prefetch(evs, j, n);
       const Py_ssize_t r = J->base[i] + j;
       PyObject* ev = PyList_GET_ITEM(evs, j);
       Row row = {0, 0, NO_NODE, 0.0, NULL};
@@ -802,6 +842,7 @@ static void* w_main(void* arg) {
       J->pend[r] = row.pending_node;
       J->phash[r] = (!redo && row.pending_node != NULL) ? w_str_hash(row.pending_node) : 0u;
     }
+  }
   }
   return NULL;
 }
@@ -977,24 +1018,49 @@ static PyObject* encode_rows(PyObject* self, PyObject* args) {
     for (Py_ssize_t i = 0; i < B; ++i) base[i + 1] = base[i] + PyList_GET_SIZE(PySequence_Fast_GET_ITEM(seq, i));
     if (threads > PAR_MAX_THREADS) threads = PAR_MAX_THREADS;
     WJob jobs[PAR_MAX_THREADS];
-    /* incident ranges of about total / threads rows each */
-    Py_ssize_t i = 0;
-    for (int t = 0; t < threads; ++t) {
-      const int64_t goal = (int64_t)((total * (t + 1)) / threads);
-      const Py_ssize_t i0 = i;
-      while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
-      jobs[t] = (WJob){PySequence_Fast_ITEMS(seq), base, i0, i, &WV, flags, vocab, err, pend, phash,
-                       ids5, redo};
-    }
+    /* every job claims W_CHUNK incidents at a time from one cursor, up to B */
+    Py_ssize_t next = 0;
+    for (int t = 0; t < threads; ++t)
+      jobs[t] = (WJob){PySequence_Fast_ITEMS(seq), base, 0, B, &WV, flags, vocab, err, pend, phash,
+                       ids5, redo, &next};
     /* (the GIL stays held: no Python code runs while the workers read) */
     pool_run(jobs, threads);
     /* node names are numbered in a C map keyed by the workers' content hashes while no Python
      * code runs and node_keys starts empty (encode_batch's fresh dict) */
     if (PyDict_GET_SIZE(V.node_keys) == 0) {
       size_t np = 0;
-      for (Py_ssize_t q = 0; q < total; ++q) np += pend[q] != NULL && !redo[q];
+      int fast = 1;                  /* no row for the serial encoder, every node name a str */
+      for (Py_ssize_t q = 0; q < total; ++q) {
+        np += pend[q] != NULL && !redo[q];
+        fast &= !redo[q] && (pend[q] == NULL || phash[q] != 0);
+      }
       if (nodemap_init(&nm, np) < 0) goto done;
       use_map = 1;
+      if (fast) {
+        /* the completion without the serial loop: the workers wrote every row's flags / vocab /
+         * err; what is left is the node numbering (first-seen order, the C map), the segment
+         * offsets and each incident's first five evidence ids -- the serial pass's results for
+         * rows it would only have copied */
+        for (Py_ssize_t q = 0; q < total; ++q)
+          node[q] = pend[q] != NULL ? nodemap_get(&nm, phash[q], pend[q]) : NO_NODE;
+        seg[0] = 0;
+        for (Py_ssize_t i = 0; i < B; ++i) {
+          const Py_ssize_t n = base[i + 1] - base[i], m = n < 5 ? n : 5;
+          PyObject* first = PyList_New(m);
+          if (!first) goto done;
+          for (Py_ssize_t j = 0; j < m; ++j) {
+            PyObject* id = ids5[5 * i + j] != NULL ? ids5[5 * i + j] : Py_None;
+            Py_INCREF(id);
+            PyList_SET_ITEM(first, j, id);
+          }
+          PyList_SET_ITEM(ids, i, first);
+          seg[i + 1] = base[i + 1];
+        }
+        /* (node_keys is left empty: no row went through Python, so nothing read the numbering
+         * from it, and encode_batch drops it -- copying the C map out was a third of this path) */
+        result = Py_BuildValue("(On)", ids, (Py_ssize_t)0);
+        goto done;
+      }
     }
   }
   /* serial pass (or the completion of the parallel one), in row order */
@@ -1762,40 +1828,16 @@ typedef struct {
   uint32_t* vert;
   float* val;
   uint8_t* redo;
+  Py_ssize_t* next;          /* the next unclaimed incident (shared; W_CHUNK per claim) */
 } SJob;
-
-/* Software pipelining of the workers' row reads: a row costs a chain of dependent cache misses
- * (the dict, its keys table, each value object), so a worker touches rows ahead of the one it
- * works on -- row j + 6's dict, row j + 3's keys table, row j + 1's values -- and the misses of
- * the next rows overlap the current row's work.  Prefetches only: no value is used. */
-static inline void row_prefetch(PyObject* evs, Py_ssize_t j, Py_ssize_t n) {
-  if (j + 6 < n) __builtin_prefetch(PyList_GET_ITEM(evs, j + 6));
-  if (j + 3 < n) {
-    PyObject* d = PyList_GET_ITEM(evs, j + 3);
-    if (PyDict_CheckExact(d)) {
-      const char* k = (const char*)((PyDictObject*)d)->ma_keys;
-      __builtin_prefetch(k);
-      __builtin_prefetch(k + 64);
-      __builtin_prefetch(k + 128);
-      __builtin_prefetch(k + 192);
-      __builtin_prefetch(k + 256);
-    }
-  }
-  if (j + 1 < n) {
-    PyObject* d = PyList_GET_ITEM(evs, j + 1);
-    if (PyDict_CheckExact(d)) {
-      Py_ssize_t pos = 0;
-      PyObject *key, *v;
-      Py_hash_t h;
-      int c = 0;
-      while (c++ < 16 && _PyDict_Next(d, &pos, &key, &v, &h)) __builtin_prefetch(v);
-    }
-  }
-}
 
 static void* s_main(void* arg) {
   const SJob* J = (const SJob*)arg;
-  for (Py_ssize_t i = J->i0; i < J->i1; ++i) {
+  for (;;) {
+  const Py_ssize_t c0 = __atomic_fetch_add(J->next, (Py_ssize_t)W_CHUNK, __ATOMIC_RELAXED);
+  if (c0 >= J->i1) break;
+  const Py_ssize_t c1 = c0 + W_CHUNK < J->i1 ? c0 + W_CHUNK : J->i1;
+  for (Py_ssize_t i = c0; i < c1; ++i) {
     PyObject* evs = J->lists[i];
     const Py_ssize_t n = PyList_GET_SIZE(evs);
     for (Py_ssize_t j = 0; j < n; ++j) {
@@ -1804,6 +1846,7 @@ static void* s_main(void* arg) {
       J->val[r] = 0.f;
       J->redo[r] = (uint8_t)s_row(PyList_GET_ITEM(evs, j), J->find, J->g, &J->vert[r], &J->val[r]);
     }
+  }
   }
   return NULL;
 }
@@ -1905,14 +1948,35 @@ static PyObject* seed_attach(PyObject* self, PyObject* args) {
     for (Py_ssize_t i = 0; i < B; ++i) base[i + 1] = base[i] + PyList_GET_SIZE(PySequence_Fast_GET_ITEM(seq, i));
     if (threads > PAR_MAX_THREADS) threads = PAR_MAX_THREADS;
     SJob jobs[PAR_MAX_THREADS];
-    Py_ssize_t i = 0;
-    for (int t = 0; t < threads; ++t) {
-      const int64_t goal = (int64_t)((total * (t + 1)) / threads);
-      const Py_ssize_t i0 = i;
-      while (i < B && (base[i + 1] <= goal || t == threads - 1)) ++i;
-      jobs[t] = (SJob){PySequence_Fast_ITEMS(seq), base, i0, i, find, g, wv, wval, redo};
-    }
+    Py_ssize_t next = 0;                 /* every job claims W_CHUNK incidents at a time */
+    for (int t = 0; t < threads; ++t)
+      jobs[t] = (SJob){PySequence_Fast_ITEMS(seq), base, 0, B, find, g, wv, wval, redo, &next};
     pool_run_fn(s_main, jobs, sizeof(SJob), threads);   /* (the GIL stays held) */
+    /* no row for the Python statement: the attached rows straight from the workers' arrays, in
+     * row order (the serial loop below would only copy them) */
+    int fast = 1;
+    for (Py_ssize_t q = 0; q < total && fast; ++q) fast = !redo[q];
+    if (fast) {
+      for (Py_ssize_t q = 0; q < total; ++q) nout += wv[q] != NO_NODE;
+      const size_t m = nout ? (size_t)nout : 1;
+      ov = PyMem_Malloc(m * sizeof(uint32_t));
+      oc = PyMem_Malloc(m * sizeof(uint32_t));
+      os = PyMem_Malloc(m * sizeof(float));
+      if (!ov || !oc || !os) { PyErr_NoMemory(); goto done; }
+      Py_ssize_t k = 0;
+      for (Py_ssize_t c = 0; c < B; ++c)
+        for (Py_ssize_t q = base[c]; q < base[c + 1]; ++q)
+          if (wv[q] != NO_NODE) {
+            ov[k] = wv[q];
+            oc[k] = (uint32_t)c;
+            os[k] = wval[q];
+            ++k;
+          }
+      result = Py_BuildValue("(y#y#y#)", (const char*)ov, nout * (Py_ssize_t)sizeof(uint32_t),
+                             (const char*)oc, nout * (Py_ssize_t)sizeof(uint32_t), (const char*)os,
+                             nout * (Py_ssize_t)sizeof(float));
+      goto done;
+    }
   }
   {
     int ran_python = 0;
